@@ -1,0 +1,241 @@
+/*
+ * mmdx — MI355X-native (gfx950) kernels for the multimodal diagnosis hot path of
+ * PravCoder/Multi-Modal-Medical-Imaging-and-Report-ML-Diagnosis-System.
+ *
+ * C ABI of libmmdx_hip.so.  Plain pointers and sizes only; every buffer is owned by the
+ * caller (PyTorch's caching allocator in the shipped host code); the library never
+ * allocates or frees caller memory.  Where a call needs scratch, the caller queries
+ * `*_workspace_size` and passes a buffer of at least that many bytes.
+ *
+ * The reference has no native code and no FFI: its hot path is pure PyTorch-CPU
+ * (backend/ml/pipelines/training_pipeline.py, "TP" below).  Each entry point names the
+ * reference operator it replaces; the Python host layer (mmdx.training_pipeline) keeps
+ * the reference's class/function surface and binds these symbols with ctypes.
+ *
+ * Conventions
+ *   dtype:      0 = fp32 (parity path, exact-f32 MFMA), 1 = bf16 (throughput path)
+ *   images:     NHWC, channels innermost; conv weights packed [Cout][R][S][Cin] ("KRSC")
+ *               for fwd and [Cin][R][S][Cout] ("CRSK") for dgrad; fp32 master weights
+ *               and gradients stay in PyTorch's [Cout][Cin][R][S] ("KCRS") layout.
+ *   matrices:   row-major; "kmajor" = the contraction index is the contiguous one.
+ *   stream:     a hipStream_t passed as void*; every call is stream-ordered, reentrant,
+ *               graph-capturable (no allocation, no sync, no host readback).
+ *   return:     0 on success, negative errno / -hipError_t on failure;
+ *               mmdx_last_error() gives a thread-local message.
+ */
+#ifndef MMDX_H_
+#define MMDX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { MMDX_F32 = 0, MMDX_BF16 = 1 };
+enum { MMDX_ACT_NONE = 0, MMDX_ACT_RELU = 1, MMDX_ACT_GELU = 2 };
+
+int mmdx_version(void);
+const char* mmdx_last_error(void);
+
+/* ---------------------------------------------------------------- GEMM (nn.Linear)
+ * C[M,N] = act(alpha * sum_k A(m,k) B(n,k) + bias[n] + addend[m,n]) + beta * C
+ * (addend: optional fp32, leading dim ldc — lets a concat-input Linear run as two GEMMs)
+ * A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m];  same for B with (n,k).
+ * c_dtype may differ from dtype (bf16 compute -> fp32 weight-gradient output).
+ * preact (optional, c_dtype, ld = ldc) receives alpha*acc + bias before the activation.
+ * Replaces: nn.Linear fwd/bwd in ImageEncoderCNN.proj/classifier (TP:189,194),
+ * TextEncoderTransformer.proj/classifier (TP:365,367), BERT dense layers (TP:360 ->
+ * transformers BertModel), fusion_mlp[0] + GELU (TP:534-536), disease_head (TP:542). */
+size_t mmdx_gemm_workspace_size(int dtype, int M, int N, int K);
+int mmdx_gemm(int dtype, int M, int N, int K,
+              const void* A, long lda, int a_kmajor,
+              const void* B, long ldb, int b_kmajor,
+              void* C, long ldc, int c_dtype,
+              const float* bias, const float* addend, int act, float alpha, float beta,
+              void* preact, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- convolution
+ * Replaces: every nn.Conv2d of torchvision resnet18/50 reached through
+ * ImageEncoderCNN._backbone_forward_grad/_nograd (TP:279-289, TP:183). */
+typedef struct {
+  int N, H, W, C;      /* input NHWC */
+  int K;               /* output channels */
+  int R, S;            /* filter height, width */
+  int stride_h, stride_w, pad_h, pad_w;
+  int P, Q;            /* output height, width */
+} mmdx_conv_desc;
+
+/* fp32 KCRS master -> packed compute-dtype copies (either output may be NULL).
+ * Channel padding: desc->C may exceed the master's Cin (c_master); pad lanes are 0. */
+int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
+                          const float* w_kcrs, void* w_krsc, void* w_crsk, void* stream);
+int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
+                  void* y, void* stream);
+/* dx = dgrad + beta * dx  (beta = 1 sums the residual-path gradient in the epilogue) */
+int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
+                    const void* w_crsk, void* dx, float beta, void* stream);
+size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc* d);
+/* dw_kcrs (fp32, master layout, Cin = c_master) = dw_kcrs*beta + grad */
+int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void* x,
+                    const void* dy, float* dw_kcrs, float beta, void* workspace,
+                    size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- batch norm (+res)(+ReLU)
+ * x, y, residual: [rows, C] (NHWC flattened).  Train mode computes batch statistics
+ * (biased var for normalisation, unbiased for running_var, momentum update as
+ * nn.BatchNorm2d(eps, momentum)); eval mode uses running stats.
+ * save_mean/save_rstd: [C] fp32, consumed by the backward.
+ * Replaces: BatchNorm2d + ReLU (+ Bottleneck residual add) inside the resnet trunk
+ * (train mode: unfreeze_backbone TP:223; eval: freeze_backbone TP:206, IP:170). */
+size_t mmdx_bn_workspace_size(long rows, int C);
+int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
+                const float* gamma, const float* beta, float* running_mean,
+                float* running_var, float momentum, float eps,
+                float* save_mean, float* save_rstd,
+                const void* residual, int relu, void* y,
+                void* workspace, size_t ws_bytes, void* stream);
+/* dy: grad w.r.t. y; y: forward output (ReLU mask source).  Writes dx, d_residual
+ * (may be NULL), and dgamma/dbeta (fp32, accumulated with beta_acc). */
+int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
+                long rows, int C, const float* gamma, const float* save_mean,
+                const float* save_rstd, int relu, void* dx, void* d_residual,
+                float* dgamma, float* dbeta, float beta_acc,
+                void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- pooling
+ * Replaces: resnet maxpool 3x3/2 (backbone[3]) and AdaptiveAvgPool2d(1) (backbone[8])
+ * followed by flatten(1) (TP:281/288). */
+/* argmax: uint8 window index (r*k+s) of the first maximum, as PyTorch CPU max_pool2d */
+int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int k, int s,
+                     int p, void* y, uint8_t* argmax, int P, int Q, void* stream);
+int mmdx_maxpool_bwd(int dtype, const uint8_t* argmax, const void* dy, int N, int H, int W,
+                     int C, int k, int s, int p, int P, int Q, void* dx, void* stream);
+int mmdx_avgpool_fwd(int dtype, const void* x, int N, int HW, int C, void* y, void* stream);
+int mmdx_avgpool_bwd(int dtype, const void* dy, int N, int HW, int C, void* dx,
+                     void* stream);
+
+/* ---------------------------------------------------------------- layout / casts
+ * NCHW fp32 image batch (output of image_transfom_into_tensor, TP:112-119) ->
+ * NHWC compute dtype with channels zero-padded to c_pad. */
+int mmdx_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int c_pad,
+                      void* y, void* stream);
+int mmdx_cast(int dst_dtype, int src_dtype, const void* x, long n, void* y, void* stream);
+
+/* ---------------------------------------------------------------- elementwise / norms
+ * LayerNorm over the last dim D (fusion_mlp[3] TP:538, BERT LayerNorms);
+ * optional residual added before the norm (BERT "Add & Norm"). */
+int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual, long rows, int D,
+                       const float* gamma, const float* beta, float eps, void* y,
+                       void* sum_out, float* save_mean, float* save_rstd, void* stream);
+int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, long rows, int D,
+                       const float* gamma, const float* save_mean, const float* save_rstd,
+                       void* dx, float* dgamma, float* dbeta, float beta_acc,
+                       void* workspace, size_t ws_bytes, void* stream);
+size_t mmdx_layernorm_workspace_size(long rows, int D);
+/* GELU backward from the pre-activation: dx = dy * gelu'(pre) */
+int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n, void* dx,
+                  void* stream);
+/* bias gradient: db[N] (+)= sum_m dy[m, N] */
+int mmdx_bias_grad(int dtype, const void* dy, long M, int N, float* db, float beta_acc,
+                   void* workspace, size_t ws_bytes, void* stream);
+size_t mmdx_bias_grad_workspace_size(long M, int N);
+/* dropout with a counter-based hash RNG: y = x * mask / (1-p); mask saved as uint8 */
+int mmdx_dropout_fwd(int dtype, const void* x, long n, float p, uint64_t seed,
+                     uint64_t offset, void* y, uint8_t* mask, void* stream);
+int mmdx_dropout_bwd(int dtype, const void* dy, const uint8_t* mask, long n, float p,
+                     void* dx, void* stream);
+
+/* ---------------------------------------------------------------- loss / heads
+ * BCEWithLogitsLoss (mean) (TP:843,1015,1049): loss[0] = mean over B*C;
+ * dlogits = (sigmoid(z) - y) / (B*C) * dloss_scale. */
+int mmdx_bce_logits_fwd(const float* logits, const float* target, int B, int C,
+                        float* loss, void* stream);
+int mmdx_bce_logits_bwd(const float* logits, const float* target, int B, int C,
+                        const float* dloss, float* dlogits, void* stream);
+
+/* ---------------------------------------------------------------- text towers
+ * BERT embeddings: word[id] + pos[i] + type[tt] -> LayerNorm (transformers BertEmbeddings,
+ * reached from TextEncoderTransformer.encode TP:470/473).  ids/tt int64 [B,L]. */
+int mmdx_embed_ln_fwd(int dtype, const int64_t* ids, const int64_t* tt, int B, int L,
+                      int D, const float* word, const float* pos, const float* type,
+                      const float* gamma, const float* beta, float eps, void* y,
+                      void* xsum, float* save_mean, float* save_rstd, void* stream);
+/* scatter-add of dx (= grad of the pre-LN sum) into dense fp32 table grads */
+int mmdx_embed_bwd(int dtype, const int64_t* ids, const int64_t* tt, int B, int L, int D,
+                   const void* dsum, float* dword, float* dpos, float* dtype_tab,
+                   void* stream);
+/* masked mean pool (TP:452-459): out[b,:] = sum_l h[b,l,:]*m[b,l] / max(sum_l m, 1e-6) */
+int mmdx_masked_mean_fwd(int dtype, const void* h, const int64_t* mask, int B, int L,
+                         int D, void* out, void* stream);
+int mmdx_masked_mean_bwd(int dtype, const void* dout, const int64_t* mask, int B, int L,
+                         int D, void* dh, void* stream);
+/* fused embedding gather + masked mean (build-defined C2 text tower):
+ * out[b,:] = sum_l E[ids[b,l],:]*m[b,l] / max(sum_l m, 1e-6) */
+int mmdx_embed_mean_fwd(int dtype, const int64_t* ids, const int64_t* mask, int B, int L,
+                        int D, const float* table, void* out, void* stream);
+int mmdx_embed_mean_bwd(int dtype, const int64_t* ids, const int64_t* mask, int B, int L,
+                        int D, const void* dout, float* dtable, void* stream);
+/* embedding gather (rows of an fp32 table -> compute dtype), for the BiLSTM tower */
+int mmdx_embed_gather(int dtype, const int64_t* ids, long n, int D, const float* table,
+                      void* out, void* stream);
+int mmdx_embed_scatter(int dtype, const int64_t* ids, long n, int D, const void* dout,
+                       float* dtable, void* stream);
+
+/* Multi-head self-attention core, head dim 64, L <= 256, with additive key mask
+ * (BertSelfAttention: softmax(QK^T/sqrt(d) + (1-mask)*min) V).
+ * qkv: [B, L, 3, H, 64] (fused projection output); out: [B, L, H, 64];
+ * probs saved for backward: [B, H, L, L] fp32 (may be NULL in inference). */
+int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
+                       int H, float scale, void* out, float* probs, void* stream);
+int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const void* dout,
+                       const int64_t* mask, int B, int L, int H, float scale, void* dqkv,
+                       void* stream);
+
+/* LSTM recurrence for one layer, both directions (build-defined C3/C4 tower).
+ * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);
+ * w_hh: [2][4H][H] compute dtype; h_out: [B, L, 2H]; saved c: [2, L, B, H] fp32,
+ * gates: [2, L, B, 4H] fp32 post-activation (for backward). */
+int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
+                  void* h_out, float* c_save, float* gates_save, void* workspace,
+                  size_t ws_bytes, void* stream);
+size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H);
+int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
+                  const float* gates_save, const void* dh_out, int B, int L, int H,
+                  void* dxg, float* dw_hh, void* workspace, size_t ws_bytes,
+                  void* stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * torch.optim.AdamW (decoupled weight decay) over every tensor of every param group in
+ * one launch (build_optimizer groups TP:238-269, TP:408-432; fusion optimiser
+ * TP:1018-1023).  `table` is a DEVICE array of descriptors sorted by `off` (prefix sum of
+ * numels, total = sum n).  step_dev (device fp32) is incremented by the call, so the
+ * update replays inside a graph.  grad_scale (device scalar or NULL) multiplies every
+ * gradient: the clip coefficient of clip_grad_norm_ (TP:1058). */
+typedef struct {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  long n;
+  long off;
+  float lr;
+  float wd;
+} mmdx_adamw_tensor;
+int mmdx_adamw_multi(int ntensors, const mmdx_adamw_tensor* table, long total, float beta1,
+                     float beta2, float eps, float* step_dev, const float* grad_scale,
+                     void* stream);
+/* global L2 norm of the .g fields of `table`; scale[0] = min(1, max_norm/(norm+1e-6))
+ * (torch.nn.utils.clip_grad_norm_); max_norm <= 0 gives scale 1. */
+size_t mmdx_grad_norm_workspace_size(void);
+int mmdx_grad_norm(int ntensors, const mmdx_adamw_tensor* table, long total, float max_norm,
+                   float* norm, float* scale, void* workspace, size_t ws_bytes, void* stream);
+/* in-place g *= scale[0] over the .g fields (the mul_ of clip_grad_norm_) */
+int mmdx_scale_grads(int ntensors, const mmdx_adamw_tensor* table, long total,
+                     const float* scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMDX_H_ */

@@ -1,0 +1,176 @@
+"""ctypes binding of libmmdx_hip.so (the C ABI declared in include/mmdx.h).
+
+The product path has exactly one implementation: these HIP kernels.  If the library is
+missing or fails to load, every op raises — there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmmdx_hip.so")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+
+vp, i32, i64, f32, sz, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_size_t, C.c_uint64
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int) for n in
+                ("N", "H", "W", "C", "K", "R", "S", "stride_h", "stride_w", "pad_h", "pad_w",
+                 "P", "Q")]
+
+
+class AdamWTensor(C.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("m", vp), ("v", vp), ("n", C.c_long), ("off", C.c_long),
+                ("lr", C.c_float), ("wd", C.c_float)]
+
+
+CD = C.POINTER(ConvDesc)
+
+# name -> (restype, argtypes).  Kept in header order; tests check this table against
+# include/mmdx.h so the binding cannot drift from the ABI.
+SIGNATURES = {
+    "mmdx_version": (i32, []),
+    "mmdx_last_error": (C.c_char_p, []),
+    "mmdx_gemm_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_gemm": (i32, [i32, i32, i32, i32, vp, i64, i32, vp, i64, i32, vp, i64, i32, vp, vp,
+                        i32, f32, f32, vp, vp, sz, vp]),
+    "mmdx_conv_pack_weight": (i32, [i32, CD, i32, vp, vp, vp, vp]),
+    "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp]),
+    "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
+    "mmdx_conv_wgrad_workspace_size": (sz, [i32, CD]),
+    "mmdx_conv_wgrad": (i32, [i32, CD, i32, vp, vp, vp, f32, vp, sz, vp]),
+    "mmdx_bn_workspace_size": (sz, [i64, i32]),
+    "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, vp, vp, vp, f32, f32, vp, vp, vp, i32, vp,
+                          vp, sz, vp]),
+    "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, i32, vp, vp, vp, vp, f32,
+                          vp, sz, vp]),
+    "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,
+                               vp]),
+    "mmdx_maxpool_bwd": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp,
+                               vp]),
+    "mmdx_avgpool_fwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),
+    "mmdx_avgpool_bwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),
+    "mmdx_nchw_to_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
+    "mmdx_cast": (i32, [i32, i32, vp, i64, vp, vp]),
+    "mmdx_layernorm_fwd": (i32, [i32, vp, vp, i64, i32, vp, vp, f32, vp, vp, vp, vp, vp]),
+    "mmdx_layernorm_bwd": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, f32, vp, sz,
+                                 vp]),
+    "mmdx_layernorm_workspace_size": (sz, [i64, i32]),
+    "mmdx_gelu_bwd": (i32, [i32, vp, vp, i64, vp, vp]),
+    "mmdx_bias_grad": (i32, [i32, vp, i64, i32, vp, f32, vp, sz, vp]),
+    "mmdx_bias_grad_workspace_size": (sz, [i64, i32]),
+    "mmdx_dropout_fwd": (i32, [i32, vp, i64, f32, u64, u64, vp, vp, vp]),
+    "mmdx_dropout_bwd": (i32, [i32, vp, vp, i64, f32, vp, vp]),
+    "mmdx_bce_logits_fwd": (i32, [vp, vp, i32, i32, vp, vp]),
+    "mmdx_bce_logits_bwd": (i32, [vp, vp, i32, i32, vp, vp, vp]),
+    "mmdx_embed_ln_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp, vp,
+                                vp, vp]),
+    "mmdx_embed_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
+    "mmdx_masked_mean_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp]),
+    "mmdx_masked_mean_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp]),
+    "mmdx_embed_mean_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp]),
+    "mmdx_embed_mean_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp]),
+    "mmdx_embed_gather": (i32, [i32, vp, i64, i32, vp, vp, vp]),
+    "mmdx_embed_scatter": (i32, [i32, vp, i64, i32, vp, vp, vp]),
+    "mmdx_attention_fwd": (i32, [i32, vp, vp, i32, i32, i32, f32, vp, vp, vp]),
+    "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp]),
+    "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp]),
+    "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
+    "mmdx_adamw_multi": (i32, [i32, vp, i64, f32, f32, f32, vp, vp, vp]),
+    "mmdx_grad_norm_workspace_size": (sz, []),
+    "mmdx_grad_norm": (i32, [i32, vp, i64, f32, vp, vp, vp, sz, vp]),
+    "mmdx_scale_grads": (i32, [i32, vp, i64, vp, vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class MmdxLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmmdx_hip.so once; raise loudly if it is absent (no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise MmdxLibraryError(
+                f"libmmdx_hip.so not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        h = C.CDLL(LIB_PATH)
+        missing = []
+        for name, (res, args) in SIGNATURES.items():
+            try:
+                fn = getattr(h, name)
+            except AttributeError:
+                missing.append(name)
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        h.mmdx_missing_symbols = missing
+        _lib = h
+    return _lib
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        msg = lib().mmdx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args):
+    """Invoke a C-ABI entry point and raise RuntimeError on a non-zero return code."""
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if fn.restype is i32 and name not in ("mmdx_version",):
+        check(rc, name)
+    return rc
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError(f"mmdx kernels compute in float32 or bfloat16, got {dt}")
+
+
+def workspace(nbytes: int, device) -> torch.Tensor | None:
+    if nbytes <= 0:
+        return None
+    return torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "mmdx ops run only on the GPU (HIP); got a CPU tensor. Move the model and "
+                "inputs to 'cuda' — there is no CPU fallback.")
+        if not t.is_contiguous():
+            raise RuntimeError("mmdx ops need contiguous tensors")

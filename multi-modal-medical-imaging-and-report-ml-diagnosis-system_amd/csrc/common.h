@@ -1,0 +1,89 @@
+// Shared device/host helpers for the mmdx HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace mmdx {
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+enum Dtype { F32 = 0, BF16 = 1 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 16-byte vector of T: 8 bf16 or 4 f32.
+template <typename T> struct Vec16;
+template <> struct Vec16<bf16> { static constexpr int N = 8; typedef bf16x8 type; };
+template <> struct Vec16<float> { static constexpr int N = 4; typedef f32x4 type; };
+
+// exact (erf) GELU as torch.nn.GELU() default / BERT "gelu"
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64); `red` needs NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+}  // namespace mmdx
+
+// Error plumbing for the C ABI (defined in capi.cpp).
+extern "C" void mmdx_set_error(const char* fmt, ...);
+
+#define MMDX_CHECK_ARG(cond, ...)                     \
+  do {                                               \
+    if (!(cond)) {                                   \
+      mmdx_set_error(__VA_ARGS__);                   \
+      return -22; /* -EINVAL */                      \
+    }                                                \
+  } while (0)
+
+#define MMDX_LAUNCH_CHECK()                                          \
+  do {                                                               \
+    hipError_t _e = hipGetLastError();                               \
+    if (_e != hipSuccess) {                                          \
+      mmdx_set_error("HIP launch failed: %s", hipGetErrorString(_e)); \
+      return -(int)_e;                                               \
+    }                                                                \
+  } while (0)

@@ -1,0 +1,211 @@
+// NHWC convolution on the implicit-GEMM core: fwd, dgrad, wgrad (+ weight packing).
+// Replaces every nn.Conv2d of the torchvision ResNet trunk that ImageEncoderCNN wraps
+// (training_pipeline.py:178-183, run through _backbone_forward_grad TP:285-289).
+#include <algorithm>
+
+#include "igemm.h"
+#include "../../include/mmdx.h"
+
+namespace mmdx {
+
+static ConvGeom geom(const mmdx_conv_desc* d) {
+  ConvGeom g;
+  g.N = d->N; g.H = d->H; g.W = d->W; g.C = d->C; g.K = d->K; g.R = d->R; g.S = d->S;
+  g.sh = d->stride_h; g.sw = d->stride_w; g.ph = d->pad_h; g.pw = d->pad_w;
+  g.P = d->P; g.Q = d->Q;
+  return g;
+}
+
+static int check_desc(const mmdx_conv_desc* d, int vec) {
+  MMDX_CHECK_ARG(d && d->N > 0 && d->H > 0 && d->W > 0 && d->C > 0 && d->K > 0 && d->R > 0 &&
+                     d->S > 0 && d->stride_h > 0 && d->stride_w > 0,
+                 "conv: bad descriptor");
+  MMDX_CHECK_ARG(d->P == (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1 &&
+                     d->Q == (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1,
+                 "conv: output size P=%d Q=%d inconsistent with input", d->P, d->Q);
+  MMDX_CHECK_ARG(d->C % vec == 0 && d->K % vec == 0,
+                 "conv: channels C=%d K=%d must be multiples of %d", d->C, d->K, vec);
+  return 0;
+}
+
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Cm, int C, int RS,
+                                   T* __restrict__ krsc, T* __restrict__ crsk) {
+  const long total = (long)K * RS * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    // i indexes KRSC order
+    const int c = (int)(i % C);
+    const long t = i / C;
+    const int rs = (int)(t % RS);
+    const int k = (int)(t / RS);
+    const float v = c < Cm ? w[((long)k * Cm + c) * RS + rs] : 0.f;
+    if (krsc) krsc[i] = from_f<T>(v);
+    if (crsk) crsk[((long)c * RS + rs) * K + k] = from_f<T>(v);
+  }
+}
+
+// partial[z][k][(r*S+s)*C + c] summed over z -> dw[k][c][r][s] (c < Cm), dw = beta*dw + sum
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int K, int C,
+                                    int Cm, int RS, float* __restrict__ dw, float beta) {
+  const long total = (long)K * Cm * RS;
+  const long slab = (long)K * RS * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int rs = (int)(i % RS);
+    const long t = i / RS;
+    const int c = (int)(t % Cm);
+    const int k = (int)(t / Cm);
+    const long src = (long)k * RS * C + (long)rs * C + c;
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[z * slab + src];
+    dw[i] = beta != 0.f ? beta * dw[i] + v : v;
+  }
+}
+
+template <typename T, int BM, int BN, class LA, class LB, class Epi>
+static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, const Epi& epi,
+                  int M, int N, int K, int splits, int kper, hipStream_t st) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_kernel<T, BM, BN, 2, 2, LA, LB, Epi>), dim3(nwg, 1, splits),
+                     dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
+                      hipStream_t st) {
+  const ConvGeom g = geom(d);
+  const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
+  Im2colK<T> sa{(const T*)x, g, M};
+  DenseK<T> sb{(const T*)w, K, N, true};
+  EpiStore<T> epi{(T*)y, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr};
+  if (N <= 64)
+    return launch<T, 128, 64, KLoad<T, 128, Im2colK<T>>, KLoad<T, 64, DenseK<T>>>(
+        sa, sb, epi, M, N, K, 1, K, st);
+  return launch<T, 128, 128, KLoad<T, 128, Im2colK<T>>, KLoad<T, 128, DenseK<T>>>(
+      sa, sb, epi, M, N, K, 1, K, st);
+}
+
+template <typename T>
+static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                        float beta, hipStream_t st) {
+  const ConvGeom g = geom(d);
+  const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
+  DgradK<T> sa{(const T*)dy, g, M};
+  DenseK<T> sb{(const T*)w_crsk, K, N, true};
+  EpiStore<T> epi{(T*)dx, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr};
+  if (N <= 64)
+    return launch<T, 128, 64, KLoad<T, 128, DgradK<T>>, KLoad<T, 64, DenseK<T>>>(
+        sa, sb, epi, M, N, K, 1, K, st);
+  return launch<T, 128, 128, KLoad<T, 128, DgradK<T>>, KLoad<T, 128, DenseK<T>>>(
+      sa, sb, epi, M, N, K, 1, K, st);
+}
+
+struct WgradPlan { int bm, bn, splits, kper; };
+static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
+  WgradPlan p;
+  const int BK = dtype == BF16 ? KTile<bf16>::BK : KTile<float>::BK;
+  const int M = d->K, N = d->R * d->S * d->C;
+  const long K = (long)d->N * d->P * d->Q;
+  p.bm = M <= 64 ? 64 : 128;
+  p.bn = N <= 64 ? 64 : 128;
+  const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+  const long ktiles = (K + BK - 1) / BK;
+  long s = (1024 + tiles - 1) / tiles;
+  s = std::max(1L, std::min(s, ktiles / 2));
+  const long kt_per = (ktiles + s - 1) / s;
+  p.kper = (int)(kt_per * BK);
+  p.splits = (int)((K + p.kper - 1) / p.kper);
+  return p;
+}
+
+template <typename T>
+static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const void* dy,
+                        float* dw, float beta, void* ws, size_t ws_bytes, hipStream_t st) {
+  const ConvGeom g = geom(d);
+  const WgradPlan p = plan_wgrad(sizeof(T) == 2 ? BF16 : F32, d);
+  const int M = g.K, N = g.R * g.S * g.C;
+  const long Kl = (long)g.N * g.P * g.Q;
+  MMDX_CHECK_ARG(Kl < (1L << 31), "conv wgrad: N*P*Q too large");
+  const int K = (int)Kl;
+  const size_t need = (size_t)p.splits * M * N * sizeof(float);
+  MMDX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu", ws_bytes, need);
+  DenseR<T> sa{(const T*)dy, g.K, M, true};
+  Im2colR<T> sb{(const T*)x, g, N};
+  EpiPartial epi{(float*)ws, M, N};
+  int rc;
+  typedef RLoad<T, 128, DenseR<T>> A128;
+  typedef RLoad<T, 64, DenseR<T>> A64;
+  typedef RLoad<T, 128, Im2colR<T>> B128;
+  typedef RLoad<T, 64, Im2colR<T>> B64;
+  if (p.bm == 128 && p.bn == 128)
+    rc = launch<T, 128, 128, A128, B128>(sa, sb, epi, M, N, K, p.splits, p.kper, st);
+  else if (p.bm == 128)
+    rc = launch<T, 128, 64, A128, B64>(sa, sb, epi, M, N, K, p.splits, p.kper, st);
+  else if (p.bn == 128)
+    rc = launch<T, 64, 128, A64, B128>(sa, sb, epi, M, N, K, p.splits, p.kper, st);
+  else
+    rc = launch<T, 64, 64, A64, B64>(sa, sb, epi, M, N, K, p.splits, p.kper, st);
+  if (rc) return rc;
+  const long total = (long)g.K * cm * g.R * g.S;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
+                     p.splits, g.K, g.C, cm, g.R * g.S, dw, beta);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mmdx
+
+using namespace mmdx;
+
+extern "C" int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
+                                     const float* w, void* krsc, void* crsk, void* stream) {
+  MMDX_CHECK_ARG(d && c_master > 0 && c_master <= d->C, "conv pack: bad channels");
+  const long total = (long)d->K * d->R * d->S * d->C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks), dim3(256), 0, st, w, d->K,
+                       c_master, d->C, d->R * d->S, (bf16*)krsc, (bf16*)crsk);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, st, w, d->K,
+                       c_master, d->C, d->R * d->S, (float*)krsc, (float*)crsk);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,
+                             const void* w, void* y, void* stream) {
+  int rc = check_desc(d, dtype == BF16 ? 8 : 4);
+  if (rc) return rc;
+  MMDX_CHECK_ARG((long)d->N * d->P * d->Q < (1L << 31), "conv fwd: too many pixels");
+  if (dtype == BF16) return conv_fwd_t<bf16>(d, x, w, y, (hipStream_t)stream);
+  return conv_fwd_t<float>(d, x, w, y, (hipStream_t)stream);
+}
+
+extern "C" int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
+                               const void* w_crsk, void* dx, float beta, void* stream) {
+  int rc = check_desc(d, dtype == BF16 ? 8 : 4);
+  if (rc) return rc;
+  if (dtype == BF16) return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, beta, (hipStream_t)stream);
+  return conv_dgrad_t<float>(d, dy, w_crsk, dx, beta, (hipStream_t)stream);
+}
+
+extern "C" size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc* d) {
+  const WgradPlan p = plan_wgrad(dtype, d);
+  return (size_t)p.splits * d->K * d->R * d->S * d->C * sizeof(float);
+}
+
+extern "C" int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master,
+                               const void* x, const void* dy, float* dw, float beta,
+                               void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_desc(d, dtype == BF16 ? 8 : 4);
+  if (rc) return rc;
+  MMDX_CHECK_ARG(c_master > 0 && c_master <= d->C, "conv wgrad: bad c_master");
+  if (dtype == BF16)
+    return conv_wgrad_t<bf16>(d, c_master, x, dy, dw, beta, ws, ws_bytes, (hipStream_t)stream);
+  return conv_wgrad_t<float>(d, c_master, x, dy, dw, beta, ws, ws_bytes, (hipStream_t)stream);
+}

@@ -1,0 +1,136 @@
+// Dense GEMM entry point (nn.Linear forward / dX / dW) on the implicit-GEMM core.
+#include <type_traits>
+
+#include "igemm.h"
+#include "../../include/mmdx.h"
+
+namespace mmdx {
+
+struct SplitPlan { int bm, bn, splits, kper; };
+
+// Tile + split-K choice; shared by the workspace query and the launch so both agree.
+static SplitPlan plan_dense(int dtype, int M, int N, int K) {
+  SplitPlan p;
+  const int BK = dtype == BF16 ? KTile<bf16>::BK : KTile<float>::BK;
+  p.bm = M <= 64 ? 64 : 128;
+  p.bn = N <= 64 ? 64 : 128;
+  const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+  const int ktiles = (K + BK - 1) / BK;
+  int s = 1;
+  if (tiles < 256 && ktiles >= 8) {
+    s = (int)((512 + tiles - 1) / tiles);
+    s = std::min(s, ktiles / 4);
+    s = std::max(s, 1);
+  }
+  const int kt_per = (ktiles + s - 1) / s;
+  p.kper = kt_per * BK;
+  p.splits = (K + p.kper - 1) / p.kper;
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
+template <typename OutT>
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                     EpiStore<OutT> epi) {
+  const long total = (long)M * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[(long)z * total + i];
+    epi.apply((int)(i / N), (int)(i % N), v);
+  }
+}
+
+template <typename T, int BM, int BN, bool AK, bool BKm, class Epi>
+static int launch_dense(const void* A, long lda, const void* B, long ldb, const Epi& epi,
+                        int M, int N, int K, int splits, int kper, hipStream_t st) {
+  typedef typename std::conditional<AK, DenseK<T>, DenseR<T>>::type SA;
+  typedef typename std::conditional<BKm, DenseK<T>, DenseR<T>>::type SB;
+  typedef typename std::conditional<AK, KLoad<T, BM, SA>, RLoad<T, BM, SA>>::type LA;
+  typedef typename std::conditional<BKm, KLoad<T, BN, SB>, RLoad<T, BN, SB>>::type LB;
+  constexpr int VEC = Vec16<T>::N;
+  const bool va = lda % VEC == 0 && ((uintptr_t)A & 15) == 0;
+  const bool vb = ldb % VEC == 0 && ((uintptr_t)B & 15) == 0;
+  SA sa{(const T*)A, lda, M, va};
+  SB sb{(const T*)B, ldb, N, vb};
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_kernel<T, BM, BN, 2, 2, LA, LB, Epi>), dim3(nwg, 1, splits),
+                     dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T, bool AK, bool BKm, class Epi>
+static int dispatch_tile(const SplitPlan& p, const void* A, long lda, const void* B, long ldb,
+                         const Epi& epi, int M, int N, int K, hipStream_t st) {
+  if (p.bm == 128 && p.bn == 128)
+    return launch_dense<T, 128, 128, AK, BKm>(A, lda, B, ldb, epi, M, N, K, p.splits, p.kper, st);
+  if (p.bm == 128)
+    return launch_dense<T, 128, 64, AK, BKm>(A, lda, B, ldb, epi, M, N, K, p.splits, p.kper, st);
+  if (p.bn == 128)
+    return launch_dense<T, 64, 128, AK, BKm>(A, lda, B, ldb, epi, M, N, K, p.splits, p.kper, st);
+  return launch_dense<T, 64, 64, AK, BKm>(A, lda, B, ldb, epi, M, N, K, p.splits, p.kper, st);
+}
+
+template <typename T, class Epi>
+static int dispatch_major(const SplitPlan& p, const void* A, long lda, int ak, const void* B,
+                          long ldb, int bk, const Epi& epi, int M, int N, int K,
+                          hipStream_t st) {
+  if (ak && bk) return dispatch_tile<T, true, true>(p, A, lda, B, ldb, epi, M, N, K, st);
+  if (ak && !bk) return dispatch_tile<T, true, false>(p, A, lda, B, ldb, epi, M, N, K, st);
+  if (!ak && !bk) return dispatch_tile<T, false, false>(p, A, lda, B, ldb, epi, M, N, K, st);
+  return dispatch_tile<T, false, true>(p, A, lda, B, ldb, epi, M, N, K, st);
+}
+
+template <typename T, typename OutT>
+static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, const void* B,
+                      long ldb, int bk, void* C, long ldc, const float* bias,
+                      const float* addend, int act,
+                      float alpha, float beta, void* preact, void* ws, size_t ws_bytes,
+                      hipStream_t st) {
+  const SplitPlan p = plan_dense(sizeof(T) == 2 ? BF16 : F32, M, N, K);
+  MMDX_CHECK_ARG(lda >= (ak ? K : M) && ldb >= (bk ? K : N) && ldc >= N,
+                 "mmdx_gemm: leading dimension too small");
+  EpiStore<OutT> epi{(OutT*)C, ldc, M, N, bias, addend, act, alpha, beta, (OutT*)preact};
+  if (p.splits == 1) return dispatch_major<T>(p, A, lda, ak, B, ldb, bk, epi, M, N, K, st);
+  const size_t need = (size_t)p.splits * M * N * sizeof(float);
+  MMDX_CHECK_ARG(ws && ws_bytes >= need, "mmdx_gemm: workspace %zu < %zu", ws_bytes, need);
+  EpiPartial part{(float*)ws, M, N};
+  int rc = dispatch_major<T>(p, A, lda, ak, B, ldb, bk, part, M, N, K, st);
+  if (rc) return rc;
+  const long total = (long)M * N;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
+                     (const float*)ws, p.splits, M, N, epi);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mmdx
+
+using namespace mmdx;
+
+extern "C" size_t mmdx_gemm_workspace_size(int dtype, int M, int N, int K) {
+  const SplitPlan p = plan_dense(dtype, M, N, K);
+  return p.splits > 1 ? (size_t)p.splits * M * N * sizeof(float) : 0;
+}
+
+extern "C" int mmdx_gemm(int dtype, int M, int N, int K, const void* A, long lda, int a_kmajor,
+                         const void* B, long ldb, int b_kmajor, void* C, long ldc, int c_dtype,
+                         const float* bias, const float* addend, int act, float alpha,
+                         float beta, void* preact, void* workspace, size_t ws_bytes,
+                         void* stream) {
+  MMDX_CHECK_ARG(M > 0 && N > 0 && K > 0, "mmdx_gemm: empty problem M=%d N=%d K=%d", M, N, K);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == F32) {
+    MMDX_CHECK_ARG(c_dtype == F32, "mmdx_gemm: fp32 compute needs fp32 output");
+    return gemm_typed<float, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
+                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+  }
+  MMDX_CHECK_ARG(dtype == BF16, "mmdx_gemm: bad dtype %d", dtype);
+  if (c_dtype == F32)
+    return gemm_typed<bf16, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
+                                   addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+  return gemm_typed<bf16, bf16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias, addend, act,
+                                alpha, beta, preact, workspace, ws_bytes, st);
+}

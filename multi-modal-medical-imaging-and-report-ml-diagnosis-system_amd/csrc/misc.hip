@@ -1,0 +1,375 @@
+// Pooling, layout conversion, casts, GELU backward, bias gradient, dropout, BCE-with-logits.
+#include <algorithm>
+
+#include "common.h"
+#include "../../include/mmdx.h"
+
+namespace mmdx {
+
+static int grid_for(long n, int per = 256) {
+  return (int)std::max<long>(1, std::min<long>((n + per - 1) / per, 8192));
+}
+
+#define GRID_STRIDE(i, n) \
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+
+// ----------------------------------------------------------------------------- maxpool
+// Semantics of PyTorch CPU max_pool2d: padded taps are skipped, the FIRST maximum in
+// row-major window order wins (strict '>'), NaN propagates.
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int k,
+                                   int s, int p, T* __restrict__ y, uint8_t* __restrict__ am,
+                                   int P, int Q) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  const int cv = C / VEC;
+  const long total = (long)N * P * Q * cv;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % cv) * VEC;
+    long t = i / cv;
+    const int q = (int)(t % Q); t /= Q;
+    const int pp = (int)(t % P);
+    const int n = (int)(t / P);
+    float best[VEC];
+    int arg[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { best[j] = -INFINITY; arg[j] = -1; }
+    for (int r = 0; r < k; ++r) {
+      const int ih = pp * s - p + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int ss = 0; ss < k; ++ss) {
+        const int iw = q * s - p + ss;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const V v = *(const V*)(x + (((long)n * H + ih) * W + iw) * C + c);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float f = to_f(v[j]);
+          if (arg[j] < 0 || f > best[j] || (f != f && best[j] == best[j])) {
+            best[j] = f;
+            arg[j] = r * k + ss;
+          }
+        }
+      }
+    }
+    V o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      o[j] = from_f<T>(best[j]);
+      am[i * VEC + j] = (uint8_t)arg[j];
+    }
+    *(V*)(y + i * VEC) = o;
+  }
+}
+
+// Gather form: each input element sums dy of the windows whose argmax points at it.
+template <typename T>
+__global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ am, const T* __restrict__ dy,
+                                   int N, int H, int W, int C, int k, int s, int p, int P, int Q,
+                                   T* __restrict__ dx) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  const int cv = C / VEC;
+  const long total = (long)N * H * W * cv;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % cv) * VEC;
+    long t = i / cv;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+    // windows (pp,q) with pp*s - p <= h <= pp*s - p + k - 1
+    const int p_lo = max(0, (h + p - k + s) / s), p_hi = min(P - 1, (h + p) / s);
+    const int q_lo = max(0, (w + p - k + s) / s), q_hi = min(Q - 1, (w + p) / s);
+    for (int pp = p_lo; pp <= p_hi; ++pp) {
+      const int r = h + p - pp * s;
+      if (r < 0 || r >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int ss = w + p - q * s;
+        if (ss < 0 || ss >= k) continue;
+        const long o = (((long)n * P + pp) * Q + q) * C + c;
+        const V g = *(const V*)(dy + o);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+          if (am[o + j] == r * k + ss) acc[j] += to_f(g[j]);
+      }
+    }
+    V out;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) out[j] = from_f<T>(acc[j]);
+    *(V*)(dx + i * VEC) = out;
+  }
+}
+
+// ----------------------------------------------------------------------------- avgpool
+template <typename T>
+__global__ void avgpool_fwd_kernel(const T* __restrict__ x, int N, int HW, int C,
+                                   T* __restrict__ y) {
+  const long total = (long)N * C;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % C);
+    const long n = i / C;
+    float acc = 0.f;
+    for (int k = 0; k < HW; ++k) acc += to_f(x[(n * HW + k) * C + c]);
+    y[i] = from_f<T>(acc / (float)HW);
+  }
+}
+
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, int N, int HW, int C,
+                                   T* __restrict__ dx) {
+  const long total = (long)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % C);
+    const long n = i / ((long)HW * C);
+    dx[i] = from_f<T>(to_f(dy[n * C + c]) * inv);
+  }
+}
+
+// ----------------------------------------------------------------------------- layout
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W,
+                                    int cp, T* __restrict__ y) {
+  const long total = (long)N * H * W;
+  GRID_STRIDE(i, total) {
+    const long hw = i % ((long)H * W);
+    const long n = i / ((long)H * W);
+    for (int c = 0; c < cp; ++c)
+      y[i * cp + c] = from_f<T>(c < C ? x[(n * C + c) * H * W + hw] : 0.f);
+  }
+}
+
+template <typename D, typename S>
+__global__ void cast_kernel(const S* __restrict__ x, long n, D* __restrict__ y) {
+  GRID_STRIDE(i, n) y[i] = from_f<D>(to_f(x[i]));
+}
+
+// ----------------------------------------------------------------------------- GELU / bias
+template <typename T>
+__global__ void gelu_bwd_kernel(const T* __restrict__ pre, const T* __restrict__ dy, long n,
+                                T* __restrict__ dx) {
+  GRID_STRIDE(i, n) dx[i] = from_f<T>(to_f(dy[i]) * gelu_erf_grad(to_f(pre[i])));
+}
+
+constexpr int BG_ROWS = 256;
+template <typename T>
+__global__ void bias_grad_partial_kernel(const T* __restrict__ dy, long M, int N,
+                                         float* __restrict__ part) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const long r0 = (long)blockIdx.y * BG_ROWS, r1 = min(M, r0 + BG_ROWS);
+  float acc = 0.f;
+  for (long r = r0; r < r1; ++r) acc += to_f(dy[r * N + n]);
+  part[(long)blockIdx.y * N + n] = acc;
+}
+__global__ void bias_grad_finalize_kernel(const float* __restrict__ part, int nb, int N,
+                                          float* db, float beta_acc) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int b = 0; b < nb; ++b) acc += part[(long)b * N + n];
+  db[n] = beta_acc != 0.f ? beta_acc * db[n] + acc : acc;
+}
+
+// ----------------------------------------------------------------------------- dropout
+__device__ __forceinline__ uint32_t hash64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+template <typename T>
+__global__ void dropout_fwd_kernel(const T* __restrict__ x, long n, float p, uint64_t seed,
+                                   uint64_t off, T* __restrict__ y, uint8_t* __restrict__ mask) {
+  const float scale = 1.f / (1.f - p);
+  GRID_STRIDE(i, n) {
+    const float u = (hash64(seed * 0x9E3779B97F4A7C15ULL + off + (uint64_t)i) >> 8) *
+                    (1.f / 16777216.f);
+    const uint8_t keep = u >= p;
+    mask[i] = keep;
+    y[i] = from_f<T>(keep ? to_f(x[i]) * scale : 0.f);
+  }
+}
+template <typename T>
+__global__ void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                   long n, float p, T* __restrict__ dx) {
+  const float scale = 1.f / (1.f - p);
+  GRID_STRIDE(i, n) dx[i] = from_f<T>(mask[i] ? to_f(dy[i]) * scale : 0.f);
+}
+
+// ----------------------------------------------------------------------------- BCE
+// loss = mean( (1-y)*z + log(1 + exp(-z)) ), in the max-shifted form PyTorch uses.
+__global__ void bce_fwd_kernel(const float* __restrict__ z, const float* __restrict__ y, int n,
+                               float* loss) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float zi = z[i], yi = y[i];
+    const float mx = fmaxf(-zi, 0.f);
+    acc += (1.f - yi) * zi + mx + logf(expf(-mx) + expf(-zi - mx));
+  }
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) loss[0] = acc / (float)n;
+}
+__global__ void bce_bwd_kernel(const float* __restrict__ z, const float* __restrict__ y, int n,
+                               const float* __restrict__ dloss, float* __restrict__ dz) {
+  const float g = (dloss ? dloss[0] : 1.f) / (float)n;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float s = 1.f / (1.f + expf(-z[i]));
+    dz[i] = (s - y[i]) * g;
+  }
+}
+
+}  // namespace mmdx
+
+using namespace mmdx;
+
+#define DISPATCH_T(dtype, ...)          \
+  do {                                 \
+    if ((dtype) == BF16) {             \
+      typedef bf16 T;                  \
+      __VA_ARGS__;                     \
+    } else {                           \
+      typedef float T;                 \
+      __VA_ARGS__;                     \
+    }                                  \
+  } while (0)
+
+extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int k,
+                                int s, int p, void* y, uint8_t* argmax, int P, int Q,
+                                void* stream) {
+  const int VEC = dtype == BF16 ? 8 : 4;
+  MMDX_CHECK_ARG(C % VEC == 0 && k * k <= 255 && argmax, "maxpool: bad args");
+  MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
+                 "maxpool: inconsistent output size");
+  const long total = (long)N * P * Q * (C / VEC);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total)), dim3(256),
+                                       0, (hipStream_t)stream, (const T*)x, N, H, W, C, k, s, p,
+                                       (T*)y, argmax, P, Q));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_maxpool_bwd(int dtype, const uint8_t* argmax, const void* dy, int N, int H,
+                                int W, int C, int k, int s, int p, int P, int Q, void* dx,
+                                void* stream) {
+  const int VEC = dtype == BF16 ? 8 : 4;
+  MMDX_CHECK_ARG(C % VEC == 0, "maxpool bwd: bad C");
+  const long total = (long)N * H * W * (C / VEC);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total)), dim3(256),
+                                       0, (hipStream_t)stream, argmax, (const T*)dy, N, H, W, C,
+                                       k, s, p, P, Q, (T*)dx));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_avgpool_fwd(int dtype, const void* x, int N, int HW, int C, void* y,
+                                void* stream) {
+  const long total = (long)N * C;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(avgpool_fwd_kernel<T>, dim3(grid_for(total)), dim3(256),
+                                       0, (hipStream_t)stream, (const T*)x, N, HW, C, (T*)y));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_avgpool_bwd(int dtype, const void* dy, int N, int HW, int C, void* dx,
+                                void* stream) {
+  const long total = (long)N * HW * C;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(grid_for(total)), dim3(256),
+                                       0, (hipStream_t)stream, (const T*)dy, N, HW, C, (T*)dx));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W,
+                                 int c_pad, void* y, void* stream) {
+  MMDX_CHECK_ARG(c_pad >= C, "nchw_to_nhwc: c_pad < C");
+  const long total = (long)N * H * W;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(grid_for(total)), dim3(256),
+                                       0, (hipStream_t)stream, x, N, C, H, W, c_pad, (T*)y));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_cast(int dst, int src, const void* x, long n, void* y, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dst == BF16 && src == F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const float*)x, n, (bf16*)y);
+  else if (dst == F32 && src == BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const bf16*)x, n, (float*)y);
+  else if (dst == F32 && src == F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const float*)x, n, (float*)y);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const bf16*)x, n, (bf16*)y);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n, void* dx,
+                             void* stream) {
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gelu_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)pre, (const T*)dy, n,
+                                       (T*)dx));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t mmdx_bias_grad_workspace_size(long M, int N) {
+  return (size_t)((M + BG_ROWS - 1) / BG_ROWS) * N * sizeof(float);
+}
+
+extern "C" int mmdx_bias_grad(int dtype, const void* dy, long M, int N, float* db,
+                              float beta_acc, void* ws, size_t ws_bytes, void* stream) {
+  const int nb = (int)((M + BG_ROWS - 1) / BG_ROWS);
+  MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_bias_grad_workspace_size(M, N),
+                 "bias_grad: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bias_grad_partial_kernel<T>, dim3((N + 255) / 256, nb),
+                                       dim3(256), 0, st, (const T*)dy, M, N, (float*)ws));
+  hipLaunchKernelGGL(bias_grad_finalize_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+                     (const float*)ws, nb, N, db, beta_acc);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_dropout_fwd(int dtype, const void* x, long n, float p, uint64_t seed,
+                                uint64_t offset, void* y, uint8_t* mask, void* stream) {
+  MMDX_CHECK_ARG(p >= 0.f && p < 1.f, "dropout: p out of range");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_fwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)x, n, p, seed, offset,
+                                       (T*)y, mask));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_dropout_bwd(int dtype, const void* dy, const uint8_t* mask, long n, float p,
+                                void* dx, void* stream) {
+  DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)dy, mask, n, p, (T*)dx));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_bce_logits_fwd(const float* logits, const float* target, int B, int C,
+                                   float* loss, void* stream) {
+  MMDX_CHECK_ARG(B > 0 && C > 0, "bce: empty");
+  hipLaunchKernelGGL(bce_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, target,
+                     B * C, loss);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_bce_logits_bwd(const float* logits, const float* target, int B, int C,
+                                   const float* dloss, float* dlogits, void* stream) {
+  const int n = B * C;
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                     logits, target, n, dloss, dlogits);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,587 @@
+// BatchNorm2d (+residual)(+ReLU) and LayerNorm, forward and backward, NHWC / row-major.
+//
+// BN statistics are reduced deterministically: every block writes a per-channel
+// (mean, M2) partial over its row slab, and a finalize kernel merges the slabs in a
+// fixed order with Chan's parallel-variance update (no float atomics, bitwise
+// reproducible, no E[x^2]-E[x]^2 cancellation across the 10^5..10^6 rows of a layer).
+// All elementwise passes move 16 B per lane (8 bf16 / 4 fp32).
+#include <algorithm>
+
+#include "common.h"
+#include "../../include/mmdx.h"
+
+namespace mmdx {
+
+constexpr int BN_NT = 256;
+
+struct BnLayout {
+  int ct;        // channel-vector threads per block
+  int rt;        // row threads per block
+  int cgroups;   // blockIdx.y extent
+  int rblocks;   // blockIdx.x extent
+  long rows_per_block;
+};
+
+static BnLayout bn_layout(long rows, int C, int vec) {
+  BnLayout L;
+  const int cv = C / vec;
+  L.ct = std::min(cv, 64);
+  L.rt = BN_NT / L.ct;
+  L.cgroups = (cv + L.ct - 1) / L.ct;
+  long target = std::max(1L, 1024L / L.cgroups);
+  long rpb = (rows + target - 1) / target;
+  rpb = std::max<long>(rpb, L.rt);
+  L.rows_per_block = (rpb + L.rt - 1) / L.rt * L.rt;
+  L.rblocks = (int)((rows + L.rows_per_block - 1) / L.rows_per_block);
+  return L;
+}
+
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb,
+                                           float m2b) {
+  const float nn = n + nb;
+  if (nb == 0.f) return;
+  if (n == 0.f) { n = nb; mean = mb; m2 = m2b; return; }
+  const float d = mb - mean;
+  const float f = nb / nn;
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
+  n = nn;
+}
+
+// partial[b][c] = (mean, M2) of rows [b*rpb, (b+1)*rpb)
+template <typename T>
+__global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x, long rows,
+                                                         int C, int ct, long rpb,
+                                                         float2* __restrict__ part) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  __shared__ float s_n[BN_NT], s_mean[BN_NT * VEC], s_m2[BN_NT * VEC];
+  const int tx = threadIdx.x % ct, ty = threadIdx.x / ct, rt = BN_NT / ct;
+  const int c0 = (blockIdx.y * ct + tx) * VEC;
+  const long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  float sum[VEC], sq[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) sum[j] = sq[j] = 0.f;
+  int cnt = 0;
+  if (c0 < C) {
+    for (long r = r0 + ty; r < r1; r += rt) {
+      const V v = *(const V*)(x + r * C + c0);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float f = to_f(v[j]);
+        sum[j] += f;
+        sq[j] += f * f;
+      }
+      ++cnt;
+    }
+  }
+  const int me = ty * ct + tx;
+  s_n[me] = (float)cnt;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const float m = cnt ? sum[j] / cnt : 0.f;
+    s_mean[me * VEC + j] = m;
+    s_m2[me * VEC + j] = cnt ? fmaxf(sq[j] - sum[j] * m, 0.f) : 0.f;
+  }
+  __syncthreads();
+  if (ty == 0 && c0 < C) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float n = 0.f, mean = 0.f, m2 = 0.f;
+      for (int y = 0; y < rt; ++y) {
+        const int o = y * ct + tx;
+        chan_merge(n, mean, m2, s_n[o], s_mean[o * VEC + j], s_m2[o * VEC + j]);
+      }
+      part[(long)blockIdx.x * C + c0 + j] = make_float2(mean, m2);
+    }
+  }
+}
+
+// Merge slab partials; update running stats; emit scale/shift for the apply pass.
+__global__ void bn_finalize_kernel(const float2* __restrict__ part, int nblk, long rows, long rpb,
+                                   int C, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* running_mean,
+                                   float* running_var, float momentum, float eps,
+                                   float* save_mean, float* save_rstd, float* scale,
+                                   float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    const long nb = min(rpb, rows - (long)b * rpb);
+    const float2 p = part[(long)b * C + c];
+    chan_merge(n, mean, m2, (float)nb, p.x, p.y);
+  }
+  const float var = m2 / (float)rows;
+  const float rstd = rsqrtf(var + eps);
+  save_mean[c] = mean;
+  save_rstd[c] = rstd;
+  if (running_mean) {
+    const float unb = rows > 1 ? m2 / (float)(rows - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  }
+  const float g = gamma ? gamma[c] : 1.f;
+  scale[c] = g * rstd;
+  shift[c] = (beta ? beta[c] : 0.f) - mean * g * rstd;
+}
+
+__global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, const float* rm,
+                                    const float* rv, float eps, float* save_mean,
+                                    float* save_rstd, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float rstd = rsqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  save_mean[c] = rm[c];
+  save_rstd[c] = rstd;
+  scale[c] = g * rstd;
+  shift[c] = (beta ? beta[c] : 0.f) - rm[c] * g * rstd;
+}
+
+// y = act(x*scale[c] + shift[c] (+ res))
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, long nvec,
+                                int C, const float* __restrict__ scale,
+                                const float* __restrict__ shift, int relu, T* __restrict__ y) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * VEC) % C);
+    const V v = ((const V*)x)[i];
+    V r{};
+    if (res) r = ((const V*)res)[i];
+    V o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float f = to_f(v[j]) * scale[c0 + j] + shift[c0 + j];
+      if (res) f += to_f(r[j]);
+      if (relu) f = fmaxf(f, 0.f);
+      o[j] = from_f<T>(f);
+    }
+    ((V*)y)[i] = o;
+  }
+}
+
+// backward reduce: partial[b][c] = (sum g, sum g*xhat), g = dy * relu'(y)
+template <typename T>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
+    const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
+    int ct, long rpb, const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
+    float2* __restrict__ part) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  __shared__ float s_a[BN_NT * VEC], s_b[BN_NT * VEC];
+  const int tx = threadIdx.x % ct, ty = threadIdx.x / ct, rt = BN_NT / ct;
+  const int c0 = (blockIdx.y * ct + tx) * VEC;
+  const long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  float sg[VEC], sgx[VEC], mu[VEC], rs[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    sg[j] = sgx[j] = 0.f;
+    mu[j] = c0 < C ? mean[c0 + j] : 0.f;
+    rs[j] = c0 < C ? rstd[c0 + j] : 0.f;
+  }
+  if (c0 < C) {
+    for (long r = r0 + ty; r < r1; r += rt) {
+      const V vx = *(const V*)(x + r * C + c0);
+      const V vd = *(const V*)(dy + r * C + c0);
+      V vy{};
+      if (relu) vy = *(const V*)(y + r * C + c0);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float g = to_f(vd[j]);
+        if (relu && !(to_f(vy[j]) > 0.f)) g = 0.f;
+        sg[j] += g;
+        sgx[j] += g * (to_f(vx[j]) - mu[j]) * rs[j];
+      }
+    }
+  }
+  const int me = ty * ct + tx;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    s_a[me * VEC + j] = sg[j];
+    s_b[me * VEC + j] = sgx[j];
+  }
+  __syncthreads();
+  if (ty == 0 && c0 < C) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float a = 0.f, b = 0.f;
+      for (int yy = 0; yy < rt; ++yy) {
+        a += s_a[(yy * ct + tx) * VEC + j];
+        b += s_b[(yy * ct + tx) * VEC + j];
+      }
+      part[(long)blockIdx.x * C + c0 + j] = make_float2(a, b);
+    }
+  }
+}
+
+// coef: a[c] = gamma*rstd, b[c] = -gamma*rstd*sum_g/n, k[c] = -gamma*rstd*sum_gx/n
+__global__ void bn_bwd_finalize_kernel(const float2* __restrict__ part, int nblk, long rows,
+                                       int C, int train, const float* __restrict__ gamma,
+                                       const float* __restrict__ rstd, float* dgamma,
+                                       float* dbeta, float beta_acc, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sg = 0.f, sgx = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    const float2 p = part[(long)b * C + c];
+    sg += p.x;
+    sgx += p.y;
+  }
+  if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
+  if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;
+  const float a = (gamma ? gamma[c] : 1.f) * rstd[c];
+  coef[c] = a;
+  coef[C + c] = train ? -a * sg / (float)rows : 0.f;
+  coef[2 * C + c] = train ? -a * sgx / (float)rows : 0.f;
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                    const T* __restrict__ dy, long nvec, int C,
+                                    const float* __restrict__ mean,
+                                    const float* __restrict__ rstd,
+                                    const float* __restrict__ coef, int relu, T* __restrict__ dx,
+                                    T* __restrict__ dres) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * VEC) % C);
+    const V vx = ((const V*)x)[i];
+    const V vd = ((const V*)dy)[i];
+    V vy{};
+    if (relu) vy = ((const V*)y)[i];
+    V o, og;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const int c = c0 + j;
+      float g = to_f(vd[j]);
+      if (relu && !(to_f(vy[j]) > 0.f)) g = 0.f;
+      const float xh = (to_f(vx[j]) - mean[c]) * rstd[c];
+      o[j] = from_f<T>(coef[c] * g + coef[C + c] + coef[2 * C + c] * xh);
+      og[j] = from_f<T>(g);
+    }
+    ((V*)dx)[i] = o;
+    if (dres) ((V*)dres)[i] = og;
+  }
+}
+
+static int grid_for(long nvec) { return (int)std::min<long>((nvec + 255) / 256, 8192); }
+
+template <typename T>
+static int bn_fwd_t(int train, const void* x, long rows, int C, const float* gamma,
+                    const float* beta, float* rm, float* rv, float momentum, float eps,
+                    float* smean, float* srstd, const void* res, int relu, void* y, void* ws,
+                    size_t ws_bytes, hipStream_t st) {
+  constexpr int VEC = Vec16<T>::N;
+  MMDX_CHECK_ARG(C % VEC == 0, "bn: C=%d must be a multiple of %d", C, VEC);
+  const BnLayout L = bn_layout(rows, C, VEC);
+  const size_t need = (size_t)L.rblocks * C * sizeof(float2) + 2 * (size_t)C * sizeof(float);
+  MMDX_CHECK_ARG(ws && ws_bytes >= need, "bn fwd: workspace %zu < %zu", ws_bytes, need);
+  float2* part = (float2*)ws;
+  float* scale = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
+  float* shift = scale + C;
+  if (train) {
+    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
+                       (const T*)x, rows, C, L.ct, L.rows_per_block, part);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                       (const float2*)part, L.rblocks, rows, L.rows_per_block, C, gamma, beta,
+                       rm, rv, momentum, eps, smean, srstd, scale, shift);
+  } else {
+    MMDX_CHECK_ARG(rm && rv, "bn eval: running stats required");
+    hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma,
+                       beta, (const float*)rm, (const float*)rv, eps, smean, srstd, scale,
+                       shift);
+  }
+  const long nvec = rows * C / VEC;
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st, (const T*)x,
+                     (const T*)res, nvec, C, (const float*)scale, (const float*)shift, relu,
+                     (T*)y);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, long rows, int C,
+                    const float* gamma, const float* smean, const float* srstd, int relu,
+                    void* dx, void* dres, float* dgamma, float* dbeta, float beta_acc, void* ws,
+                    size_t ws_bytes, hipStream_t st) {
+  constexpr int VEC = Vec16<T>::N;
+  MMDX_CHECK_ARG(C % VEC == 0, "bn bwd: C=%d must be a multiple of %d", C, VEC);
+  const BnLayout L = bn_layout(rows, C, VEC);
+  const size_t need = (size_t)L.rblocks * C * sizeof(float2) + 3 * (size_t)C * sizeof(float);
+  MMDX_CHECK_ARG(ws && ws_bytes >= need, "bn bwd: workspace %zu < %zu", ws_bytes, need);
+  float2* part = (float2*)ws;
+  float* coef = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
+                     (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
+                     smean, srstd, relu, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                     (const float2*)part, L.rblocks, rows, C, train, gamma, srstd, dgamma,
+                     dbeta, beta_acc, coef);
+  const long nvec = rows * C / VEC;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st,
+                     (const T*)x, (const T*)y, (const T*)dy, nvec, C, smean, srstd,
+                     (const float*)coef, relu, (T*)dx, (T*)dres);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+// ------------------------------------------------------------------------ LayerNorm
+// One wave per row; D <= 64 * LN_MAXV * VEC handled from registers (two-pass stats).
+constexpr int LN_MAXV = 4;
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
+                                                     const T* __restrict__ res, long rows, int D,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     T* __restrict__ y, T* __restrict__ xsum,
+                                                     float* smean, float* srstd) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = D / VEC;
+  float v[LN_MAXV][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nv) {
+      const V a = *(const V*)(x + row * D + vi * VEC);
+      V b{};
+      if (res) b = *(const V*)(res + row * D + vi * VEC);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        v[i][j] = to_f(a[j]) + (res ? to_f(b[j]) : 0.f);
+        s += v[i][j];
+      }
+      if (xsum) {
+        V o;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o[j] = from_f<T>(v[i][j]);
+        *(V*)(xsum + row * D + vi * VEC) = o;
+      }
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i)
+    if (lane + i * 64 < nv)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+  if (lane == 0) {
+    if (smean) smean[row] = mean;
+    if (srstd) srstd[row] = rstd;
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nv) {
+      V o;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const int c = vi * VEC + j;
+        o[j] = from_f<T>((v[i][j] - mean) * rstd * gamma[c] + beta[c]);
+      }
+      *(V*)(y + row * D + vi * VEC) = o;
+    }
+  }
+}
+
+constexpr int LN_BWD_ROWS = 32;  // rows per block (8 per wave)
+
+// dx per row; per-block partial dgamma/dbeta -> part[blk][2][D]
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
+                                                     const T* __restrict__ dy, long rows, int D,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ smean,
+                                                     const float* __restrict__ srstd,
+                                                     T* __restrict__ dx,
+                                                     float* __restrict__ part) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2][D]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nv = D / VEC;
+  float pg[LN_MAXV][VEC], pb[LN_MAXV][VEC];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) pg[i][j] = pb[i][j] = 0.f;
+  for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
+    const long row = blockIdx.x * (long)LN_BWD_ROWS + w * (LN_BWD_ROWS / 4) + rr;
+    if (row >= rows) break;
+    const float mean = smean[row], rstd = srstd[row];
+    float xh[LN_MAXV][VEC], g[LN_MAXV][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nv) {
+        const V a = *(const V*)(xs + row * D + vi * VEC);
+        const V d = *(const V*)(dy + row * D + vi * VEC);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const int c = vi * VEC + j;
+          xh[i][j] = (to_f(a[j]) - mean) * rstd;
+          const float dd = to_f(d[j]);
+          g[i][j] = dd * gamma[c];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+          pg[i][j] += dd * xh[i][j];
+          pb[i][j] += dd;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nv) {
+        V o;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2));
+        *(V*)(dx + row * D + vi * VEC) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nv)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        red[(w * 2 + 0) * D + vi * VEC + j] = pg[i][j];
+        red[(w * 2 + 1) * D + vi * VEC + j] = pb[i][j];
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      a += red[(ww * 2 + 0) * D + c];
+      b += red[(ww * 2 + 1) * D + c];
+    }
+    part[((long)blockIdx.x * 2 + 0) * D + c] = a;
+    part[((long)blockIdx.x * 2 + 1) * D + c] = b;
+  }
+}
+
+__global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int D,
+                                       float* dgamma, float* dbeta, float beta_acc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nblk; ++k) {
+    a += part[((long)k * 2 + 0) * D + c];
+    b += part[((long)k * 2 + 1) * D + c];
+  }
+  if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + a : a;
+  if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + b : b;
+}
+
+}  // namespace mmdx
+
+using namespace mmdx;
+
+extern "C" size_t mmdx_bn_workspace_size(long rows, int C) {
+  const BnLayout L = bn_layout(rows, C, 4);  // fp32 layout has the most row blocks
+  const BnLayout L8 = bn_layout(rows, C, 8);
+  const int nb = std::max(L.rblocks, L8.rblocks);
+  return (size_t)nb * C * sizeof(float2) + 3 * (size_t)C * sizeof(float);
+}
+
+extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
+                           const float* gamma, const float* beta, float* running_mean,
+                           float* running_var, float momentum, float eps, float* save_mean,
+                           float* save_rstd, const void* residual, int relu, void* y,
+                           void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(rows > 0 && C > 0 && save_mean && save_rstd, "bn fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    return bn_fwd_t<bf16>(train, x, rows, C, gamma, beta, running_mean, running_var, momentum,
+                          eps, save_mean, save_rstd, residual, relu, y, ws, ws_bytes, st);
+  return bn_fwd_t<float>(train, x, rows, C, gamma, beta, running_mean, running_var, momentum,
+                         eps, save_mean, save_rstd, residual, relu, y, ws, ws_bytes, st);
+}
+
+extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
+                           long rows, int C, const float* gamma, const float* save_mean,
+                           const float* save_rstd, int relu, void* dx, void* d_residual,
+                           float* dgamma, float* dbeta, float beta_acc, void* ws,
+                           size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(rows > 0 && C > 0 && (!relu || y), "bn bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    return bn_bwd_t<bf16>(train, x, y, dy, rows, C, gamma, save_mean, save_rstd, relu, dx,
+                          d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+  return bn_bwd_t<float>(train, x, y, dy, rows, C, gamma, save_mean, save_rstd, relu, dx,
+                         d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+}
+
+extern "C" int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual, long rows,
+                                  int D, const float* gamma, const float* beta, float eps,
+                                  void* y, void* sum_out, float* save_mean, float* save_rstd,
+                                  void* stream) {
+  const int VEC = dtype == BF16 ? 8 : 4;
+  MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC && gamma && beta,
+                 "layernorm: D=%d unsupported", D);
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (int)((rows + 3) / 4);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)x,
+                       (const bf16*)residual, rows, D, gamma, beta, eps, (bf16*)y,
+                       (bf16*)sum_out, save_mean, save_rstd);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)x,
+                       (const float*)residual, rows, D, gamma, beta, eps, (float*)y,
+                       (float*)sum_out, save_mean, save_rstd);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t mmdx_layernorm_workspace_size(long rows, int D) {
+  const long nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  return (size_t)nblk * 2 * D * sizeof(float);
+}
+
+extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, long rows, int D,
+                                  const float* gamma, const float* save_mean,
+                                  const float* save_rstd, void* dx, float* dgamma, float* dbeta,
+                                  float beta_acc, void* ws, size_t ws_bytes, void* stream) {
+  const int VEC = dtype == BF16 ? 8 : 4;
+  MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC, "layernorm bwd: D=%d", D);
+  const long nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_layernorm_workspace_size(rows, D),
+                 "layernorm bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t shm = 8 * (size_t)D * sizeof(float);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nblk), dim3(256), shm, st, (const bf16*)xsum,
+                       (const bf16*)dy, rows, D, gamma, save_mean, save_rstd, (bf16*)dx,
+                       (float*)ws);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), shm, st,
+                       (const float*)xsum, (const float*)dy, rows, D, gamma, save_mean,
+                       save_rstd, (float*)dx, (float*)ws);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, st,
+                     (const float*)ws, (int)nblk, D, dgamma, dbeta, beta_acc);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,277 @@
+"""Kernel-level parity: every HIP op vs a plain PyTorch fp32 reference of the same op.
+
+Tolerances: fp32 path (exact-f32 MFMA, different summation order) rel 1e-5 of the output
+scale; bf16 path rel 2e-2 (bf16 inputs, fp32 accumulation).
+"""
+import pytest
+import torch
+import torch.nn.functional as tF
+
+import mmdx
+from mmdx import _lib as L
+from mmdx import functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
+
+
+def _close(out, ref, dt, what=""):
+    out = out.float().cpu()
+    ref = ref.float().cpu()
+    scale = ref.abs().max().clamp(min=1e-6)
+    err = (out - ref).abs().max() / scale
+    assert err <= TOL[dt], f"{what}: rel err {err:.3e} > {TOL[dt]}"
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(64, 13, 1024), (200, 1024, 1536), (13, 1024, 64),
+                                   (1000, 96, 40), (37, 130, 1000), (8192, 768, 768)])
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
+def test_gemm(dev, dt, M, N, K, ak, bk):
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = A @ B.T + bias
+    Ad = (A if ak else A.T.contiguous()).to(dev, dt)
+    Bd = (B if bk else B.T.contiguous()).to(dev, dt)
+    C = torch.empty(M, N, dtype=torch.float32, device=dev)
+    F.gemm(Ad, K if ak else M, ak, Bd, K if bk else N, bk, M, N, K, C, N,
+           bias=bias.to(dev), compute_dtype=dt)
+    torch.cuda.synchronize()
+    if dt == torch.bfloat16:
+        ref = A.bfloat16().float() @ B.bfloat16().float().T + bias
+    _close(C, ref, dt, f"gemm {M}x{N}x{K} ak={ak} bk={bk}")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_gelu_preact_beta(dev, dt):
+    g = torch.Generator().manual_seed(1)
+    M, N, K = 96, 256, 128
+    A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    Ad, Bd = A.to(dev, dt), B.to(dev, dt)
+    if dt == torch.bfloat16:
+        A, B = A.bfloat16().float(), B.bfloat16().float()
+    pre_ref = A @ B.T
+    C = C0.to(dev)
+    pre = torch.empty(M, N, device=dev)
+    F.gemm(Ad, K, 1, Bd, K, 1, M, N, K, C, N, act=L.ACT_GELU, beta=0.5, preact=pre,
+           compute_dtype=dt)
+    _close(pre, pre_ref, dt, "preact")
+    _close(C, tF.gelu(pre_ref) + 0.5 * C0, dt, "gelu+beta")
+
+
+CONVS = [  # N, C, H, W, K, k, s, p
+    (2, 64, 14, 14, 64, 3, 1, 1),
+    (2, 64, 15, 15, 128, 3, 2, 1),
+    (3, 256, 7, 7, 64, 1, 1, 0),
+    (2, 64, 14, 14, 256, 1, 2, 0),
+    (2, 3, 32, 32, 64, 7, 2, 3),
+    (1, 128, 9, 9, 512, 3, 2, 1),
+]
+
+
+def _nhwc(x, cp, dt):
+    N, C, H, W = x.shape
+    y = torch.zeros(N, H, W, cp)
+    y[..., :C] = x.permute(0, 2, 3, 1)
+    return y.to(dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd_dgrad_wgrad(dev, dt, cfg):
+    N, C, H, W, K, k, s, p = cfg
+    vec = 4 if dt == torch.float32 else 8
+    cp = (C + vec - 1) // vec * vec
+    g = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, k, k, generator=g) * 0.1
+    if dt == torch.bfloat16:
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = tF.conv2d(xr, wr, stride=s, padding=p)
+    dy = torch.randn(yr.shape, generator=g)
+    if dt == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    yr.backward(dy)
+    P, Q = yr.shape[2], yr.shape[3]
+    d = L.ConvDesc(N, H, W, cp, K, k, k, s, s, p, p, P, Q)
+    dc = L.dtype_code(dt)
+    wd = w.to(dev)
+    wk = torch.empty(K, k, k, cp, dtype=dt, device=dev)
+    wc = torch.empty(cp, k, k, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", dc, d, C, wd.data_ptr(), wk.data_ptr(), wc.data_ptr(),
+           L.stream())
+    xd = _nhwc(x, cp, dt).to(dev)
+    y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_fwd", dc, d, xd.data_ptr(), wk.data_ptr(), y.data_ptr(), L.stream())
+    _close(y.permute(0, 3, 1, 2), yr.detach(), dt, f"fwd {cfg}")
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    dx = torch.empty(N, H, W, cp, dtype=dt, device=dev)
+    L.call("mmdx_conv_dgrad", dc, d, dyd.data_ptr(), wc.data_ptr(), dx.data_ptr(), 0.0,
+           L.stream())
+    if C == cp:
+        _close(dx.permute(0, 3, 1, 2), xr.grad, dt, f"dgrad {cfg}")
+    dw = torch.empty(K, C, k, k, device=dev)
+    ws_n = L.lib().mmdx_conv_wgrad_workspace_size(dc, d)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    L.call("mmdx_conv_wgrad", dc, d, C, xd.data_ptr(), dyd.data_ptr(), dw.data_ptr(), 0.0,
+           ws.data_ptr(), ws_n, L.stream())
+    _close(dw, wr.grad, dt, f"wgrad {cfg}")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("train", [1, 0])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_batchnorm(dev, dt, train, res, relu):
+    g = torch.Generator().manual_seed(3)
+    N, H, W, C = 4, 9, 7, 64
+    x = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    r = torch.randn(N, C, H, W, generator=g)
+    if dt == torch.bfloat16:
+        x, r = x.bfloat16().float(), r.bfloat16().float()
+    bn = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5, generator=g)
+        bn.bias.uniform_(-0.5, 0.5, generator=g)
+        bn.running_mean.uniform_(-0.2, 0.2, generator=g)
+        bn.running_var.uniform_(0.5, 2, generator=g)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    bn.train(bool(train))
+    xr = x.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True)
+    yr = bn(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    to = lambda t: t.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    xd, rd, dyd = to(x), to(r), to(dy)
+    rows = N * H * W
+    gam, bet = bn.weight.detach().to(dev), bn.bias.detach().to(dev)
+    rm, rv = rm0.to(dev), rv0.to(dev)
+    mean = torch.empty(C, device=dev)
+    rstd = torch.empty(C, device=dev)
+    y = torch.empty_like(xd)
+    ws_n = L.lib().mmdx_bn_workspace_size(rows, C)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    dc = L.dtype_code(dt)
+    L.call("mmdx_bn_fwd", dc, train, xd.data_ptr(), rows, C, gam.data_ptr(), bet.data_ptr(),
+           rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, mean.data_ptr(), rstd.data_ptr(),
+           rd.data_ptr() if res else None, int(relu), y.data_ptr(), ws.data_ptr(), ws_n,
+           L.stream())
+    _close(y.permute(0, 3, 1, 2), yr.detach(), dt, "bn fwd")
+    if train:
+        _close(rm, bn.running_mean, torch.float32, "running_mean")
+        _close(rv, bn.running_var, torch.float32, "running_var")
+    dx = torch.empty_like(xd)
+    dres = torch.empty_like(xd)
+    dg = torch.empty(C, device=dev)
+    db = torch.empty(C, device=dev)
+    L.call("mmdx_bn_bwd", dc, train, xd.data_ptr(), y.data_ptr(), dyd.data_ptr(), rows, C,
+           gam.data_ptr(), mean.data_ptr(), rstd.data_ptr(), int(relu), dx.data_ptr(),
+           dres.data_ptr() if res else None, dg.data_ptr(), db.data_ptr(), 0.0, ws.data_ptr(),
+           ws_n, L.stream())
+    tol_dt = dt
+    _close(dx.permute(0, 3, 1, 2), xr.grad, tol_dt, "bn dx")
+    _close(dg, bn.weight.grad, tol_dt, "dgamma")
+    _close(db, bn.bias.grad, tol_dt, "dbeta")
+    if res:
+        _close(dres.permute(0, 3, 1, 2), rr.grad, tol_dt, "dres")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pools(dev, dt):
+    g = torch.Generator().manual_seed(4)
+    N, C, H, W = 2, 64, 12, 11
+    x = torch.randn(N, C, H, W, generator=g)
+    x[:, :, :4, :4] = 0.0  # ties, as after ReLU
+    if dt == torch.bfloat16:
+        x = x.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    yr = tF.max_pool2d(xr, 3, 2, 1)
+    dy = torch.randn(yr.shape, generator=g)
+    if dt == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    yr.backward(dy)
+    P, Q = yr.shape[2:]
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    y = torch.empty(N, P, Q, C, dtype=dt, device=dev)
+    am = torch.empty(N, P, Q, C, dtype=torch.uint8, device=dev)
+    dc = L.dtype_code(dt)
+    L.call("mmdx_maxpool_fwd", dc, xd.data_ptr(), N, H, W, C, 3, 2, 1, y.data_ptr(),
+           am.data_ptr(), P, Q, L.stream())
+    _close(y.permute(0, 3, 1, 2), yr.detach(), dt, "maxpool fwd")
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    dx = torch.empty_like(xd)
+    L.call("mmdx_maxpool_bwd", dc, am.data_ptr(), dyd.data_ptr(), N, H, W, C, 3, 2, 1, P, Q,
+           dx.data_ptr(), L.stream())
+    _close(dx.permute(0, 3, 1, 2), xr.grad, dt, "maxpool bwd")
+    f = torch.empty(N, C, dtype=dt, device=dev)
+    L.call("mmdx_avgpool_fwd", dc, xd.data_ptr(), N, H * W, C, f.data_ptr(), L.stream())
+    _close(f, x.mean((2, 3)), dt, "avgpool")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_bce_gelu(dev, dt):
+    g = torch.Generator().manual_seed(5)
+    rows, D = 70, 1024
+    x = torch.randn(rows, D, generator=g) + 3.0
+    res = torch.randn(rows, D, generator=g)
+    ln = torch.nn.LayerNorm(D)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5, generator=g)
+        ln.bias.uniform_(-1, 1, generator=g)
+    if dt == torch.bfloat16:
+        x, res = x.bfloat16().float(), res.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    yr = ln(xr + res)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xd = x.to(dev, dt).requires_grad_(True)
+    y = F.layer_norm(xd, ln.weight.detach().to(dev), ln.bias.detach().to(dev), 1e-5,
+                     residual=res.to(dev, dt))
+    _close(y, yr.detach(), dt, "ln fwd")
+    y.backward(dy.to(dev, dt))
+    _close(xd.grad, xr.grad, dt, "ln dx")
+    # BCE
+    z = torch.randn(16, 13, generator=g) * 4
+    t = (torch.rand(16, 13, generator=g) < 0.15).float()
+    zr = z.clone().requires_grad_(True)
+    lr_ = tF.binary_cross_entropy_with_logits(zr, t)
+    lr_.backward()
+    zd = z.to(dev).requires_grad_(True)
+    loss = F.bce_with_logits(zd, t.to(dev))
+    loss.backward()
+    assert abs(loss.item() - lr_.item()) <= 1e-6 * max(1, abs(lr_.item()))
+    _close(zd.grad, zr.grad, torch.float32, "bce grad")
+
+
+def test_adamw_matches_torch(dev):
+    g = torch.Generator().manual_seed(6)
+    shapes = [(1024, 1536), (1024,), (13, 1024), (13,), (7, 3, 5)]
+    ps = [torch.randn(s, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [torch.nn.Parameter(p.to(dev)) for p in ps]
+    o_ref = torch.optim.AdamW([{"params": ref[:2], "lr": 5e-4},
+                               {"params": ref[2:], "lr": 1e-3}], weight_decay=1e-2)
+    o_mine = mmdx.AdamW([{"params": mine[:2], "lr": 5e-4}, {"params": mine[2:], "lr": 1e-3}],
+                        weight_decay=1e-2)
+    for step in range(3):
+        grads = [torch.randn(s, generator=g) for s in shapes]
+        for p, gr in zip(ref, grads):
+            p.grad = gr.clone()
+        for p, gr in zip(mine, grads):
+            p.grad = gr.to(dev)
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        mmdx.clip_grad_norm_(mine, 1.0)
+        o_ref.step()
+        o_mine.step()
+    for a, b in zip(mine, ref):
+        assert torch.allclose(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6)
