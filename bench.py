@@ -1,0 +1,345 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: multimodal samples/s (train fwd+bwd+AdamW) on MI355X.
+
+Workload (BASELINE.json metric "multimodal samples/sec (train fwd+bwd) at 1/2/4/8 MI355X;
+MFMA util %"): the C3/C4 model — ResNet-50 image tower + 2-layer BiLSTM report encoder +
+concat-fusion MLP + BCE — at C4's per-GPU batch (128 samples/GPU = 1024 global on 8 GPUs),
+weak scaling, bf16 compute / fp32 master weights, synthetic 224x224 images + 128-token
+reports.  `--config c2|c3|c5` selects the other BASELINE configs.
+
+One step = H2D-free synthetic batch already in HBM -> image tower || text tower (two HIP
+streams) -> fusion -> BCE -> backward -> (N>1: RCCL all-reduce of gradient buckets over
+xGMI) -> clip_grad_norm_(1.0) -> fused AdamW.  Run:  python bench.py [--gpus N --steps K
+--warmup W]; N>1 under torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    "c2": dict(image="resnet18", text="embed-mean", batch=64, seq=128,
+               name="C2: ResNet-18 + embedding-mean text tower"),
+    "c3": dict(image="resnet50", text="bilstm", batch=256, seq=128,
+               name="C3: ResNet-50 + 2-layer BiLSTM, bs 256 on 1 GPU"),
+    "c4": dict(image="resnet50", text="bilstm", batch=128, seq=128,
+               name="C4: ResNet-50 + 2-layer BiLSTM, 128 samples/GPU (1024 global at 8 GPUs)"),
+    "c5": dict(image="resnet50", text="bert-base-uncased", batch=64, seq=128,
+               name="C5-proxy: ResNet-50 + BERT-base (ViT-B/16 tower not built yet)"),
+}
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def conv_flops_per_sample(trunk, hw=224):
+    """Algorithmic conv FLOPs of one sample: fwd 2*MACs, dgrad 2*MACs (not for the stem,
+    whose input needs no gradient), wgrad 2*MACs."""
+    fwd = dgrad = 0
+    H = W = hw
+    convs = []
+
+    def conv(c, H, W):
+        k, s, p = c.kernel_size, c.stride, c.padding
+        P = (H + 2 * p - k) // s + 1
+        Q = (W + 2 * p - k) // s + 1
+        return P * Q * c.out_channels * c.in_channels * k * k, P, Q
+
+    macs, H, W = conv(trunk[0], H, W)
+    convs.append(("stem", macs))
+    fwd += macs
+    H, W = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    for layer in list(trunk)[4:8]:
+        for blk in layer:
+            Hb, Wb = H, W
+            for c, _, _ in blk.units():
+                m, H, W = conv(c, H, W)
+                fwd += m
+                dgrad += m
+            if blk.downsample is not None:
+                m, _, _ = conv(blk.downsample[0], Hb, Wb)
+                fwd += m
+                dgrad += m
+    return 2 * fwd, 2 * dgrad, 2 * fwd
+
+
+def model_flops_per_sample(cfg, img, txt):
+    f, d, w = conv_flops_per_sample(img.backbone)
+    conv_train = f + d + w
+    L = cfg["seq"]
+    text = 0
+    if cfg["text"] == "bilstm":
+        H = 256
+        for l, inp in ((0, 256), (1, 512)):
+            per_tok = 2 * (4 * H * inp + 4 * H * H)  # both directions: x2 below
+            text += 2 * per_tok * L
+    elif cfg["text"].startswith("bert"):
+        D, I, layers = 768, 3072, 12
+        text += layers * L * 2 * (4 * D * D + 2 * D * I) + layers * 2 * 2 * L * L * D
+    heads = 2 * (img.backbone.feat_dim * 1024 + 512 * txt.hidden_size + 1536 * 1024 + 1024 * 13)
+    return conv_train, conv_train + 3 * (text + heads)
+
+
+def build(cfg, dev, dtype):
+    import mmdx
+    torch.manual_seed(0)
+    img = mmdx.ImageEncoderCNN(cfg["image"], 1024, 13, compute_dtype=dtype).to(dev)
+    txt = mmdx.TextEncoderTransformer(cfg["text"], 512, 13, compute_dtype=dtype).to(dev)
+    if cfg["text"].startswith("bert"):
+        txt.encoder.config.attention_probs_dropout_prob = 0.0
+    fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13, dropout=0.1).to(dev)
+    img.unfreeze_backbone()
+    txt.unfreeze_encoder()
+    fus.train()
+    # reference learning rates: image backbone 1e-4 / heads 5e-4 (TP:866-868), text encoder
+    # 2e-5 / heads 5e-4 (TP:927), fusion 5e-4 (TP:1018-1023); weight decay 1e-2.
+    groups = [
+        {"params": list(img.backbone.parameters()), "lr": 1e-4},
+        {"params": list(img.proj.parameters()) + list(img.classifier.parameters()), "lr": 5e-4},
+        {"params": list(txt.encoder.parameters()), "lr": 2e-5},
+        {"params": list(txt.proj.parameters()) + list(txt.classifier.parameters()), "lr": 5e-4},
+        {"params": list(fus.parameters()), "lr": 5e-4},
+    ]
+    opt = mmdx.AdamW(groups, weight_decay=1e-2)
+    return img, txt, fus, opt
+
+
+def synth(cfg, B, dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.rand(B, 3, 224, 224, generator=g, device=dev)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=dev).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=dev).view(1, 3, 1, 1)
+    x = ((x - mean) / std).contiguous()
+    L = cfg["seq"]
+    ids = torch.randint(1000, 30522, (B, L), generator=g, device=dev)
+    ids[:, 0] = 101
+    ids[:, -1] = 102
+    mask = torch.ones(B, L, dtype=torch.long, device=dev)
+    y = (torch.rand(B, 13, generator=g, device=dev) < 0.15).float()
+    return x, ids, mask, y
+
+
+class StepTimer:
+    """HIP events around every implicit-GEMM conv launch (on the launching stream)."""
+
+    def __init__(self):
+        self.pairs = []
+        self.enabled = False
+
+    def __call__(self, name):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self_):
+                if timer.enabled:
+                    self_.s = torch.cuda.Event(enable_timing=True)
+                    self_.e = torch.cuda.Event(enable_timing=True)
+                    self_.s.record(torch.cuda.current_stream())
+                return self_
+
+            def __exit__(self_, *a):
+                if timer.enabled:
+                    self_.e.record(torch.cuda.current_stream())
+                    timer.pairs.append((name, self_.s, self_.e))
+        return _Ctx()
+
+
+def make_step(img, txt, fus, opt, params, world, x, ids, mask, y, side):
+    import mmdx
+    from mmdx import optim as MO
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):   # text tower concurrent with the image tower
+            z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+        z_img = img(x)["embeddings"]
+        main.wait_stream(side)
+        logits = fus(z_img, z_txt)["disease_logits"]
+        loss = mmdx.BCEWithLogitsLoss()(logits, y)
+        loss.backward()
+        if world > 1:
+            _allreduce_grads(params, world)
+        _, scale = MO.grad_norm(params, 1.0)
+        opt.step(grad_scale=scale)
+        return loss
+    return step
+
+
+_BUCKETS = {}
+
+
+def _allreduce_grads(params, world):
+    """Bucketed (~64 MB) all-reduce of fp32 grads over RCCL, averaged."""
+    grads = [p.grad for p in params if p.grad is not None]
+    key = tuple(g.data_ptr() for g in grads)
+    plan = _BUCKETS.get(key)
+    if plan is None:
+        plan, cur, size = [], [], 0
+        for g in grads:
+            cur.append(g)
+            size += g.numel()
+            if size * 4 >= 64 << 20:
+                plan.append(cur)
+                cur, size = [], 0
+        if cur:
+            plan.append(cur)
+        _BUCKETS.clear()
+        _BUCKETS[key] = plan
+    for bucket in plan:
+        flat = torch._utils._flatten_dense_tensors(bucket)
+        dist.all_reduce(flat)
+        flat.mul_(1.0 / world)
+        for g, s in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
+            g.copy_(s)
+
+
+def cpu_baseline(cfg, seconds=20.0, bs=8, threads=16):
+    """Time the CPU oracle (the reference's PyTorch-CPU path restated, oracle/ref_cpu.py)
+    on a bounded sample: fwd+bwd+AdamW steps of `bs` samples until ~`seconds` elapse."""
+    from oracle import ref_cpu as R
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    text = cfg["text"] if cfg["text"] != "bert-base-uncased" else "bert-base-uncased"
+    model = R.RefMultimodal(cfg["image"], text, dropout=0.0)
+    model.train()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-2)
+    g = torch.Generator().manual_seed(1234)
+    x = torch.rand(bs, 3, 224, 224, generator=g)
+    ids = torch.randint(1000, 30522, (bs, cfg["seq"]), generator=g)
+    mask = torch.ones(bs, cfg["seq"], dtype=torch.long)
+    y = (torch.rand(bs, 13, generator=g) < 0.15).float()
+    R.ref_train_step(model, opt, x, ids, mask, y)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        R.ref_train_step(model, opt, x, ids, mask, y)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return {"value": round(n * bs / el, 3), "unit": "samples/s", "cores": threads,
+            "kind": "port", "sample": f"{n} oracle train steps x {bs} samples "
+            f"({cfg['image']} + {text}, 224x224, L={cfg['seq']}), torch CPU fp32"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch override")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    args = ap.parse_args()
+
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    dtype = torch.bfloat16
+
+    import mmdx
+    from mmdx import resnet as RN
+    img, txt, fus, opt = build(cfg, dev, dtype)
+    params = [p for grp in opt.param_groups for p in grp["params"]]
+    if world > 1:  # identical initial weights on every rank (broadcast from rank 0)
+        with torch.no_grad():
+            for p in list(img.parameters()) + list(txt.parameters()) + list(fus.parameters()):
+                dist.broadcast(p, 0)
+    B = cfg["batch"]
+    x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
+    side = torch.cuda.Stream(device=dev)
+    step = make_step(img, txt, fus, opt, params, world, x, ids, mask, y, side)
+    timer = StepTimer()
+    RN.CONV_TIMER = timer
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.enabled = True
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    conv_ms = sum(s.elapsed_time(e) for _, s, e in timer.pairs)
+    n_conv = len(timer.pairs)
+    conv_flops, total_flops = model_flops_per_sample(cfg, img, txt)
+
+    samples = B * world * args.steps
+    value = samples / el
+    ms_step = el / args.steps * 1e3
+    conv_tf = conv_flops * B * args.steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    result = {
+        "metric": "multimodal samples/sec (train fwd+bwd) at 1/2/4/8 MI355X; MFMA util %",
+        "value": round(value, 2),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
+                "reports, Bernoulli(0.15) labels); random-init weights",
+        "config": {"workload": cfg["name"], "image_tower": cfg["image"],
+                   "text_tower": cfg["text"], "global_batch": B * world,
+                   "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,
+                   "parallelism": f"dp{world}"},
+        "loss": round(float(loss.item()), 5),
+        "model_tflops": round(total_flops * samples / el / 1e12, 2),
+        "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
+                                          (PEAK_BF16_TFLOPS * world), 2),
+        "roofline": {
+            "kernel": "igemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, all ResNet convs)",
+            "bound": "mfma",
+            "achieved": round(conv_tf, 2),
+            "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(conv_tf / PEAK_BF16_TFLOPS, 4),
+            "traffic": None,
+            "conv_ms_per_step": round(conv_ms / args.steps, 3),
+            "conv_launches_per_step": n_conv // max(1, args.steps),
+            "conv_gflop_per_sample": round(conv_flops / 1e9, 3),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -122,6 +122,9 @@ int mmdx_avgpool_bwd(int dtype, const void* dy, int N, int HW, int C, void* dx,
 int mmdx_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int c_pad,
                       void* y, void* stream);
 int mmdx_cast(int dst_dtype, int src_dtype, const void* x, long n, void* y, void* stream);
+/* out = a*x + b*y (fp32; y may be NULL) — bias folding (LSTM b_ih + b_hh), grad copies */
+int mmdx_axpby(long n, float a, const float* x, float b, const float* y, float* out,
+               void* stream);
 
 /* ---------------------------------------------------------------- elementwise / norms
  * LayerNorm over the last dim D (fusion_mlp[3] TP:538, BERT LayerNorms);
@@ -162,10 +165,11 @@ int mmdx_embed_ln_fwd(int dtype, const int64_t* ids, const int64_t* tt, int B, i
                       int D, const float* word, const float* pos, const float* type,
                       const float* gamma, const float* beta, float eps, void* y,
                       void* xsum, float* save_mean, float* save_rstd, void* stream);
-/* scatter-add of dx (= grad of the pre-LN sum) into dense fp32 table grads */
+/* scatter-add (+=) of dx (= grad of the pre-LN sum) into dense fp32 table grads;
+ * rows with id == pad_id get no gradient (nn.Embedding padding_idx; -1 = none) */
 int mmdx_embed_bwd(int dtype, const int64_t* ids, const int64_t* tt, int B, int L, int D,
                    const void* dsum, float* dword, float* dpos, float* dtype_tab,
-                   void* stream);
+                   int pad_id, void* stream);
 /* masked mean pool (TP:452-459): out[b,:] = sum_l h[b,l,:]*m[b,l] / max(sum_l m, 1e-6) */
 int mmdx_masked_mean_fwd(int dtype, const void* h, const int64_t* mask, int B, int L,
                          int D, void* out, void* stream);
@@ -183,15 +187,17 @@ int mmdx_embed_gather(int dtype, const int64_t* ids, long n, int D, const float*
 int mmdx_embed_scatter(int dtype, const int64_t* ids, long n, int D, const void* dout,
                        float* dtable, void* stream);
 
-/* Multi-head self-attention core, head dim 64, L <= 256, with additive key mask
- * (BertSelfAttention: softmax(QK^T/sqrt(d) + (1-mask)*min) V).
+/* Multi-head self-attention core, head dim 64, L <= 256, additive key mask
+ * (BertSelfAttention: softmax(QK^T*scale + (1-mask)*(-huge)) V; mask may be NULL = ViT).
  * qkv: [B, L, 3, H, 64] (fused projection output); out: [B, L, H, 64];
- * probs saved for backward: [B, H, L, L] fp32 (may be NULL in inference). */
+ * probs saved for backward: [B, H, L, L] fp32 (NULL in inference).
+ * dqkv: [B, L, 3, H, 64]; workspace holds dS ([B,H,L,roundup16(L)] compute dtype). */
 int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
                        int H, float scale, void* out, float* probs, void* stream);
+size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H);
 int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const void* dout,
                        const int64_t* mask, int B, int L, int H, float scale, void* dqkv,
-                       void* stream);
+                       void* workspace, size_t ws_bytes, void* stream);
 
 /* LSTM recurrence for one layer, both directions (build-defined C3/C4 tower).
  * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);

@@ -59,6 +59,7 @@ SIGNATURES = {
     "mmdx_avgpool_bwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),
     "mmdx_nchw_to_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
     "mmdx_cast": (i32, [i32, i32, vp, i64, vp, vp]),
+    "mmdx_axpby": (i32, [i64, f32, vp, f32, vp, vp, vp]),
     "mmdx_layernorm_fwd": (i32, [i32, vp, vp, i64, i32, vp, vp, f32, vp, vp, vp, vp, vp]),
     "mmdx_layernorm_bwd": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, f32, vp, sz,
                                  vp]),
@@ -72,7 +73,7 @@ SIGNATURES = {
     "mmdx_bce_logits_bwd": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "mmdx_embed_ln_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp, vp,
                                 vp, vp]),
-    "mmdx_embed_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
+    "mmdx_embed_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, i32, vp]),
     "mmdx_masked_mean_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp]),
     "mmdx_masked_mean_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp]),
     "mmdx_embed_mean_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp]),
@@ -80,7 +81,8 @@ SIGNATURES = {
     "mmdx_embed_gather": (i32, [i32, vp, i64, i32, vp, vp, vp]),
     "mmdx_embed_scatter": (i32, [i32, vp, i64, i32, vp, vp, vp]),
     "mmdx_attention_fwd": (i32, [i32, vp, vp, i32, i32, i32, f32, vp, vp, vp]),
-    "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp]),
+    "mmdx_attention_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp, sz, vp]),
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),

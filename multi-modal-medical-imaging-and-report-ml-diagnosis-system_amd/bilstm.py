@@ -1,0 +1,163 @@
+"""Build-defined C3/C4 report encoder: Embedding(30522, 256) -> 2-layer BiLSTM(256/dir).
+
+Parameters live in a real `nn.LSTM` (names weight_ih_l0, weight_hh_l0_reverse, ...), so the
+state_dict is interchangeable with a PyTorch BiLSTM; execution is:
+  xg   = x [W_ih_f; W_ih_r]^T + (b_ih + b_hh)   one MFMA GEMM over all B*L tokens (fp32 out)
+  h    = recurrence(xg, W_hh)                    mmdx_lstm_fwd, batch-partitioned, no grid sync
+backward: mmdx_lstm_bwd (dG + dW_hh), then dW_ih / dX / bias grads as GEMMs + column sums.
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import functional as F
+from ._lib import call, ptr, stream
+from .layers import Embedding
+
+VOCAB = 30522
+
+
+class _Out(SimpleNamespace):
+    pass
+
+
+def _cat_cast(ws, T, dev):
+    rows = sum(w.shape[0] for w in ws)
+    out = torch.empty((rows,) + tuple(ws[0].shape[1:]), dtype=T, device=dev)
+    o = 0
+    for w in ws:
+        n = w.shape[0]
+        call("mmdx_cast", L.dtype_code(T), L.F32, ptr(w), w.numel(), ptr(out[o:o + n]), stream())
+        o += n
+    return out
+
+
+class _LSTMLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, H, wih_f, whh_f, bih_f, bhh_f, wih_r, whh_r, bih_r, bhh_r):
+        B, Ls, In = x.shape
+        T = x.dtype
+        dev = x.device
+        M = B * Ls
+        G4 = 4 * H
+        wih = _cat_cast([wih_f, wih_r], T, dev)                 # [8H, In]
+        whh = _cat_cast([whh_f, whh_r], T, dev)                 # [2*4H, H]
+        bias = torch.empty(2 * G4, dtype=torch.float32, device=dev)
+        call("mmdx_axpby", G4, 1.0, ptr(bih_f), 1.0, ptr(bhh_f), ptr(bias[:G4]), stream())
+        call("mmdx_axpby", G4, 1.0, ptr(bih_r), 1.0, ptr(bhh_r), ptr(bias[G4:]), stream())
+        xg = torch.empty((M, 2 * G4), dtype=torch.float32, device=dev)
+        F.gemm(x.reshape(M, In), In, True, wih, In, True, M, 2 * G4, In, xg, 2 * G4, bias=bias,
+               compute_dtype=T)
+        hout = torch.empty((B, Ls, 2 * H), dtype=T, device=dev)
+        cs = torch.empty((2, Ls, B, H), dtype=torch.float32, device=dev)
+        gs = torch.empty((2, Ls, B, G4), dtype=torch.float32, device=dev)
+        call("mmdx_lstm_fwd", L.dtype_code(T), ptr(xg), ptr(whh), B, Ls, H, ptr(hout), ptr(cs),
+             ptr(gs), None, 0, stream())
+        ctx.save_for_backward(x, wih, whh, hout, cs, gs)
+        ctx.H = H
+        return hout
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, wih, whh, hout, cs, gs = ctx.saved_tensors
+        H = ctx.H
+        B, Ls, In = x.shape
+        T = x.dtype
+        dev = x.device
+        M = B * Ls
+        G4 = 4 * H
+        dh = F.cast(dh.contiguous(), T)
+        dxg = torch.empty((M, 2 * G4), dtype=T, device=dev)
+        dwhh = torch.empty((2 * G4, H), dtype=torch.float32, device=dev)
+        n = L.lib().mmdx_lstm_workspace_size(L.dtype_code(T), B, Ls, H)
+        ws = L.workspace(n, dev)
+        call("mmdx_lstm_bwd", L.dtype_code(T), ptr(whh), ptr(hout), ptr(cs), ptr(gs), ptr(dh), B,
+             Ls, H, ptr(dxg), ptr(dwhh), ptr(ws), n, stream())
+        dwih = torch.empty((2 * G4, In), dtype=torch.float32, device=dev)
+        F.gemm(dxg, 2 * G4, False, x.reshape(M, In), In, False, 2 * G4, In, M, dwih, In,
+               compute_dtype=T)
+        db = F._bias_grad(dxg, M, 2 * G4, torch.empty(2 * G4, dtype=torch.float32, device=dev))
+        db2 = torch.empty_like(db)
+        call("mmdx_axpby", 2 * G4, 1.0, ptr(db), 0.0, None, ptr(db2), stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, In), dtype=T, device=dev)
+            F.gemm(dxg, 2 * G4, True, wih, In, False, M, In, 2 * G4, dx, In, compute_dtype=T)
+            dx = dx.reshape(B, Ls, In)
+        return (dx, None, dwih[:G4], dwhh[:G4], db[:G4], db2[:G4], dwih[G4:], dwhh[G4:], db[G4:],
+                db2[G4:])
+
+
+class _GatherFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, table, T):
+        B, Ls = ids.shape
+        D = table.shape[1]
+        out = torch.empty((B, Ls, D), dtype=T, device=ids.device)
+        call("mmdx_embed_gather", L.dtype_code(T), ptr(ids), B * Ls, D, ptr(table), ptr(out),
+             stream())
+        ctx.save_for_backward(ids)
+        ctx.tshape = table.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        B, Ls = ids.shape
+        dout = dout.contiguous()
+        dtab = torch.zeros(ctx.tshape, dtype=torch.float32, device=dout.device)
+        call("mmdx_embed_scatter", L.dtype_code(dout.dtype), ptr(ids), B * Ls, ctx.tshape[1],
+             ptr(dout), ptr(dtab), stream())
+        return None, dtab, None
+
+
+class LSTMParams(nn.Module):
+    """Parameter container with nn.LSTM's names, shapes and init (bidirectional,
+    batch_first), without nn.LSTM's cuDNN/MIOpen weight flattening on .to(device)."""
+
+    def __init__(self, input_size, hidden_size, num_layers):
+        super().__init__()
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        k = hidden_size ** -0.5
+        for l in range(num_layers):
+            lin = input_size if l == 0 else 2 * hidden_size
+            for sfx in ("", "_reverse"):
+                for name, shape in ((f"weight_ih_l{l}", (4 * hidden_size, lin)),
+                                    (f"weight_hh_l{l}", (4 * hidden_size, hidden_size)),
+                                    (f"bias_ih_l{l}", (4 * hidden_size,)),
+                                    (f"bias_hh_l{l}", (4 * hidden_size,))):
+                    p = nn.Parameter(torch.empty(shape))
+                    nn.init.uniform_(p, -k, k)
+                    self.register_parameter(name + sfx, p)
+
+
+class BiLSTMEncoder(nn.Module):
+    def __init__(self, vocab_size=VOCAB, emb=256, hidden=256, layers=2):
+        super().__init__()
+        self.config = SimpleNamespace(hidden_size=2 * hidden, vocab_size=vocab_size,
+                                      _name_or_path="bilstm")
+        self.embed = Embedding(vocab_size, emb)
+        self.lstm = LSTMParams(emb, hidden, layers)
+        self.hidden = hidden
+        self.compute_dtype = torch.float32
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, return_dict=True):
+        T = self.compute_dtype
+        L.require_device(input_ids)
+        ids = input_ids.long().contiguous()
+        h = _GatherFn.apply(ids, self.embed.weight, T)
+        m = self.lstm
+        for l in range(m.num_layers):
+            sfx = f"_l{l}"
+            h = _LSTMLayerFn.apply(
+                h, self.hidden,
+                getattr(m, "weight_ih" + sfx), getattr(m, "weight_hh" + sfx),
+                getattr(m, "bias_ih" + sfx), getattr(m, "bias_hh" + sfx),
+                getattr(m, "weight_ih" + sfx + "_reverse"),
+                getattr(m, "weight_hh" + sfx + "_reverse"),
+                getattr(m, "bias_ih" + sfx + "_reverse"), getattr(m, "bias_hh" + sfx + "_reverse"))
+        return _Out(last_hidden_state=h)

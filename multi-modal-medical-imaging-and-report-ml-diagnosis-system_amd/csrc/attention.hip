@@ -1,0 +1,390 @@
+// Multi-head self-attention core for BERT-base / ViT-B (head dim 64, L <= 256).
+//
+// Forward: one workgroup per (query block, head, batch); K, V^T of the head and the Q block
+// live in LDS; S = Q K^T on MFMA, row softmax in registers (16-lane shuffles on the 16x16
+// C layout), P -> LDS, O = P V on MFMA.  Probabilities are saved (fp32) for the backward.
+// Backward: kernel A per query block: dP = dO V^T, dS = P o (dP - rowsum(P o dP)),
+// dQ = scale dS K; kernel B per key block, streaming query chunks: dV = P^T dO,
+// dK = scale dS^T Q.  Additive key mask as BertSelfAttention (large negative on pads).
+#include <algorithm>
+
+#include "igemm.h"
+#include "../../include/mmdx.h"
+
+namespace mmdx {
+
+constexpr int HD = 64;           // head dim
+constexpr int MAXKT = 16;        // max 16-key tiles (L <= 256)
+constexpr float MASK_NEG = -1e30f;
+
+template <typename T> struct AttnCfg;
+template <> struct AttnCfg<bf16> { static constexpr int NW = 4; };   // 64 query rows / block
+template <> struct AttnCfg<float> { static constexpr int NW = 2; };  // 32 query rows / block
+
+__device__ __forceinline__ float rowgroup_max(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float rowgroup_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_rows(T* dst, int ld, const T* src, long src_ld, int rows,
+                                          int rows_valid, int nthreads) {
+  // rows x 64 elements (16-B vectors), zero beyond rows_valid
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int VPR = HD / VEC;
+  for (int i = threadIdx.x; i < rows * VPR; i += nthreads) {
+    const int r = i / VPR, c = (i - r * VPR) * VEC;
+    V v{};
+    if (r < rows_valid) v = *(const V*)(src + r * src_ld + c);
+    *(V*)(dst + r * ld + c) = v;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void load_rows_T(T* dst, int ld, const T* src, long src_ld, int rows,
+                                            int rows_valid, int nthreads) {
+  // dst[c][r] = src[r][c] for rows x 64
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int VPR = HD / VEC;
+  for (int i = threadIdx.x; i < rows * VPR; i += nthreads) {
+    const int r = i / VPR, c = (i - r * VPR) * VEC;
+    V v{};
+    if (r < rows_valid) v = *(const V*)(src + r * src_ld + c);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) dst[(c + j) * ld + r] = v[j];
+  }
+}
+
+template <typename T>
+__global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask,
+                                int L, int H, float scale, T* __restrict__ out,
+                                float* __restrict__ probs) {
+  typedef MfmaOp<T> Op;
+  constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
+  constexpr int LDQ = HD + PAD;
+  const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
+  const int LDV = LP + PAD;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Ks = (T*)smem_raw;                 // [LP][LDQ]
+  T* Vt = Ks + LP * LDQ;                // [HD][LDV]
+  T* Ps = Vt + HD * LDV;                // [QB][LDV]
+  T* Qs = Ps + QB * LDV;                // [QB][LDQ]
+  const int q0 = blockIdx.x * QB, h = blockIdx.y, b = blockIdx.z;
+  const int nth = NW * 64;
+  const long row_ld = 3L * H * HD;
+  const T* base = qkv + (long)b * L * row_ld + h * HD;
+  load_rows<T>(Qs, LDQ, base + (long)q0 * row_ld, row_ld, QB, min(QB, L - q0), nth);
+  load_rows<T>(Ks, LDQ, base + (long)H * HD, row_ld, LP, L, nth);
+  load_rows_T<T>(Vt, LDV, base + 2L * H * HD, row_ld, LP, L, nth);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nkt = LP / 16;
+  f32x4 s[MAXKT];
+  const T* a_s = Qs + (wid * 16 + (lane & 15)) * LDQ + (lane >> 4) * Op::FRAG;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (j < nkt) {
+      const T* b_s = Ks + (j * 16 + (lane & 15)) * LDQ + (lane >> 4) * Op::FRAG;
+#pragma unroll
+      for (int k = 0; k < HD; k += Op::KS) s[j] = Op::mma(Op::ld(a_s + k), Op::ld(b_s + k), s[j]);
+    }
+  }
+  // scale + mask + row softmax (rows (lane>>4)*4+r of this wave's 16)
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+    const int key = j * 16 + (lane & 15);
+    const float madd = key < L ? (mask && mask[(long)b * L + key] == 0 ? MASK_NEG : 0.f) : -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[j][r] = s[j][r] * scale + madd;
+      mx[r] = fmaxf(mx[r], s[j][r]);
+    }
+  }
+  float sum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { mx[r] = rowgroup_max(mx[r]); sum[r] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[j][r] = __expf(s[j][r] - mx[r]);
+      sum[r] += s[j][r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sum[r] = 1.f / rowgroup_sum(sum[r]);
+  float* prow = probs ? probs + (((long)b * H + h) * L) * L : nullptr;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+    const int key = j * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wid * 16 + (lane >> 4) * 4 + r;
+      const float p = s[j][r] * sum[r];
+      Ps[rl * LDV + key] = from_f<T>(p);
+      const int q = q0 + rl;
+      if (prow && q < L && key < L) prow[(long)q * L + key] = p;
+    }
+  }
+  __syncthreads();
+  // O[16][64] = P[16][LP] V[LP][64]
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int j = 0; j < HD / 16; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* p_s = Ps + (wid * 16 + (lane & 15)) * LDV + (lane >> 4) * Op::FRAG;
+  for (int k = 0; k < LP; k += Op::KS) {
+    const typename Op::frag_t af = Op::ld(p_s + k);
+#pragma unroll
+    for (int j = 0; j < HD / 16; ++j) {
+      const T* v_s = Vt + (j * 16 + (lane & 15)) * LDV + (lane >> 4) * Op::FRAG;
+      o[j] = Op::mma(af, Op::ld(v_s + k), o[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < HD / 16; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + wid * 16 + (lane >> 4) * 4 + r;
+      if (q < L) out[(((long)b * L + q) * H + h) * HD + j * 16 + (lane & 15)] = from_f<T>(o[j][r]);
+    }
+}
+
+// Backward A: per query block -> dS (T, global scratch [B,H,L,LP]) and dQ.
+template <typename T>
+__global__ void attn_bwd_q_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
+                                  const T* __restrict__ dout, int L, int H, float scale,
+                                  T* __restrict__ dS_g, T* __restrict__ dqkv) {
+  typedef MfmaOp<T> Op;
+  constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
+  constexpr int LDQ = HD + PAD;
+  const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
+  const int LDV = LP + PAD;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Vs = (T*)smem_raw;                 // [LP][LDQ]   V rows (K-major for dP)
+  T* Kt = Vs + LP * LDQ;                // [HD][LDV]   K^T (for dQ)
+  T* dSs = Kt + HD * LDV;               // [QB][LDV]
+  T* dOs = dSs + QB * LDV;              // [QB][LDQ]
+  const int q0 = blockIdx.x * QB, h = blockIdx.y, b = blockIdx.z;
+  const int nth = NW * 64;
+  const long row_ld = 3L * H * HD;
+  const T* base = qkv + (long)b * L * row_ld + h * HD;
+  load_rows<T>(dOs, LDQ, dout + ((long)b * L + q0) * H * HD + h * HD, (long)H * HD, QB,
+               min(QB, L - q0), nth);
+  load_rows<T>(Vs, LDQ, base + 2L * H * HD, row_ld, LP, L, nth);
+  load_rows_T<T>(Kt, LDV, base + (long)H * HD, row_ld, LP, L, nth);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nkt = LP / 16;
+  f32x4 s[MAXKT];
+  const T* a_s = dOs + (wid * 16 + (lane & 15)) * LDQ + (lane >> 4) * Op::FRAG;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (j < nkt) {
+      const T* b_s = Vs + (j * 16 + (lane & 15)) * LDQ + (lane >> 4) * Op::FRAG;
+#pragma unroll
+      for (int k = 0; k < HD; k += Op::KS) s[j] = Op::mma(Op::ld(a_s + k), Op::ld(b_s + k), s[j]);
+    }
+  }
+  const float* prow = probs + (((long)b * H + h) * L) * L;
+  float pv[MAXKT][4];
+  float dot[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+    const int key = j * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + wid * 16 + (lane >> 4) * 4 + r;
+      pv[j][r] = (q < L && key < L) ? prow[(long)q * L + key] : 0.f;
+      dot[r] += pv[j][r] * s[j][r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dot[r] = rowgroup_sum(dot[r]);
+  T* dsg = dS_g + (((long)b * H + h) * L) * LP;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+    const int key = j * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wid * 16 + (lane >> 4) * 4 + r;
+      const float ds = pv[j][r] * (s[j][r] - dot[r]);
+      const T dst = from_f<T>(ds);
+      dSs[rl * LDV + key] = dst;
+      const int q = q0 + rl;
+      if (q < L) dsg[(long)q * LP + key] = dst;
+    }
+  }
+  __syncthreads();
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int j = 0; j < HD / 16; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* p_s = dSs + (wid * 16 + (lane & 15)) * LDV + (lane >> 4) * Op::FRAG;
+  for (int k = 0; k < LP; k += Op::KS) {
+    const typename Op::frag_t af = Op::ld(p_s + k);
+#pragma unroll
+    for (int j = 0; j < HD / 16; ++j) {
+      const T* k_s = Kt + (j * 16 + (lane & 15)) * LDV + (lane >> 4) * Op::FRAG;
+      o[j] = Op::mma(af, Op::ld(k_s + k), o[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < HD / 16; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + wid * 16 + (lane >> 4) * 4 + r;
+      if (q < L)
+        dqkv[((long)b * L + q) * 3 * H * HD + h * HD + j * 16 + (lane & 15)] =
+            from_f<T>(o[j][r] * scale);
+    }
+}
+
+// Backward B: per key block (16*NW keys): dV = P^T dO, dK = scale * dS^T Q, streaming
+// 32-query chunks through LDS.
+constexpr int QC = 32;
+template <typename T>
+__global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
+                                   const T* __restrict__ dout, const T* __restrict__ dS_g, int L,
+                                   int H, float scale, T* __restrict__ dqkv) {
+  typedef MfmaOp<T> Op;
+  constexpr int NW = AttnCfg<T>::NW, KB = NW * 16, PAD = Vec16<T>::N;
+  constexpr int LDC = QC + PAD;
+  __shared__ __attribute__((aligned(16))) T Pt[KB * LDC];    // [key][q]
+  __shared__ __attribute__((aligned(16))) T dSt[KB * LDC];   // [key][q]
+  __shared__ __attribute__((aligned(16))) T dOt[HD * LDC];   // [d][q]
+  __shared__ __attribute__((aligned(16))) T Qt[HD * LDC];    // [d][q]
+  const int k0 = blockIdx.x * KB, h = blockIdx.y, b = blockIdx.z;
+  const int nth = NW * 64;
+  const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
+  const long row_ld = 3L * H * HD;
+  const T* qbase = qkv + (long)b * L * row_ld + h * HD;
+  const float* pb = probs + (((long)b * H + h) * L) * L;
+  const T* dsb = dS_g + (((long)b * H + h) * L) * LP;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  f32x4 dv[HD / 16], dk[HD / 16];
+#pragma unroll
+  for (int j = 0; j < HD / 16; ++j) dv[j] = dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int qc = 0; qc < L; qc += QC) {
+    for (int i = threadIdx.x; i < KB * QC; i += nth) {
+      const int kk = i / QC, qq = i - kk * QC;
+      const int key = k0 + kk, q = qc + qq;
+      const bool ok = key < L && q < L;
+      Pt[kk * LDC + qq] = from_f<T>(ok ? pb[(long)q * L + key] : 0.f);
+      dSt[kk * LDC + qq] = ok ? dsb[(long)q * LP + key] : from_f<T>(0.f);
+    }
+    load_rows_T<T>(dOt, LDC, dout + ((long)b * L + qc) * H * HD + h * HD, (long)H * HD, QC,
+                   min(QC, L - qc), nth);
+    load_rows_T<T>(Qt, LDC, qbase + (long)qc * row_ld, row_ld, QC, min(QC, L - qc), nth);
+    __syncthreads();
+    const T* ap = Pt + (wid * 16 + (lane & 15)) * LDC + (lane >> 4) * Op::FRAG;
+    const T* as = dSt + (wid * 16 + (lane & 15)) * LDC + (lane >> 4) * Op::FRAG;
+#pragma unroll
+    for (int k = 0; k < QC; k += Op::KS) {
+      const typename Op::frag_t fp = Op::ld(ap + k), fs = Op::ld(as + k);
+#pragma unroll
+      for (int j = 0; j < HD / 16; ++j) {
+        const int off = (j * 16 + (lane & 15)) * LDC + (lane >> 4) * Op::FRAG + k;
+        dv[j] = Op::mma(fp, Op::ld(dOt + off), dv[j]);
+        dk[j] = Op::mma(fs, Op::ld(Qt + off), dk[j]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < HD / 16; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = k0 + wid * 16 + (lane >> 4) * 4 + r;
+      if (key < L) {
+        T* row = dqkv + ((long)b * L + key) * 3 * H * HD + h * HD + j * 16 + (lane & 15);
+        row[(long)H * HD] = from_f<T>(dk[j][r] * scale);
+        row[2L * H * HD] = from_f<T>(dv[j][r]);
+      }
+    }
+}
+
+template <typename T>
+static size_t fwd_smem(int L) {
+  constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
+  const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
+  return sizeof(T) * ((size_t)LP * (HD + PAD) + (size_t)HD * (LP + PAD) +
+                      (size_t)QB * (LP + PAD) + (size_t)QB * (HD + PAD));
+}
+
+}  // namespace mmdx
+
+using namespace mmdx;
+
+extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
+                                  int H, float scale, void* out, float* probs, void* stream) {
+  MMDX_CHECK_ARG(B > 0 && H > 0 && L > 0 && L <= 16 * MAXKT, "attention: L=%d > 256", L);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16) {
+    constexpr int QB = AttnCfg<bf16>::NW * 16;
+    const size_t sm = fwd_smem<bf16>(L);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL(attn_fwd_kernel<bf16>, dim3((L + QB - 1) / QB, H, B),
+                       dim3(AttnCfg<bf16>::NW * 64), sm, st, (const bf16*)qkv, mask, L, H, scale,
+                       (bf16*)out, probs);
+  } else {
+    constexpr int QB = AttnCfg<float>::NW * 16;
+    const size_t sm = fwd_smem<float>(L);
+    MMDX_CHECK_ARG(sm <= 160 * 1024, "attention fp32: L=%d needs %zu B LDS", L, sm);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<float>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL(attn_fwd_kernel<float>, dim3((L + QB - 1) / QB, H, B),
+                       dim3(AttnCfg<float>::NW * 64), sm, st, (const float*)qkv, mask, L, H,
+                       scale, (float*)out, probs);
+  }
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H) {
+  const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
+  return (size_t)B * H * L * LP * (dtype == BF16 ? 2 : 4);
+}
+
+extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs,
+                                  const void* dout, const int64_t* mask, int B, int L, int H,
+                                  float scale, void* dqkv, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  (void)mask;  // encoded in probs (masked keys have p = 0)
+  MMDX_CHECK_ARG(L <= 16 * MAXKT && probs, "attention bwd: bad args");
+  MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_attention_workspace_size(dtype, B, L, H),
+                 "attention bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+#define ATTN_BWD(T)                                                                            \
+  {                                                                                            \
+    constexpr int QB = AttnCfg<T>::NW * 16;                                                    \
+    const size_t sm = fwd_smem<T>(L);                                                          \
+    MMDX_CHECK_ARG(sm <= 160 * 1024, "attention bwd: L=%d needs %zu B LDS", L, sm);           \
+    (void)hipFuncSetAttribute((const void*)attn_bwd_q_kernel<T>,                                     \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);                  \
+    hipLaunchKernelGGL(attn_bwd_q_kernel<T>, dim3((L + QB - 1) / QB, H, B),                    \
+                       dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, probs,                \
+                       (const T*)dout, L, H, scale, (T*)ws, (T*)dqkv);                         \
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((L + QB - 1) / QB, H, B),                   \
+                       dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs, (const T*)dout, \
+                       (const T*)ws, L, H, scale, (T*)dqkv);                                   \
+  }
+  if (dtype == BF16) ATTN_BWD(bf16) else ATTN_BWD(float)
+#undef ATTN_BWD
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}

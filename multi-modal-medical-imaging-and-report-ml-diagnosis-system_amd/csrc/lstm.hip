@@ -1,0 +1,282 @@
+// Bidirectional LSTM recurrence (build-defined C3/C4 text tower, nn.LSTM semantics).
+//
+// The recurrence couples time steps only within one batch row, so the grid is
+// (direction x batch slices of 16 rows): every workgroup runs its rows through all L
+// steps with no inter-workgroup synchronisation.  Per step the gate pre-activations
+// G[16][4H] = xg[t] + h_{t-1} W_hh^T come from MFMA (h in LDS, W_hh streamed from L2),
+// the cell update runs from an fp32 LDS image of G.  Input projections (x W_ih^T + b) for
+// all steps are one large GEMM outside this kernel; so are dW_ih, dX and the bias grads.
+#include <algorithm>
+
+#include "igemm.h"
+#include "../../include/mmdx.h"
+
+namespace mmdx {
+
+constexpr int LSTM_RB = 16;   // batch rows per workgroup
+constexpr int LSTM_NW = 4;    // waves per workgroup
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// Fragment loads straight from global for a K-major [N][K] operand row block.
+template <typename T>
+__device__ __forceinline__ typename MfmaOp<T>::frag_t ldg_frag(const T* p) {
+  return MfmaOp<T>::ld(p);
+}
+
+template <typename T, int H>
+__global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
+    const float* __restrict__ xg, const T* __restrict__ whh, int B, int L,
+    T* __restrict__ hout, float* __restrict__ csave, float* __restrict__ gsave) {
+  typedef MfmaOp<T> Op;
+  constexpr int G4 = 4 * H;
+  constexpr int LDH = H + Vec16<T>::N;
+  constexpr int TILES = G4 / (LSTM_NW * 16);  // 16-col tiles per wave
+  __shared__ float sg[LSTM_RB * G4];
+  __shared__ __attribute__((aligned(16))) T sh[LSTM_RB * LDH];
+  const int dir = blockIdx.y;
+  const int b0 = blockIdx.x * LSTM_RB;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const T* W = whh + (long)dir * G4 * H;
+  for (int i = threadIdx.x; i < LSTM_RB * LDH; i += blockDim.x) sh[i] = from_f<T>(0.f);
+  float creg[LSTM_RB * H / (LSTM_NW * 64)];
+  constexpr int CPT = LSTM_RB * H / (LSTM_NW * 64);
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) creg[i] = 0.f;
+  __syncthreads();
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    f32x4 acc[TILES];
+#pragma unroll
+    for (int j = 0; j < TILES; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int col0 = wid * TILES * 16;
+    const T* a_s = sh + (lane & 15) * LDH + (lane >> 4) * Op::FRAG;
+    const T* w_s = W + (long)(col0 + (lane & 15)) * H + (lane >> 4) * Op::FRAG;
+#pragma unroll 2
+    for (int k = 0; k < H; k += Op::KS) {
+      const typename Op::frag_t af = Op::ld(a_s + k);
+#pragma unroll
+      for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, ldg_frag<T>(w_s + (long)j * 16 * H + k), acc[j]);
+    }
+    // gates (+ input projection) -> LDS fp32
+#pragma unroll
+    for (int j = 0; j < TILES; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = (lane >> 4) * 4 + r, col = col0 + j * 16 + (lane & 15);
+        const int b = b0 + row;
+        float v = acc[j][r];
+        if (b < B) v += xg[(((long)b * L + t) * 2 + dir) * G4 + col];
+        sg[row * G4 + col] = v;
+      }
+    __syncthreads();
+    // cell update: thread owns CPT (row, unit) pairs
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int e = threadIdx.x + i * LSTM_NW * 64;
+      const int row = e / H, u = e - row * H;
+      const int b = b0 + row;
+      const float gi = sigm(sg[row * G4 + u]);
+      const float gf = sigm(sg[row * G4 + H + u]);
+      const float gg = tanhf(sg[row * G4 + 2 * H + u]);
+      const float go = sigm(sg[row * G4 + 3 * H + u]);
+      const float c = gf * creg[i] + gi * gg;
+      creg[i] = c;
+      const float h = go * tanhf(c);
+      sh[row * LDH + u] = from_f<T>(h);
+      if (b < B) {
+        hout[((long)b * L + t) * 2 * H + dir * H + u] = from_f<T>(h);
+        const long sidx = (((long)dir * L + t) * B + b);
+        csave[sidx * H + u] = c;
+        float* gp = gsave + sidx * G4;
+        gp[u] = gi;
+        gp[H + u] = gf;
+        gp[2 * H + u] = gg;
+        gp[3 * H + u] = go;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Recurrent backward.  dG (pre-activation gate grads) -> dxg [B][L][2][4H] (T) and the
+// shifted hidden states hprev [2][B*L][H] (T) for the dW_hh GEMM.
+template <typename T, int H>
+__global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
+    const T* __restrict__ whhT, const T* __restrict__ hout, const float* __restrict__ csave,
+    const float* __restrict__ gsave, const T* __restrict__ dhout, int B, int L,
+    T* __restrict__ dxg, T* __restrict__ hprev) {
+  typedef MfmaOp<T> Op;
+  constexpr int G4 = 4 * H;
+  constexpr int LDG = G4 + Vec16<T>::N;
+  constexpr int TILES = H / (LSTM_NW * 16);
+  constexpr int CPT = LSTM_RB * H / (LSTM_NW * 64);
+  __shared__ __attribute__((aligned(16))) T sdg[LSTM_RB * LDG];
+  __shared__ float sdh[LSTM_RB * H];
+  const int dir = blockIdx.y;
+  const int b0 = blockIdx.x * LSTM_RB;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const T* WT = whhT + (long)dir * H * G4;  // [H][4H]
+  float dcn[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) dcn[i] = 0.f;
+  for (int i = threadIdx.x; i < LSTM_RB * H; i += blockDim.x) sdh[i] = 0.f;
+  __syncthreads();
+  for (int s = L - 1; s >= 0; --s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    const int tp = dir == 0 ? t - 1 : t + 1;  // previous step in forward order
+    const bool has_prev = s > 0;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int e = threadIdx.x + i * LSTM_NW * 64;
+      const int row = e / H, u = e - row * H;
+      const int b = b0 + row;
+      float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
+      if (b < B) {
+        const long sidx = ((long)dir * L + t) * B + b;
+        const float* gp = gsave + sidx * G4;
+        const float gi = gp[u], gf = gp[H + u], gg = gp[2 * H + u], go = gp[3 * H + u];
+        const float c = csave[sidx * H + u];
+        const float cp = has_prev ? csave[(((long)dir * L + tp) * B + b) * H + u] : 0.f;
+        const float dh = to_f(dhout[((long)b * L + t) * 2 * H + dir * H + u]) + sdh[row * H + u];
+        const float tc = tanhf(c);
+        const float dc = dh * go * (1.f - tc * tc) + dcn[i];
+        const float d_o = dh * tc;
+        dgi = dc * gg * gi * (1.f - gi);
+        dgf = dc * cp * gf * (1.f - gf);
+        dgg = dc * gi * (1.f - gg * gg);
+        dgo = d_o * go * (1.f - go);
+        dcn[i] = dc * gf;
+        T* dp = dxg + (((long)b * L + t) * 2 + dir) * G4;
+        dp[u] = from_f<T>(dgi);
+        dp[H + u] = from_f<T>(dgf);
+        dp[2 * H + u] = from_f<T>(dgg);
+        dp[3 * H + u] = from_f<T>(dgo);
+        hprev[((long)dir * B * L + (long)b * L + t) * H + u] =
+            has_prev ? hout[((long)b * L + tp) * 2 * H + dir * H + u] : from_f<T>(0.f);
+      }
+      sdg[row * LDG + u] = from_f<T>(dgi);
+      sdg[row * LDG + H + u] = from_f<T>(dgf);
+      sdg[row * LDG + 2 * H + u] = from_f<T>(dgg);
+      sdg[row * LDG + 3 * H + u] = from_f<T>(dgo);
+    }
+    __syncthreads();
+    // dh_next[16][H] = dG[16][4H] . W_hh  (B operand = W_hh^T rows, K-major)
+    f32x4 acc[TILES];
+#pragma unroll
+    for (int j = 0; j < TILES; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int col0 = wid * TILES * 16;
+    const T* a_s = sdg + (lane & 15) * LDG + (lane >> 4) * Op::FRAG;
+    const T* w_s = WT + (long)(col0 + (lane & 15)) * G4 + (lane >> 4) * Op::FRAG;
+#pragma unroll 2
+    for (int k = 0; k < G4; k += Op::KS) {
+      const typename Op::frag_t af = Op::ld(a_s + k);
+#pragma unroll
+      for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, ldg_frag<T>(w_s + (long)j * 16 * G4 + k), acc[j]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TILES; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sdh[((lane >> 4) * 4 + r) * H + col0 + j * 16 + (lane & 15)] = acc[j][r];
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ void transpose_whh_kernel(const T* __restrict__ w, int H, T* __restrict__ wt) {
+  const int G4 = 4 * H;
+  const long total = 2L * G4 * H;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i / ((long)G4 * H));
+    const long r = i - (long)d * G4 * H;
+    const int g = (int)(r / H), u = (int)(r - (long)g * H);
+    wt[(long)d * G4 * H + (long)u * G4 + g] = w[i];
+  }
+}
+
+template <typename T>
+static int lstm_fwd_t(const void* xg, const void* whh, int B, int L, int H, void* hout,
+                      float* cs, float* gs, hipStream_t st) {
+  dim3 grid((B + LSTM_RB - 1) / LSTM_RB, 2);
+  if (H == 256)
+    hipLaunchKernelGGL((lstm_fwd_kernel<T, 256>), grid, dim3(LSTM_NW * 64), 0, st,
+                       (const float*)xg, (const T*)whh, B, L, (T*)hout, cs, gs);
+  else if (H == 128)
+    hipLaunchKernelGGL((lstm_fwd_kernel<T, 128>), grid, dim3(LSTM_NW * 64), 0, st,
+                       (const float*)xg, (const T*)whh, B, L, (T*)hout, cs, gs);
+  else if (H == 64)
+    hipLaunchKernelGGL((lstm_fwd_kernel<T, 64>), grid, dim3(LSTM_NW * 64), 0, st,
+                       (const float*)xg, (const T*)whh, B, L, (T*)hout, cs, gs);
+  else {
+    mmdx_set_error("lstm: hidden size %d unsupported (64, 128, 256)", H);
+    return -22;
+  }
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mmdx
+
+using namespace mmdx;
+
+extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
+                             void* h_out, float* c_save, float* gates_save, void* ws,
+                             size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(B > 0 && L > 0 && c_save && gates_save, "lstm fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16) return lstm_fwd_t<bf16>(xg, w_hh, B, L, H, h_out, c_save, gates_save, st);
+  return lstm_fwd_t<float>(xg, w_hh, B, L, H, h_out, c_save, gates_save, st);
+}
+
+extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
+  const size_t es = dtype == BF16 ? 2 : 4;
+  // transposed W_hh + shifted hidden states + dW_hh GEMM split-K scratch
+  return 2 * (size_t)4 * H * H * es + 2 * (size_t)B * L * H * es +
+         2 * mmdx_gemm_workspace_size(dtype, 4 * H, H, B * L) + 256;
+}
+
+extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
+                             const float* gates_save, const void* dh_out, int B, int L, int H,
+                             void* dxg, float* dw_hh, void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(H == 64 || H == 128 || H == 256, "lstm bwd: hidden size %d unsupported", H);
+  MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_lstm_workspace_size(dtype, B, L, H),
+                 "lstm bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t es = dtype == BF16 ? 2 : 4;
+  char* w = (char*)ws;
+  void* whhT = w;
+  w += 2 * (size_t)4 * H * H * es;
+  void* hprev = w;
+  w += 2 * (size_t)B * L * H * es;
+  w = (char*)(((uintptr_t)w + 255) & ~(uintptr_t)255);
+  const size_t gws = mmdx_gemm_workspace_size(dtype, 4 * H, H, B * L);
+  dim3 grid((B + LSTM_RB - 1) / LSTM_RB, 2);
+  const long tw = 2L * 4 * H * H;
+  const int tb = (int)std::min<long>((tw + 255) / 256, 4096);
+#define LSTM_BWD(T, HH)                                                                         \
+  hipLaunchKernelGGL(transpose_whh_kernel<T>, dim3(tb), dim3(256), 0, st, (const T*)w_hh, HH,  \
+                     (T*)whhT);                                                                 \
+  hipLaunchKernelGGL((lstm_bwd_kernel<T, HH>), grid, dim3(LSTM_NW * 64), 0, st,                 \
+                     (const T*)whhT, (const T*)h_out, c_save, gates_save, (const T*)dh_out, B, \
+                     L, (T*)dxg, (T*)hprev)
+  if (dtype == BF16) {
+    if (H == 256) { LSTM_BWD(bf16, 256); } else if (H == 128) { LSTM_BWD(bf16, 128); } else { LSTM_BWD(bf16, 64); }
+  } else {
+    if (H == 256) { LSTM_BWD(float, 256); } else if (H == 128) { LSTM_BWD(float, 128); } else { LSTM_BWD(float, 64); }
+  }
+#undef LSTM_BWD
+  MMDX_LAUNCH_CHECK();
+  // dW_hh[d] = sum_rows dG[:, d]^T hprev[d]   ([4H] x [H] over B*L rows)
+  for (int d = 0; d < 2; ++d) {
+    const char* dg = (const char*)dxg + (size_t)d * 4 * H * es;
+    const char* hp = (const char*)hprev + (size_t)d * B * L * H * es;
+    int rc = mmdx_gemm(dtype, 4 * H, H, B * L, dg, 8L * H, 0, hp, H, 0,
+                       dw_hh + (size_t)d * 4 * H * H, H, F32, nullptr, nullptr, ACT_NONE, 1.f,
+                       0.f, nullptr, w, gws, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}

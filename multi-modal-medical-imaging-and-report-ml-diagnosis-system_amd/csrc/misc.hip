@@ -146,6 +146,11 @@ __global__ void cast_kernel(const S* __restrict__ x, long n, D* __restrict__ y) 
   GRID_STRIDE(i, n) y[i] = from_f<D>(to_f(x[i]));
 }
 
+__global__ void axpby_kernel(long n, float a, const float* __restrict__ x, float b,
+                             const float* __restrict__ y, float* __restrict__ out) {
+  GRID_STRIDE(i, n) out[i] = a * x[i] + (y ? b * y[i] : 0.f);
+}
+
 // ----------------------------------------------------------------------------- GELU / bias
 template <typename T>
 __global__ void gelu_bwd_kernel(const T* __restrict__ pre, const T* __restrict__ dy, long n,
@@ -370,6 +375,14 @@ extern "C" int mmdx_bce_logits_bwd(const float* logits, const float* target, int
   const int n = B * C;
   hipLaunchKernelGGL(bce_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                      logits, target, n, dloss, dlogits);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_axpby(long n, float a, const float* x, float b, const float* y, float* out,
+                          void* stream) {
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, a, x,
+                     b, y, out);
   MMDX_LAUNCH_CHECK();
   return 0;
 }

@@ -54,13 +54,16 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
 // word-table grads: scatter-add (fp32 atomics; repeated ids collide)
 template <typename T>
 __global__ void embed_word_bwd_kernel(const int64_t* __restrict__ ids, long rows, int D,
-                                      const T* __restrict__ ds, float* __restrict__ dword) {
+                                      const T* __restrict__ ds, float* __restrict__ dword,
+                                      int pad_id) {
   const long total = rows * D;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const long r = i / D;
     const int d = (int)(i - r * D);
-    atomicAdd(&dword[ids[r] * D + d], to_f(ds[i]));
+    const long id = ids[r];
+    if (id == pad_id) continue;  // nn.Embedding(padding_idx): no gradient for the pad row
+    atomicAdd(&dword[id * D + d], to_f(ds[i]));
   }
 }
 // position grads: dpos[l,d] = sum_b ds[b,l,d] (deterministic)
@@ -208,13 +211,13 @@ extern "C" int mmdx_embed_ln_fwd(int dtype, const int64_t* ids, const int64_t* t
 
 extern "C" int mmdx_embed_bwd(int dtype, const int64_t* ids, const int64_t* tt, int B, int L,
                               int D, const void* dsum, float* dword, float* dpos,
-                              float* dtype_tab, void* stream) {
+                              float* dtype_tab, int pad_id, void* stream) {
   const long rows = (long)B * L;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     if (dword)
       hipLaunchKernelGGL(embed_word_bwd_kernel<T>, dim3(grid_for(rows * D)), dim3(256), 0, st,
-                         ids, rows, D, (const T*)dsum, dword);
+                         ids, rows, D, (const T*)dsum, dword, pad_id);
     if (dpos)
       hipLaunchKernelGGL(embed_pos_bwd_kernel<T>, dim3(grid_for((long)L * D)), dim3(256), 0, st,
                          (const T*)dsum, B, L, D, dpos);

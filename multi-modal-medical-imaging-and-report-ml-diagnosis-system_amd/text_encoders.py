@@ -22,6 +22,9 @@ from . import _lib as L
 from . import functional as F
 from .layers import Embedding, LayerNorm, Linear
 
+from .bert import BertModel  # noqa: E402,F401
+from .bilstm import BiLSTMEncoder  # noqa: E402,F401
+
 VOCAB = 30522
 
 

@@ -1,0 +1,148 @@
+"""Text-tower parity: attention core, BiLSTM recurrence, BERT layers vs PyTorch / transformers.
+
+fp32 tolerances: outputs rel 1e-4 of scale; grads 1 - cosine <= 1e-5 (fp32 vs fp32 ref).
+bf16: rel 3e-2.
+"""
+import math
+
+import pytest
+import torch
+
+import mmdx
+from mmdx import _lib as L
+from oracle import ref_cpu as R
+from parity_util import cosine, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_attention(q, k, v, mask, scale):
+    s = torch.einsum("blhd,bmhd->bhlm", q, k) * scale
+    if mask is not None:
+        s = s + (1.0 - mask[:, None, None, :].float()) * -1e30
+    p = s.softmax(-1)
+    return torch.einsum("bhlm,bmhd->blhd", p, v)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,Ls,H", [(2, 128, 12), (3, 37, 2), (2, 197, 4), (1, 256, 1)])
+@pytest.mark.parametrize("masked", [True, False])
+def test_attention(dev, dt, B, Ls, H, masked):
+    g = torch.Generator().manual_seed(B * Ls + H)
+    qkv = torch.randn(B, Ls, 3, H, 64, generator=g)
+    if dt == torch.bfloat16:
+        qkv = qkv.bfloat16().float()
+    mask = None
+    if masked:
+        lens = torch.randint(1, Ls + 1, (B,), generator=g)
+        mask = (torch.arange(Ls)[None] < lens[:, None]).long()
+    scale = 0.125
+    qr = qkv.clone().requires_grad_(True)
+    o = _ref_attention(qr[:, :, 0], qr[:, :, 1], qr[:, :, 2], mask, scale)
+    do = torch.randn(o.shape, generator=g)
+    if dt == torch.bfloat16:
+        do = do.bfloat16().float()
+    o.backward(do)
+    dc = L.dtype_code(dt)
+    qd = qkv.to(dev, dt).contiguous()
+    md = mask.to(dev) if mask is not None else None
+    out = torch.empty(B, Ls, H, 64, dtype=dt, device=dev)
+    probs = torch.empty(B, H, Ls, Ls, device=dev)
+    L.call("mmdx_attention_fwd", dc, qd.data_ptr(), md.data_ptr() if md is not None else None,
+           B, Ls, H, scale, out.data_ptr(), probs.data_ptr(), L.stream())
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    assert rel_err(out, o) <= tol
+    dqkv = torch.empty_like(qd)
+    n = L.lib().mmdx_attention_workspace_size(dc, B, Ls, H)
+    ws = torch.empty(n, dtype=torch.uint8, device=dev)
+    L.call("mmdx_attention_bwd", dc, qd.data_ptr(), probs.data_ptr(),
+           do.to(dev, dt).contiguous().data_ptr(), md.data_ptr() if md is not None else None, B,
+           Ls, H, scale, dqkv.data_ptr(), ws.data_ptr(), n, L.stream())
+    for i, name in enumerate("qkv"):
+        e = rel_err(dqkv[:, :, i], qr.grad[:, :, i])
+        assert e <= (2e-4 if dt == torch.float32 else 5e-2), f"d{name} {e}"
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bilstm_tower(dev, dt):
+    torch.manual_seed(0)
+    ref = R.RefBiLSTM()
+    enc = mmdx.text_encoders.BiLSTMEncoder()
+    enc.load_state_dict(ref.state_dict())
+    enc.compute_dtype = dt
+    g = torch.Generator().manual_seed(2)
+    B, Ls = 20, 33
+    ids = torch.randint(1000, 30522, (B, Ls), generator=g)
+    h_ref = ref(ids).last_hidden_state
+    dh = torch.randn(h_ref.shape, generator=g)
+    h_ref.backward(dh)
+    enc.to(dev)
+    h = enc(ids.to(dev)).last_hidden_state
+    h.backward(dh.to(dev, dt))
+    torch.cuda.synchronize()
+    tol = 1e-4 if dt == torch.float32 else 5e-2
+    assert rel_err(h, h_ref) <= tol
+    gm = dict(enc.named_parameters())
+    for n, p in ref.named_parameters():
+        c = cosine(gm[n].grad, p.grad)
+        assert 1 - c <= (1e-5 if dt == torch.float32 else 2e-2), f"{n}: {c}"
+
+
+def test_bert_layers_parity_fp32(dev):
+    torch.manual_seed(0)
+    ref = R.ref_bert(num_hidden_layers=2, dropout=0.0)
+    mine = mmdx.text_encoders.BertModel.from_name("bert-base-uncased@2")
+    mine.config.hidden_dropout_prob = 0.0
+    mine.config.attention_probs_dropout_prob = 0.0
+    missing = mine.load_state_dict(ref.state_dict(), strict=False)
+    assert not missing.missing_keys and not missing.unexpected_keys, missing
+    g = torch.Generator().manual_seed(3)
+    B, Ls = 3, 40
+    ids = torch.randint(1000, 30522, (B, Ls), generator=g)
+    ids[:, 0] = 101
+    lens = torch.tensor([40, 17, 9])
+    mask = (torch.arange(Ls)[None] < lens[:, None]).long()
+    ids[mask == 0] = 0
+    ref.train()
+    h_ref = ref(input_ids=ids, attention_mask=mask).last_hidden_state
+    dh = torch.randn(h_ref.shape, generator=g) * mask[..., None]
+    h_ref.backward(dh)
+    mine.to(dev).train()
+    h = mine(ids.to(dev), mask.to(dev)).last_hidden_state
+    h.backward(dh.to(dev))
+    torch.cuda.synchronize()
+    valid = mask.bool()
+    assert rel_err(h.cpu()[valid], h_ref[valid]) <= 1e-4
+    gm = dict(mine.named_parameters())
+    for n, p in ref.named_parameters():
+        if p.grad is None:
+            assert gm[n].grad is None or gm[n].grad.abs().max() == 0, n
+            continue
+        c = cosine(gm[n].grad, p.grad)
+        assert 1 - c <= 1e-5, f"{n}: cos {c}"
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_text_encoder_transformer_bert(dev, dt):
+    torch.manual_seed(1)
+    ref = R.RefTextEncoderTransformer("bert-base-uncased", bert_layers=2, dropout=0.0)
+    mine = mmdx.TextEncoderTransformer("bert-base-uncased@2", compute_dtype=dt)
+    mine.encoder.config.hidden_dropout_prob = 0.0
+    mine.encoder.config.attention_probs_dropout_prob = 0.0
+    mine.load_state_dict(ref.state_dict())
+    tok = {"input_ids": torch.randint(1000, 30522, (2, 96)),
+           "attention_mask": torch.ones(2, 96, dtype=torch.long),
+           "token_type_ids": torch.zeros(2, 96, dtype=torch.long)}
+    tok["attention_mask"][1, 50:] = 0
+    ref.eval()
+    with torch.no_grad():
+        out_ref = ref(**tok)
+    mine.to(dev).eval()
+    with torch.no_grad():
+        out = mine(**{k: v.to(dev) for k, v in tok.items()})
+    # shape contracts of the reference (TP:898-899, TP:921)
+    assert tuple(out["embeddings"].shape) == (2, 512)
+    assert tuple(out["logits"].shape) == (2, 13)
+    tol = 1e-4 if dt == torch.float32 else 5e-2
+    assert rel_err(out["embeddings"], out_ref["embeddings"]) <= tol
+    assert rel_err(out["logits"], out_ref["logits"]) <= tol
