@@ -72,10 +72,11 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
   const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
   const int LDV = LP + PAD;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* Ks = (T*)smem_raw;                 // [LP][LDQ]
-  T* Vt = Ks + LP * LDQ;                // [HD][LDV]
-  T* Ps = Vt + HD * LDV;                // [QB][LDV]
-  T* Qs = Ps + QB * LDV;                // [QB][LDQ]
+  const int KP = max(LP * LDQ, QB * LDV);
+  T* Ks = (T*)smem_raw;                 // [LP][LDQ]; P [QB][LDV] reuses it after S = QK^T
+  T* Ps = Ks;
+  T* Vt = Ks + KP;                      // [HD][LDV]
+  T* Qs = Vt + HD * LDV;                // [QB][LDQ]
   const int q0 = blockIdx.x * QB, h = blockIdx.y, b = blockIdx.z;
   const int nth = NW * 64;
   const long row_ld = 3L * H * HD;
@@ -124,6 +125,7 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) sum[r] = 1.f / rowgroup_sum(sum[r]);
+  __syncthreads();  // every wave is done reading K: P may overwrite it
   float* prow = probs ? probs + (((long)b * H + h) * L) * L : nullptr;
 #pragma unroll
   for (int j = 0; j < MAXKT; ++j) {
@@ -172,10 +174,11 @@ __global__ void attn_bwd_q_kernel(const T* __restrict__ qkv, const float* __rest
   const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
   const int LDV = LP + PAD;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* Vs = (T*)smem_raw;                 // [LP][LDQ]   V rows (K-major for dP)
-  T* Kt = Vs + LP * LDQ;                // [HD][LDV]   K^T (for dQ)
-  T* dSs = Kt + HD * LDV;               // [QB][LDV]
-  T* dOs = dSs + QB * LDV;              // [QB][LDQ]
+  const int KP = max(LP * LDQ, QB * LDV);
+  T* Vs = (T*)smem_raw;                 // [LP][LDQ] V rows (K-major for dP); dS reuses it
+  T* dSs = Vs;                          // [QB][LDV]
+  T* Kt = Vs + KP;                      // [HD][LDV]   K^T (for dQ)
+  T* dOs = Kt + HD * LDV;               // [QB][LDQ]
   const int q0 = blockIdx.x * QB, h = blockIdx.y, b = blockIdx.z;
   const int nth = NW * 64;
   const long row_ld = 3L * H * HD;
@@ -214,6 +217,7 @@ __global__ void attn_bwd_q_kernel(const T* __restrict__ qkv, const float* __rest
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) dot[r] = rowgroup_sum(dot[r]);
+  __syncthreads();  // every wave is done reading V: dS may overwrite it
   T* dsg = dS_g + (((long)b * H + h) * L) * LP;
 #pragma unroll
   for (int j = 0; j < MAXKT; ++j) {
@@ -321,8 +325,8 @@ template <typename T>
 static size_t fwd_smem(int L) {
   constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
   const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
-  return sizeof(T) * ((size_t)LP * (HD + PAD) + (size_t)HD * (LP + PAD) +
-                      (size_t)QB * (LP + PAD) + (size_t)QB * (HD + PAD));
+  const size_t kp = std::max((size_t)LP * (HD + PAD), (size_t)QB * (LP + PAD));
+  return sizeof(T) * (kp + (size_t)HD * (LP + PAD) + (size_t)QB * (HD + PAD));
 }
 
 }  // namespace mmdx

@@ -14,15 +14,47 @@
 namespace mmdx {
 
 constexpr int LSTM_RB = 16;   // batch rows per workgroup
-constexpr int LSTM_NW = 4;    // waves per workgroup
+constexpr int LSTM_NW = 8;    // waves per workgroup
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// Fragment loads straight from global for a K-major [N][K] operand row block.
-template <typename T>
-__device__ __forceinline__ typename MfmaOp<T>::frag_t ldg_frag(const T* p) {
-  return MfmaOp<T>::ld(p);
+// acc[j] += A[16 rows][K] (LDS, row base a_row = &A[lane&15][(lane>>4)*FRAG]) x
+//           Bg^T, Bg rows = output columns (row base b_row = &Bg[col0 + lane&15][(lane>>4)*FRAG],
+//           tile j at +j*16 rows), K contiguous in global (L2-resident weights).
+// The weight stream is software-pipelined D k-steps deep (D*TILES fragments in flight).
+template <typename T, int TILES, int K, int D>
+__device__ __forceinline__ void rowblock_mfma(const T* a_row, const T* b_row, long ldb,
+                                              f32x4* acc) {
+  typedef MfmaOp<T> Op;
+  constexpr int NKS = K / Op::KS;
+  static_assert(NKS % D == 0, "pipeline depth must divide the k-steps");
+  typename Op::frag_t buf[D][TILES];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int j = 0; j < TILES; ++j) buf[d][j] = Op::ld(b_row + (long)j * 16 * ldb + d * Op::KS);
+#pragma unroll 1
+  for (int g = 0; g < NKS; g += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int ks = g + d;
+      const typename Op::frag_t af = Op::ld(a_row + ks * Op::KS);
+#pragma unroll
+      for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, buf[d][j], acc[j]);
+      if (ks + D < NKS) {
+#pragma unroll
+        for (int j = 0; j < TILES; ++j)
+          buf[d][j] = Op::ld(b_row + (long)j * 16 * ldb + (ks + D) * Op::KS);
+      }
+    }
+  }
 }
+
+template <typename T, int H> struct LstmDepth;
+template <> struct LstmDepth<bf16, 256> { static constexpr int F = 2, B = 8; };
+template <> struct LstmDepth<bf16, 128> { static constexpr int F = 4, B = 8; };
+template <> struct LstmDepth<float, 256> { static constexpr int F = 8, B = 16; };
+template <> struct LstmDepth<float, 128> { static constexpr int F = 8, B = 16; };
 
 template <typename T, int H>
 __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
@@ -32,6 +64,7 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
   constexpr int G4 = 4 * H;
   constexpr int LDH = H + Vec16<T>::N;
   constexpr int TILES = G4 / (LSTM_NW * 16);  // 16-col tiles per wave
+  constexpr int CPT = LSTM_RB * H / (LSTM_NW * 64);
   __shared__ float sg[LSTM_RB * G4];
   __shared__ __attribute__((aligned(16))) T sh[LSTM_RB * LDH];
   const int dir = blockIdx.y;
@@ -39,26 +72,19 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const T* W = whh + (long)dir * G4 * H;
   for (int i = threadIdx.x; i < LSTM_RB * LDH; i += blockDim.x) sh[i] = from_f<T>(0.f);
-  float creg[LSTM_RB * H / (LSTM_NW * 64)];
-  constexpr int CPT = LSTM_RB * H / (LSTM_NW * 64);
+  float creg[CPT];
 #pragma unroll
   for (int i = 0; i < CPT; ++i) creg[i] = 0.f;
   __syncthreads();
+  const int col0 = wid * TILES * 16;
+  const T* a_row = sh + (lane & 15) * LDH + (lane >> 4) * Op::FRAG;
+  const T* b_row = W + (long)(col0 + (lane & 15)) * H + (lane >> 4) * Op::FRAG;
   for (int s = 0; s < L; ++s) {
     const int t = dir == 0 ? s : L - 1 - s;
     f32x4 acc[TILES];
 #pragma unroll
     for (int j = 0; j < TILES; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int col0 = wid * TILES * 16;
-    const T* a_s = sh + (lane & 15) * LDH + (lane >> 4) * Op::FRAG;
-    const T* w_s = W + (long)(col0 + (lane & 15)) * H + (lane >> 4) * Op::FRAG;
-#pragma unroll 2
-    for (int k = 0; k < H; k += Op::KS) {
-      const typename Op::frag_t af = Op::ld(a_s + k);
-#pragma unroll
-      for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, ldg_frag<T>(w_s + (long)j * 16 * H + k), acc[j]);
-    }
-    // gates (+ input projection) -> LDS fp32
+    rowblock_mfma<T, TILES, H, LstmDepth<T, H>::F>(a_row, b_row, H, acc);
 #pragma unroll
     for (int j = 0; j < TILES; ++j)
 #pragma unroll
@@ -70,7 +96,6 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
         sg[row * G4 + col] = v;
       }
     __syncthreads();
-    // cell update: thread owns CPT (row, unit) pairs
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int e = threadIdx.x + i * LSTM_NW * 64;
@@ -122,6 +147,9 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
   for (int i = 0; i < CPT; ++i) dcn[i] = 0.f;
   for (int i = threadIdx.x; i < LSTM_RB * H; i += blockDim.x) sdh[i] = 0.f;
   __syncthreads();
+  const int col0 = wid * TILES * 16;
+  const T* a_row = sdg + (lane & 15) * LDG + (lane >> 4) * Op::FRAG;
+  const T* b_row = WT + (long)(col0 + (lane & 15)) * G4 + (lane >> 4) * Op::FRAG;
   for (int s = L - 1; s >= 0; --s) {
     const int t = dir == 0 ? s : L - 1 - s;
     const int tp = dir == 0 ? t - 1 : t + 1;  // previous step in forward order
@@ -165,15 +193,7 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
     f32x4 acc[TILES];
 #pragma unroll
     for (int j = 0; j < TILES; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int col0 = wid * TILES * 16;
-    const T* a_s = sdg + (lane & 15) * LDG + (lane >> 4) * Op::FRAG;
-    const T* w_s = WT + (long)(col0 + (lane & 15)) * G4 + (lane >> 4) * Op::FRAG;
-#pragma unroll 2
-    for (int k = 0; k < G4; k += Op::KS) {
-      const typename Op::frag_t af = Op::ld(a_s + k);
-#pragma unroll
-      for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, ldg_frag<T>(w_s + (long)j * 16 * G4 + k), acc[j]);
-    }
+    rowblock_mfma<T, TILES, G4, LstmDepth<T, H>::B>(a_row, b_row, G4, acc);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < TILES; ++j)
@@ -207,11 +227,8 @@ static int lstm_fwd_t(const void* xg, const void* whh, int B, int L, int H, void
   else if (H == 128)
     hipLaunchKernelGGL((lstm_fwd_kernel<T, 128>), grid, dim3(LSTM_NW * 64), 0, st,
                        (const float*)xg, (const T*)whh, B, L, (T*)hout, cs, gs);
-  else if (H == 64)
-    hipLaunchKernelGGL((lstm_fwd_kernel<T, 64>), grid, dim3(LSTM_NW * 64), 0, st,
-                       (const float*)xg, (const T*)whh, B, L, (T*)hout, cs, gs);
   else {
-    mmdx_set_error("lstm: hidden size %d unsupported (64, 128, 256)", H);
+    mmdx_set_error("lstm: hidden size %d unsupported (128, 256)", H);
     return -22;
   }
   MMDX_LAUNCH_CHECK();
@@ -241,7 +258,7 @@ extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
 extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                              const float* gates_save, const void* dh_out, int B, int L, int H,
                              void* dxg, float* dw_hh, void* ws, size_t ws_bytes, void* stream) {
-  MMDX_CHECK_ARG(H == 64 || H == 128 || H == 256, "lstm bwd: hidden size %d unsupported", H);
+  MMDX_CHECK_ARG(H == 128 || H == 256, "lstm bwd: hidden size %d unsupported", H);
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_lstm_workspace_size(dtype, B, L, H),
                  "lstm bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
@@ -263,9 +280,9 @@ extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, con
                      (const T*)whhT, (const T*)h_out, c_save, gates_save, (const T*)dh_out, B, \
                      L, (T*)dxg, (T*)hprev)
   if (dtype == BF16) {
-    if (H == 256) { LSTM_BWD(bf16, 256); } else if (H == 128) { LSTM_BWD(bf16, 128); } else { LSTM_BWD(bf16, 64); }
+    if (H == 256) { LSTM_BWD(bf16, 256); } else { LSTM_BWD(bf16, 128); }
   } else {
-    if (H == 256) { LSTM_BWD(float, 256); } else if (H == 128) { LSTM_BWD(float, 128); } else { LSTM_BWD(float, 64); }
+    if (H == 256) { LSTM_BWD(float, 256); } else { LSTM_BWD(float, 128); }
   }
 #undef LSTM_BWD
   MMDX_LAUNCH_CHECK();

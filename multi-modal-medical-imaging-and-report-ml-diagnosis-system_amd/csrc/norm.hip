@@ -28,7 +28,7 @@ static BnLayout bn_layout(long rows, int C, int vec) {
   L.ct = std::min(cv, 64);
   L.rt = BN_NT / L.ct;
   L.cgroups = (cv + L.ct - 1) / L.ct;
-  long target = std::max(1L, 1024L / L.cgroups);
+  long target = std::max(1L, 512L / L.cgroups);
   long rpb = (rows + target - 1) / target;
   rpb = std::max<long>(rpb, L.rt);
   L.rows_per_block = (rpb + L.rt - 1) / L.rt * L.rt;
@@ -98,20 +98,31 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x
 }
 
 // Merge slab partials; update running stats; emit scale/shift for the apply pass.
-__global__ void bn_finalize_kernel(const float2* __restrict__ part, int nblk, long rows, long rpb,
-                                   int C, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* running_mean,
-                                   float* running_var, float momentum, float eps,
-                                   float* save_mean, float* save_rstd, float* scale,
-                                   float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Block = 32 channels x 8 partial lanes; each lane merges every 8th slab (Chan), then the
+// 8 lane results merge in a fixed order (deterministic).
+constexpr int FIN_C = 32, FIN_P = 8;
+__global__ __launch_bounds__(FIN_C * FIN_P) void bn_finalize_kernel(
+    const float2* __restrict__ part, int nblk, long rows, long rpb, int C,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
+    float* running_var, float momentum, float eps, float* save_mean, float* save_rstd,
+    float* scale, float* shift) {
+  __shared__ float sn[FIN_P][FIN_C], sm[FIN_P][FIN_C], s2[FIN_P][FIN_C];
+  const int cl = threadIdx.x % FIN_C, pl = threadIdx.x / FIN_C;
+  const int c = blockIdx.x * FIN_C + cl;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    const long nb = min(rpb, rows - (long)b * rpb);
-    const float2 p = part[(long)b * C + c];
-    chan_merge(n, mean, m2, (float)nb, p.x, p.y);
+  if (c < C) {
+    for (int b = pl; b < nblk; b += FIN_P) {
+      const long nb = min(rpb, rows - (long)b * rpb);
+      const float2 p = part[(long)b * C + c];
+      chan_merge(n, mean, m2, (float)nb, p.x, p.y);
+    }
   }
+  sn[pl][cl] = n; sm[pl][cl] = mean; s2[pl][cl] = m2;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  n = 0.f; mean = 0.f; m2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < FIN_P; ++q) chan_merge(n, mean, m2, sn[q][cl], sm[q][cl], s2[q][cl]);
   const float var = m2 / (float)rows;
   const float rstd = rsqrtf(var + eps);
   save_mean[c] = mean;
@@ -220,18 +231,27 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
 }
 
 // coef: a[c] = gamma*rstd, b[c] = -gamma*rstd*sum_g/n, k[c] = -gamma*rstd*sum_gx/n
-__global__ void bn_bwd_finalize_kernel(const float2* __restrict__ part, int nblk, long rows,
-                                       int C, int train, const float* __restrict__ gamma,
-                                       const float* __restrict__ rstd, float* dgamma,
-                                       float* dbeta, float beta_acc, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(FIN_C * FIN_P) void bn_bwd_finalize_kernel(
+    const float2* __restrict__ part, int nblk, long rows, int C, int train,
+    const float* __restrict__ gamma, const float* __restrict__ rstd, float* dgamma,
+    float* dbeta, float beta_acc, float* coef) {
+  __shared__ float sa[FIN_P][FIN_C], sb[FIN_P][FIN_C];
+  const int cl = threadIdx.x % FIN_C, pl = threadIdx.x / FIN_C;
+  const int c = blockIdx.x * FIN_C + cl;
   float sg = 0.f, sgx = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    const float2 p = part[(long)b * C + c];
-    sg += p.x;
-    sgx += p.y;
+  if (c < C) {
+    for (int b = pl; b < nblk; b += FIN_P) {
+      const float2 p = part[(long)b * C + c];
+      sg += p.x;
+      sgx += p.y;
+    }
   }
+  sa[pl][cl] = sg; sb[pl][cl] = sgx;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  sg = 0.f; sgx = 0.f;
+#pragma unroll
+  for (int q = 0; q < FIN_P; ++q) { sg += sa[q][cl]; sgx += sb[q][cl]; }
   if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
   if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;
   const float a = (gamma ? gamma[c] : 1.f) * rstd[c];
@@ -289,7 +309,7 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* gam
   if (train) {
     hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                        (const T*)x, rows, C, L.ct, L.rows_per_block, part);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
                        (const float2*)part, L.rblocks, rows, L.rows_per_block, C, gamma, beta,
                        rm, rv, momentum, eps, smean, srstd, scale, shift);
   } else {
@@ -321,7 +341,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
                      smean, srstd, relu, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
                      (const float2*)part, L.rblocks, rows, C, train, gamma, srstd, dgamma,
                      dbeta, beta_acc, coef);
   const long nvec = rows * C / VEC;
