@@ -154,7 +154,7 @@ class StepTimer:
         return _Ctx()
 
 
-def make_step(img, txt, fus, opt, params, world, x, ids, mask, y, side):
+def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
     import mmdx
     from mmdx import optim as MO
 
@@ -169,40 +169,12 @@ def make_step(img, txt, fus, opt, params, world, x, ids, mask, y, side):
         logits = fus(z_img, z_txt)["disease_logits"]
         loss = mmdx.BCEWithLogitsLoss()(logits, y)
         loss.backward()
-        if world > 1:
-            _allreduce_grads(params, world)
+        if reducer is not None:
+            reducer.reduce()
         _, scale = MO.grad_norm(params, 1.0)
         opt.step(grad_scale=scale)
         return loss
     return step
-
-
-_BUCKETS = {}
-
-
-def _allreduce_grads(params, world):
-    """Bucketed (~64 MB) all-reduce of fp32 grads over RCCL, averaged."""
-    grads = [p.grad for p in params if p.grad is not None]
-    key = tuple(g.data_ptr() for g in grads)
-    plan = _BUCKETS.get(key)
-    if plan is None:
-        plan, cur, size = [], [], 0
-        for g in grads:
-            cur.append(g)
-            size += g.numel()
-            if size * 4 >= 64 << 20:
-                plan.append(cur)
-                cur, size = [], 0
-        if cur:
-            plan.append(cur)
-        _BUCKETS.clear()
-        _BUCKETS[key] = plan
-    for bucket in plan:
-        flat = torch._utils._flatten_dense_tensors(bucket)
-        dist.all_reduce(flat)
-        flat.mul_(1.0 / world)
-        for g, s in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
-            g.copy_(s)
 
 
 def cpu_baseline(cfg, seconds=20.0, bs=8, threads=16):
@@ -267,7 +239,9 @@ def main():
     B = cfg["batch"]
     x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
     side = torch.cuda.Stream(device=dev)
-    step = make_step(img, txt, fus, opt, params, world, x, ids, mask, y, side)
+    from mmdx.dist import GradAllReducer
+    reducer = GradAllReducer(params, world) if world > 1 else None
+    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
     timer = StepTimer()
     RN.CONV_TIMER = timer
 

@@ -73,19 +73,26 @@ static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, cons
   return 0;
 }
 
+template <typename T, class SA>
+static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
+                     hipStream_t st) {
+  DenseK<T> sb{(const T*)w, K, N, true};
+  EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr};
+  if (N <= 64)
+    return launch<T, 128, 64, KLoad<T, 128, SA>, KLoad<T, 64, DenseK<T>>>(sa, sb, epi, M, N, K,
+                                                                            1, K, st);
+  return launch<T, 128, 128, KLoad<T, 128, SA>, KLoad<T, 128, DenseK<T>>>(sa, sb, epi, M, N, K,
+                                                                            1, K, st);
+}
+
 template <typename T>
 static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
                       hipStream_t st) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
-  Im2colK<T> sa{(const T*)x, g, M};
-  DenseK<T> sb{(const T*)w, K, N, true};
-  EpiStore<T> epi{(T*)y, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr};
-  if (N <= 64)
-    return launch<T, 128, 64, KLoad<T, 128, Im2colK<T>>, KLoad<T, 64, DenseK<T>>>(
-        sa, sb, epi, M, N, K, 1, K, st);
-  return launch<T, 128, 128, KLoad<T, 128, Im2colK<T>>, KLoad<T, 128, DenseK<T>>>(
-      sa, sb, epi, M, N, K, 1, K, st);
+  if (g.C % KTile<T>::BK == 0)
+    return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st);
+  return conv_gemm<T>(Im2colK<T, false>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st);
 }
 
 template <typename T>
@@ -93,14 +100,9 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
                         float beta, hipStream_t st) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
-  DgradK<T> sa{(const T*)dy, g, M};
-  DenseK<T> sb{(const T*)w_crsk, K, N, true};
-  EpiStore<T> epi{(T*)dx, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr};
-  if (N <= 64)
-    return launch<T, 128, 64, KLoad<T, 128, DgradK<T>>, KLoad<T, 64, DenseK<T>>>(
-        sa, sb, epi, M, N, K, 1, K, st);
-  return launch<T, 128, 128, KLoad<T, 128, DgradK<T>>, KLoad<T, 128, DenseK<T>>>(
-      sa, sb, epi, M, N, K, 1, K, st);
+  if (g.K % KTile<T>::BK == 0)
+    return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
+  return conv_gemm<T>(DgradK<T, false>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
 }
 
 struct WgradPlan { int bm, bn, splits, kper; };

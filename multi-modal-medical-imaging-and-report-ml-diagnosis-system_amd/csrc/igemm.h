@@ -9,10 +9,16 @@
 // Tiling: 256 threads = 4 waves laid out WM x WN over a BM x BN block tile; each wave
 // owns (BM/WM) x (BN/WN) built from 16x16 MFMA tiles (bf16: v_mfma_f32_16x16x32_bf16,
 // f32: v_mfma_f32_16x16x4_f32 = exact f32 fmaf chain, used for the parity path).
-// Operands are staged global -> registers -> LDS (two buffers, one barrier per K tile);
-// the LDS image is always [row][k] (k contiguous, rows padded by 16 B so the 16 lanes of
-// a ds_read_b128 group hit 16 distinct 16-B slots).  Operands whose K is not the
-// contiguous global dimension ("R-major") are transposed on the LDS write.
+// Operands are staged global -> registers -> LDS (two buffers, one barrier per K tile).
+//   * K-major operands (k contiguous in global): LDS image [row][k], rows padded 16 B so
+//     a ds_read_b128 lane group touches 16 distinct 16-B slots.
+//   * R-major operands (rows contiguous in global; wgrad/Linear-dW): LDS image [k][row]
+//     written with 16-B stores as loaded; bf16 fragments come back k-contiguous through
+//     ds_read_b64_tr_b16 (hardware transpose), fp32 fragments through ds_read_b32.
+// The k decomposition of a gather (filter tap, channel block) is computed ONCE per K tile
+// in scalar registers when the channel count is a multiple of the K tile (every ResNet
+// layer but the 3-channel stem), so the per-vector address math is an add + bounds check.
+// The epilogue stages the fp32 accumulators through LDS and stores 4 outputs per lane.
 #pragma once
 #include "common.h"
 
@@ -44,34 +50,35 @@ template <typename T> struct KTile;               // K depth of one LDS stage
 template <> struct KTile<bf16> { static constexpr int BK = 64; };
 template <> struct KTile<float> { static constexpr int BK = 32; };
 
-template <typename T, int BK>
-struct LdsGeom {
-  static constexpr int VEC = Vec16<T>::N;
-  static constexpr int LDK = BK + VEC;  // +16 B row pad
-};
+// Generic per-K-tile context: just the tile origin and the split's k bound.
+struct KCtx { int k0, klim; };
 
 // --------------------------------------------------------------------------------------
-// Operand sources. Each maps (row, k) -> element pointer or nullptr (= zero).
-// K-major sources return a pointer to VEC consecutive k's; R-major ones to VEC
-// consecutive rows.  `klim` is the exclusive K bound of the current split.
+// Operand sources.  `row(r)` -> per-row state (computed once per block), `ktile(k0,klim)`
+// -> per-K-tile state (scalar, once per tile), `load(rs, kt, off)` -> one 16-B vector:
+// K-major sources: VEC consecutive k at k0+off of row rs; R-major: VEC consecutive rows
+// starting at rs, at k = k0+off.  Out-of-range elements read as zero.
 // --------------------------------------------------------------------------------------
 
-// Dense, K contiguous: element (r, k) at base[r*ld + k].  `vec` = ld and base allow
-// 16-B vector loads; otherwise (and for a vector crossing klim) elements load one by one.
+// Dense, K contiguous: element (r, k) at base[r*ld + k].  `vec` = ld and base allow 16-B
+// vector loads; otherwise (and for a vector crossing klim) elements load one by one.
 template <typename T>
 struct DenseK {
   const T* base; long ld; int R; bool vec;
   typedef const T* RowState;
+  typedef KCtx KT;
   typedef typename Vec16<T>::type V;
   __device__ RowState row(int r) const { return r < R ? base + (long)r * ld : nullptr; }
-  __device__ V load(RowState rs, int k, int klim) const {
+  __device__ KT ktile(int k0, int klim) const { return KT{k0, klim}; }
+  __device__ V load(RowState rs, const KT& kt, int off) const {
     constexpr int VEC = Vec16<T>::N;
+    const int k = kt.k0 + off;
     V v{};
-    if (!rs || k >= klim) return v;
-    if (vec && k + VEC <= klim) return *(const V*)(rs + k);
+    if (!rs || k >= kt.klim) return v;
+    if (vec && k + VEC <= kt.klim) return *(const V*)(rs + k);
 #pragma unroll
     for (int j = 0; j < VEC; ++j)
-      if (k + j < klim) v[j] = rs[k + j];
+      if (k + j < kt.klim) v[j] = rs[k + j];
     return v;
   }
 };
@@ -81,12 +88,15 @@ template <typename T>
 struct DenseR {
   const T* base; long ld; int R; bool vec;
   typedef int RowState;
+  typedef KCtx KT;
   typedef typename Vec16<T>::type V;
   __device__ RowState row(int r) const { return r < R ? r : -1; }
-  __device__ V load(RowState rs, int k, int klim) const {
+  __device__ KT ktile(int k0, int klim) const { return KT{k0, klim}; }
+  __device__ V load(RowState rs, const KT& kt, int off) const {
     constexpr int VEC = Vec16<T>::N;
+    const int k = kt.k0 + off;
     V v{};
-    if (rs < 0 || k >= klim) return v;
+    if (rs < 0 || k >= kt.klim) return v;
     const T* p = base + (long)k * ld + rs;
     if (vec && rs + VEC <= R) return *(const V*)p;
 #pragma unroll
@@ -105,66 +115,113 @@ struct ConvGeom {
 };
 
 // conv fwd A operand: rows = output pixels (n,p,q), k = (r, s, c) with c contiguous.
-template <typename T>
+// FAST: C % BK == 0, so one K tile = one filter tap and a contiguous channel block.
+template <typename T, bool FAST>
 struct Im2colK {
   const T* x; ConvGeom g; int M;
-  struct RowState { const T* img; int ih0, iw0; };
+  struct RowState { const T* base; int ih0, iw0; };  // base = &x[n, ih0, iw0, 0]
+  struct KT { int r, s, k0, klim; long off; };
+  typedef typename Vec16<T>::type V;
   __device__ RowState row(int m) const {
     RowState rs;
-    if (m >= M) { rs.img = nullptr; rs.ih0 = rs.iw0 = 0; return rs; }
+    if (m >= M) { rs.base = nullptr; rs.ih0 = rs.iw0 = 0; return rs; }
     const int pq = g.P * g.Q;
     const int n = m / pq, rem = m - n * pq;
     const int p = rem / g.Q, q = rem - p * g.Q;
-    rs.img = x + (long)n * g.H * g.W * g.C;
     rs.ih0 = p * g.sh - g.ph;
     rs.iw0 = q * g.sw - g.pw;
+    rs.base = x + (((long)n * g.H + rs.ih0) * g.W + rs.iw0) * g.C;
     return rs;
   }
-  typedef typename Vec16<T>::type V;
-  __device__ V load(const RowState& rs, int k, int klim) const {
-    const T* p = at(rs, k, klim);
-    return p ? *(const V*)p : V{};
+  __device__ KT ktile(int k0, int klim) const {
+    KT kt;
+    kt.k0 = k0; kt.klim = klim;
+    kt.r = kt.s = 0; kt.off = 0;
+    if (FAST) {
+      const int tap = k0 / g.C;
+      const int c0 = k0 - tap * g.C;
+      kt.r = tap / g.S;
+      kt.s = tap - kt.r * g.S;
+      kt.off = ((long)kt.r * g.W + kt.s) * g.C + c0;
+    }
+    return kt;
   }
-  __device__ const T* at(const RowState& rs, int k, int klim) const {
-    if (!rs.img || k >= klim) return nullptr;
-    const int tap = k / g.C, c = k - tap * g.C;
-    const int r = tap / g.S, s = tap - r * g.S;
+  __device__ V load(const RowState& rs, const KT& kt, int off) const {
+    if (!rs.base) return V{};
+    int r, s;
+    long o;
+    if (FAST) {
+      r = kt.r; s = kt.s;
+      o = kt.off + off;
+    } else {
+      const int k = kt.k0 + off;
+      if (k >= kt.klim) return V{};
+      const int tap = k / g.C, c = k - tap * g.C;
+      r = tap / g.S;
+      s = tap - r * g.S;
+      o = ((long)r * g.W + s) * g.C + c;
+    }
     const int ih = rs.ih0 + r, iw = rs.iw0 + s;
-    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return nullptr;
-    return rs.img + ((long)ih * g.W + iw) * g.C + c;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return V{};
+    return *(const V*)(rs.base + o);
   }
 };
 
 // conv dgrad A operand: rows = input pixels (n,h,w), k = (r, s, kout) with kout contiguous.
 // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+ph-r)/sh,(w+pw-s)/sw,k] * W[k,r,s,c]  (divisible taps only)
-template <typename T>
+template <typename T, bool FAST>
 struct DgradK {
   const T* dy; ConvGeom g; int M;
   struct RowState { const T* img; int h, w; };
+  struct KT { int r, s, k0, klim, kb; };
+  typedef typename Vec16<T>::type V;
   __device__ RowState row(int m) const {
     RowState rs;
     if (m >= M) { rs.img = nullptr; rs.h = rs.w = 0; return rs; }
     const int hw = g.H * g.W;
     const int n = m / hw, rem = m - n * hw;
-    rs.h = rem / g.W + g.ph;
-    rs.w = rem - (rem / g.W) * g.W + g.pw;
+    const int hh = rem / g.W;
+    rs.h = hh + g.ph;
+    rs.w = rem - hh * g.W + g.pw;
     rs.img = dy + (long)n * g.P * g.Q * g.K;
     return rs;
   }
-  typedef typename Vec16<T>::type V;
-  __device__ V load(const RowState& rs, int k, int klim) const {
-    const T* p = at(rs, k, klim);
-    return p ? *(const V*)p : V{};
+  __device__ KT ktile(int k0, int klim) const {
+    KT kt;
+    kt.k0 = k0; kt.klim = klim;
+    kt.r = kt.s = kt.kb = 0;
+    if (FAST) {
+      const int tap = k0 / g.K;
+      kt.kb = k0 - tap * g.K;
+      kt.r = tap / g.S;
+      kt.s = tap - kt.r * g.S;
+    }
+    return kt;
   }
-  __device__ const T* at(const RowState& rs, int k, int klim) const {
-    if (!rs.img || k >= klim) return nullptr;
-    const int tap = k / g.K, ko = k - tap * g.K;
-    const int r = tap / g.S, s = tap - r * g.S;
+  __device__ V load(const RowState& rs, const KT& kt, int off) const {
+    if (!rs.img) return V{};
+    int r, s, ko;
+    if (FAST) {
+      r = kt.r; s = kt.s; ko = kt.kb + off;
+    } else {
+      const int k = kt.k0 + off;
+      if (k >= kt.klim) return V{};
+      const int tap = k / g.K;
+      ko = k - tap * g.K;
+      r = tap / g.S;
+      s = tap - r * g.S;
+    }
     const int th = rs.h - r, tw = rs.w - s;
-    if (th < 0 || tw < 0) return nullptr;
-    const int p = th / g.sh, q = tw / g.sw;
-    if (p * g.sh != th || q * g.sw != tw || p >= g.P || q >= g.Q) return nullptr;
-    return rs.img + ((long)p * g.Q + q) * g.K + ko;
+    if (th < 0 || tw < 0) return V{};
+    int p, q;
+    if (g.sh == 1 && g.sw == 1) {
+      p = th; q = tw;
+    } else {
+      p = th / g.sh; q = tw / g.sw;
+      if (p * g.sh != th || q * g.sw != tw) return V{};
+    }
+    if (p >= g.P || q >= g.Q) return V{};
+    return *(const V*)(rs.img + ((long)p * g.Q + q) * g.K + ko);
   }
 };
 
@@ -173,6 +230,8 @@ template <typename T>
 struct Im2colR {
   const T* x; ConvGeom g; int Rows;
   struct RowState { int r, s, c; };
+  typedef KCtx KT;
+  typedef typename Vec16<T>::type V;
   __device__ RowState row(int row) const {
     RowState rs;
     if (row >= Rows) { rs.r = -1; rs.s = rs.c = 0; return rs; }
@@ -182,29 +241,29 @@ struct Im2colR {
     rs.s = tap - rs.r * g.S;
     return rs;
   }
-  typedef typename Vec16<T>::type V;
-  __device__ V load(const RowState& rs, int k, int klim) const {
-    const T* p = at(rs, k, klim);
-    return p ? *(const V*)p : V{};
-  }
-  __device__ const T* at(const RowState& rs, int k, int klim) const {
-    if (rs.r < 0 || k >= klim) return nullptr;
+  __device__ KT ktile(int k0, int klim) const { return KT{k0, klim}; }
+  __device__ V load(const RowState& rs, const KT& kt, int off) const {
+    const int k = kt.k0 + off;
+    if (rs.r < 0 || k >= kt.klim) return V{};
     const int pq = g.P * g.Q;
     const int n = k / pq, rem = k - n * pq;
     const int p = rem / g.Q, q = rem - p * g.Q;
     const int ih = p * g.sh - g.ph + rs.r, iw = q * g.sw - g.pw + rs.s;
-    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return nullptr;
-    return x + (((long)n * g.H + ih) * g.W + iw) * g.C + rs.c;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return V{};
+    return *(const V*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + rs.c);
   }
 };
 
 // --------------------------------------------------------------------------------------
-// Tile loaders (global -> registers -> LDS).
+// Tile loaders (global -> registers -> LDS) and MFMA fragment reads from their LDS image.
 // --------------------------------------------------------------------------------------
 template <typename T, int ROWS, int BK, class Src>
 struct KMajorLoader {
   typedef typename Vec16<T>::type V;
+  typedef Src SrcT;
   static constexpr int VEC = Vec16<T>::N;
+  static constexpr int LDK = BK + VEC;   // +16 B row pad
+  static constexpr int LDS_ELEMS = ROWS * LDK;
   static constexpr int KV = BK / VEC;    // vectors per row
   static constexpr int RPP = NT / KV;    // rows per pass
   static constexpr int CH = ROWS / RPP;  // vectors per thread
@@ -218,25 +277,36 @@ struct KMajorLoader {
     for (int i = 0; i < CH; ++i) rs[i] = s.row(row0 + r0 + i * RPP);
   }
   __device__ void fetch(const Src& s, int k0, int klim, V* regs) const {
-    const int k = k0 + kv * VEC;
+    const typename Src::KT kt = s.ktile(k0, klim);
 #pragma unroll
-    for (int i = 0; i < CH; ++i) regs[i] = s.load(rs[i], k, klim);
+    for (int i = 0; i < CH; ++i) regs[i] = s.load(rs[i], kt, kv * VEC);
   }
   __device__ void store(T* lds, const V* regs) const {
-    constexpr int LDK = LdsGeom<T, BK>::LDK;
 #pragma unroll
     for (int i = 0; i < CH; ++i) *(V*)(lds + (r0 + i * RPP) * LDK + kv * VEC) = regs[i];
+  }
+  // fragment of the 16-row MFMA tile starting at row `r16`, k-step `ks`
+  __device__ static typename MfmaOp<T>::frag_t frag(const T* lds, int r16, int ks) {
+    const int lane = threadIdx.x & 63;
+    return MfmaOp<T>::ld(lds + (r16 + (lane & 15)) * LDK + ks + (lane >> 4) * MfmaOp<T>::FRAG);
   }
 };
 
 template <typename T, int ROWS, int BK, class Src>
 struct RMajorLoader {
   typedef typename Vec16<T>::type V;
+  typedef Src SrcT;
   static constexpr int VEC = Vec16<T>::N;
   static constexpr int RV = ROWS / VEC;  // vectors per k
   static constexpr int KPP = NT / RV;    // k per pass
   static constexpr int CH = BK / KPP;
   static_assert(NT % RV == 0 && BK % KPP == 0, "tile shape");
+  // [k][row] image; each group of 8 consecutive k rows is skewed by 64 elements so the
+  // 4-row blocks that the two 16-lane groups of a ds_read_b64_tr_b16 half-wave read
+  // (k and k+8) land on different banks.
+  static constexpr int LDR = ROWS + 16;
+  static constexpr int LDS_ELEMS = BK * LDR + (BK / 8) * 64;
+  __device__ static int kaddr(int k) { return k * LDR + (k >> 3) * 64; }
   typename Src::RowState rs;
   int rv, kk0;
   __device__ void init(const Src& s, int row0) {
@@ -245,29 +315,46 @@ struct RMajorLoader {
     rs = s.row(row0 + rv * VEC);
   }
   __device__ void fetch(const Src& s, int k0, int klim, V* regs) const {
+    const typename Src::KT kt = s.ktile(k0, klim);
 #pragma unroll
-    for (int i = 0; i < CH; ++i) regs[i] = s.load(rs, k0 + kk0 + i * KPP, klim);
+    for (int i = 0; i < CH; ++i) regs[i] = s.load(rs, kt, kk0 + i * KPP);
   }
   __device__ void store(T* lds, const V* regs) const {
-    constexpr int LDK = LdsGeom<T, BK>::LDK;
 #pragma unroll
-    for (int i = 0; i < CH; ++i)
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) lds[(rv * VEC + j) * LDK + kk0 + i * KPP] = regs[i][j];
+    for (int i = 0; i < CH; ++i) *(V*)(lds + kaddr(kk0 + i * KPP) + rv * VEC) = regs[i];
+  }
+  __device__ static typename MfmaOp<T>::frag_t frag(const T* lds, int r16, int ks) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (sizeof(T) == 2) {
+      // lane 4q+p of 16-lane group g addresses row k = ks+8g+q (+4), columns 4p..4p+3 and
+      // receives column (lane&15) of the 4 rows: 8 consecutive k, as the MFMA wants.
+      const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+      const int k = ks + 8 * g + q;
+      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(lds + kaddr(k) + r16 + 4 * p));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(lds + kaddr(k + 4) + r16 + 4 * p));
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(typename MfmaOp<T>::frag_t, v);
+    } else {
+      return lds[kaddr(ks + (lane >> 4)) + r16 + (lane & 15)];
+    }
   }
 };
 
 // --------------------------------------------------------------------------------------
-// Epilogues. `apply(m, n, v)` is called per output element with the fp32 accumulator.
+// Epilogues. `apply4(m, n, v)` handles 4 consecutive columns n..n+3 of row m.
 // --------------------------------------------------------------------------------------
 template <typename OutT>
 struct EpiStore {
   OutT* C; long ldc; int M, N;
-  const float* bias;  // [N] or null
+  const float* bias;    // [N] or null
   const float* addend;  // [M][ldc] fp32 or null, added before the activation
-  int act;            // Act
-  float alpha, beta;  // C = act(alpha*acc + bias) + beta*C
-  OutT* preact;       // optional copy of alpha*acc+bias (for GELU backward), ld = ldc
+  int act;              // Act
+  float alpha, beta;    // C = act(alpha*acc + bias + addend) + beta*C
+  OutT* preact;         // optional copy of the pre-activation value, ld = ldc
   __device__ __forceinline__ void apply(int m, int n, float v) const {
     if (m >= M || n >= N) return;
     v = alpha * v;
@@ -280,6 +367,28 @@ struct EpiStore {
     if (beta != 0.f) v += beta * to_f(C[off]);
     C[off] = from_f<OutT>(v);
   }
+  __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
+    if (m >= M) return;
+    const long off = (long)m * ldc + n;
+    const bool fast = n + 4 <= N && (off & 3) == 0 && !bias && !addend && !preact &&
+                      act == ACT_NONE;
+    if (!fast) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);
+      return;
+    }
+    typedef __attribute__((ext_vector_type(4))) OutT O4;
+    O4 o;
+    if (beta != 0.f) {
+      const O4 c = *(const O4*)(C + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = from_f<OutT>(alpha * v[j] + beta * to_f(c[j]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = from_f<OutT>(alpha * v[j]);
+    }
+    *(O4*)(C + off) = o;
+  }
 };
 
 // Raw fp32 partial for split-K: ws[z][M][N].
@@ -288,6 +397,16 @@ struct EpiPartial {
   __device__ __forceinline__ void apply(int m, int n, float v) const {
     if (m >= M || n >= N) return;
     ws[((long)blockIdx.z * M + m) * N + n] = v;
+  }
+  __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
+    if (m >= M) return;
+    const long off = ((long)blockIdx.z * M + m) * N + n;
+    if (n + 4 <= N && (off & 3) == 0) {
+      *(f32x4*)(ws + off) = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);
+    }
   }
 };
 
@@ -301,13 +420,17 @@ template <typename T, int BM, int BN, int WM, int WN, class LA, class LB, class 
 __global__ __launch_bounds__(NT, 2) void igemm_kernel(typename LA::SrcT sa, typename LB::SrcT sb,
                                                       Epi epi, int M, int N, int K, int kper) {
   constexpr int BK = KTile<T>::BK;
-  constexpr int LDK = LdsGeom<T, BK>::LDK;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int A_EL = LA::LDS_ELEMS, B_EL = LB::LDS_ELEMS;
+  constexpr int OP_BYTES = 2 * (A_EL + B_EL) * (int)sizeof(T);
+  constexpr int LDC = BN + 4;
+  constexpr int EPI_BYTES = BM * LDC * 4;
+  constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
   typedef MfmaOp<T> Op;
-  __shared__ __attribute__((aligned(16))) T lds[2 * (BM + BN) * LDK];
-  T* const As = lds;                  // [2][BM][LDK]
-  T* const Bs = lds + 2 * BM * LDK;   // [2][BN][LDK]
+  __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
+  T* const As = (T*)lds_raw;          // [2][A_EL]
+  T* const Bs = As + 2 * A_EL;        // [2][B_EL]
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
@@ -338,7 +461,6 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(typename LA::SrcT sa, type
     lb.store(Bs, rb);
     __syncthreads();
   }
-  const int frow = lane & 15, fk = (lane >> 4) * Op::FRAG;
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < nt;
@@ -346,42 +468,51 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(typename LA::SrcT sa, type
       la.fetch(sa, kbeg + (t + 1) * BK, kend, ra);
       lb.fetch(sb, kbeg + (t + 1) * BK, kend, rb);
     }
-    const T* a_s = As + cur * BM * LDK + (wm * WTM + frow) * LDK + fk;
-    const T* b_s = Bs + cur * BN * LDK + (wn * WTN + frow) * LDK + fk;
+    const T* a_s = As + cur * A_EL;
+    const T* b_s = Bs + cur * B_EL;
 #pragma unroll
     for (int ks = 0; ks < BK; ks += Op::KS) {
       typename Op::frag_t af[RM], bfr[RN];
 #pragma unroll
-      for (int i = 0; i < RM; ++i) af[i] = Op::ld(a_s + i * 16 * LDK + ks);
+      for (int i = 0; i < RM; ++i) af[i] = LA::frag(a_s, wm * WTM + i * 16, ks);
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bfr[j] = Op::ld(b_s + j * 16 * LDK + ks);
+      for (int j = 0; j < RN; ++j) bfr[j] = LB::frag(b_s, wn * WTN + j * 16, ks);
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = Op::mma(af[i], bfr[j], acc[i][j]);
     }
     if (more) {
-      la.store(As + (cur ^ 1) * BM * LDK, ra);
-      lb.store(Bs + (cur ^ 1) * BN * LDK, rb);
+      la.store(As + (cur ^ 1) * A_EL, ra);
+      lb.store(Bs + (cur ^ 1) * B_EL, rb);
     }
     __syncthreads();
   }
 
-  // C/D map of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + reg.
-  const int m0 = tm * BM + wm * WTM + (lane >> 4) * 4;
-  const int n0 = tn * BN + wn * WTN + (lane & 15);
+  // Epilogue: C/D map of 16x16 MFMA (col = lane&15, row = (lane>>4)*4 + reg) -> fp32 LDS
+  // tile [BM][BN+4] -> 4 consecutive columns per lane per store.
+  float* cst = (float*)lds_raw;
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) epi.apply(m0 + i * 16 + r, n0 + j * 16, acc[i][j][r]);
+      for (int r = 0; r < 4; ++r)
+        cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 + (lane & 15)] =
+            acc[i][j][r];
+  __syncthreads();
+  constexpr int C4 = BN / 4;
+  for (int c = threadIdx.x; c < BM * C4; c += NT) {
+    const int row = c / C4, col = (c - row * C4) * 4;
+    const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
+    epi.apply4(tm * BM + row, tn * BN + col, v);
+  }
 }
 
 // Loader bundles (give the kernel template one type per operand).
 template <typename T, int ROWS, class Src>
-struct KLoad : KMajorLoader<T, ROWS, KTile<T>::BK, Src> { typedef Src SrcT; };
+struct KLoad : KMajorLoader<T, ROWS, KTile<T>::BK, Src> {};
 template <typename T, int ROWS, class Src>
-struct RLoad : RMajorLoader<T, ROWS, KTile<T>::BK, Src> { typedef Src SrcT; };
+struct RLoad : RMajorLoader<T, ROWS, KTile<T>::BK, Src> {};
 
 }  // namespace mmdx

@@ -81,7 +81,7 @@ def image_transfom_into_tensor(img) -> torch.Tensor:
     arr = np.asarray(img)
     if arr.ndim == 2:
         arr = arr[:, :, None]
-    x = torch.from_numpy(np.ascontiguousarray(arr)).permute(2, 0, 1).float().div(255.0)
+    x = torch.from_numpy(np.array(arr, copy=True)).permute(2, 0, 1).float().div(255.0)
     if x.shape[0] == 1:
         x = x.repeat(3, 1, 1)
     mean = torch.tensor(IMAGENET_MEAN).view(3, 1, 1)

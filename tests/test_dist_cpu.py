@@ -1,0 +1,49 @@
+"""CPU: the DP gradient all-reduce (mmdx.dist.GradAllReducer) over gloo, world_size 2."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mmdx
+    from mmdx.dist import GradAllReducer, shard_batch
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(s)) for s in ((300, 70), (70,), (13, 5), (4,))]
+    g = torch.Generator().manual_seed(100 + rank)
+    for p in params:
+        p.grad = torch.randn(p.shape, generator=g)
+    red = GradAllReducer(params, world, bucket_bytes=4096)
+    red.reduce()
+    out[rank] = [p.grad.clone() for p in params]
+    assert shard_batch(1024, rank, world) == (rank * 512, (rank + 1) * 512)
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_mean_gloo():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+    exp = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(100 + r)
+        exp.append([torch.randn(s, generator=g) for s in ((300, 70), (70,), (13, 5), (4,))])
+    mean = [(a + b) / 2 for a, b in zip(*exp)]
+    for r in range(world):
+        for got, want in zip(out[r], mean):
+            assert torch.allclose(got, want, atol=1e-6)

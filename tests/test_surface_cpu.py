@@ -1,0 +1,97 @@
+"""CPU: the mmdx operator surface mirrors the reference (names, kwargs, state_dict keys,
+optimizer groups, errors, preprocessing) without touching a GPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+import mmdx
+from oracle import ref_cpu as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_image_state_dict_keys(arch):
+    ref = R.RefImageEncoderCNN(arch)
+    mine = mmdx.ImageEncoderCNN(arch)
+    assert list(ref.state_dict()) == list(mine.state_dict())
+    for (k, a), (_, b) in zip(ref.state_dict().items(), mine.state_dict().items()):
+        assert a.shape == b.shape and a.dtype == b.dtype, k
+    mine.load_state_dict(ref.state_dict())  # strict round trip
+
+
+@pytest.mark.parametrize("name,ref_name", [("bert-base-uncased@2", "bert-base-uncased"),
+                                           ("embed-mean", "embed-mean"), ("bilstm", "bilstm")])
+def test_text_state_dict_keys(name, ref_name):
+    ref = R.RefTextEncoderTransformer(ref_name, bert_layers=2)
+    mine = mmdx.TextEncoderTransformer(name)
+    assert set(ref.state_dict()) == set(mine.state_dict())
+    mine.load_state_dict(ref.state_dict())
+
+
+def test_bert_full_key_set_matches_transformers():
+    from transformers import BertConfig, BertModel
+    hf = BertModel(BertConfig())
+    mine = mmdx.text_encoders.BertModel()
+    assert set(hf.state_dict()) == set(mine.state_dict())
+    assert sum(p.numel() for p in mine.parameters()) == 109482240
+
+
+def test_fusion_keys_and_forward_contract():
+    fus = mmdx.FusionTransformerModel(d_img=1024, d_txt=512, n_disease=13)
+    keys = set(fus.state_dict())
+    for k in ("fusion_mlp.0.weight", "fusion_mlp.3.weight", "disease_head.weight",
+              "cond_proj.0.weight"):
+        assert k in keys
+    assert fus.d_fuse == 1536 and fus.n_cond == 4
+
+
+def test_unsupported_backbone_raises_valueerror():
+    with pytest.raises(ValueError):
+        mmdx.ImageEncoderCNN("vgg16")
+
+
+def test_build_optimizer_groups_follow_reference():
+    m = mmdx.ImageEncoderCNN("resnet18")
+    m.freeze_backbone()
+    o1 = m.build_optimizer(phase=1, lr_head=5e-4, weight_decay=1e-2)
+    assert [g["lr"] for g in o1.param_groups] == [5e-4, 5e-4]
+    m.unfreeze_backbone()
+    o2 = m.build_optimizer(phase=2, lr_backbone=1e-4, lr_head=5e-4)
+    assert [g["lr"] for g in o2.param_groups] == [1e-4, 5e-4, 5e-4]
+    assert all(g["weight_decay"] == 1e-2 for g in o2.param_groups)
+    t = mmdx.TextEncoderTransformer("embed-mean")
+    t.unfreeze_encoder()
+    o3 = t.build_optimizer(phase=2, lr_enc=2e-5, lr_head=5e-4)
+    assert [g["lr"] for g in o3.param_groups] == [2e-5, 5e-4, 5e-4]
+    # the reference's default lr_head is the literal 54-4 (=50), kept verbatim (TP:408)
+    assert t.build_optimizer(phase=1).param_groups[0]["lr"] == 50
+
+
+def test_image_transform_matches_oracle_on_sample():
+    img = Image.open(os.path.join(HERE, "golden", "e1.jpg")).convert("RGB")
+    a = mmdx.image_transfom_into_tensor(img)
+    b = R.reference_transform(img)
+    assert a.shape == (3, 224, 224) and a.dtype == torch.float32  # TP:823-824
+    assert torch.allclose(a, b, atol=1e-6)
+    gray = img.convert("L")
+    g = mmdx.image_transfom_into_tensor(gray)
+    assert g.shape == (3, 224, 224)
+
+
+def test_tokenize_contract():
+    tok = mmdx.tokenize_patient_details(["67M, smoker; dyspnea; CHF history.",
+                                         "54F, no smoking; cough; asthma."], max_len=96)
+    assert tuple(tok["input_ids"].shape) == (2, 96)  # TP:898-899
+    assert (tok["input_ids"][:, 0] == 101).all()
+    assert tok["attention_mask"].sum(1).min() >= 2
+
+
+def test_cpu_tensors_fail_loudly():
+    m = mmdx.TextEncoderTransformer("embed-mean")
+    with pytest.raises(RuntimeError):
+        m(input_ids=torch.randint(0, 100, (1, 8)), attention_mask=torch.ones(1, 8,
+                                                                             dtype=torch.long))
