@@ -71,8 +71,12 @@ typedef struct {
  * Channel padding: desc->C may exceed the master's Cin (c_master); pad lanes are 0. */
 int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
                           const float* w_kcrs, void* w_krsc, void* w_crsk, void* stream);
+/* stat_part (optional, fp32 pairs [mmdx_conv_fwd_stat_blocks(d)][K]): per-channel
+ * (mean, M2) of each 128-row block of the output, computed from the fp32 accumulators in
+ * the GEMM epilogue — the BatchNorm batch statistics without a separate pass over y. */
+int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d);
 int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
-                  void* y, void* stream);
+                  void* y, float* stat_part, void* stream);
 /* dx = dgrad + beta * dx  (beta = 1 sums the residual-path gradient in the epilogue) */
 int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
                     const void* w_crsk, void* dx, float beta, void* stream);
@@ -90,7 +94,10 @@ int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void
  * Replaces: BatchNorm2d + ReLU (+ Bottleneck residual add) inside the resnet trunk
  * (train mode: unfreeze_backbone TP:223; eval: freeze_backbone TP:206, IP:170). */
 size_t mmdx_bn_workspace_size(long rows, int C);
+/* stat_part: optional precomputed per-block (mean, M2) pairs [stat_blocks][C] over
+ * consecutive stat_rows-row blocks (e.g. from mmdx_conv_fwd's epilogue); NULL = reduce x. */
 int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
+                const float* stat_part, int stat_blocks, long stat_rows,
                 const float* gamma, const float* beta, float* running_mean,
                 float* running_var, float momentum, float eps,
                 float* save_mean, float* save_rstd,
@@ -215,31 +222,32 @@ int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.AdamW (decoupled weight decay) over every tensor of every param group in
  * one launch (build_optimizer groups TP:238-269, TP:408-432; fusion optimiser
- * TP:1018-1023).  `table` is a DEVICE array of descriptors sorted by `off` (prefix sum of
- * numels, total = sum n).  step_dev (device fp32) is incremented by the call, so the
- * update replays inside a graph.  grad_scale (device scalar or NULL) multiplies every
- * gradient: the clip coefficient of clip_grad_norm_ (TP:1058). */
+ * TP:1018-1023).  `table` is a DEVICE array of chunk descriptors: each parameter tensor is
+ * split into chunks (host side, <= 64K elements) and each descriptor carries the chunk's
+ * p/g/m/v pointers, its length n and its group's lr/wd; one workgroup per chunk.
+ * step_dev (device fp32) is incremented by the call, so the update replays inside a
+ * graph.  grad_scale (device scalar or NULL) multiplies every gradient: the clip
+ * coefficient of clip_grad_norm_ (TP:1058). */
 typedef struct {
   float* p;
   const float* g;
   float* m;
   float* v;
   long n;
-  long off;
+  long off;   /* informational: element offset of the chunk in its tensor */
   float lr;
   float wd;
 } mmdx_adamw_tensor;
-int mmdx_adamw_multi(int ntensors, const mmdx_adamw_tensor* table, long total, float beta1,
-                     float beta2, float eps, float* step_dev, const float* grad_scale,
-                     void* stream);
+int mmdx_adamw_multi(int nchunks, const mmdx_adamw_tensor* table, float beta1, float beta2,
+                     float eps, float* step_dev, const float* grad_scale, void* stream);
 /* global L2 norm of the .g fields of `table`; scale[0] = min(1, max_norm/(norm+1e-6))
  * (torch.nn.utils.clip_grad_norm_); max_norm <= 0 gives scale 1. */
-size_t mmdx_grad_norm_workspace_size(void);
-int mmdx_grad_norm(int ntensors, const mmdx_adamw_tensor* table, long total, float max_norm,
-                   float* norm, float* scale, void* workspace, size_t ws_bytes, void* stream);
+size_t mmdx_grad_norm_workspace_size(int nchunks);
+int mmdx_grad_norm(int nchunks, const mmdx_adamw_tensor* table, float max_norm, float* norm,
+                   float* scale, void* workspace, size_t ws_bytes, void* stream);
 /* in-place g *= scale[0] over the .g fields (the mul_ of clip_grad_norm_) */
-int mmdx_scale_grads(int ntensors, const mmdx_adamw_tensor* table, long total,
-                     const float* scale, void* stream);
+int mmdx_scale_grads(int nchunks, const mmdx_adamw_tensor* table, const float* scale,
+                     void* stream);
 
 #ifdef __cplusplus
 }

@@ -42,13 +42,14 @@ SIGNATURES = {
     "mmdx_gemm": (i32, [i32, i32, i32, i32, vp, i64, i32, vp, i64, i32, vp, i64, i32, vp, vp,
                         i32, f32, f32, vp, vp, sz, vp]),
     "mmdx_conv_pack_weight": (i32, [i32, CD, i32, vp, vp, vp, vp]),
-    "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp]),
+    "mmdx_conv_fwd_stat_blocks": (i32, [CD]),
+    "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
     "mmdx_conv_wgrad_workspace_size": (sz, [i32, CD]),
     "mmdx_conv_wgrad": (i32, [i32, CD, i32, vp, vp, vp, f32, vp, sz, vp]),
     "mmdx_bn_workspace_size": (sz, [i64, i32]),
-    "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, vp, vp, vp, f32, f32, vp, vp, vp, i32, vp,
-                          vp, sz, vp]),
+    "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, i32, i64, vp, vp, vp, vp, f32, f32, vp, vp,
+                          vp, i32, vp, vp, sz, vp]),
     "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, i32, vp, vp, vp, vp, f32,
                           vp, sz, vp]),
     "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,
@@ -86,10 +87,10 @@ SIGNATURES = {
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
-    "mmdx_adamw_multi": (i32, [i32, vp, i64, f32, f32, f32, vp, vp, vp]),
-    "mmdx_grad_norm_workspace_size": (sz, []),
-    "mmdx_grad_norm": (i32, [i32, vp, i64, f32, vp, vp, vp, sz, vp]),
-    "mmdx_scale_grads": (i32, [i32, vp, i64, vp, vp]),
+    "mmdx_adamw_multi": (i32, [i32, vp, f32, f32, f32, vp, vp, vp]),
+    "mmdx_grad_norm_workspace_size": (sz, [i32]),
+    "mmdx_grad_norm": (i32, [i32, vp, f32, vp, vp, vp, sz, vp]),
+    "mmdx_scale_grads": (i32, [i32, vp, vp, vp]),
 }
 
 _lib = None

@@ -48,18 +48,19 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Cm, i
 // partial[z][k][(r*S+s)*C + c] summed over z -> dw[k][c][r][s] (c < Cm), dw = beta*dw + sum
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int K, int C,
                                     int Cm, int RS, float* __restrict__ dw, float beta) {
-  const long total = (long)K * Cm * RS;
+  // iterate in the slab's KRSC order (coalesced reads of every split), scatter to KCRS
   const long slab = (long)K * RS * C;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < slab;
        i += (long)gridDim.x * blockDim.x) {
-    const int rs = (int)(i % RS);
-    const long t = i / RS;
-    const int c = (int)(t % Cm);
-    const int k = (int)(t / Cm);
-    const long src = (long)k * RS * C + (long)rs * C + c;
+    const int c = (int)(i % C);
+    if (c >= Cm) continue;
+    const long t = i / C;
+    const int rs = (int)(t % RS);
+    const int k = (int)(t / RS);
     float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += ws[z * slab + src];
-    dw[i] = beta != 0.f ? beta * dw[i] + v : v;
+    for (int z = 0; z < splits; ++z) v += ws[z * slab + i];
+    const long o = ((long)k * Cm + c) * RS + rs;
+    dw[o] = beta != 0.f ? beta * dw[o] + v : v;
   }
 }
 
@@ -75,9 +76,10 @@ static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, cons
 
 template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
-                     hipStream_t st) {
+                     hipStream_t st, float* stats = nullptr) {
   DenseK<T> sb{(const T*)w, K, N, true};
-  EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr};
+  EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
+                  (float2*)stats};
   if (N <= 64)
     return launch<T, 128, 64, KLoad<T, 128, SA>, KLoad<T, 64, DenseK<T>>>(sa, sb, epi, M, N, K,
                                                                             1, K, st);
@@ -87,12 +89,12 @@ static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K
 
 template <typename T>
 static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
-                      hipStream_t st) {
+                      float* stats, hipStream_t st) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
   if (g.C % KTile<T>::BK == 0)
-    return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st);
-  return conv_gemm<T>(Im2colK<T, false>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st);
+    return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats);
+  return conv_gemm<T>(Im2colK<T, false>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats);
 }
 
 template <typename T>
@@ -115,8 +117,9 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   p.bn = N <= 64 ? 64 : 128;
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
   const long ktiles = (K + BK - 1) / BK;
-  long s = (1024 + tiles - 1) / tiles;
-  s = std::max(1L, std::min(s, ktiles / 2));
+  // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small)
+  long s = (512 + tiles - 1) / tiles;
+  s = std::max(1L, std::min(s, ktiles / 16));
   const long kt_per = (ktiles + s - 1) / s;
   p.kper = (int)(kt_per * BK);
   p.splits = (int)((K + p.kper - 1) / p.kper);
@@ -151,7 +154,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   else
     rc = launch<T, 64, 64, A64, B64>(sa, sb, epi, M, N, K, p.splits, p.kper, st);
   if (rc) return rc;
-  const long total = (long)g.K * cm * g.R * g.S;
+  const long total = (long)g.K * g.C * g.R * g.S;
   const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
                      p.splits, g.K, g.C, cm, g.R * g.S, dw, beta);
@@ -179,13 +182,17 @@ extern "C" int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_m
   return 0;
 }
 
+extern "C" int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d) {
+  return (int)(((long)d->N * d->P * d->Q + 127) / 128);
+}
+
 extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,
-                             const void* w, void* y, void* stream) {
+                             const void* w, void* y, float* stat_part, void* stream) {
   int rc = check_desc(d, dtype == BF16 ? 8 : 4);
   if (rc) return rc;
   MMDX_CHECK_ARG((long)d->N * d->P * d->Q < (1L << 31), "conv fwd: too many pixels");
-  if (dtype == BF16) return conv_fwd_t<bf16>(d, x, w, y, (hipStream_t)stream);
-  return conv_fwd_t<float>(d, x, w, y, (hipStream_t)stream);
+  if (dtype == BF16) return conv_fwd_t<bf16>(d, x, w, y, stat_part, (hipStream_t)stream);
+  return conv_fwd_t<float>(d, x, w, y, stat_part, (hipStream_t)stream);
 }
 
 extern "C" int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,

@@ -355,6 +355,49 @@ struct EpiStore {
   int act;              // Act
   float alpha, beta;    // C = act(alpha*acc + bias + addend) + beta*C
   OutT* preact;         // optional copy of the pre-activation value, ld = ldc
+  float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [tiles_m][N]
+  // Per-column (mean, M2) over this tile's valid rows, from the fp32 accumulators staged in
+  // LDS (cst [BM][LDC]) — the BatchNorm statistics of a conv output without re-reading it.
+  // Two passes (mean, then squared deviations) over NT/BN row slices, merged with Chan.
+  template <int BM, int BN, int LDC>
+  __device__ __forceinline__ void tile_stats(const float* cst, float* red, int tm, int tn) const {
+    if (!stats) return;
+    constexpr int PARTS = NT / BN, RPP = BM / PARTS;
+    const int col = threadIdx.x % BN, part = threadIdx.x / BN;
+    const int rows_valid = min(BM, M - tm * BM);
+    const int r0 = part * RPP, r1 = min(r0 + RPP, rows_valid);
+    // one pass, shifted by the slice's first value (no cancellation within <= 64 rows)
+    const float x0 = r1 > r0 ? cst[r0 * LDC + col] : 0.f;
+    float s = 0.f, q = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const float d = cst[r * LDC + col] - x0;
+      s += d;
+      q += d * d;
+    }
+    const float cnt = (float)max(r1 - r0, 0);
+    const float mean = cnt > 0.f ? x0 + s / cnt : 0.f;
+    const float m2 = cnt > 0.f ? fmaxf(q - s * s / cnt, 0.f) : 0.f;
+    red[threadIdx.x * 3 + 0] = cnt;
+    red[threadIdx.x * 3 + 1] = mean;
+    red[threadIdx.x * 3 + 2] = m2;
+    __syncthreads();
+    const int n = tn * BN + col;
+    if (part == 0 && n < N) {
+      float nn = 0.f, mu = 0.f, mm = 0.f;
+#pragma unroll
+      for (int q = 0; q < PARTS; ++q) {
+        const int o = (q * BN + col) * 3;
+        const float nb = red[o], mb = red[o + 1], m2b = red[o + 2];
+        if (nb == 0.f) continue;
+        if (nn == 0.f) { nn = nb; mu = mb; mm = m2b; continue; }
+        const float tot = nn + nb, d = mb - mu, f = nb / tot;
+        mu += d * f;
+        mm += m2b + d * d * nn * f;
+        nn = tot;
+      }
+      stats[(long)tm * N + n] = make_float2(mu, mm);
+    }
+  }
   __device__ __forceinline__ void apply(int m, int n, float v) const {
     if (m >= M || n >= N) return;
     v = alpha * v;
@@ -408,6 +451,8 @@ struct EpiPartial {
       for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);
     }
   }
+  template <int BM, int BN, int LDC>
+  __device__ __forceinline__ void tile_stats(const float*, float*, int, int) const {}
 };
 
 // Bijective XCD-aware remap: blocks that share an A panel land on one XCD's L2.
@@ -425,7 +470,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(typename LA::SrcT sa, type
   constexpr int A_EL = LA::LDS_ELEMS, B_EL = LB::LDS_ELEMS;
   constexpr int OP_BYTES = 2 * (A_EL + B_EL) * (int)sizeof(T);
   constexpr int LDC = BN + 4;
-  constexpr int EPI_BYTES = BM * LDC * 4;
+  constexpr int EPI_BYTES = BM * LDC * 4 + NT * 3 * 4;  // staged tile + stats scratch
   constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
   typedef MfmaOp<T> Op;
   __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
@@ -501,6 +546,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(typename LA::SrcT sa, type
         cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 + (lane & 15)] =
             acc[i][j][r];
   __syncthreads();
+  epi.template tile_stats<BM, BN, LDC>(cst, cst + BM * LDC, tm, tn);
   constexpr int C4 = BN / 4;
   for (int c = threadIdx.x; c < BM * C4; c += NT) {
     const int row = c / C4, col = (c - row * C4) * 4;

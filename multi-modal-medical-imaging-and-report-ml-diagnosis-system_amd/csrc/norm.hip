@@ -98,9 +98,10 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x
 }
 
 // Merge slab partials; update running stats; emit scale/shift for the apply pass.
-// Block = 32 channels x 8 partial lanes; each lane merges every 8th slab (Chan), then the
-// 8 lane results merge in a fixed order (deterministic).
-constexpr int FIN_C = 32, FIN_P = 8;
+// Block = 8 channels x 32 partial lanes; each lane merges every 32nd slab (Chan), then the
+// 32 lane results merge in a fixed order (deterministic).  Conv-epilogue statistics give
+// one slab per 128 output rows (thousands per layer), so the slab dimension is the wide one.
+constexpr int FIN_C = 8, FIN_P = 32;
 __global__ __launch_bounds__(FIN_C * FIN_P) void bn_finalize_kernel(
     const float2* __restrict__ part, int nblk, long rows, long rpb, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
@@ -151,28 +152,51 @@ __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma,
   shift[c] = (beta ? beta[c] : 0.f) - rm[c] * g * rstd;
 }
 
+// Row-tiled channel-vector layout for the elementwise BN passes: a 256-thread block covers
+// `tpr` 16-B channel vectors of `rpi` rows; each thread keeps its channels' coefficients in
+// registers for every row it visits (no per-element index math or coefficient reloads).
+struct RowTile { int cv, tpr, rpi; };
+__host__ __device__ inline RowTile row_tile(int C, int vec) {
+  RowTile t;
+  t.cv = C / vec;
+  t.tpr = t.cv < 256 ? t.cv : 256;
+  t.rpi = 256 / t.tpr;
+  return t;
+}
+
 // y = act(x*scale[c] + shift[c] (+ res))
 template <typename T>
-__global__ void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, long nvec,
-                                int C, const float* __restrict__ scale,
-                                const float* __restrict__ shift, int relu, T* __restrict__ y) {
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
+                                                       const T* __restrict__ res, long rows,
+                                                       int C, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int relu,
+                                                       T* __restrict__ y) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
-       i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * VEC) % C);
-    const V v = ((const V*)x)[i];
-    V r{};
-    if (res) r = ((const V*)res)[i];
-    V o;
+  const RowTile rt = row_tile(C, VEC);
+  const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
+  for (int j = j0; j < rt.cv; j += rt.tpr) {
+    float sc[VEC], sh[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      float f = to_f(v[j]) * scale[c0 + j] + shift[c0 + j];
-      if (res) f += to_f(r[j]);
-      if (relu) f = fmaxf(f, 0.f);
-      o[j] = from_f<T>(f);
+    for (int e = 0; e < VEC; ++e) {
+      sc[e] = scale[j * VEC + e];
+      sh[e] = shift[j * VEC + e];
     }
-    ((V*)y)[i] = o;
+    for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
+      const long i = r * rt.cv + j;
+      const V v = ((const V*)x)[i];
+      V rr{};
+      if (res) rr = ((const V*)res)[i];
+      V o;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float f = to_f(v[e]) * sc[e] + sh[e];
+        if (res) f += to_f(rr[e]);
+        if (relu) f = fmaxf(f, 0.f);
+        o[e] = from_f<T>(f);
+      }
+      ((V*)y)[i] = o;
+    }
   }
 }
 
@@ -260,68 +284,90 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void bn_bwd_finalize_kernel(
   coef[2 * C + c] = train ? -a * sgx / (float)rows : 0.f;
 }
 
+// dx = a*g + b + k*xhat  ==  a*g + (b - k*mean*rstd) + (k*rstd)*x,  g = dy*relu'(y)
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ y,
-                                    const T* __restrict__ dy, long nvec, int C,
-                                    const float* __restrict__ mean,
-                                    const float* __restrict__ rstd,
-                                    const float* __restrict__ coef, int relu, T* __restrict__ dx,
-                                    T* __restrict__ dres) {
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ coef, int relu, T* __restrict__ dx, T* __restrict__ dres) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
-       i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * VEC) % C);
-    const V vx = ((const V*)x)[i];
-    const V vd = ((const V*)dy)[i];
-    V vy{};
-    if (relu) vy = ((const V*)y)[i];
-    V o, og;
+  const RowTile rt = row_tile(C, VEC);
+  const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
+  for (int j = j0; j < rt.cv; j += rt.tpr) {
+    float ca[VEC], cb[VEC], ck[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      const int c = c0 + j;
-      float g = to_f(vd[j]);
-      if (relu && !(to_f(vy[j]) > 0.f)) g = 0.f;
-      const float xh = (to_f(vx[j]) - mean[c]) * rstd[c];
-      o[j] = from_f<T>(coef[c] * g + coef[C + c] + coef[2 * C + c] * xh);
-      og[j] = from_f<T>(g);
+    for (int e = 0; e < VEC; ++e) {
+      const int c = j * VEC + e;
+      const float k = coef[2 * C + c] * rstd[c];
+      ca[e] = coef[c];
+      cb[e] = coef[C + c] - k * mean[c];
+      ck[e] = k;
     }
-    ((V*)dx)[i] = o;
-    if (dres) ((V*)dres)[i] = og;
+    for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
+      const long i = r * rt.cv + j;
+      const V vx = ((const V*)x)[i];
+      const V vd = ((const V*)dy)[i];
+      V vy{};
+      if (relu) vy = ((const V*)y)[i];
+      V o, og;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = to_f(vd[e]);
+        if (relu && !(to_f(vy[e]) > 0.f)) g = 0.f;
+        o[e] = from_f<T>(ca[e] * g + cb[e] + ck[e] * to_f(vx[e]));
+        og[e] = from_f<T>(g);
+      }
+      ((V*)dx)[i] = o;
+      if (dres) ((V*)dres)[i] = og;
+    }
   }
 }
 
-static int grid_for(long nvec) { return (int)std::min<long>((nvec + 255) / 256, 8192); }
+static int grid_rows(long rows, int C, int vec) {
+  const RowTile rt = row_tile(C, vec);
+  return (int)std::max<long>(1, std::min<long>((rows + rt.rpi - 1) / rt.rpi, 4096));
+}
 
 template <typename T>
-static int bn_fwd_t(int train, const void* x, long rows, int C, const float* gamma,
-                    const float* beta, float* rm, float* rv, float momentum, float eps,
-                    float* smean, float* srstd, const void* res, int relu, void* y, void* ws,
-                    size_t ws_bytes, hipStream_t st) {
+static int bn_fwd_t(int train, const void* x, long rows, int C, const float* stat_part,
+                    int stat_blocks, long stat_rows, const float* gamma, const float* beta,
+                    float* rm, float* rv, float momentum, float eps, float* smean, float* srstd,
+                    const void* res, int relu, void* y, void* ws, size_t ws_bytes,
+                    hipStream_t st) {
   constexpr int VEC = Vec16<T>::N;
   MMDX_CHECK_ARG(C % VEC == 0, "bn: C=%d must be a multiple of %d", C, VEC);
   const BnLayout L = bn_layout(rows, C, VEC);
-  const size_t need = (size_t)L.rblocks * C * sizeof(float2) + 2 * (size_t)C * sizeof(float);
+  const bool ext = train && stat_part;
+  const size_t part_bytes = ext ? 0 : (size_t)L.rblocks * C * sizeof(float2);
+  const size_t need = part_bytes + 2 * (size_t)C * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "bn fwd: workspace %zu < %zu", ws_bytes, need);
   float2* part = (float2*)ws;
-  float* scale = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
+  float* scale = (float*)((char*)ws + part_bytes);
   float* shift = scale + C;
   if (train) {
-    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
-                       (const T*)x, rows, C, L.ct, L.rows_per_block, part);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
-                       (const float2*)part, L.rblocks, rows, L.rows_per_block, C, gamma, beta,
-                       rm, rv, momentum, eps, smean, srstd, scale, shift);
+    int nblk = L.rblocks;
+    long rpb = L.rows_per_block;
+    if (ext) {
+      part = (float2*)stat_part;
+      nblk = stat_blocks;
+      rpb = stat_rows;
+    } else {
+      hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
+                         (const T*)x, rows, C, L.ct, L.rows_per_block, part);
+    }
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0,
+                       st, (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv,
+                       momentum, eps, smean, srstd, scale, shift);
   } else {
     MMDX_CHECK_ARG(rm && rv, "bn eval: running stats required");
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma,
                        beta, (const float*)rm, (const float*)rv, eps, smean, srstd, scale,
                        shift);
   }
-  const long nvec = rows * C / VEC;
-  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st, (const T*)x,
-                     (const T*)res, nvec, C, (const float*)scale, (const float*)shift, relu,
-                     (T*)y);
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
+                     (const T*)x, (const T*)res, rows, C, (const float*)scale,
+                     (const float*)shift, relu, (T*)y);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -344,9 +390,8 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
                      (const float2*)part, L.rblocks, rows, C, train, gamma, srstd, dgamma,
                      dbeta, beta_acc, coef);
-  const long nvec = rows * C / VEC;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st,
-                     (const T*)x, (const T*)y, (const T*)dy, nvec, C, smean, srstd,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
+                     (const T*)x, (const T*)y, (const T*)dy, rows, C, smean, srstd,
                      (const float*)coef, relu, (T*)dx, (T*)dres);
   MMDX_LAUNCH_CHECK();
   return 0;
@@ -528,17 +573,23 @@ extern "C" size_t mmdx_bn_workspace_size(long rows, int C) {
 }
 
 extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
+                           const float* stat_part, int stat_blocks, long stat_rows,
                            const float* gamma, const float* beta, float* running_mean,
                            float* running_var, float momentum, float eps, float* save_mean,
                            float* save_rstd, const void* residual, int relu, void* y,
                            void* ws, size_t ws_bytes, void* stream) {
   MMDX_CHECK_ARG(rows > 0 && C > 0 && save_mean && save_rstd, "bn fwd: bad args");
+  MMDX_CHECK_ARG(!stat_part || (stat_blocks > 0 && stat_rows > 0 &&
+                                (long)stat_blocks * stat_rows >= rows),
+                 "bn fwd: bad precomputed statistics layout");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == BF16)
-    return bn_fwd_t<bf16>(train, x, rows, C, gamma, beta, running_mean, running_var, momentum,
-                          eps, save_mean, save_rstd, residual, relu, y, ws, ws_bytes, st);
-  return bn_fwd_t<float>(train, x, rows, C, gamma, beta, running_mean, running_var, momentum,
-                         eps, save_mean, save_rstd, residual, relu, y, ws, ws_bytes, st);
+    return bn_fwd_t<bf16>(train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma, beta,
+                          running_mean, running_var, momentum, eps, save_mean, save_rstd,
+                          residual, relu, y, ws, ws_bytes, st);
+  return bn_fwd_t<float>(train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma, beta,
+                         running_mean, running_var, momentum, eps, save_mean, save_rstd,
+                         residual, relu, y, ws, ws_bytes, st);
 }
 
 extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,

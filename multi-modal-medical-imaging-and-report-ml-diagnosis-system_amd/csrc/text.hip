@@ -113,15 +113,22 @@ __global__ void masked_mean_fwd_kernel(const T* __restrict__ h, const int64_t* _
 template <typename T>
 __global__ void masked_mean_bwd_kernel(const T* __restrict__ dout, const int64_t* __restrict__ m,
                                        int B, int L, int D, T* __restrict__ dh) {
-  const long total = (long)B * L * D;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int d = (int)(i % D);
-    const long bl = i / D;
-    const int b = (int)(bl / L);
+  // one block per sample: token count once, then every (l, d) of the sample
+  __shared__ float s_inv;
+  const int b = blockIdx.x;
+  if (threadIdx.x < 64) {
     float cnt = 0.f;
-    for (int l = 0; l < L; ++l) cnt += (float)m[(long)b * L + l];
-    dh[i] = from_f<T>(to_f(dout[(long)b * D + d]) * (float)m[bl] / fmaxf(cnt, 1e-6f));
+    for (int l = threadIdx.x; l < L; l += 64) cnt += (float)m[(long)b * L + l];
+    cnt = wave_sum(cnt);
+    if (threadIdx.x == 0) s_inv = 1.f / fmaxf(cnt, 1e-6f);
+  }
+  __syncthreads();
+  const float inv = s_inv;
+  for (int l = 0; l < L; ++l) {
+    const float w = (float)m[(long)b * L + l] * inv;
+    T* row = dh + ((long)b * L + l) * D;
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      row[d] = from_f<T>(to_f(dout[(long)b * D + d]) * w);
   }
 }
 
@@ -240,8 +247,7 @@ extern "C" int mmdx_masked_mean_fwd(int dtype, const void* h, const int64_t* mas
 
 extern "C" int mmdx_masked_mean_bwd(int dtype, const void* dout, const int64_t* mask, int B,
                                     int L, int D, void* dh, void* stream) {
-  DISPATCH_T(dtype, hipLaunchKernelGGL(masked_mean_bwd_kernel<T>,
-                                       dim3(grid_for((long)B * L * D)), dim3(256), 0,
+  DISPATCH_T(dtype, hipLaunchKernelGGL(masked_mean_bwd_kernel<T>, dim3(B), dim3(256), 0,
                                        (hipStream_t)stream, (const T*)dout, mask, B, L, D,
                                        (T*)dh));
   MMDX_LAUNCH_CHECK();

@@ -18,23 +18,34 @@ from . import _lib as L
 from ._lib import call, ptr, stream
 
 
+CHUNK = 1 << 16  # elements per workgroup descriptor
+
+
 class _Table:
-    """Device copy of an mmdx_adamw_tensor[] (kept alive with its pinned host source)."""
+    """Device copy of an mmdx_adamw_tensor[] chunk table (kept alive with its pinned host
+    source): every tensor split into <= CHUNK-element pieces, one workgroup each."""
 
     def __init__(self, entries, device):
-        n = len(entries)
+        descs = []
+        total = 0
+        for p, g, m, v, lr, wd in entries:
+            n = p.numel()
+            pp, gp, mp, vp = ptr(p), ptr(g), ptr(m), ptr(v)
+            for o in range(0, n, CHUNK):
+                c = min(CHUNK, n - o)
+                b = 4 * o
+                descs.append((pp + b, gp + b, mp + b, vp + b, c, o, float(lr), float(wd)))
+            total += n
+        n = len(descs)
         arr = (L.AdamWTensor * n)()
-        off = 0
-        for i, (p, g, m, v, lr, wd) in enumerate(entries):
-            arr[i] = L.AdamWTensor(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), off, float(lr),
-                                   float(wd))
-            off += p.numel()
+        for i, d in enumerate(descs):
+            arr[i] = L.AdamWTensor(*d)
         nbytes = C.sizeof(arr)
         self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         C.memmove(self.host.data_ptr(), C.addressof(arr), nbytes)
         self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
         self.dev.copy_(self.host, non_blocking=True)
-        self.n, self.total = n, off
+        self.n, self.total = n, total
 
 
 def _table_for(cache: dict, entries, device):
@@ -96,8 +107,8 @@ class AdamW(torch.optim.Optimizer):
             for e in entries:
                 self.state[e[0]]["step"] = self._step_t
         tab = _table_for(self._tables, entries, dev)
-        call("mmdx_adamw_multi", tab.n, ptr(tab.dev), tab.total, float(b1), float(b2),
-             float(eps), ptr(self._step_t), ptr(grad_scale), stream())
+        call("mmdx_adamw_multi", tab.n, ptr(tab.dev), float(b1), float(b2), float(eps),
+             ptr(self._step_t), ptr(grad_scale), stream())
         return loss
 
 
@@ -118,12 +129,12 @@ def grad_norm(parameters, max_norm: float = 0.0, apply: bool = False):
     tab = _table_for(_clip_cache, entries, dev)
     norm = torch.empty((), dtype=torch.float32, device=dev)
     scale = torch.empty((), dtype=torch.float32, device=dev)
-    ws_n = L.lib().mmdx_grad_norm_workspace_size()
+    ws_n = L.lib().mmdx_grad_norm_workspace_size(tab.n)
     ws = L.workspace(ws_n, dev)
-    call("mmdx_grad_norm", tab.n, ptr(tab.dev), tab.total, float(max_norm), ptr(norm),
-         ptr(scale), ptr(ws), ws_n, stream())
+    call("mmdx_grad_norm", tab.n, ptr(tab.dev), float(max_norm), ptr(norm), ptr(scale),
+         ptr(ws), ws_n, stream())
     if apply:
-        call("mmdx_scale_grads", tab.n, ptr(tab.dev), tab.total, ptr(scale), stream())
+        call("mmdx_scale_grads", tab.n, ptr(tab.dev), ptr(scale), stream())
     return norm, scale
 
 

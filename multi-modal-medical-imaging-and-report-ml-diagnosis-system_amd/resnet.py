@@ -203,17 +203,20 @@ def _conv_bn(conv, bn, relu, x, N, H, W, C, cm, res, train, keep):
     st = stream()
     call("mmdx_conv_pack_weight", dt, d, cm, ptr(conv.weight), ptr(wk), ptr(wc), st)
     y = torch.empty((N, d.P, d.Q, K), dtype=T, device=dev)
+    nstat = L.lib().mmdx_conv_fwd_stat_blocks(d) if train else 0
+    # BN batch statistics come out of the conv epilogue (per 128-row block, fp32 accums)
+    part = torch.empty((nstat, K, 2), dtype=torch.float32, device=dev) if train else None
     with CONV_TIMER("fwd"):
-        call("mmdx_conv_fwd", dt, d, ptr(x), ptr(wk), ptr(y), st)
+        call("mmdx_conv_fwd", dt, d, ptr(x), ptr(wk), ptr(y), ptr(part), st)
     out = torch.empty_like(y)
     rows = N * d.P * d.Q
     mean = torch.empty(K, dtype=torch.float32, device=dev)
     rstd = torch.empty(K, dtype=torch.float32, device=dev)
     ws_n = L.lib().mmdx_bn_workspace_size(rows, K)
     ws = L.workspace(ws_n, dev)
-    call("mmdx_bn_fwd", dt, int(train), ptr(y), rows, K, ptr(bn.weight), ptr(bn.bias),
-         ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum), float(bn.eps),
-         ptr(mean), ptr(rstd), ptr(res), int(relu), ptr(out), ptr(ws), ws_n, st)
+    call("mmdx_bn_fwd", dt, int(train), ptr(y), rows, K, ptr(part), nstat, 128, ptr(bn.weight),
+         ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum),
+         float(bn.eps), ptr(mean), ptr(rstd), ptr(res), int(relu), ptr(out), ptr(ws), ws_n, st)
     if train:
         bn.num_batches_tracked.add_(1)
     u = None

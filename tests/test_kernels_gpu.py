@@ -108,8 +108,20 @@ def test_conv_fwd_dgrad_wgrad(dev, dt, cfg):
            L.stream())
     xd = _nhwc(x, cp, dt).to(dev)
     y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
-    L.call("mmdx_conv_fwd", dc, d, xd.data_ptr(), wk.data_ptr(), y.data_ptr(), L.stream())
+    nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
+    part = torch.empty(nst, K, 2, device=dev)
+    L.call("mmdx_conv_fwd", dc, d, xd.data_ptr(), wk.data_ptr(), y.data_ptr(), part.data_ptr(),
+           L.stream())
     _close(y.permute(0, 3, 1, 2), yr.detach(), dt, f"fwd {cfg}")
+    # epilogue BatchNorm statistics: merge the per-128-row (mean, M2) blocks on the host
+    M = N * P * Q
+    cnt = torch.tensor([min(128, M - 128 * b) for b in range(nst)], dtype=torch.float64)
+    pm, p2 = part[..., 0].double().cpu(), part[..., 1].double().cpu()
+    mean = (pm * cnt[:, None]).sum(0) / M
+    m2 = (p2 + cnt[:, None] * (pm - mean) ** 2).sum(0)
+    yref = yr.detach().double()
+    _close(mean, yref.mean((0, 2, 3)), torch.float32 if dt == torch.float32 else dt, "stat mean")
+    _close(m2 / M, yref.var((0, 2, 3), unbiased=False), dt, "stat var")
     dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, dt)
     dx = torch.empty(N, H, W, cp, dtype=dt, device=dev)
     L.call("mmdx_conv_dgrad", dc, d, dyd.data_ptr(), wc.data_ptr(), dx.data_ptr(), 0.0,
@@ -162,7 +174,8 @@ def test_batchnorm(dev, dt, train, res, relu):
     ws_n = L.lib().mmdx_bn_workspace_size(rows, C)
     ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
     dc = L.dtype_code(dt)
-    L.call("mmdx_bn_fwd", dc, train, xd.data_ptr(), rows, C, gam.data_ptr(), bet.data_ptr(),
+    L.call("mmdx_bn_fwd", dc, train, xd.data_ptr(), rows, C, None, 0, 0, gam.data_ptr(),
+           bet.data_ptr(),
            rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, mean.data_ptr(), rstd.data_ptr(),
            rd.data_ptr() if res else None, int(relu), y.data_ptr(), ws.data_ptr(), ws_n,
            L.stream())
