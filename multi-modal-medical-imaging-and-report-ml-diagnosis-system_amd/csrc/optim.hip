@@ -45,8 +45,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(const mmdx_adamw_tensor* __r
       f32x4 p = ((f32x4*)d.p)[i], m = ((f32x4*)d.m)[i], v = ((f32x4*)d.v)[i];
       const f32x4 g = ((const f32x4*)d.g)[i];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        adamw_elem(p[j], g[j] * gs, m[j], v[j], decay, beta1, beta2, step_size, bc2s, eps);
+      for (int j = 0; j < 4; ++j) {
+        float pj = p[j], mj = m[j], vj = v[j];
+        adamw_elem(pj, g[j] * gs, mj, vj, decay, beta1, beta2, step_size, bc2s, eps);
+        p[j] = pj;
+        m[j] = mj;
+        v[j] = vj;
+      }
       ((f32x4*)d.p)[i] = p;
       ((f32x4*)d.m)[i] = m;
       ((f32x4*)d.v)[i] = v;
