@@ -222,9 +222,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MMDX_DIST_BACKEND=gloo rehearses the DP path with several ranks on one GPU (RCCL
+    # refuses two ranks per device); the real multi-GPU run uses "nccl" (= RCCL over xGMI).
+    backend = os.environ.get("MMDX_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     dtype = torch.bfloat16
 

@@ -1,0 +1,86 @@
+"""DP parity on one GPU (SURVEY §8(e) check (i)): two ranks (gloo, both on cuda:0), each
+with half of the batch, all-reduce-averaged gradients == single-process full-batch
+gradients, with BatchNorm in eval mode so per-replica statistics do not enter.
+fp32 path; tolerance 1 - cosine <= 1e-6 per tensor (reduction order only)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    sys.path.insert(0, HERE)
+    from parity_util import build_pair
+    _, img, txt, fus = build_pair("resnet18", "embed-mean")
+    return img, txt, fus
+
+
+def _grads(img, txt, fus, x, ids, mask, y):
+    import mmdx
+    from parity_util import mmdx_forward
+    dev = torch.device("cuda", 0)
+    for m in (img, txt, fus):
+        m.to(dev)
+    img.unfreeze_backbone()
+    img.backbone.eval()  # BN on running statistics: no per-replica batch statistics
+    txt.train()
+    fus.train()
+    logits = mmdx_forward(img, txt, fus, x.to(dev), ids.to(dev), mask.to(dev))
+    mmdx.BCEWithLogitsLoss()(logits, y.to(dev)).backward()
+    return [(n, p) for mod in (img, txt, fus) for n, p in mod.named_parameters()]
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx.dist import GradAllReducer, shard_batch
+    from parity_util import synth_batch
+    x, ids, mask, y = synth_batch(4, 16, hw=64)
+    a, b = shard_batch(4, rank, world)
+    img, txt, fus = _model()
+    named = _grads(img, txt, fus, x[a:b], ids[a:b], mask[a:b], y[a:b])
+    GradAllReducer([p for _, p in named], world).reduce()
+    torch.cuda.synchronize()
+    out[rank] = {n: p.grad.detach().cpu() for n, p in named if p.grad is not None}
+    dist.destroy_process_group()
+
+
+def test_dp_two_ranks_match_full_batch(dev):
+    from parity_util import cosine, synth_batch
+    x, ids, mask, y = synth_batch(4, 16, hw=64)
+    img, txt, fus = _model()
+    ref = {n: p.grad.detach().cpu() for n, p in _grads(img, txt, fus, x, ids, mask, y)
+           if p.grad is not None}
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    for r in range(2):
+        g = out[r]
+        assert set(g) == set(ref)
+        for n in ref:
+            c = cosine(g[n], ref[n])
+            assert 1 - c <= 1e-6, f"rank {r} {n}: 1-cos {1 - c:.2e}"
