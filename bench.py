@@ -73,6 +73,59 @@ def conv_flops_per_sample(trunk, hw=224):
     return 2 * fwd, 2 * dgrad, 2 * fwd
 
 
+def conv_bytes_per_step(trunk, B, hw=224, elt=2):
+    """Algorithmic HBM bytes of one step's conv launches (each tensor touched once):
+    fwd x + w + y; dgrad dy + w + dx (+dx read when accumulating a residual branch, ignored);
+    wgrad x + dy + dw (fp32).  Returns (total bytes, number of conv launches)."""
+    tot = 0
+    n = 0
+    H = W = hw
+
+    def one(c, H, W, dgrad):
+        k, s, p = c.kernel_size, c.stride, c.padding
+        P = (H + 2 * p - k) // s + 1
+        Q = (W + 2 * p - k) // s + 1
+        x = B * H * W * c.in_channels * elt
+        y = B * P * Q * c.out_channels * elt
+        w = c.out_channels * c.in_channels * k * k
+        b = (x + w * elt + y) + (x + w * 4 + y)  # fwd, wgrad
+        if dgrad:
+            b += y + w * elt + x
+        return b, (3 if dgrad else 2), P, Q
+
+    b, m, H, W = one(trunk[0], H, W, False)
+    tot += b
+    n += m
+    H, W = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    for layer in list(trunk)[4:8]:
+        for blk in layer:
+            Hb, Wb = H, W
+            for c, _, _ in blk.units():
+                b, m, H, W = one(c, H, W, True)
+                tot += b
+                n += m
+            if blk.downsample is not None:
+                b, m, _, _ = one(blk.downsample[0], Hb, Wb, True)
+                tot += b
+                n += m
+    return tot, n
+
+
+def load_traffic(cfg_name, batch):
+    """HBM bytes per conv launch from the committed PMC pass (tools/pmc_traffic.py), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_conv_traffic.json"))):
+        try:
+            with open(f) as fh:
+                t = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if t.get("config") == cfg_name and t.get("per_gpu_batch") == batch:
+            best = (t["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def model_flops_per_sample(cfg, img, txt):
     f, d, w = conv_flops_per_sample(img.backbone)
     conv_train = f + d + w
@@ -280,6 +333,8 @@ def main():
     value = samples / el
     ms_step = el / args.steps * 1e3
     conv_tf = conv_flops * B * args.steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    alg_bytes, alg_launches = conv_bytes_per_step(img.backbone, B)
+    traffic = load_traffic(args.config, B)
     result = {
         "metric": "multimodal samples/sec (train fwd+bwd) at 1/2/4/8 MI355X; MFMA util %",
         "value": round(value, 2),
@@ -309,7 +364,10 @@ def main():
             "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(conv_tf / PEAK_BF16_TFLOPS, 4),
-            "traffic": None,
+            "traffic": traffic[0] if traffic else None,
+            "traffic_unit": "HBM bytes per conv launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)",
+            "traffic_source": traffic[1] if traffic else None,
+            "algorithmic_bytes_per_launch": round(alg_bytes / alg_launches),
             "conv_ms_per_step": round(conv_ms / args.steps, 3),
             "conv_launches_per_step": n_conv // max(1, args.steps),
             "conv_gflop_per_sample": round(conv_flops / 1e9, 3),

@@ -1,0 +1,110 @@
+"""Drop-in for the hot-path part of backend/ml/pipelines/inference_pipeline.py ("IP").
+
+`inference(model_bundle, image_pil, patient_details, device=None, gen_kwargs=None)` keeps
+IP:151's signature, argument checks and return dict; the two towers and the disease head
+run on the mmdx kernels.  The report text needs the T5 head (outside the hot path,
+SURVEY §8(f)): it is generated only when the bundle's fusion model carries one, otherwise
+`report_text` is "" and `report_generated` is False.
+
+`load_model_bundle(path)` rebuilds the bundle from a local `model_bundle.pt` written by the
+reference's save path (TP:773-796: keys cfg, fusion_state, image_state, text_state,
+t5_tokenizer_name, bert_tokenizer_name, version), with the same key validation and errors
+as the Django loader (VW:196-204).  Loading uses weights_only=True.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .training_pipeline import (DISEASES, FusionTransformerModel, ImageEncoderCNN,
+                                TextEncoderTransformer, image_transfom_into_tensor,
+                                tokenize_patient_details)
+
+BUNDLE_KEYS = ("cfg", "fusion_state", "image_state", "text_state", "t5_tokenizer_name",
+               "bert_tokenizer_name", "version")
+
+
+def load_model_bundle(path: str, device="cuda", compute_dtype=torch.float32):
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"Model bundle not found at {path}")  # VW:178
+    raw = torch.load(path, map_location="cpu", weights_only=True)
+    missing = [k for k in BUNDLE_KEYS if k not in raw]
+    if missing:
+        raise ValueError(f"Bundle missing keys: {missing}")  # VW:204
+    cfg = raw["cfg"] or {}
+    fc = cfg.get("fusion", {}) or {}
+    d_img = fc.get("d_img", 1024)
+    d_txt = fc.get("d_txt", 512)  # VW:209 fallback (IP:74 uses 1024)
+    fusion = FusionTransformerModel(d_img=d_img, d_txt=d_txt,
+                                    d_fuse_hidden=fc.get("d_fuse_hidden", 1024),
+                                    n_disease=fc.get("n_disease", 13),
+                                    n_cond_tokens=fc.get("n_cond_tokens", 4))
+    fs = {k: v for k, v in raw["fusion_state"].items() if not k.startswith("report_model.")}
+    fusion.load_state_dict(fs, strict=False)
+    backbone = ((cfg.get("image_encoder", {}) or {}).get("backbone")) or "resnet50"
+    image = ImageEncoderCNN(backbone, d_img, compute_dtype=compute_dtype)
+    image.load_state_dict(raw["image_state"])
+    text = TextEncoderTransformer(raw["bert_tokenizer_name"] or "bert-base-uncased", d_txt,
+                                  compute_dtype=compute_dtype)
+    text.load_state_dict(raw["text_state"])
+    arts = cfg.get("artifacts", {}) or {}
+    return {
+        "cfg": cfg,
+        "version": raw["version"],
+        "fusion_model": fusion.to(device).eval(),
+        "image_encoder": image.to(device).eval(),
+        "text_encoder": text.to(device).eval(),
+        "t5_tok": None,
+        "bert_tok": None,
+        "class_names": arts.get("class_names", DISEASES),
+        "thresholds": arts.get("thresholds", [0.5] * len(DISEASES)),
+    }
+
+
+@torch.no_grad()
+def inference(model_bundle, image_pil, patient_details, device=None, gen_kwargs=None):
+    if isinstance(device, torch.device):  # IP:152-159
+        dev = device
+    elif isinstance(device, str):
+        dev = torch.device(device)
+    elif device is None:
+        dev = torch.device("cuda")
+    else:
+        raise TypeError(f"'device' must be str|torch.device|None, got {type(device)}")
+    fusion = model_bundle["fusion_model"].to(dev)
+    class_names = model_bundle["class_names"]
+    thresholds = torch.tensor(model_bundle["thresholds"], device=dev)
+    image_encoder = model_bundle["image_encoder"].to(dev).eval()
+    text_encoder = model_bundle["text_encoder"].to(dev).eval()
+
+    x_img = image_transfom_into_tensor(image_pil).unsqueeze(0).to(dev)  # IP:174
+    tok = tokenize_patient_details([patient_details], max_len=96)       # IP:175
+    tok = {k: v.to(dev) for k, v in tok.items()}
+    z_img = image_encoder(x_img)["embeddings"]                          # IP:179
+    z_txt = text_encoder(**tok)["embeddings"]                           # IP:180
+    out = fusion(z_img=z_img, z_txt=z_txt, report_labels=None)          # IP:183
+    logits = out["disease_logits"]
+    probs = torch.sigmoid(logits.float())[0]                            # IP:185
+    vector = (probs >= thresholds).int().tolist()                       # IP:186
+
+    report = ""
+    generated = False
+    if getattr(fusion, "report_model", None) is not None and model_bundle.get("t5_tok"):
+        t5_tok = model_bundle["t5_tok"]
+        gen = dict(max_new_tokens=180, min_new_tokens=150, num_beams=4, no_repeat_ngram_size=3,
+                   length_penalty=1.1, early_stopping=True, eos_token_id=t5_tok.eos_token_id,
+                   pad_token_id=t5_tok.pad_token_id)  # IP:190
+        if gen_kwargs:
+            gen.update(gen_kwargs)
+        fusion.report_model.to(dev)
+        ids = fusion.generate(z_img, z_txt, **gen)
+        report = t5_tok.batch_decode(ids, skip_special_tokens=True)[0]
+        generated = True
+    return {
+        "report_text": report,
+        "disease_probs": {class_names[j]: float(probs[j]) for j in range(len(class_names))},
+        "disease_vector": vector,
+        "model_version": model_bundle["version"],
+        "report_generated": generated,
+    }

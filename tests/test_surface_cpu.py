@@ -95,3 +95,45 @@ def test_cpu_tensors_fail_loudly():
     with pytest.raises(RuntimeError):
         m(input_ids=torch.randint(0, 100, (1, 8)), attention_mask=torch.ones(1, 8,
                                                                              dtype=torch.long))
+
+
+def _write_bundle(path, drop=None):
+    torch.manual_seed(0)
+    img = mmdx.ImageEncoderCNN("resnet18", 1024, 13)
+    txt = mmdx.TextEncoderTransformer("embed-mean", 512, 13)
+    fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13)
+    bundle = {"cfg": {"fusion": {"d_img": 1024, "d_txt": 512},
+                      "image_encoder": {"backbone": "resnet18"}},
+              "fusion_state": fus.state_dict(), "image_state": img.state_dict(),
+              "text_state": txt.state_dict(), "t5_tokenizer_name": "t5-small",
+              "bert_tokenizer_name": "embed-mean", "version": 999}  # TP:783-791
+    if drop:
+        bundle.pop(drop)
+    torch.save(bundle, path)
+    return img, txt, fus
+
+
+def test_bundle_roundtrip_and_key_validation(tmp_path):
+    from mmdx.inference_pipeline import load_model_bundle
+    with pytest.raises(FileNotFoundError):  # VW:178
+        load_model_bundle(str(tmp_path / "missing.pt"), device="cpu")
+    bad = tmp_path / "bad.pt"
+    _write_bundle(bad, drop="text_state")
+    with pytest.raises(ValueError):  # VW:204
+        load_model_bundle(str(bad), device="cpu")
+    good = tmp_path / "model_bundle.pt"
+    img, txt, fus = _write_bundle(good)
+    b = load_model_bundle(str(good), device="cpu")
+    assert b["version"] == 999 and len(b["class_names"]) == 13 and b["thresholds"] == [0.5] * 13
+    for mine, ref in ((b["image_encoder"], img), (b["text_encoder"], txt),
+                      (b["fusion_model"], fus)):
+        sd, rsd = mine.state_dict(), ref.state_dict()
+        assert set(sd) == set(rsd)
+        for k in rsd:
+            assert torch.equal(sd[k], rsd[k]), k
+
+
+def test_inference_rejects_bad_device_type():
+    from mmdx.inference_pipeline import inference
+    with pytest.raises(TypeError):  # IP:159
+        inference({}, None, "x", device=3)

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: parity tests, headline bench, kernel-trace profile, two PMC passes.
+# usage (from the repo root, under gpurun): bash tools/gpu_round.sh <tag> <phases> [steps]
+#   phases: comma list of tests,bench,prof,pmc
+# Every GPU step has its own time limit; the script stops at the first step that faults,
+# aborts or times out (rc > 1), so nothing else touches the GPU after a failure.
+set -u
+tag=${1:-r01}; phases=${2:-tests,bench}; steps=${3:-20}
+has() { [[ ",$phases," == *",$1,"* ]]; }
+R=$(pwd)
+mkdir -p gpurun_out
+step() {  # step <label> <timeout> <cmd...>
+  local label=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "$R/gpurun_out/$label.log" 2>&1
+  local rc=$?
+  echo "[$label] rc=$rc"; tail -4 "$R/gpurun_out/$label.log"
+  [ $rc -le 1 ] || exit $rc
+}
+export TMPDIR=/tmp
+has tests && step tests 900 python -m pytest tests -m gpu -q -x
+has bench && step bench 600 python bench.py --steps "$steps" --warmup 5
+cd /tmp
+has prof && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$tag" \
+  -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
+has pmc && step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmcf_$tag" \
+  -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+has pmc && step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmcw_$tag" \
+  -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+cd "$R"
+has pmc && python tools/pmc_traffic.py "gpurun_out/pmcf_$tag" "gpurun_out/pmcw_$tag" --config c4 \
+  --batch 128 -o "gpurun_out/${tag}_conv_traffic.json"
+exit 0

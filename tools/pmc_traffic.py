@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""HBM traffic of the conv kernels from two rocprofv3 PMC passes.
+
+    rocprofv3 --pmc FETCH_SIZE  --output-format csv -d <dir_f> -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE  --output-format csv -d <dir_w> -- python3 bench.py ...
+    python tools/pmc_traffic.py <dir_f> <dir_w> --config c4 --batch 128 -o profiles/r01_conv_traffic.json
+
+FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the bytes of a wide
+coalesced read (MI355X_MICROARCH.md §HBM), so  bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
+Conv kernels are the implicit-GEMM instantiations whose operand source is an im2col/dgrad
+gather (`Im2colK`, `DgradK`, `Im2colR`) plus the split-K `wgrad_reduce_kernel`; the per-launch
+figure divides by the number of conv igemm dispatches (one per conv call, as bench.py's
+`roofline.achieved` counts them).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+
+CONV = re.compile(r"igemm_kernel.*(Im2col|Dgrad)")
+REDUCE = re.compile(r"wgrad_reduce_kernel")
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    per_dispatch = {}
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != counter:
+                continue
+            key = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+            name = row.get("Kernel_Name", "")
+            v = float(row["Counter_Value"])
+            prev = per_dispatch.get(key, (name, 0.0))
+            per_dispatch[key] = (name, prev[1] + v)
+    conv_kb = red_kb = 0.0
+    n_conv = 0
+    for name, v in per_dispatch.values():
+        if CONV.search(name):
+            conv_kb += v
+            n_conv += 1
+        elif REDUCE.search(name):
+            red_kb += v
+    return conv_kb, red_kb, n_conv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("-o", "--out", required=True)
+    a = ap.parse_args()
+    f_conv, f_red, n_f = load(a.fetch_dir, "FETCH_SIZE")
+    w_conv, w_red, n_w = load(a.write_dir, "WRITE_SIZE")
+    if n_f == 0 or n_f != n_w:
+        raise SystemExit(f"conv dispatch counts differ or zero: {n_f} vs {n_w}")
+    fetch = 2.0 * (f_conv + f_red) * 1024 / n_f
+    write = (w_conv + w_red) * 1024 / n_w
+    out = {
+        "config": a.config, "per_gpu_batch": a.batch, "launches": n_f,
+        "kernels": "igemm_kernel (Im2colK/DgradK/Im2colR sources) + wgrad_reduce_kernel",
+        "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
+        "traffic_bytes_per_launch": round(fetch + write),
+        "reduce_share": round(2 * f_red * 1024 / n_f + w_red * 1024 / n_w) / max(1.0, fetch + write),
+        "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
+    }
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
