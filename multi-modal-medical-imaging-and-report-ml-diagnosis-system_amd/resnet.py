@@ -174,7 +174,8 @@ class ResNetTrunk(nn.Sequential):
     def forward(self, x):
         params = self.engine_params()
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-        feats = _TrunkFn.apply(x, self, need_grad, *params)
+        # torch convs accept any strides (e.g. a channels-last view from a PIL transform)
+        feats = _TrunkFn.apply(x.contiguous(), self, need_grad, *params)
         return feats.view(feats.shape[0], feats.shape[1], 1, 1)
 
 

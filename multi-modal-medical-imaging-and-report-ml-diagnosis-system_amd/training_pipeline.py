@@ -86,7 +86,7 @@ def image_transfom_into_tensor(img) -> torch.Tensor:
         x = x.repeat(3, 1, 1)
     mean = torch.tensor(IMAGENET_MEAN).view(3, 1, 1)
     std = torch.tensor(IMAGENET_STD).view(3, 1, 1)
-    return (x - mean) / std
+    return ((x - mean) / std).contiguous()
 
 
 # =====================================================================================

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, headline bench, kernel-trace profile, two PMC passes.
 # usage (from the repo root, under gpurun): bash tools/gpu_round.sh <tag> <phases> [steps]
-#   phases: comma list of tests,bench,prof,pmc
+#   phases: comma list of tests,bench,convb,prof,pmc
 # Every GPU step has its own time limit; the script stops at the first step that faults,
 # aborts or times out (rc > 1), so nothing else touches the GPU after a failure.
 set -u
@@ -19,6 +19,7 @@ step() {  # step <label> <timeout> <cmd...>
 export TMPDIR=/tmp
 has tests && step tests 900 python -m pytest tests -m gpu -q -x
 has bench && step bench 600 python bench.py --steps "$steps" --warmup 5
+has convb && step convb 600 python tools/conv_bench.py --json "gpurun_out/${tag}_conv_shapes.json"
 cd /tmp
 has prof && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$tag" \
   -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
