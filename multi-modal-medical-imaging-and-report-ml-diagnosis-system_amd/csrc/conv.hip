@@ -97,10 +97,48 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
   return conv_gemm<T>(Im2colK<T, false>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats);
 }
 
+// Strided dgrad as sh*sw phase GEMMs (see DgradPhaseK); phases no tap reaches are written
+// as zeros (beta = 0) or left untouched (beta != 0).
+template <typename T>
+static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_crsk, void* dx,
+                             float beta, hipStream_t st) {
+  for (int a = 0; a < g.sh; ++a) {
+    for (int b = 0; b < g.sw; ++b) {
+      PhaseGeom ph;
+      ph.Hp = g.H > a ? (g.H - a + g.sh - 1) / g.sh : 0;
+      ph.Wp = g.W > b ? (g.W - b + g.sw - 1) / g.sw : 0;
+      if (ph.Hp == 0 || ph.Wp == 0) continue;
+      ph.r0 = (a + g.ph) % g.sh;
+      ph.s0 = (b + g.pw) % g.sw;
+      ph.ntr = ph.r0 < g.R ? (g.R - 1 - ph.r0) / g.sh + 1 : 0;
+      ph.nts = ph.s0 < g.S ? (g.S - 1 - ph.s0) / g.sw + 1 : 0;
+      ph.dr0 = (a + g.ph - ph.r0) / g.sh;
+      ph.ds0 = (b + g.pw - ph.s0) / g.sw;
+      const int K = ph.ntr * ph.nts * g.K;
+      if (K == 0 && beta != 0.f) continue;
+      const int M = g.N * ph.Hp * ph.Wp, N = g.C;
+      DgradPhaseK<T> sa{(const T*)dy, g, ph, M};
+      PhaseTapK<T> sb{(const T*)w_crsk, (long)g.R * g.S * g.K, g.C, g.K, g.S, g.sh, g.sw, ph};
+      EpiPhase<T> epi{(T*)dx, g.C, M, N, beta, ph.Hp, ph.Wp, g.H, g.W, a, b, g.sh, g.sw};
+      int rc;
+      if (N <= 64)
+        rc = launch<T, 128, 64, KLoad<T, 128, DgradPhaseK<T>>, KLoad<T, 64, PhaseTapK<T>>>(
+            sa, sb, epi, M, N, K, 1, K, st);
+      else
+        rc = launch<T, 128, 128, KLoad<T, 128, DgradPhaseK<T>>, KLoad<T, 128, PhaseTapK<T>>>(
+            sa, sb, epi, M, N, K, 1, K, st);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
 template <typename T>
 static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
                         float beta, hipStream_t st) {
   const ConvGeom g = geom(d);
+  if ((g.sh > 1 || g.sw > 1) && g.K % KTile<T>::BK == 0)
+    return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
   if (g.K % KTile<T>::BK == 0)
     return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);

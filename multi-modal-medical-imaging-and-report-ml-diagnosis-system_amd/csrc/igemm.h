@@ -225,6 +225,74 @@ struct DgradK {
   }
 };
 
+// Strided-conv dgrad, one output phase (a, b) = (h mod sh, w mod sw) at a time: only the
+// taps r = r0 + sh*u (s = s0 + sw*v) reach those pixels, so the GEMM runs over
+// M = N*Hp*Wp phase pixels and K = ntaps*Kout instead of all H*W pixels and all R*S taps
+// (a stride-2 3x3 conv does 1/4 of the MACs of the dense dgrad; a stride-2 1x1 only the
+// (0,0) phase).  Requires Kout % BK == 0 (each K tile = one tap, contiguous channel block).
+struct PhaseGeom {
+  int Hp, Wp;      // phase grid
+  int r0, s0;      // first tap of the phase
+  int ntr, nts;    // taps in r / s
+  int dr0, ds0;    // (a + ph - r0) / sh, (b + pw - s0) / sw
+};
+
+template <typename T>
+struct DgradPhaseK {
+  const T* dy; ConvGeom g; PhaseGeom ph; int M;
+  struct RowState { const T* img; int i, j; };
+  struct KT { int dr, ds, kb, k0, klim; };
+  typedef typename Vec16<T>::type V;
+  __device__ RowState row(int m) const {
+    RowState rs;
+    if (m >= M) { rs.img = nullptr; rs.i = rs.j = 0; return rs; }
+    const int hw = ph.Hp * ph.Wp;
+    const int n = m / hw, rem = m - n * hw;
+    rs.i = rem / ph.Wp;
+    rs.j = rem - rs.i * ph.Wp;
+    rs.img = dy + (long)n * g.P * g.Q * g.K;
+    return rs;
+  }
+  __device__ KT ktile(int k0, int klim) const {
+    KT kt;
+    const int t = k0 / g.K;
+    kt.kb = k0 - t * g.K;
+    const int u = t / ph.nts, v = t - u * ph.nts;
+    kt.dr = ph.dr0 - u;  // tap r0 + sh*u moves the source row up by u
+    kt.ds = ph.ds0 - v;
+    kt.k0 = k0; kt.klim = klim;
+    return kt;
+  }
+  __device__ V load(const RowState& rs, const KT& kt, int off) const {
+    if (!rs.img || kt.k0 + off >= kt.klim) return V{};
+    const int p = rs.i + kt.dr, q = rs.j + kt.ds;
+    if ((unsigned)p >= (unsigned)g.P || (unsigned)q >= (unsigned)g.Q) return V{};
+    return *(const V*)(rs.img + ((long)p * g.Q + q) * g.K + kt.kb + off);
+  }
+};
+
+// B operand of the phase dgrad: packed CRSK weights, k = (phase tap t, kout).
+template <typename T>
+struct PhaseTapK {
+  const T* w; long ld; int C, K, S, sh, sw; PhaseGeom ph;  // w[c][r][s][k], ld = R*S*K
+  typedef const T* RowState;
+  struct KT { long kg; int k0, klim; };
+  typedef typename Vec16<T>::type V;
+  __device__ RowState row(int c) const { return c < C ? w + (long)c * ld : nullptr; }
+  __device__ KT ktile(int k0, int klim) const {
+    KT kt;
+    const int t = k0 / K, kb = k0 - t * K;
+    const int u = t / ph.nts, v = t - u * ph.nts;
+    kt.kg = ((long)(ph.r0 + sh * u) * S + (ph.s0 + sw * v)) * K + kb;
+    kt.k0 = k0; kt.klim = klim;
+    return kt;
+  }
+  __device__ V load(RowState rs, const KT& kt, int off) const {
+    if (!rs || kt.k0 + off >= kt.klim) return V{};
+    return *(const V*)(rs + kt.kg + off);
+  }
+};
+
 // conv wgrad B operand: rows = (r, s, c) with c contiguous, k = output pixel (n,p,q).
 template <typename T>
 struct Im2colR {
@@ -450,6 +518,48 @@ struct EpiPartial {
 #pragma unroll
       for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);
     }
+  }
+  template <int BM, int BN, int LDC>
+  __device__ __forceinline__ void tile_stats(const float*, float*, int, int) const {}
+};
+
+// Phase-dgrad epilogue: GEMM row m = phase pixel (n, i, j) -> dX pixel (n, a+sh*i, b+sw*j);
+// dX = acc + beta*dX (beta = 1 accumulates a residual branch's gradient).
+template <typename OutT>
+struct EpiPhase {
+  OutT* C; int ldc, M, N; float beta;
+  int Hp, Wp, H, W, a, b, sh, sw;
+  __device__ __forceinline__ long pix(int m) const {
+    const int hw = Hp * Wp;
+    const int n = m / hw, rem = m - n * hw;
+    const int i = rem / Wp, j = rem - i * Wp;
+    return ((long)n * H + a + sh * i) * W + b + sw * j;
+  }
+  __device__ __forceinline__ void apply(int m, int n, float v) const {
+    if (m >= M || n >= N) return;
+    const long off = pix(m) * ldc + n;
+    if (beta != 0.f) v += beta * to_f(C[off]);
+    C[off] = from_f<OutT>(v);
+  }
+  __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
+    if (m >= M) return;
+    if (n + 4 > N) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);
+      return;
+    }
+    const long off = pix(m) * ldc + n;
+    typedef __attribute__((ext_vector_type(4))) OutT O4;
+    O4 o;
+    if (beta != 0.f) {
+      const O4 c = *(const O4*)(C + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = from_f<OutT>(v[j] + beta * to_f(c[j]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = from_f<OutT>(v[j]);
+    }
+    *(O4*)(C + off) = o;
   }
   template <int BM, int BN, int LDC>
   __device__ __forceinline__ void tile_stats(const float*, float*, int, int) const {}
