@@ -74,12 +74,51 @@ static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, cons
   return 0;
 }
 
+template <int BM, int BN, class OA, class OB, class Epi>
+static int launch_dma_ops(const typename OA::SrcT& sa, const typename OB::SrcT& sb,
+                          const Epi& epi, int M, int N, int K, int splits, int kper,
+                          hipStream_t st) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi>), dim3(nwg, 1, splits), dim3(NT), 0,
+                     st, sa, sb, epi, M, N, K, kper);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+// both operands k-major
+template <int BM, int BN, class SA, class SB, class Epi>
+static int launch_dma(const SA& sa, const SB& sb, const Epi& epi, int M, int N, int K,
+                      int splits, int kper, hipStream_t st) {
+  return launch_dma_ops<BM, BN, DmaK<BM, SA>, DmaK<BN, SB>>(sa, sb, epi, M, N, K, splits, kper,
+                                                            st);
+}
+
+// bf16 gathers whose K tiles are whole filter taps (C % 64 == 0) take the LDS-DMA kernel
+template <class S> struct DmaOk { static constexpr bool value = false; };
+template <> struct DmaOk<Im2colK<bf16, true>> { static constexpr bool value = true; };
+template <> struct DmaOk<DgradK<bf16, true>> { static constexpr bool value = true; };
+
+// buffer-DMA preconditions: 32-bit byte offsets (< 2 GiB) and a 32-bit tap-validity mask
+static bool dma_geom_ok(const ConvGeom& g, bool dgrad) {
+  const long xb = (long)g.N * g.H * g.W * g.C * 2, yb = (long)g.N * g.P * g.Q * g.K * 2;
+  if (xb >= (1L << 31) || yb >= (1L << 31) || g.R * g.S > 32) return false;
+  return !dgrad || (g.sh == 1 && g.sw == 1);
+}
+
 template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
-                     hipStream_t st, float* stats = nullptr) {
+                     hipStream_t st, float* stats = nullptr, bool dma_ok = false) {
   DenseK<T> sb{(const T*)w, K, N, true};
   EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
                   (float2*)stats};
+  if constexpr (DmaOk<SA>::value) {
+    if (dma_ok) {
+    // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
+    const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+    if (N <= 64 || tiles128 < 384) return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
+    return launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
+    }
+  }
   if (N <= 64)
     return launch<T, 128, 64, KLoad<T, 128, SA>, KLoad<T, 64, DenseK<T>>>(sa, sb, epi, M, N, K,
                                                                             1, K, st);
@@ -93,7 +132,8 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
   if (g.C % KTile<T>::BK == 0)
-    return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats);
+    return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
+                        dma_geom_ok(g, false));
   return conv_gemm<T>(Im2colK<T, false>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats);
 }
 
@@ -120,13 +160,25 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       DgradPhaseK<T> sa{(const T*)dy, g, ph, M};
       PhaseTapK<T> sb{(const T*)w_crsk, (long)g.R * g.S * g.K, g.C, g.K, g.S, g.sh, g.sw, ph};
       EpiPhase<T> epi{(T*)dx, g.C, M, N, beta, ph.Hp, ph.Wp, g.H, g.W, a, b, g.sh, g.sw};
-      int rc;
-      if (N <= 64)
+      int rc = -1;
+      if constexpr (sizeof(T) == 2) {
+        if (dma_geom_ok(g, false)) {
+          const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+          if (N <= 64 || tiles128 < 384)
+            rc = launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
+          else
+            rc = launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
+          if (rc) return rc;
+          continue;
+        }
+      }
+      if (N <= 64) {
         rc = launch<T, 128, 64, KLoad<T, 128, DgradPhaseK<T>>, KLoad<T, 64, PhaseTapK<T>>>(
             sa, sb, epi, M, N, K, 1, K, st);
-      else
+      } else {
         rc = launch<T, 128, 128, KLoad<T, 128, DgradPhaseK<T>>, KLoad<T, 128, PhaseTapK<T>>>(
             sa, sb, epi, M, N, K, 1, K, st);
+      }
       if (rc) return rc;
     }
   }
@@ -141,7 +193,8 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
     return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
   if (g.K % KTile<T>::BK == 0)
-    return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
+    return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
+                        nullptr, dma_geom_ok(g, true));
   return conv_gemm<T>(DgradK<T, false>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
 }
 
@@ -175,10 +228,34 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   const int K = (int)Kl;
   const size_t need = (size_t)p.splits * M * N * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu", ws_bytes, need);
-  DenseR<T> sa{(const T*)dy, g.K, M, true};
-  Im2colR<T> sb{(const T*)x, g, N};
+  DenseR<T> sa{(const T*)dy, g.K, M, true, K};
+  Im2colR<T> sb{(const T*)x, g, N, 1.f / (float)(g.P * g.Q), 1.f / (float)g.Q};
   EpiPartial epi{(float*)ws, M, N};
   int rc;
+  if constexpr (sizeof(T) == 2) {
+   if (dma_geom_ok(g, false) && K < (1 << 23)) {
+    // LDS-DMA wgrad: both operands R-major (M = Kout and N = R*S*C are multiples of 8)
+    if (p.bm == 128 && p.bn == 128)
+      rc = launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, Im2colR<T>>>(
+          sa, sb, epi, M, N, K, p.splits, p.kper, st);
+    else if (p.bm == 128)
+      rc = launch_dma_ops<128, 64, DmaR<128, DenseR<T>>, DmaR<64, Im2colR<T>>>(
+          sa, sb, epi, M, N, K, p.splits, p.kper, st);
+    else if (p.bn == 128)
+      rc = launch_dma_ops<64, 128, DmaR<64, DenseR<T>>, DmaR<128, Im2colR<T>>>(
+          sa, sb, epi, M, N, K, p.splits, p.kper, st);
+    else
+      rc = launch_dma_ops<64, 64, DmaR<64, DenseR<T>>, DmaR<64, Im2colR<T>>>(
+          sa, sb, epi, M, N, K, p.splits, p.kper, st);
+    if (rc) return rc;
+    const long total = (long)g.K * g.C * g.R * g.S;
+    const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
+                       p.splits, g.K, g.C, cm, g.R * g.S, dw, beta);
+    MMDX_LAUNCH_CHECK();
+    return 0;
+   }
+  }
   typedef RLoad<T, 128, DenseR<T>> A128;
   typedef RLoad<T, 64, DenseR<T>> A64;
   typedef RLoad<T, 128, Im2colR<T>> B128;

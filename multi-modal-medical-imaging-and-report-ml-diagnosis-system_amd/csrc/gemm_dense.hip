@@ -53,7 +53,24 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
   const bool vb = ldb % VEC == 0 && ((uintptr_t)B & 15) == 0;
   SA sa{(const T*)A, lda, M, va};
   SB sb{(const T*)B, ldb, N, vb};
+  if constexpr (!AK) sa.vrows = K;  // R-major: k runs over the leading-dimension rows
+  if constexpr (!BKm) sb.vrows = K;
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if constexpr (std::is_same<T, bf16>::value) {
+    // LDS-DMA kernel when every 16-B chunk is either wholly inside or wholly outside the
+    // operand: k-major needs K % 8 == 0, row-major needs its row count % 8 == 0
+    const long abytes = (long)(AK ? M : K) * lda * 2, bbytes = (long)(BKm ? N : K) * ldb * 2;
+    const bool oka = va && (AK ? K % 8 == 0 : M % 8 == 0) && abytes < (1L << 31);
+    const bool okb = vb && (BKm ? K % 8 == 0 : N % 8 == 0) && bbytes < (1L << 31);
+    if (oka && okb) {
+      typedef typename std::conditional<AK, DmaK<BM, SA>, DmaR<BM, SA>>::type OA;
+      typedef typename std::conditional<BKm, DmaK<BN, SB>, DmaR<BN, SB>>::type OB;
+      hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi>), dim3(nwg, 1, splits),
+                         dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+      MMDX_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((igemm_kernel<T, BM, BN, 2, 2, LA, LB, Epi>), dim3(nwg, 1, splits),
                      dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
   MMDX_LAUNCH_CHECK();

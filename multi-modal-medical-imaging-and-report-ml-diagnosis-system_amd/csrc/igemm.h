@@ -81,12 +81,25 @@ struct DenseK {
       if (k + j < kt.klim) v[j] = rs[k + j];
     return v;
   }
+  // LDS-DMA path (vec, K tiles whole): address of the VEC elements at k0+off, or null = zeros
+  __device__ const T* ptr(RowState rs, const KT& kt, int off) const {
+    return rs && kt.k0 + off < kt.klim ? rs + kt.k0 + off : nullptr;
+  }
+  // buffer-DMA interface: byte offset of (row, k = 0) and tap-validity bits; per K tile the
+  // uniform byte offset and tap index.  Offsets are relative to bbase().
+  __device__ const void* bbase() const { return base; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)R * ld * sizeof(T)); }
+  __device__ int brow(int r, unsigned& mask) const {
+    mask = r < R ? ~0u : 0u;
+    return r < R ? (int)((long)r * ld * sizeof(T)) : 0;
+  }
+  __device__ void btile(int k0, int& toff, int& tap) const { toff = k0 * (int)sizeof(T); tap = 0; }
 };
 
 // Dense, rows contiguous: element (r, k) at base[k*ld + r].
 template <typename T>
 struct DenseR {
-  const T* base; long ld; int R; bool vec;
+  const T* base; long ld; int R; bool vec; int vrows;  // vrows: k extent (buffer size)
   typedef int RowState;
   typedef KCtx KT;
   typedef typename Vec16<T>::type V;
@@ -103,6 +116,17 @@ struct DenseR {
     for (int j = 0; j < VEC; ++j)
       if (rs + j < R) v[j] = p[j];
     return v;
+  }
+  // LDS-DMA path (vec, R % 8 == 0): the 8 rows from rs at k = k0 + kk, or null = zeros
+  __device__ const T* ptr(RowState rs, const KT& kt, int kk) const {
+    const int k = kt.k0 + kk;
+    return rs >= 0 && k < kt.klim ? base + (long)k * ld + rs : nullptr;
+  }
+  __device__ const void* bbase() const { return base; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)vrows * ld * sizeof(T)); }
+  // byte offset of the 8 rows from rs at k, or -1 (zeros)
+  __device__ int roff(RowState rs, int k, int klim) const {
+    return rs >= 0 && k < klim ? (int)(((long)k * ld + rs) * sizeof(T)) : -1;
   }
 };
 
@@ -165,6 +189,32 @@ struct Im2colK {
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return V{};
     return *(const V*)(rs.base + o);
   }
+  __device__ const T* ptr(const RowState& rs, const KT& kt, int off) const {  // FAST only
+    const int ih = rs.ih0 + kt.r, iw = rs.iw0 + kt.s;
+    if (!rs.base || (unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
+      return nullptr;
+    return rs.base + kt.off + off;
+  }
+  __device__ const void* bbase() const { return x; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.H * g.W * g.C * sizeof(T)); }
+  __device__ int brow(int m, unsigned& mask) const {  // FAST, R*S <= 32
+    mask = 0u;
+    if (m >= M) return 0;
+    const int pq = g.P * g.Q;
+    const int n = m / pq, rem = m - n * pq;
+    const int p = rem / g.Q, q = rem - p * g.Q;
+    const int ih0 = p * g.sh - g.ph, iw0 = q * g.sw - g.pw;
+    for (int r = 0; r < g.R; ++r)
+      for (int s = 0; s < g.S; ++s)
+        if ((unsigned)(ih0 + r) < (unsigned)g.H && (unsigned)(iw0 + s) < (unsigned)g.W)
+          mask |= 1u << (r * g.S + s);
+    return (int)((((long)n * g.H + ih0) * g.W + iw0) * g.C * (long)sizeof(T));
+  }
+  __device__ void btile(int k0, int& toff, int& tap) const {
+    tap = k0 / g.C;
+    const int c0 = k0 - tap * g.C, r = tap / g.S, s = tap - r * g.S;
+    toff = ((r * g.W + s) * g.C + c0) * (int)sizeof(T);
+  }
 };
 
 // conv dgrad A operand: rows = input pixels (n,h,w), k = (r, s, kout) with kout contiguous.
@@ -223,6 +273,37 @@ struct DgradK {
     if (p >= g.P || q >= g.Q) return V{};
     return *(const V*)(rs.img + ((long)p * g.Q + q) * g.K + ko);
   }
+  __device__ const T* ptr(const RowState& rs, const KT& kt, int off) const {  // FAST only
+    if (!rs.img) return nullptr;
+    const int th = rs.h - kt.r, tw = rs.w - kt.s;
+    if (th < 0 || tw < 0) return nullptr;
+    int p = th, q = tw;
+    if (g.sh != 1 || g.sw != 1) {
+      p = th / g.sh; q = tw / g.sw;
+      if (p * g.sh != th || q * g.sw != tw) return nullptr;
+    }
+    if (p >= g.P || q >= g.Q) return nullptr;
+    return rs.img + ((long)p * g.Q + q) * g.K + kt.kb + off;
+  }
+  __device__ const void* bbase() const { return dy; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.P * g.Q * g.K * sizeof(T)); }
+  __device__ int brow(int m, unsigned& mask) const {  // FAST, stride 1, R*S <= 32
+    mask = 0u;
+    if (m >= M) return 0;
+    const int hw = g.H * g.W;
+    const int n = m / hw, rem = m - n * hw;
+    const int h = rem / g.W, w = rem - h * g.W;
+    for (int r = 0; r < g.R; ++r)
+      for (int s = 0; s < g.S; ++s)
+        if ((unsigned)(h + g.ph - r) < (unsigned)g.P && (unsigned)(w + g.pw - s) < (unsigned)g.Q)
+          mask |= 1u << (r * g.S + s);
+    return (int)((((long)n * g.P + h + g.ph) * g.Q + w + g.pw) * g.K * (long)sizeof(T));
+  }
+  __device__ void btile(int k0, int& toff, int& tap) const {
+    tap = k0 / g.K;
+    const int kb = k0 - tap * g.K, r = tap / g.S, s = tap - r * g.S;
+    toff = (kb - (r * g.Q + s) * g.K) * (int)sizeof(T);
+  }
 };
 
 // Strided-conv dgrad, one output phase (a, b) = (h mod sh, w mod sw) at a time: only the
@@ -269,6 +350,31 @@ struct DgradPhaseK {
     if ((unsigned)p >= (unsigned)g.P || (unsigned)q >= (unsigned)g.Q) return V{};
     return *(const V*)(rs.img + ((long)p * g.Q + q) * g.K + kt.kb + off);
   }
+  __device__ const T* ptr(const RowState& rs, const KT& kt, int off) const {
+    if (!rs.img || kt.k0 + off >= kt.klim) return nullptr;
+    const int p = rs.i + kt.dr, q = rs.j + kt.ds;
+    if ((unsigned)p >= (unsigned)g.P || (unsigned)q >= (unsigned)g.Q) return nullptr;
+    return rs.img + ((long)p * g.Q + q) * g.K + kt.kb + off;
+  }
+  __device__ const void* bbase() const { return dy; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.P * g.Q * g.K * sizeof(T)); }
+  __device__ int brow(int m, unsigned& mask) const {  // ntr * nts <= 32
+    mask = 0u;
+    if (m >= M) return 0;
+    const int hw = ph.Hp * ph.Wp;
+    const int n = m / hw, rem = m - n * hw;
+    const int i = rem / ph.Wp, j = rem - i * ph.Wp;
+    for (int u = 0; u < ph.ntr; ++u)
+      for (int v = 0; v < ph.nts; ++v)
+        if ((unsigned)(i + ph.dr0 - u) < (unsigned)g.P && (unsigned)(j + ph.ds0 - v) < (unsigned)g.Q)
+          mask |= 1u << (u * ph.nts + v);
+    return (int)((((long)n * g.P + i) * g.Q + j) * g.K * (long)sizeof(T));
+  }
+  __device__ void btile(int k0, int& toff, int& tap) const {
+    tap = k0 / g.K;
+    const int kb = k0 - tap * g.K, u = tap / ph.nts, v = tap - u * ph.nts;
+    toff = (((ph.dr0 - u) * g.Q + (ph.ds0 - v)) * g.K + kb) * (int)sizeof(T);
+  }
 };
 
 // B operand of the phase dgrad: packed CRSK weights, k = (phase tap t, kout).
@@ -291,12 +397,27 @@ struct PhaseTapK {
     if (!rs || kt.k0 + off >= kt.klim) return V{};
     return *(const V*)(rs + kt.kg + off);
   }
+  __device__ const T* ptr(RowState rs, const KT& kt, int off) const {
+    return rs && kt.k0 + off < kt.klim ? rs + kt.kg + off : nullptr;
+  }
+  __device__ const void* bbase() const { return w; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)C * ld * sizeof(T)); }
+  __device__ int brow(int c, unsigned& mask) const {
+    mask = c < C ? ~0u : 0u;
+    return c < C ? (int)((long)c * ld * sizeof(T)) : 0;
+  }
+  __device__ void btile(int k0, int& toff, int& tap) const {
+    const int t = k0 / K, kb = k0 - t * K;
+    const int u = t / ph.nts, v = t - u * ph.nts;
+    toff = (((ph.r0 + sh * u) * S + (ph.s0 + sw * v)) * K + kb) * (int)sizeof(T);
+    tap = 0;
+  }
 };
 
 // conv wgrad B operand: rows = (r, s, c) with c contiguous, k = output pixel (n,p,q).
 template <typename T>
 struct Im2colR {
-  const T* x; ConvGeom g; int Rows;
+  const T* x; ConvGeom g; int Rows; float inv_pq, inv_q;  // 1/(P*Q), 1/Q for roff()
   struct RowState { int r, s, c; };
   typedef KCtx KT;
   typedef typename Vec16<T>::type V;
@@ -319,6 +440,32 @@ struct Im2colR {
     const int ih = p * g.sh - g.ph + rs.r, iw = q * g.sw - g.pw + rs.s;
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return V{};
     return *(const V*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + rs.c);
+  }
+  __device__ const T* ptr(const RowState& rs, const KT& kt, int kk) const {
+    const int k = kt.k0 + kk;
+    if (rs.r < 0 || k >= kt.klim) return nullptr;
+    const int pq = g.P * g.Q;
+    const int n = k / pq, rem = k - n * pq;
+    const int p = rem / g.Q, q = rem - p * g.Q;
+    const int ih = p * g.sh - g.ph + rs.r, iw = q * g.sw - g.pw + rs.s;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return nullptr;
+    return x + (((long)n * g.H + ih) * g.W + iw) * g.C + rs.c;
+  }
+  __device__ const void* bbase() const { return x; }
+  __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.H * g.W * g.C * sizeof(T)); }
+  // pixel k -> (n, p, q) by float reciprocals (k < 2^23: one correction step is exact)
+  __device__ int roff(const RowState& rs, int k, int klim) const {
+    if (rs.r < 0 || k >= klim) return -1;
+    const int pq = g.P * g.Q;
+    int n = (int)((float)k * inv_pq);
+    int rem = k - n * pq;
+    if (rem < 0) { --n; rem += pq; } else if (rem >= pq) { ++n; rem -= pq; }
+    int p = (int)((float)rem * inv_q);
+    int q = rem - p * g.Q;
+    if (q < 0) { --p; q += g.Q; } else if (q >= g.Q) { ++p; q -= g.Q; }
+    const int ih = p * g.sh - g.ph + rs.r, iw = q * g.sw - g.pw + rs.s;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return -1;
+    return (int)(((((long)n * g.H + ih) * g.W + iw) * g.C + rs.c) * (long)sizeof(T));
   }
 };
 
@@ -646,6 +793,205 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(typename LA::SrcT sa, type
 
   // Epilogue: C/D map of 16x16 MFMA (col = lane&15, row = (lane>>4)*4 + reg) -> fp32 LDS
   // tile [BM][BN+4] -> 4 consecutive columns per lane per store.
+  float* cst = (float*)lds_raw;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 + (lane & 15)] =
+            acc[i][j][r];
+  __syncthreads();
+  epi.template tile_stats<BM, BN, LDC>(cst, cst + BM * LDC, tm, tn);
+  constexpr int C4 = BN / 4;
+  for (int c = threadIdx.x; c < BM * C4; c += NT) {
+    const int row = c / C4, col = (c - row * C4) * 4;
+    const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
+    epi.apply4(tm * BM + row, tn * BN + col, v);
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// LDS-DMA variant (bf16, both operands k-major, whole 64-deep K tiles): global_load_lds
+// moves each 16-B chunk straight into LDS, so no staging registers and no ds_write pass.
+// LDS image per operand and stage: [ROWS][64] bf16, 128-B rows, logical chunk c of row r at
+// slot c ^ (r & 7) — conflict-free for the ds_read_b128 fragment reads.  Wave instruction j
+// of wave w fills rows (4j + w)*8 .. +7 (1 KiB, lane-linear); each lane fetches the chunk
+// that belongs at its slot (zeros through a zero line for padding / out-of-range rows).
+// Two stages, one raw barrier per K tile: wait for this wave's DMAs of tile t, barrier,
+// issue tile t+1 into the other stage, compute tile t.
+// --------------------------------------------------------------------------------------
+// Every DMA goes through a raw buffer resource over the operand tensor: a lane whose chunk is
+// padding / out of range gets voffset = DMA_OOB, and the range check makes the hardware write
+// zeros into LDS (verified on gfx950: tools/lab/oob_lds.hip).  Per K tile a lane's cost is
+// one tap-validity bit test, an add and a select.
+constexpr unsigned DMA_OOB = 0x80000000u;  // operand tensors are < 2 GiB (host-checked)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, char* lds, unsigned voff) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int ROWS, class Src>
+struct DmaK {
+  static constexpr int NW = NT / 64;
+  static constexpr int INSTR = ROWS / (8 * NW);  // DMAs per wave per stage
+  static constexpr int BYTES = ROWS * 128;
+  static_assert(ROWS % (8 * NW) == 0, "rows per wave");
+  typedef Src SrcT;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int off[INSTR];       // byte offset of this lane's chunk at tap 0
+  unsigned mask[INSTR]; // valid taps of the row
+  int coff;             // element offset of this lane's logical chunk within the K tile
+  __device__ void init(const Src& s, int row0, int lane, int wid) {
+    const int rr = lane >> 3, slot = lane & 7;
+    coff = (slot ^ rr) * 8;  // rows of an instruction start at a multiple of 8: r & 7 == rr
+    rsrc = dma_rsrc(s.bbase(), s.bbytes());
+#pragma unroll
+    for (int j = 0; j < INSTR; ++j)
+      off[j] = s.brow(row0 + (j * NW + wid) * 8 + rr, mask[j]) + coff * 2;
+  }
+  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) const {
+    int toff, tap;
+    s.btile(k0, toff, tap);
+    const bool kok = k0 + coff < klim;
+#pragma unroll
+    for (int j = 0; j < INSTR; ++j) {
+      const bool ok = kok && ((mask[j] >> tap) & 1u);
+      dma16(rsrc, stage + (j * NW + wid) * 1024, ok ? (unsigned)(off[j] + toff) : DMA_OOB);
+    }
+  }
+  __device__ static bf16x8 frag(const char* stage, int r16, int ks, int lane) {
+    const int row = r16 + (lane & 15);
+    const int c = (ks >> 3) + (lane >> 4);
+    return *(const bf16x8*)(stage + row * 128 + ((c ^ (row & 7)) << 4));
+  }
+};
+
+// R-major operand (rows contiguous in global: dY^T / im2col^T of the wgrad GEMM): LDS image
+// [64 k][ROWS] bf16, one ROWS*2-byte line per k; a DMA instruction fills 1 KiB = KPI whole
+// k-lines.  Chunk slots are XOR-swizzled per k so the ds_read_b64_tr_b16 fragment reads (8
+// k-lines x 32 B per 32-lane group) hit every bank once.
+template <int ROWS, class Src>
+struct DmaR {
+  static constexpr int NW = NT / 64;
+  static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
+  static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
+  static constexpr int INSTR = 64 / (KPI * NW); // DMAs per wave per stage (BK = 64)
+  static constexpr int BYTES = 64 * ROWS * 2;
+  static_assert(ROWS == 64 || ROWS == 128, "R-major DMA tile rows");
+  typedef Src SrcT;
+  __amdgpu_buffer_rsrc_t rsrc;
+  typename Src::RowState rs[INSTR];
+  int kr[INSTR];
+  __device__ static int sw(int k) {
+    return ROWS == 128 ? 2 * ((k & 3) | (((k >> 3) & 1) << 2))
+                       : 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  }
+  __device__ void init(const Src& s, int row0, int lane, int wid) {
+    const int slot = lane % CPR;
+    rsrc = dma_rsrc(s.bbase(), s.bbytes());
+#pragma unroll
+    for (int j = 0; j < INSTR; ++j) {
+      kr[j] = (j * NW + wid) * KPI + lane / CPR;
+      rs[j] = s.row(row0 + (slot ^ sw(kr[j])) * 8);
+    }
+  }
+  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) const {
+#pragma unroll
+    for (int j = 0; j < INSTR; ++j) {
+      const int o = s.roff(rs[j], k0 + kr[j], klim);
+      dma16(rsrc, stage + (j * NW + wid) * 1024, o >= 0 ? (unsigned)o : DMA_OOB);
+    }
+  }
+  // lane 4q+p of 16-lane group g reads k-line ks+8g+q (and +4), columns r16+4p..+3, and gets
+  // column (lane & 15) of those 4 lines: 8 consecutive k, as the MFMA operand wants
+  __device__ static bf16x8 frag(const char* stage, int r16, int ks, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = ks + 8 * g + q;
+    const int col = r16 + 4 * p;
+    const int o = (((col >> 3) ^ sw(k)) << 4) + ((col >> 2) & 1) * 8;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(stage + k * (ROWS * 2) + o));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(stage + (k + 4) * (ROWS * 2) + o));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
+
+template <int BM, int BN, class OA, class OB, class Epi>
+__global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
+                                                          typename OB::SrcT sb, Epi epi, int M,
+                                                          int N, int K, int kper) {
+  constexpr int BK = 64, WM = 2, WN = 2;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  constexpr int OP_BYTES = 2 * STAGE;
+  constexpr int LDC = BN + 4;
+  constexpr int EPI_BYTES = BM * LDC * 4 + NT * 3 * 4;
+  constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];  // the only LDS object
+
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tile = xcd_swizzle(blockIdx.x, tiles_m * tiles_n);
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int kbeg = blockIdx.z * kper;
+  const int kend = min(K, kbeg + kper);
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  OA oa;
+  OB ob;
+  oa.init(sa, tm * BM, lane, wid);
+  ob.init(sb, tn * BN, lane, wid);
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    oa.issue(sa, lds_raw, kbeg, kend, wid);
+    ob.issue(sb, lds_raw + OA::BYTES, kbeg, kend, wid);
+  }
+  for (int t = 0; t < nt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 < nt) {
+      char* st = lds_raw + ((t + 1) & 1) * STAGE;
+      oa.issue(sa, st, kbeg + (t + 1) * BK, kend, wid);
+      ob.issue(sb, st + OA::BYTES, kbeg + (t + 1) * BK, kend, wid);
+    }
+    const char* as = lds_raw + (t & 1) * STAGE;
+    const char* bs = as + OA::BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = OA::frag(as, wm * WTM + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfr[j] = OB::frag(bs, wn * WTN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
   float* cst = (float*)lds_raw;
 #pragma unroll
   for (int i = 0; i < RM; ++i)

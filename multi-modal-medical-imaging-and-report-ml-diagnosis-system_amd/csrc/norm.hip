@@ -98,32 +98,35 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x
 }
 
 // Merge slab partials; update running stats; emit scale/shift for the apply pass.
-// Block = 8 channels x 32 partial lanes; each lane merges every 32nd slab (Chan), then the
-// 32 lane results merge in a fixed order (deterministic).  Conv-epilogue statistics give
-// one slab per 128 output rows (thousands per layer), so the slab dimension is the wide one.
-constexpr int FIN_C = 8, FIN_P = 32;
-__global__ __launch_bounds__(FIN_C * FIN_P) void bn_finalize_kernel(
+// One wave per channel, two passes over the slabs (all loads independent, so they pipeline):
+// mean = sum(n_b mean_b) / N, then M2 = sum(M2_b + n_b (mean_b - mean)^2) — the exact
+// two-level decomposition of the variance, reduced in a fixed lane/shuffle order
+// (deterministic).  Conv-epilogue statistics give one slab per 128 output rows.
+constexpr int FIN_W = 4;  // channels (waves) per block
+__global__ __launch_bounds__(64 * FIN_W) void bn_finalize_kernel(
     const float2* __restrict__ part, int nblk, long rows, long rpb, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
     float* running_var, float momentum, float eps, float* save_mean, float* save_rstd,
     float* scale, float* shift) {
-  __shared__ float sn[FIN_P][FIN_C], sm[FIN_P][FIN_C], s2[FIN_P][FIN_C];
-  const int cl = threadIdx.x % FIN_C, pl = threadIdx.x / FIN_C;
-  const int c = blockIdx.x * FIN_C + cl;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < C) {
-    for (int b = pl; b < nblk; b += FIN_P) {
-      const long nb = min(rpb, rows - (long)b * rpb);
-      const float2 p = part[(long)b * C + c];
-      chan_merge(n, mean, m2, (float)nb, p.x, p.y);
-    }
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * FIN_W + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const long last = rows - (long)(nblk - 1) * rpb;  // rows of the final (short) slab
+  float s = 0.f;
+  for (int b = lane; b < nblk; b += 64) {
+    const float nb = b == nblk - 1 ? (float)last : (float)rpb;
+    s += nb * part[(long)b * C + c].x;
   }
-  sn[pl][cl] = n; sm[pl][cl] = mean; s2[pl][cl] = m2;
-  __syncthreads();
-  if (pl != 0 || c >= C) return;
-  n = 0.f; mean = 0.f; m2 = 0.f;
-#pragma unroll
-  for (int q = 0; q < FIN_P; ++q) chan_merge(n, mean, m2, sn[q][cl], sm[q][cl], s2[q][cl]);
+  const float mean = wave_sum(s) / (float)rows;
+  float q = 0.f;
+  for (int b = lane; b < nblk; b += 64) {
+    const float nb = b == nblk - 1 ? (float)last : (float)rpb;
+    const float2 p = part[(long)b * C + c];
+    const float d = p.x - mean;
+    q += p.y + nb * d * d;
+  }
+  const float m2 = wave_sum(q);
+  if (lane != 0) return;
   const float var = m2 / (float)rows;
   const float rstd = rsqrtf(var + eps);
   save_mean[c] = mean;
@@ -255,6 +258,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
 }
 
 // coef: a[c] = gamma*rstd, b[c] = -gamma*rstd*sum_g/n, k[c] = -gamma*rstd*sum_gx/n
+constexpr int FIN_C = 8, FIN_P = 32;  // channels x slab lanes per block
 __global__ __launch_bounds__(FIN_C * FIN_P) void bn_bwd_finalize_kernel(
     const float2* __restrict__ part, int nblk, long rows, int C, int train,
     const float* __restrict__ gamma, const float* __restrict__ rstd, float* dgamma,
@@ -356,7 +360,7 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
       hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                          (const T*)x, rows, C, L.ct, L.rows_per_block, part);
     }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_W - 1) / FIN_W), dim3(64 * FIN_W), 0,
                        st, (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv,
                        momentum, eps, smean, srstd, scale, shift);
   } else {

@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default="")
+    ap.add_argument("--filter", default="", help="substring of the shape string to run")
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
     import mmdx
     from mmdx import _lib as L
@@ -66,6 +68,8 @@ def main():
     rows = []
     tot = collections.Counter()
     for (H, W, C, K, k, s, p), info in shapes().items():
+        if a.filter and a.filter not in f"{H}x{W} C{C} K{K} {k}x{k}/{s}":
+            continue
         Cp = (C + 7) // 8 * 8
         P = (H + 2 * p - k) // s + 1
         Q = (W + 2 * p - k) // s + 1
@@ -96,6 +100,8 @@ def main():
         xb, yb, wb = B * H * W * Cp * 2, B * P * Q * K * 2, K * Cp * k * k * 2
         nbytes = {"fwd": xb + wb + yb, "dgrad": yb + wb + xb, "wgrad": xb + yb + 2 * wb}
         for name, fn in ops.items():
+            if name not in a.ops.split(","):
+                continue
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()
