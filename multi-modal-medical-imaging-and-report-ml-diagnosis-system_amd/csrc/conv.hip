@@ -57,8 +57,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, in
     const long t = i / C;
     const int rs = (int)(t % RS);
     const int k = (int)(t / RS);
-    float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += ws[z * slab + i];
+    // 8 independent partial sums keep 8 slab loads in flight (fixed order: deterministic)
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += ws[(long)(z + j) * slab + i];
+    }
+    for (int j = 0; z < splits; ++z, ++j) a[j] += ws[(long)z * slab + i];
+    const float v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     const long o = ((long)k * Cm + c) * RS + rs;
     dw[o] = beta != 0.f ? beta * dw[o] + v : v;
   }
@@ -97,11 +104,12 @@ static int launch_dma(const SA& sa, const SB& sb, const Epi& epi, int M, int N, 
 template <class S> struct DmaOk { static constexpr bool value = false; };
 template <> struct DmaOk<Im2colK<bf16, true>> { static constexpr bool value = true; };
 template <> struct DmaOk<DgradK<bf16, true>> { static constexpr bool value = true; };
+template <> struct DmaOk<Im2colK<bf16, false>> { static constexpr bool value = true; };
 
 // buffer-DMA preconditions: 32-bit byte offsets (< 2 GiB) and a 32-bit tap-validity mask
-static bool dma_geom_ok(const ConvGeom& g, bool dgrad) {
+static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32) {
   const long xb = (long)g.N * g.H * g.W * g.C * 2, yb = (long)g.N * g.P * g.Q * g.K * 2;
-  if (xb >= (1L << 31) || yb >= (1L << 31) || g.R * g.S > 32) return false;
+  if (xb >= (1L << 31) || yb >= (1L << 31) || g.R * g.S > max_taps) return false;
   return !dgrad || (g.sh == 1 && g.sw == 1);
 }
 
@@ -134,7 +142,10 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
                         dma_geom_ok(g, false));
-  return conv_gemm<T>(Im2colK<T, false>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats);
+  // channel count a power of two: the LDS-DMA kernel decodes each lane's tap itself
+  const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
+  Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
+  return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64));
 }
 
 // Strided dgrad as sh*sw phase GEMMs (see DgradPhaseK); phases no tap reaches are written
@@ -233,7 +244,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   EpiPartial epi{(float*)ws, M, N};
   int rc;
   if constexpr (sizeof(T) == 2) {
-   if (dma_geom_ok(g, false) && K < (1 << 23)) {
+   if (dma_geom_ok(g, false, 1 << 30) && K < (1 << 23)) {
     // LDS-DMA wgrad: both operands R-major (M = Kout and N = R*S*C are multiples of 8)
     if (p.bm == 128 && p.bn == 128)
       rc = launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, Im2colR<T>>>(

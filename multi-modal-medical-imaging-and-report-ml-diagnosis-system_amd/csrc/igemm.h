@@ -20,6 +20,8 @@
 // layer but the 3-channel stem), so the per-vector address math is an add + bounds check.
 // The epilogue stages the fp32 accumulators through LDS and stores 4 outputs per lane.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace mmdx {
@@ -89,6 +91,10 @@ struct DenseK {
   // uniform byte offset and tap index.  Offsets are relative to bbase().
   __device__ const void* bbase() const { return base; }
   __device__ unsigned bbytes() const { return (unsigned)((long)R * ld * sizeof(T)); }
+  typedef unsigned Mask;
+  static constexpr bool LANE_TAP = false;
+  __device__ void lane_decode(int, int&, int&, int&) const {}
+  __device__ bool lane_ok(unsigned, int, int) const { return false; }
   __device__ int brow(int r, unsigned& mask) const {
     mask = r < R ? ~0u : 0u;
     return r < R ? (int)((long)r * ld * sizeof(T)) : 0;
@@ -142,7 +148,7 @@ struct ConvGeom {
 // FAST: C % BK == 0, so one K tile = one filter tap and a contiguous channel block.
 template <typename T, bool FAST>
 struct Im2colK {
-  const T* x; ConvGeom g; int M;
+  const T* x; ConvGeom g; int M; int cshift = 0; float inv_s = 0.f;  // !FAST DMA: log2(C), 1/S
   struct RowState { const T* base; int ih0, iw0; };  // base = &x[n, ih0, iw0, 0]
   struct KT { int r, s, k0, klim; long off; };
   typedef typename Vec16<T>::type V;
@@ -197,18 +203,39 @@ struct Im2colK {
   }
   __device__ const void* bbase() const { return x; }
   __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.H * g.W * g.C * sizeof(T)); }
-  __device__ int brow(int m, unsigned& mask) const {  // FAST, R*S <= 32
-    mask = 0u;
-    if (m >= M) return 0;
+  // FAST: 32-bit tap mask (R*S <= 32), one tap per K tile.  !FAST (power-of-two C >= 8,
+  // e.g. the 3-channel stem padded to 8): every lane's 8-channel chunk is its own tap,
+  // decoded per lane; the row keeps its packed (ih0, iw0) instead of a mask.
+  typedef typename std::conditional<FAST, unsigned, int>::type Mask;
+  static constexpr bool LANE_TAP = !FAST;
+  __device__ int brow(int m, Mask& mask) const {
     const int pq = g.P * g.Q;
     const int n = m / pq, rem = m - n * pq;
     const int p = rem / g.Q, q = rem - p * g.Q;
     const int ih0 = p * g.sh - g.ph, iw0 = q * g.sw - g.pw;
-    for (int r = 0; r < g.R; ++r)
-      for (int s = 0; s < g.S; ++s)
-        if ((unsigned)(ih0 + r) < (unsigned)g.H && (unsigned)(iw0 + s) < (unsigned)g.W)
-          mask |= 1u << (r * g.S + s);
+    if constexpr (FAST) {
+      mask = 0u;
+      if (m >= M) return 0;
+      for (int r = 0; r < g.R; ++r)
+        for (int s = 0; s < g.S; ++s)
+          if ((unsigned)(ih0 + r) < (unsigned)g.H && (unsigned)(iw0 + s) < (unsigned)g.W)
+            mask |= 1u << (r * g.S + s);
+    } else {
+      mask = m < M ? (int)(((unsigned)ih0 << 16) | ((unsigned)iw0 & 0xffffu)) : (int)0x80008000;
+      if (m >= M) return 0;
+    }
     return (int)((((long)n * g.H + ih0) * g.W + iw0) * g.C * (long)sizeof(T));
+  }
+  // per-lane tap of element k: byte offset from the row base, and the (r, s) it needs
+  __device__ void lane_decode(int k, int& toff, int& r, int& s) const {
+    const int tap = k >> cshift, c = k & (g.C - 1);
+    r = (int)((float)tap * inv_s + 1e-3f);  // tap < 64: exact
+    s = tap - r * g.S;
+    toff = ((r * g.W + s) * g.C + c) * (int)sizeof(T);
+  }
+  __device__ bool lane_ok(Mask mk, int r, int s) const {
+    const int ih = (mk >> 16) + r, iw = (int)(short)(mk & 0xffff) + s;
+    return (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
   }
   __device__ void btile(int k0, int& toff, int& tap) const {
     tap = k0 / g.C;
@@ -287,6 +314,10 @@ struct DgradK {
   }
   __device__ const void* bbase() const { return dy; }
   __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.P * g.Q * g.K * sizeof(T)); }
+  typedef unsigned Mask;
+  static constexpr bool LANE_TAP = false;
+  __device__ void lane_decode(int, int&, int&, int&) const {}
+  __device__ bool lane_ok(unsigned, int, int) const { return false; }
   __device__ int brow(int m, unsigned& mask) const {  // FAST, stride 1, R*S <= 32
     mask = 0u;
     if (m >= M) return 0;
@@ -358,6 +389,10 @@ struct DgradPhaseK {
   }
   __device__ const void* bbase() const { return dy; }
   __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.P * g.Q * g.K * sizeof(T)); }
+  typedef unsigned Mask;
+  static constexpr bool LANE_TAP = false;
+  __device__ void lane_decode(int, int&, int&, int&) const {}
+  __device__ bool lane_ok(unsigned, int, int) const { return false; }
   __device__ int brow(int m, unsigned& mask) const {  // ntr * nts <= 32
     mask = 0u;
     if (m >= M) return 0;
@@ -402,6 +437,10 @@ struct PhaseTapK {
   }
   __device__ const void* bbase() const { return w; }
   __device__ unsigned bbytes() const { return (unsigned)((long)C * ld * sizeof(T)); }
+  typedef unsigned Mask;
+  static constexpr bool LANE_TAP = false;
+  __device__ void lane_decode(int, int&, int&, int&) const {}
+  __device__ bool lane_ok(unsigned, int, int) const { return false; }
   __device__ int brow(int c, unsigned& mask) const {
     mask = c < C ? ~0u : 0u;
     return c < C ? (int)((long)c * ld * sizeof(T)) : 0;
@@ -844,22 +883,33 @@ struct DmaK {
   static constexpr int BYTES = ROWS * 128;
   static_assert(ROWS % (8 * NW) == 0, "rows per wave");
   typedef Src SrcT;
+  typedef typename Src::Mask Mask;
   __amdgpu_buffer_rsrc_t rsrc;
   int off[INSTR];       // byte offset of this lane's chunk at tap 0
-  unsigned mask[INSTR]; // valid taps of the row
+  Mask mask[INSTR];     // valid taps of the row
   int coff;             // element offset of this lane's logical chunk within the K tile
   __device__ void init(const Src& s, int row0, int lane, int wid) {
     const int rr = lane >> 3, slot = lane & 7;
     coff = (slot ^ rr) * 8;  // rows of an instruction start at a multiple of 8: r & 7 == rr
     rsrc = dma_rsrc(s.bbase(), s.bbytes());
 #pragma unroll
-    for (int j = 0; j < INSTR; ++j)
-      off[j] = s.brow(row0 + (j * NW + wid) * 8 + rr, mask[j]) + coff * 2;
+    for (int j = 0; j < INSTR; ++j)  // LANE_TAP sources fold the chunk offset into toff
+      off[j] = s.brow(row0 + (j * NW + wid) * 8 + rr, mask[j]) + (Src::LANE_TAP ? 0 : coff * 2);
   }
   __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) const {
-    int toff, tap;
-    s.btile(k0, toff, tap);
     const bool kok = k0 + coff < klim;
+    if constexpr (Src::LANE_TAP) {  // this lane's chunk has its own tap
+      int toff, r, sx;
+      s.lane_decode(k0 + coff, toff, r, sx);
+#pragma unroll
+      for (int j = 0; j < INSTR; ++j) {
+        const bool ok = kok && s.lane_ok(mask[j], r, sx);
+        dma16(rsrc, stage + (j * NW + wid) * 1024, ok ? (unsigned)(off[j] + toff) : DMA_OOB);
+      }
+      return;
+    }
+    int toff, tap;
+    s.btile(k0, toff, tap);  // one tap for the whole K tile (uniform)
 #pragma unroll
     for (int j = 0; j < INSTR; ++j) {
       const bool ok = kok && ((mask[j] >> tap) & 1u);

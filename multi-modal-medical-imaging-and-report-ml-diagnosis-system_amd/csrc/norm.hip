@@ -112,20 +112,30 @@ __global__ __launch_bounds__(64 * FIN_W) void bn_finalize_kernel(
   const int c = blockIdx.x * FIN_W + (threadIdx.x >> 6);
   if (c >= C) return;
   const long last = rows - (long)(nblk - 1) * rpb;  // rows of the final (short) slab
-  float s = 0.f;
-  for (int b = lane; b < nblk; b += 64) {
-    const float nb = b == nblk - 1 ? (float)last : (float)rpb;
-    s += nb * part[(long)b * C + c].x;
+  // 4 independent accumulators per lane keep 4 slab loads in flight (fixed order)
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = lane; b0 < nblk; b0 += 256) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + 64 * j;
+      if (b < nblk) s4[j] += (b == nblk - 1 ? (float)last : (float)rpb) * part[(long)b * C + c].x;
+    }
   }
-  const float mean = wave_sum(s) / (float)rows;
-  float q = 0.f;
-  for (int b = lane; b < nblk; b += 64) {
-    const float nb = b == nblk - 1 ? (float)last : (float)rpb;
-    const float2 p = part[(long)b * C + c];
-    const float d = p.x - mean;
-    q += p.y + nb * d * d;
+  const float mean = wave_sum((s4[0] + s4[1]) + (s4[2] + s4[3])) / (float)rows;
+  float q4[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = lane; b0 < nblk; b0 += 256) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + 64 * j;
+      if (b < nblk) {
+        const float nb = b == nblk - 1 ? (float)last : (float)rpb;
+        const float2 p = part[(long)b * C + c];
+        const float d = p.x - mean;
+        q4[j] += p.y + nb * d * d;
+      }
+    }
   }
-  const float m2 = wave_sum(q);
+  const float m2 = wave_sum((q4[0] + q4[1]) + (q4[2] + q4[3]));
   if (lane != 0) return;
   const float var = m2 / (float)rows;
   const float rstd = rsqrtf(var + eps);

@@ -218,8 +218,6 @@ def _conv_bn(conv, bn, relu, x, N, H, W, C, cm, res, train, keep):
     call("mmdx_bn_fwd", dt, int(train), ptr(y), rows, K, ptr(part), nstat, 128, ptr(bn.weight),
          ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum),
          float(bn.eps), ptr(mean), ptr(rstd), ptr(res), int(relu), ptr(out), ptr(ws), ws_n, st)
-    if train:
-        bn.num_batches_tracked.add_(1)
     u = None
     if keep:
         u = _Unit()
@@ -328,6 +326,9 @@ class _TrunkFn(torch.autograd.Function):
                 x_cur, H, W, C = h, hH, hW, hC
         feats = torch.empty((N, C), dtype=T, device=dev)
         call("mmdx_avgpool_fwd", dt, ptr(x_cur), N, H * W, C, ptr(feats), st)
+        if train:  # every BN's num_batches_tracked += 1, in one multi-tensor launch
+            torch._foreach_add_([m.num_batches_tracked for m in trunk.modules()
+                                 if isinstance(m, BatchNorm2d)], 1)
         if keep:
             ctx.state = (stem_state, blocks, (N, H, W, C), x.dtype == torch.float32)
             ctx.trunk = trunk
