@@ -240,7 +240,9 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   const size_t need = (size_t)p.splits * M * N * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu", ws_bytes, need);
   DenseR<T> sa{(const T*)dy, g.K, M, true, K};
-  Im2colR<T> sb{(const T*)x, g, N, 1.f / (float)(g.P * g.Q), 1.f / (float)g.Q};
+  const int pq = g.P * g.Q;
+  Im2colR<T> sb{(const T*)x, g, N, 1.f / (float)pq, 1.f / (float)g.Q, 64 / pq, (64 % pq) / g.Q,
+                (64 % pq) % g.Q};
   EpiPartial epi{(float*)ws, M, N};
   int rc;
   if constexpr (sizeof(T) == 2) {

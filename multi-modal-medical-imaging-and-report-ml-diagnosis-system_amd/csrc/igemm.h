@@ -130,6 +130,11 @@ struct DenseR {
   }
   __device__ const void* bbase() const { return base; }
   __device__ unsigned bbytes() const { return (unsigned)((long)vrows * ld * sizeof(T)); }
+  static constexpr bool STEP = false;
+  struct Lane {};
+  __device__ Lane lane_at(int) const { return Lane{}; }
+  __device__ void lane_step(Lane&) const {}
+  __device__ int roff_at(RowState rs, const Lane&, int k, int klim) const { return roff(rs, k, klim); }
   // byte offset of the 8 rows from rs at k, or -1 (zeros)
   __device__ int roff(RowState rs, int k, int klim) const {
     return rs >= 0 && k < klim ? (int)(((long)k * ld + rs) * sizeof(T)) : -1;
@@ -457,6 +462,7 @@ struct PhaseTapK {
 template <typename T>
 struct Im2colR {
   const T* x; ConvGeom g; int Rows; float inv_pq, inv_q;  // 1/(P*Q), 1/Q for roff()
+  int dn, dp, dq;  // one 64-pixel K tile = dn*P*Q + dp*Q + dq pixels (lane stepping)
   struct RowState { int r, s, c; };
   typedef KCtx KT;
   typedef typename Vec16<T>::type V;
@@ -492,6 +498,31 @@ struct Im2colR {
   }
   __device__ const void* bbase() const { return x; }
   __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.H * g.W * g.C * sizeof(T)); }
+  // LDS-DMA lane state: (n, p, q) of this lane's pixel, advanced one K tile per issue
+  static constexpr bool STEP = true;
+  struct Lane { int n, p, q; };
+  __device__ Lane lane_at(int k) const {
+    const int pq = g.P * g.Q;
+    Lane l;
+    l.n = (int)((float)k * inv_pq);
+    int rem = k - l.n * pq;
+    if (rem < 0) { --l.n; rem += pq; } else if (rem >= pq) { ++l.n; rem -= pq; }
+    l.p = (int)((float)rem * inv_q);
+    l.q = rem - l.p * g.Q;
+    if (l.q < 0) { --l.p; l.q += g.Q; } else if (l.q >= g.Q) { ++l.p; l.q -= g.Q; }
+    return l;
+  }
+  __device__ void lane_step(Lane& l) const {
+    l.q += dq; l.p += dp; l.n += dn;
+    if (l.q >= g.Q) { l.q -= g.Q; ++l.p; }
+    if (l.p >= g.P) { l.p -= g.P; ++l.n; }
+  }
+  __device__ int roff_at(const RowState& rs, const Lane& l, int k, int klim) const {
+    if (rs.r < 0 || k >= klim) return -1;
+    const int ih = l.p * g.sh - g.ph + rs.r, iw = l.q * g.sw - g.pw + rs.s;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return -1;
+    return (int)(((((long)l.n * g.H + ih) * g.W + iw) * g.C + rs.c) * (long)sizeof(T));
+  }
   // pixel k -> (n, p, q) by float reciprocals (k < 2^23: one correction step is exact)
   __device__ int roff(const RowState& rs, int k, int klim) const {
     if (rs.r < 0 || k >= klim) return -1;
@@ -888,7 +919,7 @@ struct DmaK {
   int off[INSTR];       // byte offset of this lane's chunk at tap 0
   Mask mask[INSTR];     // valid taps of the row
   int coff;             // element offset of this lane's logical chunk within the K tile
-  __device__ void init(const Src& s, int row0, int lane, int wid) {
+  __device__ void init(const Src& s, int row0, int lane, int wid, int /*kbeg*/) {
     const int rr = lane >> 3, slot = lane & 7;
     coff = (slot ^ rr) * 8;  // rows of an instruction start at a multiple of 8: r & 7 == rr
     rsrc = dma_rsrc(s.bbase(), s.bbytes());
@@ -938,25 +969,29 @@ struct DmaR {
   typedef Src SrcT;
   __amdgpu_buffer_rsrc_t rsrc;
   typename Src::RowState rs[INSTR];
+  typename Src::Lane ln[INSTR];  // per-lane pixel state of stepping sources (im2col^T)
   int kr[INSTR];
   __device__ static int sw(int k) {
     return ROWS == 128 ? 2 * ((k & 3) | (((k >> 3) & 1) << 2))
                        : 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
   }
-  __device__ void init(const Src& s, int row0, int lane, int wid) {
+  __device__ void init(const Src& s, int row0, int lane, int wid, int kbeg) {
     const int slot = lane % CPR;
     rsrc = dma_rsrc(s.bbase(), s.bbytes());
 #pragma unroll
     for (int j = 0; j < INSTR; ++j) {
       kr[j] = (j * NW + wid) * KPI + lane / CPR;
       rs[j] = s.row(row0 + (slot ^ sw(kr[j])) * 8);
+      if constexpr (Src::STEP) ln[j] = s.lane_at(kbeg + kr[j]);
     }
   }
-  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) const {
+  // called once per K tile, in order (k0 = kbeg, kbeg + 64, ...)
+  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) {
 #pragma unroll
     for (int j = 0; j < INSTR; ++j) {
-      const int o = s.roff(rs[j], k0 + kr[j], klim);
+      const int o = s.roff_at(rs[j], ln[j], k0 + kr[j], klim);
       dma16(rsrc, stage + (j * NW + wid) * 1024, o >= 0 ? (unsigned)o : DMA_OOB);
+      if constexpr (Src::STEP) s.lane_step(ln[j]);
     }
   }
   // lane 4q+p of 16-lane group g reads k-line ks+8g+q (and +4), columns r16+4p..+3, and gets
@@ -1002,8 +1037,8 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 
   OA oa;
   OB ob;
-  oa.init(sa, tm * BM, lane, wid);
-  ob.init(sb, tn * BN, lane, wid);
+  oa.init(sa, tm * BM, lane, wid, kbeg);
+  ob.init(sb, tn * BN, lane, wid, kbeg);
 
   f32x4 acc[RM][RN];
 #pragma unroll
