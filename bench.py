@@ -210,6 +210,7 @@ class StepTimer:
 def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
     import mmdx
     from mmdx import optim as MO
+    from mmdx.schedule import two_tower_backward
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -221,7 +222,8 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
         main.wait_stream(side)
         logits = fus(z_img, z_txt)["disease_logits"]
         loss = mmdx.BCEWithLogitsLoss()(logits, y)
-        loss.backward()
+        # = loss.backward(), with the text tower's backward queued before the image trunk's
+        two_tower_backward(loss, z_img, z_txt, fus.parameters(), text_stream=side)
         if reducer is not None:
             reducer.reduce()
         _, scale = MO.grad_norm(params, 1.0)
@@ -309,17 +311,43 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # The whole train step (both streams, backward, clip, AdamW) is captured once into a
+    # hipGraph and replayed: no per-kernel host launch cost inside the timed region.  N>1
+    # stays eager unless MMDX_GRAPH_DIST=1 (RCCL collectives inside the capture).
+    use_graph = os.environ.get("MMDX_GRAPH", "1") == "1" and (
+        world == 1 or os.environ.get("MMDX_GRAPH_DIST") == "1")
+    run = step
+    static_loss = None
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            static_loss = step()
+        torch.cuda.synchronize()
+        run = graph.replay
+        for _ in range(2):
+            run()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.enabled = True
+    timer.enabled = not use_graph
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    if use_graph:
+        loss = static_loss
+        # conv kernel durations for the roofline: HIP events around each conv launch in a few
+        # eager steps after the timed region (same kernels as the replayed graph)
+        timer.enabled = True
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+    conv_steps = 3 if use_graph else args.steps
     timer.enabled = False
     if world > 1:
         t = torch.tensor([el], device=dev)
@@ -332,7 +360,7 @@ def main():
     samples = B * world * args.steps
     value = samples / el
     ms_step = el / args.steps * 1e3
-    conv_tf = conv_flops * B * args.steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    conv_tf = conv_flops * B * conv_steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
     alg_bytes, alg_launches = conv_bytes_per_step(img.backbone, B)
     traffic = load_traffic(args.config, B)
     result = {
@@ -349,6 +377,7 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
+        "launch": "hipgraph" if use_graph else "eager",
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,
                    "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,
@@ -368,8 +397,8 @@ def main():
             "traffic_unit": "HBM bytes per conv launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)",
             "traffic_source": traffic[1] if traffic else None,
             "algorithmic_bytes_per_launch": round(alg_bytes / alg_launches),
-            "conv_ms_per_step": round(conv_ms / args.steps, 3),
-            "conv_launches_per_step": n_conv // max(1, args.steps),
+            "conv_ms_per_step": round(conv_ms / conv_steps, 3),
+            "conv_launches_per_step": n_conv // max(1, conv_steps),
             "conv_gflop_per_sample": round(conv_flops / 1e9, 3),
         },
     }

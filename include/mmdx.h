@@ -151,9 +151,12 @@ int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n, void* dx,
 int mmdx_bias_grad(int dtype, const void* dy, long M, int N, float* db, float beta_acc,
                    void* workspace, size_t ws_bytes, void* stream);
 size_t mmdx_bias_grad_workspace_size(long M, int N);
-/* dropout with a counter-based hash RNG: y = x * mask / (1-p); mask saved as uint8 */
+/* dropout with a counter-based hash RNG: y = x * mask / (1-p); mask saved as uint8.
+ * counter: optional device uint64.  When given, the RNG stream is (seed, offset + *counter
+ * << 32) and *counter is incremented after the launch (stream-ordered), so the call can be
+ * captured in a hipGraph and every replay draws a fresh mask (torch.nn.Dropout, TP:538). */
 int mmdx_dropout_fwd(int dtype, const void* x, long n, float p, uint64_t seed,
-                     uint64_t offset, void* y, uint8_t* mask, void* stream);
+                     uint64_t offset, uint64_t* counter, void* y, uint8_t* mask, void* stream);
 int mmdx_dropout_bwd(int dtype, const void* dy, const uint8_t* mask, long n, float p,
                      void* dx, void* stream);
 

@@ -68,7 +68,7 @@ SIGNATURES = {
     "mmdx_gelu_bwd": (i32, [i32, vp, vp, i64, vp, vp]),
     "mmdx_bias_grad": (i32, [i32, vp, i64, i32, vp, f32, vp, sz, vp]),
     "mmdx_bias_grad_workspace_size": (sz, [i64, i32]),
-    "mmdx_dropout_fwd": (i32, [i32, vp, i64, f32, u64, u64, vp, vp, vp]),
+    "mmdx_dropout_fwd": (i32, [i32, vp, i64, f32, u64, u64, vp, vp, vp, vp]),
     "mmdx_dropout_bwd": (i32, [i32, vp, vp, i64, f32, vp, vp]),
     "mmdx_bce_logits_fwd": (i32, [vp, vp, i32, i32, vp, vp]),
     "mmdx_bce_logits_bwd": (i32, [vp, vp, i32, i32, vp, vp, vp]),
@@ -159,6 +159,19 @@ def dtype_code(dt: torch.dtype) -> int:
     if dt == torch.bfloat16:
         return BF16
     raise TypeError(f"mmdx kernels compute in float32 or bfloat16, got {dt}")
+
+
+_RNG_COUNTERS: dict = {}
+
+
+def rng_counter(device) -> torch.Tensor:
+    """Per-device uint64 dropout counter (int64 storage) advanced on the GPU by every dropout
+    launch, so RNG state lives on the device and graph replays draw fresh masks."""
+    key = (device.type, device.index)
+    t = _RNG_COUNTERS.get(key)
+    if t is None:
+        t = _RNG_COUNTERS[key] = torch.zeros(1, dtype=torch.int64, device=device)
+    return t
 
 
 def workspace(nbytes: int, device) -> torch.Tensor | None:

@@ -71,8 +71,8 @@ def _ln_fwd(x, res, gamma, beta, eps):
 def _dropout_fwd(x, p, seed):
     y = torch.empty_like(x)
     m = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
-    call("mmdx_dropout_fwd", L.dtype_code(x.dtype), ptr(x), x.numel(), float(p), seed, 0, ptr(y),
-         ptr(m), stream())
+    call("mmdx_dropout_fwd", L.dtype_code(x.dtype), ptr(x), x.numel(), float(p), seed, 0,
+         ptr(L.rng_counter(x.device)), ptr(y), ptr(m), stream())
     return y, m
 
 

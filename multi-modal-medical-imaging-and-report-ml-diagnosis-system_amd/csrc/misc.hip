@@ -187,8 +187,10 @@ __device__ __forceinline__ uint32_t hash64(uint64_t x) {
 }
 template <typename T>
 __global__ void dropout_fwd_kernel(const T* __restrict__ x, long n, float p, uint64_t seed,
-                                   uint64_t off, T* __restrict__ y, uint8_t* __restrict__ mask) {
+                                   uint64_t off, const uint64_t* __restrict__ ctr,
+                                   T* __restrict__ y, uint8_t* __restrict__ mask) {
   const float scale = 1.f / (1.f - p);
+  if (ctr) off += ctr[0] << 32;
   GRID_STRIDE(i, n) {
     const float u = (hash64(seed * 0x9E3779B97F4A7C15ULL + off + (uint64_t)i) >> 8) *
                     (1.f / 16777216.f);
@@ -197,6 +199,8 @@ __global__ void dropout_fwd_kernel(const T* __restrict__ x, long n, float p, uin
     y[i] = from_f<T>(keep ? to_f(x[i]) * scale : 0.f);
   }
 }
+__global__ void counter_incr_kernel(uint64_t* c) { c[0] += 1; }
+
 template <typename T>
 __global__ void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                    long n, float p, T* __restrict__ dx) {
@@ -344,11 +348,14 @@ extern "C" int mmdx_bias_grad(int dtype, const void* dy, long M, int N, float* d
 }
 
 extern "C" int mmdx_dropout_fwd(int dtype, const void* x, long n, float p, uint64_t seed,
-                                uint64_t offset, void* y, uint8_t* mask, void* stream) {
+                                uint64_t offset, uint64_t* counter, void* y, uint8_t* mask,
+                                void* stream) {
   MMDX_CHECK_ARG(p >= 0.f && p < 1.f, "dropout: p out of range");
   DISPATCH_T(dtype, hipLaunchKernelGGL(dropout_fwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0,
                                        (hipStream_t)stream, (const T*)x, n, p, seed, offset,
-                                       (T*)y, mask));
+                                       (const uint64_t*)counter, (T*)y, mask));
+  if (counter)
+    hipLaunchKernelGGL(counter_incr_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter);
   MMDX_LAUNCH_CHECK();
   return 0;
 }

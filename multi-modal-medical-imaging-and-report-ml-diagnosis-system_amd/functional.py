@@ -205,7 +205,7 @@ class _DropoutFn(torch.autograd.Function):
         y = torch.empty_like(x)
         mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
         call("mmdx_dropout_fwd", L.dtype_code(x.dtype), ptr(x), x.numel(), float(p), seed,
-             offset, ptr(y), ptr(mask), stream())
+             offset, ptr(L.rng_counter(x.device)), ptr(y), ptr(mask), stream())
         ctx.save_for_backward(mask)
         ctx.p = p
         return y
@@ -223,7 +223,8 @@ class _DropoutFn(torch.autograd.Function):
 def dropout(x, p, training):
     if not training or p == 0.0:
         return x
-    _DROPOUT_SEED[0] += 1
+    # the device counter (L.rng_counter) advances per launch; the host seed stays fixed so
+    # the call is graph-replayable
     return _DropoutFn.apply(x, p, _DROPOUT_SEED[0], 0)
 
 

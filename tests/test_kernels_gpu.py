@@ -288,3 +288,40 @@ def test_adamw_matches_torch(dev):
         o_mine.step()
     for a, b in zip(mine, ref):
         assert torch.allclose(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_dropout_counter_rng_and_graph_replay(dev, dt):
+    """nn.Dropout semantics (TP:538): keep rate 1-p, kept values scaled by 1/(1-p), backward
+    = dy * mask / (1-p); the device counter gives a fresh mask on every call, also when the
+    launch is replayed from a captured graph."""
+    from mmdx import functional as F
+    n, p = 1 << 18, 0.1
+    x = torch.ones(n, dtype=dt, device=dev)
+    y1 = F.dropout(x, p, True)
+    y2 = F.dropout(x, p, True)
+    keep = (y1 != 0).float().mean().item()
+    assert abs(keep - (1 - p)) < 0.005
+    kept = y1[y1 != 0].float()
+    assert torch.allclose(kept, torch.full_like(kept, 1 / (1 - p)), rtol=1e-2 if dt != torch.float32 else 1e-6)
+    assert not torch.equal(y1 != 0, y2 != 0)
+    xr = torch.randn(n, dtype=torch.float32, device=dev).to(dt).requires_grad_(True)
+    yr = F.dropout(xr, p, True)
+    dy = torch.randn(n, dtype=torch.float32, device=dev).to(dt)
+    yr.backward(dy)
+    m = (yr != 0) | (xr == 0)
+    ref = torch.where(m, dy.float() / (1 - p), torch.zeros_like(dy.float()))
+    assert torch.allclose(xr.grad.float(), ref, rtol=1e-2 if dt != torch.float32 else 1e-6, atol=1e-6)
+    # graph capture: two replays, two different masks
+    static_x = torch.ones(n, dtype=dt, device=dev)
+    F.dropout(static_x, p, True)  # warm up allocations
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_y = F.dropout(static_x, p, True)
+    g.replay()
+    m1 = (static_y != 0).clone()
+    g.replay()
+    m2 = (static_y != 0).clone()
+    assert not torch.equal(m1, m2)
+    assert abs(m2.float().mean().item() - (1 - p)) < 0.005
