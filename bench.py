@@ -311,14 +311,18 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # The whole train step (both streams, backward, clip, AdamW) is captured once into a
-    # hipGraph and replayed: no per-kernel host launch cost inside the timed region.  N>1
-    # stays eager unless MMDX_GRAPH_DIST=1 (RCCL collectives inside the capture).
-    use_graph = os.environ.get("MMDX_GRAPH", "1") == "1" and (
-        world == 1 or os.environ.get("MMDX_GRAPH_DIST") == "1")
+    # Launch mode.  Default "0": eager launches from the host (the two towers overlap on two
+    # streams).  "step" (MMDX_GRAPH=step): the whole step captured into one hipGraph and
+    # replayed — measured slower on ROCm 7 (the replay runs the two stream branches one after
+    # the other: 26.8 vs 22.5 ms/step at C4), so it is opt-in.  N>1 always eager.
+    mode = os.environ.get("MMDX_GRAPH", "0")
+    if world > 1:
+        mode = "0"
+    use_graph = mode != "0"
     run = step
+    eager_step = step
     static_loss = None
-    if use_graph:
+    if mode == "step":
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(graph):
@@ -339,13 +343,14 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if use_graph:
+    if mode == "step":
         loss = static_loss
+    if use_graph:
         # conv kernel durations for the roofline: HIP events around each conv launch in a few
         # eager steps after the timed region (same kernels as the replayed graph)
         timer.enabled = True
         for _ in range(3):
-            step()
+            eager_step()
         torch.cuda.synchronize()
     conv_steps = 3 if use_graph else args.steps
     timer.enabled = False
@@ -377,7 +382,7 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
-        "launch": "hipgraph" if use_graph else "eager",
+        "launch": "hipgraph-step" if mode == "step" else "eager",
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,
                    "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,

@@ -20,6 +20,22 @@ from ._lib import call, ptr, stream
 
 CHUNK = 1 << 16  # elements per workgroup descriptor
 
+# Pinned staging buffers cannot be allocated while a stream is capturing a graph, so every
+# eagerly built table leaves a spare of its size behind for a later capture to take.
+_PINNED_SPARES: list = []
+
+
+def _pinned(nbytes: int) -> torch.Tensor:
+    if torch.cuda.is_current_stream_capturing():
+        for i, t in enumerate(_PINNED_SPARES):
+            if t.numel() >= nbytes:
+                return _PINNED_SPARES.pop(i)
+        raise RuntimeError("mmdx AdamW: no pinned staging buffer reserved for graph capture; "
+                           "run one eager step before capturing")
+    while sum(t.numel() >= nbytes for t in _PINNED_SPARES) < 2:  # AdamW + grad-norm tables
+        _PINNED_SPARES.append(torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+    return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+
 
 class _Table:
     """Device copy of an mmdx_adamw_tensor[] chunk table (kept alive with its pinned host
@@ -41,11 +57,14 @@ class _Table:
         for i, d in enumerate(descs):
             arr[i] = L.AdamWTensor(*d)
         nbytes = C.sizeof(arr)
-        self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.host = _pinned(nbytes)
         C.memmove(self.host.data_ptr(), C.addressof(arr), nbytes)
         self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
         self.dev.copy_(self.host, non_blocking=True)
         self.n, self.total = n, total
+
+
+_CAPTURED: list = []  # tables referenced by captured graphs: their host/device copies must live
 
 
 def _table_for(cache: dict, entries, device):
@@ -55,6 +74,8 @@ def _table_for(cache: dict, entries, device):
         if len(cache) > 8:
             cache.clear()
         t = cache[key] = _Table(entries, device)
+        if torch.cuda.is_current_stream_capturing():
+            _CAPTURED.append(t)
     return t
 
 
