@@ -106,10 +106,13 @@ int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
 /* dy: grad w.r.t. y; y: forward output (ReLU mask source).  Writes dx, d_residual
  * (may be NULL), and dgamma/dbeta (fp32, accumulated with beta_acc). */
 int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
-                long rows, int C, const float* gamma, const float* save_mean,
-                const float* save_rstd, int relu, void* dx, void* d_residual,
-                float* dgamma, float* dbeta, float beta_acc,
+                long rows, int C, const float* gamma, const float* bn_beta,
+                const float* save_mean, const float* save_rstd, int relu, void* dx,
+                void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                 void* workspace, size_t ws_bytes, void* stream);
+/* relu with y == NULL (a unit without residual): the ReLU mask is recomputed from x as
+ * x*scale + shift > 0 with the forward's own scale/shift (gamma, bn_beta, save_mean,
+ * save_rstd), so the post-activation tensor is not read. */
 
 /* ---------------------------------------------------------------- pooling
  * Replaces: resnet maxpool 3x3/2 (backbone[3]) and AdaptiveAvgPool2d(1) (backbone[8])

@@ -50,8 +50,8 @@ SIGNATURES = {
     "mmdx_bn_workspace_size": (sz, [i64, i32]),
     "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, i32, i64, vp, vp, vp, vp, f32, f32, vp, vp,
                           vp, i32, vp, vp, sz, vp]),
-    "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, i32, vp, vp, vp, vp, f32,
-                          vp, sz, vp]),
+    "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp,
+                          f32, vp, sz, vp]),
     "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,
                                vp]),
     "mmdx_maxpool_bwd": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp,

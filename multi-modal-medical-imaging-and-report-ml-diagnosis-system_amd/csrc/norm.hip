@@ -177,6 +177,15 @@ __host__ __device__ inline RowTile row_tile(int C, int vec) {
   return t;
 }
 
+// The forward's per-channel scale/shift, recomputed with the same expression order as
+// bn_finalize_kernel / bn_eval_coef_kernel so the recomputed pre-activation is bit-equal.
+__device__ __forceinline__ void bn_coef(const float* gamma, const float* beta, float mean,
+                                        float rstd, int c, float& scale, float& shift) {
+  const float g = gamma ? gamma[c] : 1.f;
+  scale = g * rstd;
+  shift = (beta ? beta[c] : 0.f) - mean * g * rstd;
+}
+
 // y = act(x*scale[c] + shift[c] (+ res))
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
@@ -218,30 +227,33 @@ template <typename T>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
     int ct, long rpb, const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
-    float2* __restrict__ part) {
+    const float* __restrict__ gamma, const float* __restrict__ bbeta, float2* __restrict__ part) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   __shared__ float s_a[BN_NT * VEC], s_b[BN_NT * VEC];
   const int tx = threadIdx.x % ct, ty = threadIdx.x / ct, rt = BN_NT / ct;
   const int c0 = (blockIdx.y * ct + tx) * VEC;
   const long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  float sg[VEC], sgx[VEC], mu[VEC], rs[VEC];
+  float sg[VEC], sgx[VEC], mu[VEC], rs[VEC], sc[VEC], sh[VEC];
+  const bool mask_x = relu && !y;  // ReLU mask recomputed from x (no residual)
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {
     sg[j] = sgx[j] = 0.f;
     mu[j] = c0 < C ? mean[c0 + j] : 0.f;
     rs[j] = c0 < C ? rstd[c0 + j] : 0.f;
+    bn_coef(gamma, bbeta, mu[j], rs[j], c0 < C ? c0 + j : 0, sc[j], sh[j]);
   }
   if (c0 < C) {
     for (long r = r0 + ty; r < r1; r += rt) {
       const V vx = *(const V*)(x + r * C + c0);
       const V vd = *(const V*)(dy + r * C + c0);
       V vy{};
-      if (relu) vy = *(const V*)(y + r * C + c0);
+      if (relu && !mask_x) vy = *(const V*)(y + r * C + c0);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         float g = to_f(vd[j]);
-        if (relu && !(to_f(vy[j]) > 0.f)) g = 0.f;
+        const float a = mask_x ? to_f(vx[j]) * sc[j] + sh[j] : to_f(vy[j]);
+        if (relu && !(a > 0.f)) g = 0.f;
         sg[j] += g;
         sgx[j] += g * (to_f(vx[j]) - mu[j]) * rs[j];
       }
@@ -303,13 +315,15 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
     const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ coef, int relu, T* __restrict__ dx, T* __restrict__ dres) {
+    const float* __restrict__ coef, int relu, const float* __restrict__ gamma,
+    const float* __restrict__ bbeta, T* __restrict__ dx, T* __restrict__ dres) {
+  const bool mask_x = relu && !y;
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   const RowTile rt = row_tile(C, VEC);
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
-    float ca[VEC], cb[VEC], ck[VEC];
+    float ca[VEC], cb[VEC], ck[VEC], sc[VEC], sh[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
       const int c = j * VEC + e;
@@ -317,18 +331,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       ca[e] = coef[c];
       cb[e] = coef[C + c] - k * mean[c];
       ck[e] = k;
+      bn_coef(gamma, bbeta, mean[c], rstd[c], c, sc[e], sh[e]);
     }
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
       const V vx = ((const V*)x)[i];
       const V vd = ((const V*)dy)[i];
       V vy{};
-      if (relu) vy = ((const V*)y)[i];
+      if (relu && !mask_x) vy = ((const V*)y)[i];
       V o, og;
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         float g = to_f(vd[e]);
-        if (relu && !(to_f(vy[e]) > 0.f)) g = 0.f;
+        const float a = mask_x ? to_f(vx[e]) * sc[e] + sh[e] : to_f(vy[e]);
+        if (relu && !(a > 0.f)) g = 0.f;
         o[e] = from_f<T>(ca[e] * g + cb[e] + ck[e] * to_f(vx[e]));
         og[e] = from_f<T>(g);
       }
@@ -388,7 +404,8 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
 
 template <typename T>
 static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, long rows, int C,
-                    const float* gamma, const float* smean, const float* srstd, int relu,
+                    const float* gamma, const float* bbeta, const float* smean,
+                    const float* srstd, int relu,
                     void* dx, void* dres, float* dgamma, float* dbeta, float beta_acc, void* ws,
                     size_t ws_bytes, hipStream_t st) {
   constexpr int VEC = Vec16<T>::N;
@@ -400,13 +417,13 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   float* coef = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
   hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
-                     smean, srstd, relu, part);
+                     smean, srstd, relu, gamma, bbeta, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
                      (const float2*)part, L.rblocks, rows, C, train, gamma, srstd, dgamma,
                      dbeta, beta_acc, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, smean, srstd,
-                     (const float*)coef, relu, (T*)dx, (T*)dres);
+                     (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -607,17 +624,18 @@ extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C
 }
 
 extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
-                           long rows, int C, const float* gamma, const float* save_mean,
-                           const float* save_rstd, int relu, void* dx, void* d_residual,
-                           float* dgamma, float* dbeta, float beta_acc, void* ws,
-                           size_t ws_bytes, void* stream) {
-  MMDX_CHECK_ARG(rows > 0 && C > 0 && (!relu || y), "bn bwd: bad args");
+                           long rows, int C, const float* gamma, const float* bn_beta,
+                           const float* save_mean, const float* save_rstd, int relu, void* dx,
+                           void* d_residual, float* dgamma, float* dbeta, float beta_acc,
+                           void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(rows > 0 && C > 0, "bn bwd: bad args");
+  MMDX_CHECK_ARG(!(relu && !y && d_residual), "bn bwd: a residual unit needs its output y");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == BF16)
-    return bn_bwd_t<bf16>(train, x, y, dy, rows, C, gamma, save_mean, save_rstd, relu, dx,
-                          d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
-  return bn_bwd_t<float>(train, x, y, dy, rows, C, gamma, save_mean, save_rstd, relu, dx,
-                         d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+    return bn_bwd_t<bf16>(train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd, relu,
+                          dx, d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+  return bn_bwd_t<float>(train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd, relu,
+                         dx, d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
 }
 
 extern "C" int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual, long rows,

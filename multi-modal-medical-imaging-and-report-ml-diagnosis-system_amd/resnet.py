@@ -242,8 +242,11 @@ def _unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False):
     db = torch.empty(K, dtype=torch.float32, device=dev)
     ws_n = L.lib().mmdx_bn_workspace_size(rows, K)
     ws = L.workspace(ws_n, dev)
-    call("mmdx_bn_bwd", dt, int(u.train), ptr(u.y), ptr(u.out), ptr(dout), rows, K,
-         ptr(u.bn.weight), ptr(u.mean), ptr(u.rstd), int(u.relu), ptr(dconv), ptr(dres),
+    # units without a residual recompute their ReLU mask from y (out is not read)
+    out = u.out if want_res else None
+    call("mmdx_bn_bwd", dt, int(u.train), ptr(u.y), ptr(out), ptr(dout), rows, K,
+         ptr(u.bn.weight), ptr(u.bn.bias), ptr(u.mean), ptr(u.rstd), int(u.relu), ptr(dconv),
+         ptr(dres),
          ptr(dg), ptr(db), 0.0, ptr(ws), ws_n, st)
     dw = torch.empty_like(u.conv.weight)
     ws_n = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)

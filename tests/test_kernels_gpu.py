@@ -188,9 +188,15 @@ def test_batchnorm(dev, dt, train, res, relu):
     dg = torch.empty(C, device=dev)
     db = torch.empty(C, device=dev)
     L.call("mmdx_bn_bwd", dc, train, xd.data_ptr(), y.data_ptr(), dyd.data_ptr(), rows, C,
-           gam.data_ptr(), mean.data_ptr(), rstd.data_ptr(), int(relu), dx.data_ptr(),
-           dres.data_ptr() if res else None, dg.data_ptr(), db.data_ptr(), 0.0, ws.data_ptr(),
-           ws_n, L.stream())
+           gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), int(relu),
+           dx.data_ptr(), dres.data_ptr() if res else None, dg.data_ptr(), db.data_ptr(), 0.0,
+           ws.data_ptr(), ws_n, L.stream())
+    if relu and not res:  # mask recomputed from x instead of read from y: identical result
+        dx2 = torch.empty_like(xd)
+        L.call("mmdx_bn_bwd", dc, train, xd.data_ptr(), None, dyd.data_ptr(), rows, C,
+               gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
+               dx2.data_ptr(), None, None, None, 0.0, ws.data_ptr(), ws_n, L.stream())
+        assert torch.equal(dx2, dx)
     tol_dt = dt
     _close(dx.permute(0, 3, 1, 2), xr.grad, tol_dt, "bn dx")
     _close(dg, bn.weight.grad, tol_dt, "dgamma")
