@@ -216,6 +216,10 @@ int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const voi
  * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);
  * w_hh: [2][4H][H] compute dtype; h_out: [B, L, 2H]; saved c: [2, L, B, H] fp32,
  * gates: [2, L, B, 4H] fp32 post-activation (for backward). */
+/* Workspace for the cooperative bf16 forward (H = 256, B <= 256): h exchange + counters.
+ * 0 when that path does not apply (then ws may be NULL and the batch-partitioned kernel
+ * runs). */
+size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H);
 int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
                   void* h_out, float* c_save, float* gates_save, void* workspace,
                   size_t ws_bytes, void* stream);

@@ -86,6 +86,7 @@ SIGNATURES = {
     "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp, sz, vp]),
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_lstm_fwd_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
     "mmdx_adamw_multi": (i32, [i32, vp, f32, f32, f32, vp, vp, vp]),
     "mmdx_grad_norm_workspace_size": (sz, [i32]),

@@ -55,8 +55,10 @@ class _LSTMLayerFn(torch.autograd.Function):
         hout = torch.empty((B, Ls, 2 * H), dtype=T, device=dev)
         cs = torch.empty((2, Ls, B, H), dtype=torch.float32, device=dev)
         gs = torch.empty((2, Ls, B, G4), dtype=torch.float32, device=dev)
+        fw = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(T), B, Ls, H)
+        fws = L.workspace(fw, dev)
         call("mmdx_lstm_fwd", L.dtype_code(T), ptr(xg), ptr(whh), B, Ls, H, ptr(hout), ptr(cs),
-             ptr(gs), None, 0, stream())
+             ptr(gs), ptr(fws), fw, stream())
         ctx.save_for_backward(x, wih, whh, hout, cs, gs)
         ctx.H = H
         return hout

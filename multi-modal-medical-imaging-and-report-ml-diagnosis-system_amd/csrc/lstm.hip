@@ -204,6 +204,124 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Cooperative forward (bf16, H = 256): per direction a group of COOP_NB workgroups, each
+// owning COOP_UB hidden units (their i, f, g, o rows of W_hh = 128 x 256 bf16, held in
+// REGISTERS for all L steps) and every batch row.  Per step a workgroup loads h_{t-1}
+// (B x 256) into LDS, computes its 128 gate columns with MFMA, does the cell update in
+// registers (each lane holds i, f, g, o of the same (row, unit) in the same accumulator
+// slot), publishes its h_t slice to a double-buffered exchange array, and meets the other
+// workgroups of its direction at a counter barrier (agent-scope release / acquire).
+// W_hh is read once instead of once per step per workgroup, and no gate tile goes
+// through LDS.  Outputs use the batch-partitioned kernel's layouts (same backward).
+// ---------------------------------------------------------------------------------------
+constexpr int COOP_NB = 8;                 // workgroups per direction
+constexpr int COOP_H = 256;
+constexpr int COOP_UB = COOP_H / COOP_NB;  // 32 units per workgroup
+constexpr int COOP_LDH = COOP_H + 8;       // padded h row (bf16): conflict-free b128 reads
+constexpr long COOP_SPIN_MAX = 1L << 26;   // bounded wait: a lost peer ends the kernel
+
+__device__ __forceinline__ void coop_barrier(unsigned* ctr, unsigned target, int* err) {
+  // every wave's stores are issued; make them visible at agent scope, then arrive
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > COOP_SPIN_MAX) { *err = 1; break; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// RT = 16-row tiles per wave (B <= 64 * RT): 8 waves = 2 unit groups x 4 row groups.
+template <int RT>
+__global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
+    const float* __restrict__ xg, const bf16* __restrict__ whh, int B, int L,
+    bf16* __restrict__ hout, float* __restrict__ csave, float* __restrict__ gsave,
+    bf16* __restrict__ hx, unsigned* __restrict__ ctr, int* __restrict__ err) {
+  constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
+  __shared__ __attribute__((aligned(16))) bf16 sh[64 * RT * COOP_LDH];
+  const int dir = blockIdx.y, blk = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ug = wid & 1, rg = wid >> 1;
+  const int u0 = blk * COOP_UB + ug * 16;   // this wave's 16 units
+  const int ucol = u0 + (lane & 15);        // this lane's unit (accumulator column)
+  // W fragments: gate g, unit u0 + (lane & 15), k = ks*32 + 8*(lane >> 4) .. +7
+  const bf16* W = whh + (long)dir * G4 * H;
+  bf16x8 wf[4][KS];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[g][ks] = *(const bf16x8*)(W + (long)(g * H + ucol) * H + ks * 32 + 8 * (lane >> 4));
+  float creg[RT][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) creg[i][r] = 0.f;
+  unsigned* myctr = ctr + dir;
+  bf16* hxd = hx + (long)dir * 2 * B * H;
+  const int nrows = 64 * RT;
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    // h_{t-1} -> LDS (zeros at the first step)
+    const bf16* hsrc = hxd + (long)((s + 1) & 1) * B * H;
+    for (int e = threadIdx.x; e < nrows * (H / 8); e += 512) {
+      const int row = e / (H / 8), c8 = e - row * (H / 8);
+      bf16x8 v{};
+      if (s > 0 && row < B) v = *(const bf16x8*)(hsrc + (long)row * H + c8 * 8);
+      *(bf16x8*)(sh + row * COOP_LDH + c8 * 8) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      const int rt16 = (rg + 4 * i) * 16;  // this row tile's first row
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bf16* arow = sh + (rt16 + (lane & 15)) * COOP_LDH + 8 * (lane >> 4);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 af = *(const bf16x8*)(arow + ks * 32);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[g][ks], acc[g], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = rt16 + (lane >> 4) * 4 + r;
+        if (b >= B) continue;
+        const float* xp = xg + (((long)b * L + t) * 2 + dir) * G4;
+        const float gi = sigm(acc[0][r] + xp[ucol]);
+        const float gf = sigm(acc[1][r] + xp[H + ucol]);
+        const float gg = tanhf(acc[2][r] + xp[2 * H + ucol]);
+        const float go = sigm(acc[3][r] + xp[3 * H + ucol]);
+        const float c = gf * creg[i][r] + gi * gg;
+        creg[i][r] = c;
+        const bf16 h = from_f<bf16>(go * tanhf(c));
+        hxd[(long)(s & 1) * B * H + (long)b * H + ucol] = h;
+        hout[((long)b * L + t) * 2 * H + dir * H + ucol] = h;
+        const long sidx = ((long)dir * L + t) * B + b;
+        csave[sidx * H + ucol] = c;
+        float* gp = gsave + sidx * G4;
+        gp[ucol] = gi;
+        gp[H + ucol] = gf;
+        gp[2 * H + ucol] = gg;
+        gp[3 * H + ucol] = go;
+      }
+    }
+    if (s + 1 < L) coop_barrier(myctr, (unsigned)(COOP_NB * (s + 1)), err);
+    if (*(volatile int*)err) return;  // a peer never arrived: give up (results invalid)
+  }
+}
+
 template <typename T>
 __global__ void transpose_whh_kernel(const T* __restrict__ w, int H, T* __restrict__ wt) {
   const int G4 = 4 * H;
@@ -239,11 +357,40 @@ static int lstm_fwd_t(const void* xg, const void* whh, int B, int L, int H, void
 
 using namespace mmdx;
 
+// cooperative forward applies to bf16, H = 256, B <= 256
+static bool coop_ok(int dtype, int B, int H) { return dtype == BF16 && H == COOP_H && B <= 256; }
+
+extern "C" size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H) {
+  (void)L;
+  if (!coop_ok(dtype, B, H)) return 0;
+  // h exchange [2 dir][2 parity][B][H] bf16 + 2 counters + error flag
+  return (size_t)2 * 2 * B * H * 2 + 256;
+}
+
 extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
                              void* h_out, float* c_save, float* gates_save, void* ws,
                              size_t ws_bytes, void* stream) {
   MMDX_CHECK_ARG(B > 0 && L > 0 && c_save && gates_save, "lstm fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
+  const size_t need = mmdx_lstm_fwd_workspace_size(dtype, B, L, H);
+  if (need && ws && ws_bytes >= need) {
+    bf16* hx = (bf16*)ws;
+    unsigned* ctr = (unsigned*)((char*)ws + (size_t)2 * 2 * B * H * 2);
+    int* err = (int*)(ctr + 4);
+    hipMemsetAsync(ctr, 0, 64, st);
+    const dim3 grid(COOP_NB, 2);
+    if (B <= 64)
+      hipLaunchKernelGGL(lstm_fwd_coop_kernel<1>, grid, dim3(512), 0, st, (const float*)xg,
+                         (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr, err);
+    else if (B <= 128)
+      hipLaunchKernelGGL(lstm_fwd_coop_kernel<2>, grid, dim3(512), 0, st, (const float*)xg,
+                         (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr, err);
+    else
+      hipLaunchKernelGGL(lstm_fwd_coop_kernel<4>, grid, dim3(512), 0, st, (const float*)xg,
+                         (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr, err);
+    MMDX_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == BF16) return lstm_fwd_t<bf16>(xg, w_hh, B, L, H, h_out, c_save, gates_save, st);
   return lstm_fwd_t<float>(xg, w_hh, B, L, H, h_out, c_save, gates_save, st);
 }

@@ -177,6 +177,16 @@ __host__ __device__ inline RowTile row_tile(int C, int vec) {
   return t;
 }
 
+// VEC consecutive per-channel floats (16-B aligned: C % VEC == 0) with vector loads
+template <int VEC>
+__device__ __forceinline__ void load_coef(const float* p, float* out) {
+#pragma unroll
+  for (int e = 0; e < VEC; e += 4) {
+    const f32x4 v = *(const f32x4*)(p + e);
+    out[e] = v[0]; out[e + 1] = v[1]; out[e + 2] = v[2]; out[e + 3] = v[3];
+  }
+}
+
 // The forward's per-channel scale/shift, recomputed with the same expression order as
 // bn_finalize_kernel / bn_eval_coef_kernel so the recomputed pre-activation is bit-equal.
 __device__ __forceinline__ void bn_coef(const float* gamma, const float* beta, float mean,
@@ -199,11 +209,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
     float sc[VEC], sh[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      sc[e] = scale[j * VEC + e];
-      sh[e] = shift[j * VEC + e];
-    }
+    load_coef<VEC>(scale + j * VEC, sc);
+    load_coef<VEC>(shift + j * VEC, sh);
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
       const V v = ((const V*)x)[i];
@@ -283,7 +290,8 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
 constexpr int FIN_C = 8, FIN_P = 32;  // channels x slab lanes per block
 __global__ __launch_bounds__(FIN_C * FIN_P) void bn_bwd_finalize_kernel(
     const float2* __restrict__ part, int nblk, long rows, int C, int train,
-    const float* __restrict__ gamma, const float* __restrict__ rstd, float* dgamma,
+    const float* __restrict__ gamma, const float* __restrict__ bbeta,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* dgamma,
     float* dbeta, float beta_acc, float* coef) {
   __shared__ float sa[FIN_P][FIN_C], sb[FIN_P][FIN_C];
   const int cl = threadIdx.x % FIN_C, pl = threadIdx.x / FIN_C;
@@ -304,10 +312,17 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void bn_bwd_finalize_kernel(
   for (int q = 0; q < FIN_P; ++q) { sg += sa[q][cl]; sgx += sb[q][cl]; }
   if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
   if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;
+  // dx = a*g + cb + ck*x  (== a*g + b + k*xhat);  scale/shift: the forward's pre-activation
   const float a = (gamma ? gamma[c] : 1.f) * rstd[c];
+  const float b = train ? -a * sg / (float)rows : 0.f;
+  const float k = (train ? -a * sgx / (float)rows : 0.f) * rstd[c];
   coef[c] = a;
-  coef[C + c] = train ? -a * sg / (float)rows : 0.f;
-  coef[2 * C + c] = train ? -a * sgx / (float)rows : 0.f;
+  coef[C + c] = b - k * mean[c];
+  coef[2 * C + c] = k;
+  float sc, sh;
+  bn_coef(gamma, bbeta, mean[c], rstd[c], c, sc, sh);
+  coef[3 * C + c] = sc;
+  coef[4 * C + c] = sh;
 }
 
 // dx = a*g + b + k*xhat  ==  a*g + (b - k*mean*rstd) + (k*rstd)*x,  g = dy*relu'(y)
@@ -324,15 +339,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
     float ca[VEC], cb[VEC], ck[VEC], sc[VEC], sh[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const int c = j * VEC + e;
-      const float k = coef[2 * C + c] * rstd[c];
-      ca[e] = coef[c];
-      cb[e] = coef[C + c] - k * mean[c];
-      ck[e] = k;
-      bn_coef(gamma, bbeta, mean[c], rstd[c], c, sc[e], sh[e]);
-    }
+    load_coef<VEC>(coef + j * VEC, ca);
+    load_coef<VEC>(coef + C + j * VEC, cb);
+    load_coef<VEC>(coef + 2 * C + j * VEC, ck);
+    load_coef<VEC>(coef + 3 * C + j * VEC, sc);
+    load_coef<VEC>(coef + 4 * C + j * VEC, sh);
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
       const V vx = ((const V*)x)[i];
@@ -354,9 +365,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// >= 4 row iterations per block so the per-channel coefficient loads are amortised
 static int grid_rows(long rows, int C, int vec) {
   const RowTile rt = row_tile(C, vec);
-  return (int)std::max<long>(1, std::min<long>((rows + rt.rpi - 1) / rt.rpi, 4096));
+  const long iters = (rows + rt.rpi - 1) / rt.rpi;
+  return (int)std::max<long>(1, std::min<long>((iters + 3) / 4, 4096));
 }
 
 template <typename T>
@@ -411,7 +424,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   constexpr int VEC = Vec16<T>::N;
   MMDX_CHECK_ARG(C % VEC == 0, "bn bwd: C=%d must be a multiple of %d", C, VEC);
   const BnLayout L = bn_layout(rows, C, VEC);
-  const size_t need = (size_t)L.rblocks * C * sizeof(float2) + 3 * (size_t)C * sizeof(float);
+  const size_t need = (size_t)L.rblocks * C * sizeof(float2) + 5 * (size_t)C * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "bn bwd: workspace %zu < %zu", ws_bytes, need);
   float2* part = (float2*)ws;
   float* coef = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
@@ -419,8 +432,8 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
                      smean, srstd, relu, gamma, bbeta, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
-                     (const float2*)part, L.rblocks, rows, C, train, gamma, srstd, dgamma,
-                     dbeta, beta_acc, coef);
+                     (const float2*)part, L.rblocks, rows, C, train, gamma, bbeta, smean, srstd,
+                     dgamma, dbeta, beta_acc, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, smean, srstd,
                      (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres);
@@ -600,7 +613,7 @@ extern "C" size_t mmdx_bn_workspace_size(long rows, int C) {
   const BnLayout L = bn_layout(rows, C, 4);  // fp32 layout has the most row blocks
   const BnLayout L8 = bn_layout(rows, C, 8);
   const int nb = std::max(L.rblocks, L8.rblocks);
-  return (size_t)nb * C * sizeof(float2) + 3 * (size_t)C * sizeof(float);
+  return (size_t)nb * C * sizeof(float2) + 5 * (size_t)C * sizeof(float);
 }
 
 extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,

@@ -156,3 +156,31 @@ def test_text_encoder_transformer_bert(dev, dt):
     tol = 1e-4 if dt == torch.float32 else 5e-2
     assert rel_err(out["embeddings"], out_ref["embeddings"]) <= tol
     assert rel_err(out["logits"], out_ref["logits"]) <= tol
+
+
+@pytest.mark.parametrize("B", [128, 200])
+def test_lstm_coop_forward_matches_partitioned(dev, B):
+    """The cooperative bf16 recurrence (W_hh in registers, h exchanged through a counter
+    barrier) reproduces the batch-partitioned kernel (same MFMA k order; fp32 contraction
+    order of the cell update may differ, so h may differ by one bf16 ulp): max abs
+    difference <= 1e-2 on h (bf16, |h| < 1), c and gates."""
+    H, Ls = 256, 24
+    g = torch.Generator().manual_seed(B)
+    xg = (torch.randn(B * Ls, 2 * 4 * H, generator=g) * 0.5).to(dev)
+    whh = (torch.randn(2 * 4 * H, H, generator=g) * 0.05).to(dev, torch.bfloat16)
+    outs = []
+    for coop in (True, False):
+        hout = torch.empty(B, Ls, 2 * H, dtype=torch.bfloat16, device=dev)
+        cs = torch.empty(2, Ls, B, H, device=dev)
+        gs = torch.empty(2, Ls, B, 4 * H, device=dev)
+        n = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(torch.bfloat16), B, Ls, H) if coop else 0
+        assert (n > 0) == coop
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=dev)
+        L.call("mmdx_lstm_fwd", L.dtype_code(torch.bfloat16), xg.data_ptr(), whh.data_ptr(), B,
+               Ls, H, hout.data_ptr(), cs.data_ptr(), gs.data_ptr(),
+               ws.data_ptr() if coop else None, n, L.stream())
+        torch.cuda.synchronize()
+        outs.append((hout.float(), cs, gs))
+    for a, b in zip(outs[0], outs[1]):
+        assert (a - b).abs().max().item() <= 1e-2 * max(1.0, b.abs().max().item())
+        assert (a - b).abs().mean().item() <= 1e-4
