@@ -28,7 +28,7 @@ static BnLayout bn_layout(long rows, int C, int vec) {
   L.ct = std::min(cv, 64);
   L.rt = BN_NT / L.ct;
   L.cgroups = (cv + L.ct - 1) / L.ct;
-  long target = std::max(1L, 512L / L.cgroups);
+  long target = std::max(1L, 2048L / L.cgroups);  // ~8 blocks per CU for latency hiding
   long rpb = (rows + target - 1) / target;
   rpb = std::max<long>(rpb, L.rt);
   L.rows_per_block = (rpb + L.rt - 1) / L.rt * L.rt;
@@ -102,40 +102,47 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x
 // mean = sum(n_b mean_b) / N, then M2 = sum(M2_b + n_b (mean_b - mean)^2) — the exact
 // two-level decomposition of the variance, reduced in a fixed lane/shuffle order
 // (deterministic).  Conv-epilogue statistics give one slab per 128 output rows.
-constexpr int FIN_W = 4;  // channels (waves) per block
-__global__ __launch_bounds__(64 * FIN_W) void bn_finalize_kernel(
+constexpr int FIN_W = 4;  // channels per 256-thread block when one wave serves a channel
+
+// sum over this channel's slabs of f(b): TPC threads, 4 independent accumulators each
+// (4 slab loads in flight), fixed-order wave / block reduction (deterministic)
+template <int TPC, class F>
+__device__ __forceinline__ float slab_sum(int nblk, int sub, float* red, F f) {
+  float a4[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = sub; b0 < nblk; b0 += 4 * TPC) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + TPC * j;
+      if (b < nblk) a4[j] += f(b);
+    }
+  }
+  const float v = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  if constexpr (TPC == 64) return wave_sum(v);
+  else return block_sum<256>(v, red);
+}
+
+// TPC = threads per channel: 64 (one wave; few slabs) or 256 (whole block; thousands of
+// slabs, e.g. the 3136 per-128-row slabs of a layer1 conv at batch 128)
+template <int TPC>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
     const float2* __restrict__ part, int nblk, long rows, long rpb, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
     float* running_var, float momentum, float eps, float* save_mean, float* save_rstd,
     float* scale, float* shift) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * FIN_W + (threadIdx.x >> 6);
-  if (c >= C) return;
+  __shared__ float red[4];
+  const int sub = threadIdx.x % TPC;
+  const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
+  if (c >= C) return;  // uniform per wave (TPC = 64) or per block (TPC = 256)
   const long last = rows - (long)(nblk - 1) * rpb;  // rows of the final (short) slab
-  // 4 independent accumulators per lane keep 4 slab loads in flight (fixed order)
-  float s4[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b0 = lane; b0 < nblk; b0 += 256) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int b = b0 + 64 * j;
-      if (b < nblk) s4[j] += (b == nblk - 1 ? (float)last : (float)rpb) * part[(long)b * C + c].x;
-    }
-  }
-  const float mean = wave_sum((s4[0] + s4[1]) + (s4[2] + s4[3])) / (float)rows;
-  float q4[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b0 = lane; b0 < nblk; b0 += 256) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int b = b0 + 64 * j;
-      if (b < nblk) {
-        const float nb = b == nblk - 1 ? (float)last : (float)rpb;
-        const float2 p = part[(long)b * C + c];
-        const float d = p.x - mean;
-        q4[j] += p.y + nb * d * d;
-      }
-    }
-  }
-  const float m2 = wave_sum((q4[0] + q4[1]) + (q4[2] + q4[3]));
+  const float mean = slab_sum<TPC>(nblk, sub, red, [&](int b) {
+    return (b == nblk - 1 ? (float)last : (float)rpb) * part[(long)b * C + c].x;
+  }) / (float)rows;
+  const float m2 = slab_sum<TPC>(nblk, sub, red, [&](int b) {
+    const float2 p = part[(long)b * C + c];
+    const float d = p.x - mean;
+    return p.y + (b == nblk - 1 ? (float)last : (float)rpb) * d * d;
+  });
+  const int lane = sub;
   if (lane != 0) return;
   const float var = m2 / (float)rows;
   const float rstd = rsqrtf(var + eps);
@@ -244,11 +251,21 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
   float sg[VEC], sgx[VEC], mu[VEC], rs[VEC], sc[VEC], sh[VEC];
   const bool mask_x = relu && !y;  // ReLU mask recomputed from x (no residual)
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) {
-    sg[j] = sgx[j] = 0.f;
-    mu[j] = c0 < C ? mean[c0 + j] : 0.f;
-    rs[j] = c0 < C ? rstd[c0 + j] : 0.f;
-    bn_coef(gamma, bbeta, mu[j], rs[j], c0 < C ? c0 + j : 0, sc[j], sh[j]);
+  for (int j = 0; j < VEC; ++j) sg[j] = sgx[j] = mu[j] = rs[j] = sc[j] = sh[j] = 0.f;
+  if (c0 < C) {
+    load_coef<VEC>(mean + c0, mu);
+    load_coef<VEC>(rstd + c0, rs);
+    if (mask_x) {
+      float ga[VEC], be[VEC];
+      if (gamma) load_coef<VEC>(gamma + c0, ga);
+      if (bbeta) load_coef<VEC>(bbeta + c0, be);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {  // same expression order as bn_coef / the forward
+        const float g = gamma ? ga[j] : 1.f;
+        sc[j] = g * rs[j];
+        sh[j] = (bbeta ? be[j] : 0.f) - mu[j] * g * rs[j];
+      }
+    }
   }
   if (c0 < C) {
     for (long r = r0 + ty; r < r1; r += rt) {
@@ -287,29 +304,21 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
 }
 
 // coef: a[c] = gamma*rstd, b[c] = -gamma*rstd*sum_g/n, k[c] = -gamma*rstd*sum_gx/n
-constexpr int FIN_C = 8, FIN_P = 32;  // channels x slab lanes per block
-__global__ __launch_bounds__(FIN_C * FIN_P) void bn_bwd_finalize_kernel(
+// Per channel: sum the (sum g, sum g*xhat) slab partials (slab_sum), then the apply-pass
+// coefficients.
+template <int TPC>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     const float2* __restrict__ part, int nblk, long rows, int C, int train,
     const float* __restrict__ gamma, const float* __restrict__ bbeta,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* dgamma,
     float* dbeta, float beta_acc, float* coef) {
-  __shared__ float sa[FIN_P][FIN_C], sb[FIN_P][FIN_C];
-  const int cl = threadIdx.x % FIN_C, pl = threadIdx.x / FIN_C;
-  const int c = blockIdx.x * FIN_C + cl;
-  float sg = 0.f, sgx = 0.f;
-  if (c < C) {
-    for (int b = pl; b < nblk; b += FIN_P) {
-      const float2 p = part[(long)b * C + c];
-      sg += p.x;
-      sgx += p.y;
-    }
-  }
-  sa[pl][cl] = sg; sb[pl][cl] = sgx;
-  __syncthreads();
-  if (pl != 0 || c >= C) return;
-  sg = 0.f; sgx = 0.f;
-#pragma unroll
-  for (int q = 0; q < FIN_P; ++q) { sg += sa[q][cl]; sgx += sb[q][cl]; }
+  __shared__ float red[4];
+  const int sub = threadIdx.x % TPC;
+  const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
+  if (c >= C) return;
+  const float sg = slab_sum<TPC>(nblk, sub, red, [&](int b) { return part[(long)b * C + c].x; });
+  const float sgx = slab_sum<TPC>(nblk, sub, red, [&](int b) { return part[(long)b * C + c].y; });
+  if (sub != 0) return;
   if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
   if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;
   // dx = a*g + cb + ck*x  (== a*g + b + k*xhat);  scale/shift: the forward's pre-activation
@@ -399,9 +408,14 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
       hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                          (const T*)x, rows, C, L.ct, L.rows_per_block, part);
     }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_W - 1) / FIN_W), dim3(64 * FIN_W), 0,
-                       st, (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv,
-                       momentum, eps, smean, srstd, scale, shift);
+    if (nblk > 512)
+      hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
+                         (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv, momentum,
+                         eps, smean, srstd, scale, shift);
+    else
+      hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0,
+                         st, (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv,
+                         momentum, eps, smean, srstd, scale, shift);
   } else {
     MMDX_CHECK_ARG(rm && rv, "bn eval: running stats required");
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma,
@@ -431,9 +445,14 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
                      smean, srstd, relu, gamma, bbeta, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st,
-                     (const float2*)part, L.rblocks, rows, C, train, gamma, bbeta, smean, srstd,
-                     dgamma, dbeta, beta_acc, coef);
+  if (L.rblocks > 512)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
+                       (const float2*)part, L.rblocks, rows, C, train, gamma, bbeta, smean,
+                       srstd, dgamma, dbeta, beta_acc, coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0,
+                       st, (const float2*)part, L.rblocks, rows, C, train, gamma, bbeta, smean,
+                       srstd, dgamma, dbeta, beta_acc, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, smean, srstd,
                      (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres);
