@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -37,46 +38,77 @@ def _pinned(nbytes: int) -> torch.Tensor:
     return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
 
 
-class _Table:
-    """Device copy of an mmdx_adamw_tensor[] chunk table (kept alive with its pinned host
-    source): every tensor split into <= CHUNK-element pieces, one workgroup each."""
+# mirrors struct mmdx_adamw_tensor (include/mmdx.h): 4 pointers, long n, long off, 2 floats
+_DESC = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("n", "<i8"),
+                  ("off", "<i8"), ("lr", "<f4"), ("wd", "<f4")])
+assert _DESC.itemsize == C.sizeof(L.AdamWTensor)
 
-    def __init__(self, entries, device):
-        descs = []
-        total = 0
-        for p, g, m, v, lr, wd in entries:
+_CAPTURED: list = []  # staging buffers referenced by captured graphs: they must stay alive
+
+
+class _Plan:
+    """Chunk table of one parameter set: every tensor split into <= CHUNK-element pieces,
+    one workgroup each.  Everything but the gradient pointers is built once; per step only
+    the gradient column is refreshed (numpy) and copied to the device through a small ring
+    of pinned staging buffers (skipped when the gradient buffers did not move)."""
+
+    RING = 3
+
+    def __init__(self, params, ms, vs, lrs, wds, device):
+        tidx, boff, rows = [], [], []
+        for i, (p, m, v, lr, wd) in enumerate(zip(params, ms, vs, lrs, wds)):
             n = p.numel()
-            pp, gp, mp, vp = ptr(p), ptr(g), ptr(m), ptr(v)
+            pp, mp, vp = ptr(p), ptr(m), ptr(v)
             for o in range(0, n, CHUNK):
                 c = min(CHUNK, n - o)
-                b = 4 * o
-                descs.append((pp + b, gp + b, mp + b, vp + b, c, o, float(lr), float(wd)))
-            total += n
-        n = len(descs)
-        arr = (L.AdamWTensor * n)()
-        for i, d in enumerate(descs):
-            arr[i] = L.AdamWTensor(*d)
-        nbytes = C.sizeof(arr)
-        self.host = _pinned(nbytes)
-        C.memmove(self.host.data_ptr(), C.addressof(arr), nbytes)
-        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        self.dev.copy_(self.host, non_blocking=True)
-        self.n, self.total = n, total
+                tidx.append(i)
+                boff.append(4 * o)
+                rows.append((pp + 4 * o, 0, mp + 4 * o, vp + 4 * o, c, o, lr, wd))
+        self.desc = np.array(rows, dtype=_DESC)
+        self.tidx = np.asarray(tidx, dtype=np.int64)
+        self.boff = np.asarray(boff, dtype=np.uint64)
+        self.n = len(rows)
+        self.nbytes = self.desc.nbytes
+        self.dev = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+        self.ring = [torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
+                     for _ in range(self.RING)]
+        self.events = [None] * self.RING
+        self.k = 0
+        self.last = None
+        _PINNED_SPARES.append(torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True))
+
+    def upload(self, grads):
+        gp = np.fromiter((g.data_ptr() for g in grads), dtype=np.uint64, count=len(grads))
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing and self.last is not None and np.array_equal(gp, self.last):
+            return
+        self.desc["g"] = gp[self.tidx] + self.boff
+        if capturing:  # the graph keeps reading this buffer: never reuse it
+            host = _pinned(self.nbytes)
+            _CAPTURED.append(host)
+            self.last = None
+        else:
+            host = self.ring[self.k]
+            if self.events[self.k] is not None:
+                self.events[self.k].synchronize()  # its previous copy has been consumed
+            self.last = gp
+        host.numpy()[: self.nbytes] = self.desc.view(np.uint8)
+        self.dev.copy_(host, non_blocking=True)
+        if not capturing:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[self.k] = ev
+            self.k = (self.k + 1) % self.RING
 
 
-_CAPTURED: list = []  # tables referenced by captured graphs: their host/device copies must live
-
-
-def _table_for(cache: dict, entries, device):
-    key = tuple((ptr(p), ptr(g), float(lr), float(wd)) for p, g, _, _, lr, wd in entries)
-    t = cache.get(key)
-    if t is None:
+def _plan_for(cache: dict, params, ms, vs, lrs, wds, device):
+    key = (tuple(map(id, params)), tuple(lrs), tuple(wds))
+    plan = cache.get(key)
+    if plan is None:
         if len(cache) > 8:
             cache.clear()
-        t = cache[key] = _Table(entries, device)
-        if torch.cuda.is_current_stream_capturing():
-            _CAPTURED.append(t)
-    return t
+        plan = cache[key] = _Plan(params, ms, vs, lrs, wds, device)
+    return plan
 
 
 class AdamW(torch.optim.Optimizer):
@@ -95,7 +127,7 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        entries = []
+        params, grads, ms, vs, lrs, wds = [], [], [], [], [], []
         dev = None
         b1 = b2 = eps = None
         for group in self.param_groups:
@@ -117,18 +149,23 @@ class AdamW(torch.optim.Optimizer):
                 g = p.grad
                 if not g.is_contiguous():
                     g = p.grad = g.contiguous()
-                entries.append((p, g, st["exp_avg"], st["exp_avg_sq"], group["lr"],
-                                group["weight_decay"]))
+                params.append(p)
+                grads.append(g)
+                ms.append(st["exp_avg"])
+                vs.append(st["exp_avg_sq"])
+                lrs.append(float(group["lr"]))
+                wds.append(float(group["weight_decay"]))
                 dev = p.device
-        if not entries:
+        if not params:
             return loss
-        L.require_device(entries[0][0])
+        L.require_device(params[0])
         if self._step_t is None:
             self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)
-            for e in entries:
-                self.state[e[0]]["step"] = self._step_t
-        tab = _table_for(self._tables, entries, dev)
-        call("mmdx_adamw_multi", tab.n, ptr(tab.dev), float(b1), float(b2), float(eps),
+            for p in params:
+                self.state[p]["step"] = self._step_t
+        plan = _plan_for(self._tables, params, ms, vs, lrs, wds, dev)
+        plan.upload(grads)
+        call("mmdx_adamw_multi", plan.n, ptr(plan.dev), float(b1), float(b2), float(eps),
              ptr(self._step_t), ptr(grad_scale), stream())
         return loss
 
@@ -146,8 +183,8 @@ def grad_norm(parameters, max_norm: float = 0.0, apply: bool = False):
         z = torch.zeros((), dtype=torch.float32)
         return z, torch.ones((), dtype=torch.float32)
     dev = ps[0].device
-    entries = [(p, p.grad, p, p, 0.0, 0.0) for p in ps]
-    tab = _table_for(_clip_cache, entries, dev)
+    tab = _plan_for(_clip_cache, ps, ps, ps, [0.0] * len(ps), [0.0] * len(ps), dev)
+    tab.upload([p.grad for p in ps])
     norm = torch.empty((), dtype=torch.float32, device=dev)
     scale = torch.empty((), dtype=torch.float32, device=dev)
     ws_n = L.lib().mmdx_grad_norm_workspace_size(tab.n)
