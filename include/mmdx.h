@@ -136,6 +136,24 @@ int mmdx_cast(int dst_dtype, int src_dtype, const void* x, long n, void* y, void
 int mmdx_axpby(long n, float a, const float* x, float b, const float* y, float* out,
                void* stream);
 
+/* ---------------------------------------------------------------- ViT-B/16 tower (C5)
+ * torchvision vit_b_16 (build-defined backbone name):
+ * patchify: x NCHW fp32 -> [N*(H/p)*(W/p)][C*p*p] rows in (c, ky, kx) order, so the
+ *   Conv2d(C, D, p, stride p) patch embedding is one GEMM against its [D][C*p*p] weight;
+ * vit_tokens: tokens[n][0] = class_token + pos[0], tokens[n][1+q] = emb[n][q] + pos[1+q];
+ *   backward returns d emb (the class-token / pos gradients are column sums, bias_grad);
+ * rows_copy: strided row copy (class-token rows in and out of the token matrix);
+ * add: out = x + y in the compute dtype (residual gradient sums). */
+int mmdx_patchify(int dtype, const float* x, int N, int C, int H, int W, int p, void* out,
+                  void* stream);
+int mmdx_vit_tokens_fwd(int dtype, const void* emb, const float* cls, const float* pos, int N,
+                        int S, int D, void* tokens, void* stream);
+int mmdx_vit_tokens_bwd(int dtype, const void* dtokens, int N, int S, int D, void* demb,
+                        void* stream);
+int mmdx_rows_copy(int dtype, const void* src, long src_ld, void* dst, long dst_ld, long rows,
+                   int D, void* stream);
+int mmdx_add(int dtype, long n, const void* x, const void* y, void* out, void* stream);
+
 /* ---------------------------------------------------------------- elementwise / norms
  * LayerNorm over the last dim D (fusion_mlp[3] TP:538, BERT LayerNorms);
  * optional residual added before the norm (BERT "Add & Norm"). */

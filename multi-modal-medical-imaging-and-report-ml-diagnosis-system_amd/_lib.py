@@ -88,6 +88,11 @@ SIGNATURES = {
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_fwd_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
+    "mmdx_patchify": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
+    "mmdx_vit_tokens_fwd": (i32, [i32, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "mmdx_vit_tokens_bwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),
+    "mmdx_rows_copy": (i32, [i32, vp, i64, vp, i64, i64, i32, vp]),
+    "mmdx_add": (i32, [i32, i64, vp, vp, vp, vp]),
     "mmdx_adamw_multi": (i32, [i32, vp, f32, f32, f32, vp, vp, vp]),
     "mmdx_grad_norm_workspace_size": (sz, [i32]),
     "mmdx_grad_norm": (i32, [i32, vp, f32, vp, vp, vp, sz, vp]),

@@ -23,6 +23,7 @@ from . import text_encoders as TE
 from .layers import Dropout, GELU, LayerNorm, Linear
 from .optim import AdamW
 from .resnet import ResNetTrunk
+from .vit import VitTrunk
 
 IMG_SIZE = 224  # TP:65
 TEXT_ENCODER_MODEl_NAME = "bert-base-uncased"  # TP:66 (name kept verbatim)
@@ -93,7 +94,7 @@ def image_transfom_into_tensor(img) -> torch.Tensor:
 # Image encoder (TP:157-311)
 # =====================================================================================
 class ImageEncoderCNN(nn.Module):
-    SUPPORTED = ("resnet50", "resnet18", "resnet34", "resnet101")
+    SUPPORTED = ("resnet50", "resnet18", "resnet34", "resnet101", "vit_b_16")
 
     def __init__(self, backbone_name="resnet50", d_img=1024, n_disease_classes=13,
                  use_warmup_classifier=True, pretrained_weights=None, compute_dtype=None):
@@ -113,7 +114,11 @@ class ImageEncoderCNN(nn.Module):
         self.load_pretrained_backbone()
 
     def load_pretrained_backbone(self):  # TP:176-197
-        if self.backbone_name.lower() in self.SUPPORTED:
+        if self.backbone_name.lower() == "vit_b_16":  # build-defined
+            self.backbone = VitTrunk()
+            self.backbone.compute_dtype = self.compute_dtype
+            feat_dim = self.backbone.feat_dim
+        elif self.backbone_name.lower() in self.SUPPORTED:
             self.backbone = ResNetTrunk(self.backbone_name.lower())
             self.backbone.compute_dtype = self.compute_dtype
             feat_dim = self.backbone.feat_dim
@@ -121,8 +126,9 @@ class ImageEncoderCNN(nn.Module):
             raise ValueError(f"Unsupported backbone model: {self.backbone}")
         if isinstance(self.pretrained_weights, str) and os.path.exists(self.pretrained_weights):
             sd = torch.load(self.pretrained_weights, map_location="cpu", weights_only=True)
-            sd = {k: v for k, v in sd.items() if not k.startswith("fc.")}
-            self.backbone.load_state_dict(_tv_to_seq(sd))
+            sd = {k: v for k, v in sd.items() if not k.startswith(("fc.", "heads."))}
+            self.backbone.load_state_dict(sd if self.backbone_name.lower() == "vit_b_16"
+                                          else _tv_to_seq(sd))
         self.proj = Linear(feat_dim, self.d_img)
         if self.use_warmup_classifier:
             self.classifier = Linear(self.d_img, self.n_disease_classes)

@@ -137,3 +137,14 @@ def test_inference_rejects_bad_device_type():
     from mmdx.inference_pipeline import inference
     with pytest.raises(TypeError):  # IP:159
         inference({}, None, "x", device=3)
+
+
+def test_vit_b_16_tower_keys_match_torchvision_layout():
+    """vit_b_16 (C5, build-defined name): torchvision state_dict keys minus `heads`, and
+    torchvision's parameter count (86,567,656 - 769,000 head parameters)."""
+    m = mmdx.ImageEncoderCNN("vit_b_16", 1024, 13)
+    r = R.RefImageEncoderCNN("vit_b_16")
+    assert set(m.state_dict()) == set(r.state_dict())
+    assert "backbone.encoder.layers.encoder_layer_11.self_attention.in_proj_weight" in m.state_dict()
+    assert sum(p.numel() for p in m.backbone.parameters()) == 85798656
+    assert m.backbone.feat_dim == 768 and m.proj.in_features == 768
