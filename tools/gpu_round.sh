@@ -17,7 +17,7 @@ step() {  # step <label> <timeout> <cmd...>
   [ $rc -le 1 ] || exit $rc
 }
 export TMPDIR=/tmp
-has tests && step tests 900 python -m pytest tests -m gpu -q -x
+has tests && step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 has bench && step bench 600 python bench.py --steps "$steps" --warmup 5
 has convb && step convb 600 python tools/conv_bench.py --json "gpurun_out/${tag}_conv_shapes.json"
 cd /tmp
