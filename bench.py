@@ -33,8 +33,9 @@ CONFIGS = {
                name="C3: ResNet-50 + 2-layer BiLSTM, bs 256 on 1 GPU"),
     "c4": dict(image="resnet50", text="bilstm", batch=128, seq=128,
                name="C4: ResNet-50 + 2-layer BiLSTM, 128 samples/GPU (1024 global at 8 GPUs)"),
-    "c5": dict(image="resnet50", text="bert-base-uncased", batch=64, seq=128,
-               name="C5-proxy: ResNet-50 + BERT-base (ViT-B/16 tower not built yet)"),
+    "c5": dict(image="vit_b_16", text="bert-base-uncased", batch=64, seq=128,
+               name="C5: ViT-B/16 + BERT-base, concat-fusion MLP, 64 samples/GPU "
+                    "(512 global at 8 GPUs)"),
 }
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
@@ -126,10 +127,25 @@ def load_traffic(cfg_name, batch):
     return best
 
 
+def vit_flops_per_sample(layers=12, S=197, D=768, I=3072, patches=196, kpatch=768):
+    """ViT-B/16 forward FLOPs of one 224x224 image (2 per MAC): patch embedding GEMM, per
+    layer the QKV/out/MLP GEMMs and the two attention contractions (QK^T, PV)."""
+    per_layer = S * (4 * D * D + 2 * D * I) + 2 * S * S * D
+    return 2 * (patches * kpatch * D + layers * per_layer)
+
+
 def model_flops_per_sample(cfg, img, txt):
+    """(dominant-kernel-family train FLOPs, whole-model train FLOPs) per sample."""
+    L = cfg["seq"]
+    if cfg["image"] == "vit_b_16":
+        D, I, layers = 768, 3072, 12
+        bert = layers * L * 2 * (4 * D * D + 2 * D * I) + layers * 2 * 2 * L * L * D
+        heads = 2 * (768 * 1024 + 768 * 512 + 1536 * 1024 + 1024 * 13)
+        vit = vit_flops_per_sample()
+        total = 3 * (vit + bert + heads)
+        return None, total
     f, d, w = conv_flops_per_sample(img.backbone)
     conv_train = f + d + w
-    L = cfg["seq"]
     text = 0
     if cfg["text"] == "bilstm":
         H = 256
@@ -183,7 +199,8 @@ def synth(cfg, B, dev, seed):
 
 
 class StepTimer:
-    """HIP events around every implicit-GEMM conv launch (on the launching stream)."""
+    """HIP events around every implicit-GEMM conv launch (or, for C5, every dense GEMM
+    launch; the tag is then its FLOP count), recorded on the launching stream."""
 
     def __init__(self):
         self.pairs = []
@@ -293,7 +310,9 @@ def main():
 
     import mmdx
     from mmdx import resnet as RN
+    from mmdx import functional as MF
     img, txt, fus, opt = build(cfg, dev, dtype)
+    vit = cfg["image"] == "vit_b_16"
     params = [p for grp in opt.param_groups for p in grp["params"]]
     if world > 1:  # identical initial weights on every rank (broadcast from rank 0)
         with torch.no_grad():
@@ -306,7 +325,10 @@ def main():
     reducer = GradAllReducer(params, world) if world > 1 else None
     step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
     timer = StepTimer()
-    RN.CONV_TIMER = timer
+    if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders
+        MF.GEMM_TIMER = timer
+    else:     # dominant kernel family: the implicit-GEMM conv launches
+        RN.CONV_TIMER = timer
 
     for _ in range(args.warmup):
         step()
@@ -365,8 +387,14 @@ def main():
     samples = B * world * args.steps
     value = samples / el
     ms_step = el / args.steps * 1e3
-    conv_tf = conv_flops * B * conv_steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-    alg_bytes, alg_launches = conv_bytes_per_step(img.backbone, B)
+    if vit:
+        gemm_flops = sum(f for f, _, _ in timer.pairs)   # all timed steps
+        conv_tf = gemm_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        conv_flops = gemm_flops / max(1, conv_steps) / B
+        alg_bytes, alg_launches = 0, max(1, n_conv // max(1, conv_steps))
+    else:
+        conv_tf = conv_flops * B * conv_steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        alg_bytes, alg_launches = conv_bytes_per_step(img.backbone, B)
     traffic = load_traffic(args.config, B)
     result = {
         "metric": "multimodal samples/sec (train fwd+bwd) at 1/2/4/8 MI355X; MFMA util %",
@@ -392,7 +420,9 @@ def main():
         "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
                                           (PEAK_BF16_TFLOPS * world), 2),
         "roofline": {
-            "kernel": "igemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad, all ResNet convs)",
+            "kernel": ("igemm_dma_kernel (dense GEMMs of the ViT-B/16 and BERT-base encoders, "
+                       "fwd + both backward GEMMs)") if vit else
+                      "igemm_dma_kernel (implicit-GEMM conv fwd/dgrad/wgrad, all ResNet convs)",
             "bound": "mfma",
             "achieved": round(conv_tf, 2),
             "peak": PEAK_BF16_TFLOPS,
@@ -401,10 +431,11 @@ def main():
             "traffic": traffic[0] if traffic else None,
             "traffic_unit": "HBM bytes per conv launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)",
             "traffic_source": traffic[1] if traffic else None,
-            "algorithmic_bytes_per_launch": round(alg_bytes / alg_launches),
-            "conv_ms_per_step": round(conv_ms / conv_steps, 3),
-            "conv_launches_per_step": n_conv // max(1, conv_steps),
-            "conv_gflop_per_sample": round(conv_flops / 1e9, 3),
+            "algorithmic_bytes_per_launch": (round(alg_bytes / alg_launches) if not vit
+                                             else None),
+            "family_ms_per_step": round(conv_ms / conv_steps, 3),
+            "family_launches_per_step": n_conv // max(1, conv_steps),
+            "family_gflop_per_sample": round(conv_flops / 1e9, 3),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

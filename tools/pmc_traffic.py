@@ -9,8 +9,8 @@ FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the byte
 coalesced read (MI355X_MICROARCH.md §HBM), so  bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
 Conv kernels are the implicit-GEMM instantiations whose operand source is an im2col/dgrad
 gather (`Im2colK`, `DgradK`, `Im2colR`) plus the split-K `wgrad_reduce_kernel`; the per-launch
-figure divides by the number of conv igemm dispatches (one per conv call, as bench.py's
-`roofline.achieved` counts them).
+figure divides by the number of conv CALLS (steps x --calls-per-step; steps = AdamW
+dispatches), the unit bench.py's `roofline.achieved` times.
 """
 import argparse
 import csv
@@ -19,7 +19,8 @@ import json
 import os
 import re
 
-CONV = re.compile(r"igemm_kernel.*(Im2col|Dgrad)")
+CONV = re.compile(r"igemm(_dma)?_kernel.*(Im2col|Dgrad|PhaseTap)")
+STEP = re.compile(r"adamw_kernel")
 REDUCE = re.compile(r"wgrad_reduce_kernel")
 
 
@@ -38,14 +39,16 @@ def load(d, counter):
             prev = per_dispatch.get(key, (name, 0.0))
             per_dispatch[key] = (name, prev[1] + v)
     conv_kb = red_kb = 0.0
-    n_conv = 0
+    n_conv = n_step = 0
     for name, v in per_dispatch.values():
+        if STEP.search(name):
+            n_step += 1
         if CONV.search(name):
             conv_kb += v
             n_conv += 1
         elif REDUCE.search(name):
             red_kb += v
-    return conv_kb, red_kb, n_conv
+    return conv_kb, red_kb, n_conv, n_step
 
 
 def main():
@@ -54,20 +57,26 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--config", default="c4")
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--calls-per-step", type=int, default=158,
+                    help="conv calls per train step (bench.py's conv_launches_per_step)")
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
-    f_conv, f_red, n_f = load(a.fetch_dir, "FETCH_SIZE")
-    w_conv, w_red, n_w = load(a.write_dir, "WRITE_SIZE")
-    if n_f == 0 or n_f != n_w:
-        raise SystemExit(f"conv dispatch counts differ or zero: {n_f} vs {n_w}")
-    fetch = 2.0 * (f_conv + f_red) * 1024 / n_f
-    write = (w_conv + w_red) * 1024 / n_w
+    f_conv, f_red, n_f, s_f = load(a.fetch_dir, "FETCH_SIZE")
+    w_conv, w_red, n_w, s_w = load(a.write_dir, "WRITE_SIZE")
+    if n_f == 0 or n_f != n_w or s_f == 0 or s_f != s_w:
+        raise SystemExit(f"dispatch counts differ or zero: conv {n_f}/{n_w}, steps {s_f}/{s_w}")
+    # per conv CALL (the unit bench.py's roofline times: one fwd, dgrad or wgrad call, which
+    # may be several dispatches: phase dgrad, split-K wgrad + reduce)
+    calls = s_f * a.calls_per_step
+    fetch = 2.0 * (f_conv + f_red) * 1024 / calls
+    write = (w_conv + w_red) * 1024 / calls
     out = {
-        "config": a.config, "per_gpu_batch": a.batch, "launches": n_f,
-        "kernels": "igemm_kernel (Im2colK/DgradK/Im2colR sources) + wgrad_reduce_kernel",
+        "config": a.config, "per_gpu_batch": a.batch, "dispatches": n_f, "steps": s_f,
+        "calls": calls,
+        "kernels": "igemm(_dma)_kernel (Im2colK/DgradK/DgradPhaseK/Im2colR sources) + wgrad_reduce_kernel",
         "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
         "traffic_bytes_per_launch": round(fetch + write),
-        "reduce_share": round(2 * f_red * 1024 / n_f + w_red * 1024 / n_w) / max(1.0, fetch + write),
+        "reduce_share": round((2 * f_red + w_red) * 1024 / calls / max(1.0, fetch + write), 4),
         "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
     }
     with open(a.out, "w") as fh:
