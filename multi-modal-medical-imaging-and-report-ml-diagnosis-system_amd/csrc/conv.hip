@@ -81,13 +81,24 @@ static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, cons
   return 0;
 }
 
+// Three operand stages when the grid gives at most one block per CU anyway (the third
+// stage costs occupancy only where there would be a second block to lose) and the K loop
+// is long enough to keep two tiles in flight.
+static bool use_three_stages(long blocks, int ktiles_per_block) {
+  return blocks <= 256 && ktiles_per_block >= 4;
+}
+
 template <int BM, int BN, class OA, class OB, class Epi>
 static int launch_dma_ops(const typename OA::SrcT& sa, const typename OB::SrcT& sb,
                           const Epi& epi, int M, int N, int K, int splits, int kper,
                           hipStream_t st) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi>), dim3(nwg, 1, splits), dim3(NT), 0,
-                     st, sa, sb, epi, M, N, K, kper);
+  if (use_three_stages((long)nwg * splits, (kper + 63) / 64))
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3>), dim3(nwg, 1, splits),
+                       dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+  else
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 2>), dim3(nwg, 1, splits),
+                       dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
   MMDX_LAUNCH_CHECK();
   return 0;
 }

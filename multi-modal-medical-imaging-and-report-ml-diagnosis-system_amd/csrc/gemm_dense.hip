@@ -65,8 +65,13 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
     if (oka && okb) {
       typedef typename std::conditional<AK, DmaK<BM, SA>, DmaR<BM, SA>>::type OA;
       typedef typename std::conditional<BKm, DmaK<BN, SB>, DmaR<BN, SB>>::type OB;
-      hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi>), dim3(nwg, 1, splits),
-                         dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+      // three operand stages where the grid leaves one block per CU and K is long
+      if ((long)nwg * splits <= 256 && kper >= 256)
+        hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3>), dim3(nwg, 1, splits),
+                           dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+      else
+        hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 2>), dim3(nwg, 1, splits),
+                           dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
       MMDX_LAUNCH_CHECK();
       return 0;
     }

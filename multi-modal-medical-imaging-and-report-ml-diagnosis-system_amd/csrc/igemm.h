@@ -695,6 +695,105 @@ struct EpiStore {
     if (beta != 0.f) v += beta * to_f(C[off]);
     C[off] = from_f<OutT>(v);
   }
+  // Block-uniform: every 8-column chunk can take one 16-B (bf16) / 2x16-B (fp32) store.
+  __device__ __forceinline__ bool vec8_ok() const {
+    return !bias && !addend && !preact && act == ACT_NONE && ldc % 8 == 0 &&
+           ((uintptr_t)C & 15) == 0;
+  }
+  // 8 consecutive columns n..n+7 of row m (vec8_ok() checked by the caller)
+  __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
+    if (m >= M) return;
+    if (n + 8 > N) {
+      apply4(m, n, lo);
+      if (n + 4 < N) apply4(m, n + 4, hi);
+      return;
+    }
+    const long off = (long)m * ldc + n;
+    typedef __attribute__((ext_vector_type(8))) OutT O8;
+    O8 o;
+    if (beta != 0.f) {
+      const O8 c = *(const O8*)(C + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = from_f<OutT>(alpha * lo[j] + beta * to_f(c[j]));
+        o[j + 4] = from_f<OutT>(alpha * hi[j] + beta * to_f(c[j + 4]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = from_f<OutT>(alpha * lo[j]);
+        o[j + 4] = from_f<OutT>(alpha * hi[j]);
+      }
+    }
+    *(O8*)(C + off) = o;
+  }
+  // Per-column (mean, M2) of this BM-row tile straight from the MFMA accumulators: each lane
+  // reduces its 4*RM rows of a column exactly (two passes in registers), the four lane groups
+  // sharing a column merge by Chan's formula through xor-shuffles, and the WM waves of a
+  // column merge in LDS (`red`, WM*BN*3 floats).  Same result layout as tile_stats.
+  static constexpr bool REG_STATS = true;
+  template <int BM, int BN, int WM, int WN, int RM, int RN>
+  __device__ __forceinline__ void reg_stats(const f32x4 (&acc)[RM][RN], float* red, int tm,
+                                            int tn, int wm, int wn, int lane) const {
+    if (!stats) return;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    const int rows_valid = min(BM, M - tm * BM);
+    const bool full = rows_valid == BM;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      float cnt = 0.f, s = 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = full || wm * WTM + i * 16 + (lane >> 4) * 4 + r < rows_valid;
+          cnt += ok ? 1.f : 0.f;
+          s += ok ? acc[i][j][r] : 0.f;
+        }
+      const float mean = cnt > 0.f ? s / cnt : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = full || wm * WTM + i * 16 + (lane >> 4) * 4 + r < rows_valid;
+          const float d = acc[i][j][r] - mean;
+          m2 += ok ? d * d : 0.f;
+        }
+      float n_a = cnt, mu = mean, mm = m2;
+#pragma unroll
+      for (int x = 16; x <= 32; x <<= 1) {
+        const float n_b = __shfl_xor(n_a, x, 64), mu_b = __shfl_xor(mu, x, 64),
+                    mm_b = __shfl_xor(mm, x, 64);
+        const float tot = n_a + n_b;
+        const float d = mu_b - mu, f = tot > 0.f ? n_b / tot : 0.f;
+        mu += d * f;
+        mm += mm_b + d * d * n_a * f;
+        n_a = tot;
+      }
+      if (lane < 16) {
+        float* o = red + (wm * BN + wn * WTN + j * 16 + lane) * 3;
+        o[0] = n_a; o[1] = mu; o[2] = mm;
+      }
+    }
+    __syncthreads();
+    const int col = threadIdx.x;
+    if (col < BN && tn * BN + col < N) {
+      float nn = 0.f, mu = 0.f, mm = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) {
+        const float* o = red + (q * BN + col) * 3;
+        const float nb = o[0], mb = o[1], m2b = o[2];
+        if (nb == 0.f) continue;
+        if (nn == 0.f) { nn = nb; mu = mb; mm = m2b; continue; }
+        const float tot = nn + nb, d = mb - mu, f = nb / tot;
+        mu += d * f;
+        mm += m2b + d * d * nn * f;
+        nn = tot;
+      }
+      stats[(long)tm * N + tn * BN + col] = make_float2(mu, mm);
+    }
+  }
   __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
     if (m >= M) return;
     const long off = (long)m * ldc + n;
@@ -738,6 +837,17 @@ struct EpiPartial {
   }
   template <int BM, int BN, int LDC>
   __device__ __forceinline__ void tile_stats(const float*, float*, int, int) const {}
+  static constexpr bool REG_STATS = false;
+  template <int BM, int BN, int WM, int WN, int RM, int RN>
+  __device__ __forceinline__ void reg_stats(const f32x4 (&)[RM][RN], float*, int, int, int,
+                                            int, int) const {}
+  __device__ __forceinline__ bool vec8_ok() const { return N % 4 == 0; }
+  __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
+    if (m >= M) return;
+    const long off = ((long)blockIdx.z * M + m) * N + n;
+    if (n + 4 <= N) *(f32x4*)(ws + off) = lo;
+    if (n + 8 <= N) *(f32x4*)(ws + off + 4) = hi;
+  }
 };
 
 // Phase-dgrad epilogue: GEMM row m = phase pixel (n, i, j) -> dX pixel (n, a+sh*i, b+sw*j);
@@ -780,6 +890,37 @@ struct EpiPhase {
   }
   template <int BM, int BN, int LDC>
   __device__ __forceinline__ void tile_stats(const float*, float*, int, int) const {}
+  static constexpr bool REG_STATS = false;
+  template <int BM, int BN, int WM, int WN, int RM, int RN>
+  __device__ __forceinline__ void reg_stats(const f32x4 (&)[RM][RN], float*, int, int, int,
+                                            int, int) const {}
+  __device__ __forceinline__ bool vec8_ok() const { return ldc % 8 == 0 && ((uintptr_t)C & 15) == 0; }
+  __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
+    if (m >= M) return;
+    if (n + 8 > N) {
+      apply4(m, n, lo);
+      if (n + 4 < N) apply4(m, n + 4, hi);
+      return;
+    }
+    const long off = pix(m) * ldc + n;
+    typedef __attribute__((ext_vector_type(8))) OutT O8;
+    O8 o;
+    if (beta != 0.f) {
+      const O8 c = *(const O8*)(C + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = from_f<OutT>(lo[j] + beta * to_f(c[j]));
+        o[j + 4] = from_f<OutT>(hi[j] + beta * to_f(c[j + 4]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = from_f<OutT>(lo[j]);
+        o[j + 4] = from_f<OutT>(hi[j]);
+      }
+    }
+    *(O8*)(C + off) = o;
+  }
 };
 
 // Bijective XCD-aware remap: blocks that share an A panel land on one XCD's L2.
@@ -1011,7 +1152,11 @@ struct DmaR {
   }
 };
 
-template <int BM, int BN, class OA, class OB, class Epi>
+// NS operand stages (2 or 3): with NS = 3 two K tiles are in flight while one is consumed
+// (counted vmcnt); used where the grid leaves one block per CU anyway (LDS 3 x STAGE).
+// Epilogue: BatchNorm tile statistics straight from the accumulators (reg_stats), fp32
+// staging through LDS, then 8 consecutive columns per lane -> one 16-B bf16 store.
+template <int BM, int BN, class OA, class OB, class Epi, int NS = 2>
 __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                           typename OB::SrcT sb, Epi epi, int M,
                                                           int N, int K, int kper) {
@@ -1019,10 +1164,13 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
-  constexpr int OP_BYTES = 2 * STAGE;
+  constexpr int OP_BYTES = NS * STAGE;
   constexpr int LDC = BN + 4;
-  constexpr int EPI_BYTES = BM * LDC * 4 + NT * 3 * 4;
+  constexpr int EPI_BYTES = BM * LDC * 4 + WM * BN * 3 * 4;
   constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
+  // DMA instructions one wave issues per K tile (both operands)
+  constexpr int PER_TILE = OA::INSTR + OB::INSTR;
+  static_assert(NS == 2 || NS == 3, "stages");
   __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];  // the only LDS object
 
   const int tiles_n = (N + BN - 1) / BN;
@@ -1046,19 +1194,27 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nt > 0) {
-    oa.issue(sa, lds_raw, kbeg, kend, wid);
-    ob.issue(sb, lds_raw + OA::BYTES, kbeg, kend, wid);
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) {
+    if (t < nt) {
+      char* st = lds_raw + t * STAGE;
+      oa.issue(sa, st, kbeg + t * BK, kend, wid);
+      ob.issue(sb, st + OA::BYTES, kbeg + t * BK, kend, wid);
+    }
   }
   for (int t = 0; t < nt; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // wait for this wave's DMAs of tile t (tiles t+1 .. t+NS-2 may stay in flight)
+    if (NS == 3 && t + 1 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (t + 1 < nt) {
-      char* st = lds_raw + ((t + 1) & 1) * STAGE;
-      oa.issue(sa, st, kbeg + (t + 1) * BK, kend, wid);
-      ob.issue(sb, st + OA::BYTES, kbeg + (t + 1) * BK, kend, wid);
+    if (t + NS - 1 < nt) {  // its stage was consumed in iteration t-1 by every wave
+      char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
+      oa.issue(sa, st, kbeg + (t + NS - 1) * BK, kend, wid);
+      ob.issue(sb, st + OA::BYTES, kbeg + (t + NS - 1) * BK, kend, wid);
     }
-    const char* as = lds_raw + (t & 1) * STAGE;
+    const char* as = lds_raw + (t % NS) * STAGE;
     const char* bs = as + OA::BYTES;
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 32) {
@@ -1078,6 +1234,9 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   __syncthreads();
 
   float* cst = (float*)lds_raw;
+  float* red = cst + BM * LDC;
+  if constexpr (Epi::REG_STATS)
+    epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1087,12 +1246,23 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
         cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 + (lane & 15)] =
             acc[i][j][r];
   __syncthreads();
-  epi.template tile_stats<BM, BN, LDC>(cst, cst + BM * LDC, tm, tn);
-  constexpr int C4 = BN / 4;
-  for (int c = threadIdx.x; c < BM * C4; c += NT) {
-    const int row = c / C4, col = (c - row * C4) * 4;
-    const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
-    epi.apply4(tm * BM + row, tn * BN + col, v);
+  if constexpr (!Epi::REG_STATS) epi.template tile_stats<BM, BN, LDC>(cst, red, tm, tn);
+  if (epi.vec8_ok()) {
+    constexpr int C8 = BN / 8;
+#pragma unroll 2
+    for (int c = threadIdx.x; c < BM * C8; c += NT) {
+      const int row = c / C8, col = (c - row * C8) * 8;
+      const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
+      const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
+      epi.apply8_fast(tm * BM + row, tn * BN + col, lo, hi);
+    }
+  } else {
+    constexpr int C4 = BN / 4;
+    for (int c = threadIdx.x; c < BM * C4; c += NT) {
+      const int row = c / C4, col = (c - row * C4) * 4;
+      const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
+      epi.apply4(tm * BM + row, tn * BN + col, v);
+    }
   }
 }
 
