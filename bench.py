@@ -200,11 +200,39 @@ def synth(cfg, B, dev, seed):
 
 class StepTimer:
     """HIP events around every implicit-GEMM conv launch (or, for C5, every dense GEMM
-    launch; the tag is then its FLOP count), recorded on the launching stream."""
+    launch; the tag is then its FLOP count), recorded on the launching stream.  Events come
+    from a pool created before the timed region (creating them inside it costs host time)."""
 
     def __init__(self):
         self.pairs = []
         self.enabled = False
+        self.pool = []
+
+    @property
+    def active(self):
+        return self.enabled
+
+    def reserve(self, n):
+        st = torch.cuda.current_stream()
+        while len(self.pool) < 2 * n:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(st)  # creates the HIP event, so native code can record it by handle
+            self.pool.append(e)
+        torch.cuda.synchronize()
+
+    def _event(self):
+        if not self.pool:
+            self.reserve(64)
+        return self.pool.pop()
+
+    def take(self, names):
+        """(start, end) events for each named launch of a native plan run, in order."""
+        evs = []
+        for name in names:
+            s, e = self._event(), self._event()
+            self.pairs.append((name, s, e))
+            evs += [s, e]
+        return evs
 
     def __call__(self, name):
         timer = self
@@ -212,8 +240,8 @@ class StepTimer:
         class _Ctx:
             def __enter__(self_):
                 if timer.enabled:
-                    self_.s = torch.cuda.Event(enable_timing=True)
-                    self_.e = torch.cuda.Event(enable_timing=True)
+                    self_.s = timer._event()
+                    self_.e = timer._event()
                     self_.s.record(torch.cuda.current_stream())
                 return self_
 
@@ -356,11 +384,13 @@ def main():
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.enabled = not use_graph
+    timer.enabled = not use_graph and os.environ.get("MMDX_BENCH_EVENTS", "1") != "0"
+    timer.reserve(400 * args.steps)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = run()
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (no device sync)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -416,6 +446,7 @@ def main():
                    "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,
                    "parallelism": f"dp{world}"},
         "loss": round(float(loss.item()), 5),
+        "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "model_tflops": round(total_flops * samples / el / 1e12, 2),
         "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
                                           (PEAK_BF16_TFLOPS * world), 2),

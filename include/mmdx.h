@@ -71,7 +71,7 @@ typedef struct {
  * Channel padding: desc->C may exceed the master's Cin (c_master); pad lanes are 0. */
 int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
                           const float* w_kcrs, void* w_krsc, void* w_crsk, void* stream);
-/* stat_part (optional, fp32 pairs [mmdx_conv_fwd_stat_blocks(d)][K]): per-channel
+/* stat_part (optional, fp32 pairs [K][mmdx_conv_fwd_stat_blocks(d)], channel-major): per-channel
  * (mean, M2) of each 128-row block of the output, computed from the fp32 accumulators in
  * the GEMM epilogue — the BatchNorm batch statistics without a separate pass over y. */
 int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d);
@@ -94,7 +94,7 @@ int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void
  * Replaces: BatchNorm2d + ReLU (+ Bottleneck residual add) inside the resnet trunk
  * (train mode: unfreeze_backbone TP:223; eval: freeze_backbone TP:206, IP:170). */
 size_t mmdx_bn_workspace_size(long rows, int C);
-/* stat_part: optional precomputed per-block (mean, M2) pairs [stat_blocks][C] over
+/* stat_part: optional precomputed per-block (mean, M2) pairs [C][stat_blocks] over
  * consecutive stat_rows-row blocks (e.g. from mmdx_conv_fwd's epilogue); NULL = reduce x. */
 int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
                 const float* stat_part, int stat_blocks, long stat_rows,
@@ -113,6 +113,34 @@ int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* 
 /* relu with y == NULL (a unit without residual): the ReLU mask is recomputed from x as
  * x*scale + shift > 0 with the forward's own scale/shift (gamma, bn_beta, save_mean,
  * save_rstd), so the post-activation tensor is not read. */
+
+/* ---------------------------------------------------------------- launch plans
+ * A plan is a host array of operations over caller-owned buffers, recorded once by the
+ * host layer (the ResNet trunk forward or backward for one batch shape and parameter set)
+ * and replayed with ONE call per step, so the per-step host cost is the launches alone.
+ * Operand j of an op is o.p[j] itself when o.ext[j] < 0, else ext[o.ext[j]] + (intptr)o.p[j]
+ * (per-call buffers: the image batch, the upstream gradient, the gradient arena).
+ * MMDX_OP_EVENT records events[o.i[0]] on the stream (skipped when events is NULL).
+ * Argument packing per op: see csrc/plan.cpp (each op forwards to the entry point of the
+ * same name above/below with its i/l/f/p fields in signature order).
+ * Replaces: the per-layer Python dispatch of ImageEncoderCNN's trunk (TP:279-289). */
+enum {
+  MMDX_OP_EVENT = 1, MMDX_OP_NCHW2NHWC, MMDX_OP_CONV_PACK, MMDX_OP_CONV_FWD, MMDX_OP_BN_FWD,
+  MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
+  MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD
+};
+typedef struct {
+  int op, dtype;
+  int i[8];
+  long l[4];
+  float f[4];
+  const void* p[12];
+  int ext[12];
+  mmdx_conv_desc d;
+} mmdx_plan_op;
+int mmdx_plan_run(const mmdx_plan_op* ops, int n_ops, void* const* ext, void* const* events,
+                  void* stream);
+size_t mmdx_plan_op_size(void); /* sizeof(mmdx_plan_op): binding layout check */
 
 /* ---------------------------------------------------------------- pooling
  * Replaces: resnet maxpool 3x3/2 (backbone[3]) and AdaptiveAvgPool2d(1) (backbone[8])

@@ -640,7 +640,7 @@ struct EpiStore {
   int act;              // Act
   float alpha, beta;    // C = act(alpha*acc + bias + addend) + beta*C
   OutT* preact;         // optional copy of the pre-activation value, ld = ldc
-  float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [tiles_m][N]
+  float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [N][tiles_m]
   // Per-column (mean, M2) over this tile's valid rows, from the fp32 accumulators staged in
   // LDS (cst [BM][LDC]) — the BatchNorm statistics of a conv output without re-reading it.
   // Two passes (mean, then squared deviations) over NT/BN row slices, merged with Chan.
@@ -680,7 +680,7 @@ struct EpiStore {
         mm += m2b + d * d * nn * f;
         nn = tot;
       }
-      stats[(long)tm * N + n] = make_float2(mu, mm);
+      stats[(long)n * ((M + BM - 1) / BM) + tm] = make_float2(mu, mm);  // [N][tiles_m]
     }
   }
   __device__ __forceinline__ void apply(int m, int n, float v) const {
@@ -791,7 +791,7 @@ struct EpiStore {
         mm += m2b + d * d * nn * f;
         nn = tot;
       }
-      stats[(long)tm * N + tn * BN + col] = make_float2(mu, mm);
+      stats[(long)(tn * BN + col) * ((M + BM - 1) / BM) + tm] = make_float2(mu, mm);
     }
   }
   __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {

@@ -48,7 +48,8 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nn;
 }
 
-// partial[b][c] = (mean, M2) of rows [b*rpb, (b+1)*rpb)
+// partial[c][b] = (mean, M2) of rows [b*rpb, (b+1)*rpb) (channel-major: the finalize reads
+// one channel's slabs contiguously)
 template <typename T>
 __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x, long rows,
                                                          int C, int ct, long rpb,
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x
         const int o = y * ct + tx;
         chan_merge(n, mean, m2, s_n[o], s_mean[o * VEC + j], s_m2[o * VEC + j]);
       }
-      part[(long)blockIdx.x * C + c0 + j] = make_float2(mean, m2);
+      part[(long)(c0 + j) * gridDim.x + blockIdx.x] = make_float2(mean, m2);
     }
   }
 }
@@ -134,11 +135,12 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
   if (c >= C) return;  // uniform per wave (TPC = 64) or per block (TPC = 256)
   const long last = rows - (long)(nblk - 1) * rpb;  // rows of the final (short) slab
+  const float2* pc = part + (long)c * nblk;          // this channel's slabs, contiguous
   const float mean = slab_sum<TPC>(nblk, sub, red, [&](int b) {
-    return (b == nblk - 1 ? (float)last : (float)rpb) * part[(long)b * C + c].x;
+    return (b == nblk - 1 ? (float)last : (float)rpb) * pc[b].x;
   }) / (float)rows;
   const float m2 = slab_sum<TPC>(nblk, sub, red, [&](int b) {
-    const float2 p = part[(long)b * C + c];
+    const float2 p = pc[b];
     const float d = p.x - mean;
     return p.y + (b == nblk - 1 ? (float)last : (float)rpb) * d * d;
   });
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
   }
 }
 
-// backward reduce: partial[b][c] = (sum g, sum g*xhat), g = dy * relu'(y)
+// backward reduce: partial[c][b] = (sum g, sum g*xhat), g = dy * relu'(y)
 template <typename T>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
         a += s_a[(yy * ct + tx) * VEC + j];
         b += s_b[(yy * ct + tx) * VEC + j];
       }
-      part[(long)blockIdx.x * C + c0 + j] = make_float2(a, b);
+      part[(long)(c0 + j) * gridDim.x + blockIdx.x] = make_float2(a, b);
     }
   }
 }
@@ -316,8 +318,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
   const int sub = threadIdx.x % TPC;
   const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
   if (c >= C) return;
-  const float sg = slab_sum<TPC>(nblk, sub, red, [&](int b) { return part[(long)b * C + c].x; });
-  const float sgx = slab_sum<TPC>(nblk, sub, red, [&](int b) { return part[(long)b * C + c].y; });
+  const float2* pc = part + (long)c * nblk;  // this channel's slabs, contiguous
+  const float sg = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].x; });
+  const float sgx = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].y; });
   if (sub != 0) return;
   if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
   if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;

@@ -11,7 +11,9 @@ with the residual-path gradient summed inside the dgrad epilogue (beta = 1).
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import weakref
 
 import torch
 import torch.nn as nn
@@ -23,6 +25,8 @@ _VEC = {torch.float32: 4, torch.bfloat16: 8}
 
 
 class _NoTimer:
+    active = False
+
     def __call__(self, name):
         return self
 
@@ -33,7 +37,8 @@ class _NoTimer:
         return False
 
 
-# bench.py installs a HIP-event timer here to measure the implicit-GEMM conv launches.
+# bench.py installs a HIP-event timer here to measure the implicit-GEMM conv launches: when
+# `active`, `take(names)` hands out a (start, end) event pair per conv op of a plan run.
 CONV_TIMER = _NoTimer()
 
 
@@ -180,11 +185,12 @@ class ResNetTrunk(nn.Sequential):
 
 
 # ----------------------------------------------------------------------------- engine
-class _Unit:
-    """One conv + BN (+residual)(+ReLU) step; holds its forward state for the backward."""
-    __slots__ = ("conv", "bn", "relu", "desc", "cm", "x", "y", "out", "mean", "rstd", "wc",
-                 "shape_in", "train")
-
+# The trunk is executed from launch plans (include/mmdx.h, csrc/plan.cpp): the forward and
+# the backward of one (batch shape, dtype, mode, parameter set) are recorded once as op
+# lists over a buffer arena, then every step replays each with ONE C call.  Per-call
+# buffers (the image batch, the upstream gradient, the gradient arena) enter as external
+# bases.  An arena holds one forward's saved activations until its backward has run, so a
+# second forward while a backward is pending records a second arena instead of clobbering.
 
 def _desc(N, H, W, C, conv):
     k, s, p = conv.kernel_size, conv.stride, conv.padding
@@ -193,78 +199,264 @@ def _desc(N, H, W, C, conv):
     return L.ConvDesc(N, H, W, C, conv.out_channels, k, k, s, s, p, p, P, Q)
 
 
-def _conv_bn(conv, bn, relu, x, N, H, W, C, cm, res, train, keep):
-    T = x.dtype
-    dt = L.dtype_code(T)
-    d = _desc(N, H, W, C, conv)
-    K, k = conv.out_channels, conv.kernel_size
-    dev = x.device
-    wk = torch.empty((K, k, k, C), dtype=T, device=dev)
-    wc = torch.empty((C, k, k, K), dtype=T, device=dev) if keep else None
-    st = stream()
-    call("mmdx_conv_pack_weight", dt, d, cm, ptr(conv.weight), ptr(wk), ptr(wc), st)
-    y = torch.empty((N, d.P, d.Q, K), dtype=T, device=dev)
-    nstat = L.lib().mmdx_conv_fwd_stat_blocks(d) if train else 0
-    # BN batch statistics come out of the conv epilogue (per 128-row block, fp32 accums)
-    part = torch.empty((nstat, K, 2), dtype=torch.float32, device=dev) if train else None
-    with CONV_TIMER("fwd"):
-        call("mmdx_conv_fwd", dt, d, ptr(x), ptr(wk), ptr(y), ptr(part), st)
-    out = torch.empty_like(y)
-    rows = N * d.P * d.Q
-    mean = torch.empty(K, dtype=torch.float32, device=dev)
-    rstd = torch.empty(K, dtype=torch.float32, device=dev)
-    ws_n = L.lib().mmdx_bn_workspace_size(rows, K)
-    ws = L.workspace(ws_n, dev)
-    call("mmdx_bn_fwd", dt, int(train), ptr(y), rows, K, ptr(part), nstat, 128, ptr(bn.weight),
-         ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum),
-         float(bn.eps), ptr(mean), ptr(rstd), ptr(res), int(relu), ptr(out), ptr(ws), ws_n, st)
-    u = None
-    if keep:
-        u = _Unit()
-        u.conv, u.bn, u.relu, u.desc, u.cm = conv, bn, relu, d, cm
-        u.x, u.y, u.out, u.mean, u.rstd, u.wc, u.train = x, y, out, mean, rstd, wc, train
-    return out, d, u
+class _Ext:
+    """An operand taken from the per-call external base `k` (+ byte offset)."""
+    __slots__ = ("k", "off")
+
+    def __init__(self, k, off=0):
+        self.k, self.off = k, off
 
 
-def _unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False):
-    """BN(+res)(+ReLU) backward then conv wgrad/dgrad. Returns (dx, dres, dw, dgamma, dbeta).
-    If dx_acc is given, dgrad accumulates into it (beta = 1) and it is returned as dx."""
-    d = u.desc
-    T = u.y.dtype
-    dt = L.dtype_code(T)
-    dev = u.y.device
-    st = stream()
-    rows = d.N * d.P * d.Q
-    K = d.K
-    dconv = torch.empty_like(u.y)
-    dres = torch.empty_like(u.y) if want_res else None
-    dg = torch.empty(K, dtype=torch.float32, device=dev)
-    db = torch.empty(K, dtype=torch.float32, device=dev)
-    ws_n = L.lib().mmdx_bn_workspace_size(rows, K)
-    ws = L.workspace(ws_n, dev)
-    # units without a residual recompute their ReLU mask from y (out is not read)
-    out = u.out if want_res else None
-    call("mmdx_bn_bwd", dt, int(u.train), ptr(u.y), ptr(out), ptr(dout), rows, K,
-         ptr(u.bn.weight), ptr(u.bn.bias), ptr(u.mean), ptr(u.rstd), int(u.relu), ptr(dconv),
-         ptr(dres),
-         ptr(dg), ptr(db), 0.0, ptr(ws), ws_n, st)
-    dw = torch.empty_like(u.conv.weight)
-    ws_n = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
-    ws = L.workspace(ws_n, dev)
-    with CONV_TIMER("wgrad"):
-        call("mmdx_conv_wgrad", dt, d, u.cm, ptr(u.x), ptr(dconv), ptr(dw), 0.0, ptr(ws), ws_n,
-             st)
-    dx = None
-    if want_dx:
-        if dx_acc is not None:
-            dx = dx_acc
-            beta = 1.0
+class _OpList:
+    def __init__(self):
+        self.ops = []
+        self.conv_names = []   # per timed conv op, its tag (fwd / dgrad / wgrad)
+
+    def add(self, code, dtype=0, i=(), l=(), f=(), p=(), d=None):
+        o = L.PlanOp()
+        o.op, o.dtype = code, dtype
+        for j, v in enumerate(i):
+            o.i[j] = int(v)
+        for j, v in enumerate(l):
+            o.l[j] = int(v)
+        for j, v in enumerate(f):
+            o.f[j] = float(v)
+        for j in range(12):
+            o.ext[j] = -1
+        for j, v in enumerate(p):
+            if isinstance(v, _Ext):
+                o.ext[j] = v.k
+                o.p[j] = v.off
+            elif isinstance(v, torch.Tensor):
+                o.p[j] = v.data_ptr()
+            else:
+                o.p[j] = v  # None or int
+        if d is not None:
+            o.d = d
+        self.ops.append(o)
+
+    def timed(self, name, code, **kw):
+        k = len(self.conv_names)
+        self.add(L.OP_EVENT, i=(2 * k,))
+        self.add(code, **kw)
+        self.add(L.OP_EVENT, i=(2 * k + 1,))
+        self.conv_names.append(name)
+
+    def freeze(self):
+        arr = (L.PlanOp * len(self.ops))(*self.ops)
+        self.arr, self.n = arr, len(self.ops)
+        self.ops = None
+        return self
+
+    def run(self, ext):
+        exts = (ctypes.c_void_p * max(1, len(ext)))(*ext)
+        evs = None
+        if CONV_TIMER.active and self.conv_names:
+            evs = CONV_TIMER.take(self.conv_names)
+            evs = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
+        call("mmdx_plan_run", self.arr, self.n, exts, evs, stream())
+
+
+class _Arena:
+    """Buffers of one recorded forward (+ backward) of the trunk."""
+
+    def __init__(self):
+        self.bufs = []
+        self.owner = None  # weakref to the autograd ctx token holding the saved activations
+
+    def new(self, shape, dtype, dev):
+        t = torch.empty(shape, dtype=dtype, device=dev)
+        self.bufs.append(t)
+        return t
+
+    def busy(self):
+        return self.owner is not None and self.owner() is not None
+
+
+class _Plan:
+    """Recorded forward / backward op lists of one trunk configuration (one arena)."""
+
+    def __init__(self, trunk, N, H, W, in_nchw, cin, T, train, keep, dev):
+        dt = L.dtype_code(T)
+        vec = _VEC[T]
+        A = self.arena = _Arena()
+        fw = _OpList()
+        ws_need = [0]
+
+        def ws_for(n):
+            ws_need[0] = max(ws_need[0], int(n))
+
+        # ---- forward
+        if in_nchw:
+            cp = vec
+            x0 = A.new((N, H, W, cp), T, dev)
+            fw.add(L.OP_NCHW2NHWC, dt, i=(N, cin, H, W, cp), p=(_Ext(0), x0))
         else:
-            dx = torch.empty((d.N, d.H, d.W, d.C), dtype=T, device=dev)
-            beta = 0.0
-        with CONV_TIMER("dgrad"):
-            call("mmdx_conv_dgrad", dt, d, ptr(dconv), ptr(u.wc), ptr(dx), beta, st)
-    return dx, dres, dw, dg, db
+            cp = cin
+            x0 = _Ext(0)
+        self.x0 = x0
+        units = []
+
+        def unit(conv, bn, relu, x, N, H, W, C, cm, res):
+            d = _desc(N, H, W, C, conv)
+            K, k = conv.out_channels, conv.kernel_size
+            wk = A.new((K, k, k, C), T, dev)
+            wc = A.new((C, k, k, K), T, dev) if keep else None
+            fw.add(L.OP_CONV_PACK, dt, i=(cm,), p=(conv.weight, wk, wc), d=d)
+            y = A.new((N, d.P, d.Q, K), T, dev)
+            nstat = L.lib().mmdx_conv_fwd_stat_blocks(d) if train else 0
+            part = A.new((K, nstat, 2), torch.float32, dev) if train else None
+            fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
+            out = A.new((N, d.P, d.Q, K), T, dev)
+            rows = N * d.P * d.Q
+            mean = A.new((K,), torch.float32, dev)
+            rstd = A.new((K,), torch.float32, dev)
+            wsn = L.lib().mmdx_bn_workspace_size(rows, K)
+            ws_for(wsn)
+            fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, 128, wsn),
+                   f=(bn.momentum, bn.eps),
+                   p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
+                      res, out, _WS))
+            u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
+                     rstd=rstd, wc=wc)
+            units.append(u)
+            return out, d, u
+
+        stem = trunk[0]
+        a, d, stem_u = unit(stem, trunk[1], True, x0, N, H, W, cp, 3, None)
+        H, W, C = d.P, d.Q, d.K
+        mp = trunk[3]
+        P = (H + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
+        Q = (W + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
+        pooled = A.new((N, P, Q, C), T, dev)
+        am = A.new((N, P, Q, C), torch.uint8, dev)
+        fw.add(L.OP_MAXPOOL_FWD, dt, i=(N, H, W, C, mp.kernel_size, mp.stride, mp.padding, P),
+               l=(Q,), p=(a, pooled, am))
+        stem_geom = (N, H, W, C, P, Q)
+        x_cur, H, W = pooled, P, Q
+        blocks = []
+        for layer in list(trunk)[4:8]:
+            for blk in layer:
+                x_in = x_cur
+                bu = []
+                h, hH, hW, hC = x_in, H, W, C
+                ds_u = None
+                if blk.downsample is not None:
+                    idn, _, ds_u = unit(blk.downsample[0], blk.downsample[1], False, x_in, N, H,
+                                        W, C, C, None)
+                else:
+                    idn = x_in
+                specs = blk.units()
+                for i, (conv, bn, relu) in enumerate(specs):
+                    res = idn if i == len(specs) - 1 else None
+                    h, dd, uu = unit(conv, bn, relu, h, N, hH, hW, hC, hC, res)
+                    hH, hW, hC = dd.P, dd.Q, dd.K
+                    bu.append(uu)
+                blocks.append((bu, ds_u, (H, W, C)))
+                x_cur, H, W, C = h, hH, hW, hC
+        self.feats = A.new((N, C), T, dev)
+        fw.add(L.OP_AVGPOOL_FWD, dt, i=(N, H * W, C), p=(x_cur, self.feats))
+        self.out_geom = (N, H, W, C)
+
+        # ---- backward (ext: 0 = dfeats in T, 1 = gradient arena base, 2 = trunk input x0)
+        self.bwd = None
+        if keep:
+            bw = _OpList()
+            params = trunk.engine_params()
+            self.grad_off = {}
+            off = 0
+            for prm in params:
+                self.grad_off[id(prm)] = off
+                off += (prm.numel() * 4 + 255) // 256 * 256
+            self.grad_bytes = off
+            self.params = params
+
+            def g(prm):
+                return _Ext(1, self.grad_off[id(prm)])
+
+            def xref(x):
+                return _Ext(2) if isinstance(x, _Ext) else x
+
+            def unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False):
+                d = u["d"]
+                K = d.K
+                rows = d.N * d.P * d.Q
+                dconv = A.new(tuple(u["y"].shape), T, dev)
+                dres = A.new(tuple(u["y"].shape), T, dev) if want_res else None
+                wsn = L.lib().mmdx_bn_workspace_size(rows, K)
+                ws_for(wsn)
+                out = u["out"] if want_res else None  # no residual: mask recomputed from y
+                bw.add(L.OP_BN_BWD, dt, i=(int(train), K, int(u["relu"])), l=(rows, wsn),
+                       f=(0.0,),
+                       p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"], u["rstd"],
+                          dconv, dres, g(u["bn"].weight), g(u["bn"].bias), _WS))
+                wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
+                ws_for(wsn)
+                bw.timed("wgrad", L.OP_CONV_WGRAD, dtype=dt, i=(u["cm"],), l=(wsn,), f=(0.0,),
+                         p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS), d=d)
+                dx = None
+                if want_dx:
+                    if dx_acc is not None:
+                        dx, beta = dx_acc, 1.0
+                    else:
+                        dx, beta = A.new((d.N, d.H, d.W, d.C), T, dev), 0.0
+                    bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(beta,),
+                             p=(dconv, u["wc"], dx), d=d)
+                return dx, dres
+
+            N_, H_, W_, C_ = self.out_geom
+            dx = A.new((N_, H_, W_, C_), T, dev)
+            bw.add(L.OP_AVGPOOL_BWD, dt, i=(N_, H_ * W_, C_), p=(_Ext(0), dx))
+            for bu, ds_u, _shape in reversed(blocks):
+                dh, dres = unit_bwd(bu[-1], dx, True, want_res=True)
+                for uu in reversed(bu[:-1]):
+                    if uu is bu[0]:
+                        # d(block input) = dgrad(conv1) + identity-path grad (beta = 1)
+                        if ds_u is not None:
+                            dxi, _ = unit_bwd(ds_u, dres, True)
+                        else:
+                            dxi = dres
+                        dh, _ = unit_bwd(uu, dh, True, dx_acc=dxi)
+                    else:
+                        dh, _ = unit_bwd(uu, dh, True)
+                dx = dh
+            n0, h0, w0, c0, p0, q0 = stem_geom
+            da = A.new((n0, h0, w0, c0), T, dev)
+            bw.add(L.OP_MAXPOOL_BWD, dt, i=(n0, h0, w0, c0, mp.kernel_size, mp.stride,
+                                            mp.padding, p0), l=(q0,), p=(am, dx, da))
+            unit_bwd(stem_u, da, False)
+            self.bwd = bw
+        # one workspace for every op of this plan (they run in stream order)
+        ws = A.new((max(1, ws_need[0]),), torch.uint8, dev)
+        for lst in (fw,) + ((self.bwd,) if self.bwd is not None else ()):
+            for o in lst.ops:
+                for j in range(12):
+                    if o.p[j] == _WS_TOKEN and o.ext[j] == -1:
+                        o.p[j] = ws.data_ptr()
+        self.fwd = fw.freeze()
+        if self.bwd is not None:
+            self.bwd.freeze()
+
+
+# placeholder operand for the plan's shared workspace, patched once the size is known
+_WS_TOKEN = 0x1
+_WS = _WS_TOKEN
+
+
+def _plans_for(trunk, key, build):
+    """A free arena for `key` (recording a new one if every recorded arena is held)."""
+    cache = trunk.__dict__.setdefault("_mmdx_plans", {})
+    lst = cache.setdefault(key, [])
+    for pl in lst:
+        if not pl.arena.busy():
+            return pl
+    pl = build()
+    lst.append(pl)
+    return pl
+
+
+class _Token:
+    pass
 
 
 class _TrunkFn(torch.autograd.Function):
@@ -272,124 +464,52 @@ class _TrunkFn(torch.autograd.Function):
     def forward(ctx, x, trunk, need_grad, *params):
         L.require_device(x)
         T = trunk.compute_dtype
-        dt = L.dtype_code(T)
         train = trunk.training
         keep = bool(need_grad)
-        st = stream()
         dev = x.device
-        vec = _VEC[T]
         if x.dim() != 4:
             raise ValueError("expected images [B,3,H,W]")
         if x.dtype == torch.float32 and x.shape[1] == 3:
-            N, Cin, H, W = x.shape
-            cp = vec
-            x0 = torch.empty((N, H, W, cp), dtype=T, device=dev)
-            call("mmdx_nchw_to_nhwc", dt, ptr(x.contiguous()), N, Cin, H, W, cp, ptr(x0), st)
+            N, cin, H, W = x.shape
+            in_nchw = True
         else:  # pre-converted NHWC, channel-padded
-            N, H, W, cp = x.shape
+            N, H, W, cin = x.shape
+            in_nchw = False
             if x.dtype != T:
                 raise TypeError("NHWC trunk input must already be in the compute dtype")
-            x0 = x
-        units = []          # forward order, for the backward
-        plan = []           # structure: ("stem"), ("block", [u...], ds_unit, has_ds)
-        stem = trunk[0]
-        a, d, u = _conv_bn(stem, trunk[1], True, x0, N, H, W, cp, 3, None, train, keep)
-        H, W, C = d.P, d.Q, d.K
-        # maxpool 3x3/2 pad 1
-        mp = trunk[3]
-        P = (H + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
-        Q = (W + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
-        pooled = torch.empty((N, P, Q, C), dtype=T, device=dev)
-        am = torch.empty((N, P, Q, C), dtype=torch.uint8, device=dev)
-        call("mmdx_maxpool_fwd", dt, ptr(a), N, H, W, C, mp.kernel_size, mp.stride, mp.padding,
-             ptr(pooled), ptr(am), P, Q, st)
-        stem_state = (u, am, (N, H, W, C, P, Q))
-        x_cur, H, W = pooled, P, Q
-        blocks = []
-        for layer in list(trunk)[4:8]:
-            for blk in layer:
-                x_in = x_cur
-                Hin, Win, Cin_b = H, W, C
-                bu = []
-                h = x_in
-                hH, hW, hC = H, W, C
-                specs = blk.units()
-                ds_u = None
-                if blk.downsample is not None:
-                    idn, dd, ds_u = _conv_bn(blk.downsample[0], blk.downsample[1], False, x_in,
-                                             N, H, W, C, C, None, train, keep)
-                else:
-                    idn = x_in
-                for i, (conv, bn, relu) in enumerate(specs):
-                    res = idn if i == len(specs) - 1 else None
-                    h, dd, uu = _conv_bn(conv, bn, relu, h, N, hH, hW, hC, hC, res, train, keep)
-                    hH, hW, hC = dd.P, dd.Q, dd.K
-                    bu.append(uu)
-                blocks.append((bu, ds_u, (Hin, Win, Cin_b)))
-                x_cur, H, W, C = h, hH, hW, hC
-        feats = torch.empty((N, C), dtype=T, device=dev)
-        call("mmdx_avgpool_fwd", dt, ptr(x_cur), N, H * W, C, ptr(feats), st)
+        key = (N, H, W, cin, in_nchw, T, train, keep, dev.index,
+               tuple(p.data_ptr() for p in params))
+        plan = _plans_for(trunk, key,
+                          lambda: _Plan(trunk, N, H, W, in_nchw, cin, T, train, keep, dev))
+        plan.fwd.run([x.data_ptr()])
         if train:  # every BN's num_batches_tracked += 1, in one multi-tensor launch
             torch._foreach_add_([m.num_batches_tracked for m in trunk.modules()
                                  if isinstance(m, BatchNorm2d)], 1)
         if keep:
-            ctx.state = (stem_state, blocks, (N, H, W, C), x.dtype == torch.float32)
-            ctx.trunk = trunk
-        return feats
+            tok = _Token()
+            plan.arena.owner = weakref.ref(tok)
+            ctx.tok = tok
+            ctx.plan = plan
+            ctx.x = None if in_nchw else x  # the stem's wgrad reads an NHWC input directly
+        return plan.feats.clone()
 
     @staticmethod
     def backward(ctx, dfeats):
-        stem_state, blocks, (N, H, W, C), _ = ctx.state
-        trunk = ctx.trunk
-        T = trunk.compute_dtype
-        dt = L.dtype_code(T)
-        st = stream()
-        dev = dfeats.device
+        plan = ctx.plan
+        trunk_params = plan.params
         from .functional import cast
-        dfeats = cast(dfeats.contiguous(), T)
-        grads = {}
-        dx = torch.empty((N, H, W, C), dtype=T, device=dev)
-        call("mmdx_avgpool_bwd", dt, ptr(dfeats), N, H * W, C, ptr(dx), st)
-        for bu, ds_u, _shape in reversed(blocks):
-            dout = dx
-            # last unit carries the residual
-            n = len(bu)
-            last = bu[-1]
-            dh, dres, dw, dg, db = _unit_bwd(last, dout, True, want_res=True)
-            grads[id(last.conv.weight)] = dw
-            grads[id(last.bn.weight)] = dg
-            grads[id(last.bn.bias)] = db
-            for uu in reversed(bu[:-1]):
-                is_first = uu is bu[0]
-                if is_first:
-                    # d(block input) = dgrad(conv1) + identity-path grad
-                    if ds_u is not None:
-                        dxi, _, dw2, dg2, db2 = _unit_bwd(ds_u, dres, True)
-                        grads[id(ds_u.conv.weight)] = dw2
-                        grads[id(ds_u.bn.weight)] = dg2
-                        grads[id(ds_u.bn.bias)] = db2
-                    else:
-                        dxi = dres
-                    dh, _, dw, dg, db = _unit_bwd(uu, dh, True, dx_acc=dxi)
-                else:
-                    dh, _, dw, dg, db = _unit_bwd(uu, dh, True)
-                grads[id(uu.conv.weight)] = dw
-                grads[id(uu.bn.weight)] = dg
-                grads[id(uu.bn.bias)] = db
-            dx = dh
-        # stem: maxpool backward then conv/BN (no dgrad into the image)
-        u, am, (N0, H0, W0, C0, P0, Q0) = stem_state
-        da = torch.empty((N0, H0, W0, C0), dtype=T, device=dev)
-        mp = trunk[3]
-        call("mmdx_maxpool_bwd", dt, ptr(am), ptr(dx), N0, H0, W0, C0, mp.kernel_size, mp.stride,
-             mp.padding, P0, Q0, ptr(da), st)
-        _, _, dw, dg, db = _unit_bwd(u, da, False)
-        grads[id(u.conv.weight)] = dw
-        grads[id(u.bn.weight)] = dg
-        grads[id(u.bn.bias)] = db
-        params = trunk.engine_params()
+        dfeats = cast(dfeats.contiguous(), plan.feats.dtype)
+        dev = dfeats.device
+        grads = torch.empty(plan.grad_bytes // 4, dtype=torch.float32, device=dev)
+        x0 = ctx.x.data_ptr() if isinstance(plan.x0, _Ext) else plan.x0.data_ptr()
+        plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0])
+        plan.arena.owner = None
+        ctx.plan = ctx.x = ctx.tok = None
         out = [None, None, None]
-        for p in params:
-            out.append(grads.get(id(p)) if p.requires_grad else None)
-        ctx.state = None
+        for prm in trunk_params:
+            if prm.requires_grad:
+                o = plan.grad_off[id(prm)] // 4
+                out.append(grads[o:o + prm.numel()].view(prm.shape))
+            else:
+                out.append(None)
         return tuple(out)

@@ -48,3 +48,9 @@ def test_workspace_queries_are_host_only(lib):
     assert lib.mmdx_conv_wgrad_workspace_size(1, d) > 0
     assert lib.mmdx_gemm_workspace_size(1, 8192, 768, 768) >= 0
     assert lib.mmdx_bn_workspace_size(128 * 56 * 56, 64) > 0
+
+
+def test_plan_op_layout_matches_c(lib):
+    import ctypes
+    import mmdx._lib as L
+    assert lib.mmdx_plan_op_size() == ctypes.sizeof(L.PlanOp)

@@ -109,14 +109,14 @@ def test_conv_fwd_dgrad_wgrad(dev, dt, cfg):
     xd = _nhwc(x, cp, dt).to(dev)
     y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
     nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
-    part = torch.empty(nst, K, 2, device=dev)
+    part = torch.empty(K, nst, 2, device=dev)  # channel-major [K][blocks] (mean, M2)
     L.call("mmdx_conv_fwd", dc, d, xd.data_ptr(), wk.data_ptr(), y.data_ptr(), part.data_ptr(),
            L.stream())
     _close(y.permute(0, 3, 1, 2), yr.detach(), dt, f"fwd {cfg}")
     # epilogue BatchNorm statistics: merge the per-128-row (mean, M2) blocks on the host
     M = N * P * Q
     cnt = torch.tensor([min(128, M - 128 * b) for b in range(nst)], dtype=torch.float64)
-    pm, p2 = part[..., 0].double().cpu(), part[..., 1].double().cpu()
+    pm, p2 = part[..., 0].t().double().cpu(), part[..., 1].t().double().cpu()
     mean = (pm * cnt[:, None]).sum(0) / M
     m2 = (p2 + cnt[:, None] * (pm - mean) ** 2).sum(0)
     yref = yr.detach().double()
