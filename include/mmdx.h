@@ -120,17 +120,21 @@ int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* 
  * and replayed with ONE call per step, so the per-step host cost is the launches alone.
  * Operand j of an op is o.p[j] itself when o.ext[j] < 0, else ext[o.ext[j]] + (intptr)o.p[j]
  * (per-call buffers: the image batch, the upstream gradient, the gradient arena).
- * MMDX_OP_EVENT records events[o.i[0]] on the stream (skipped when events is NULL).
+ * Each op runs on streams[o.stream] (streams[0] = the caller's stream).  MMDX_OP_EVENT
+ * records timing event events[o.i[0]] (skipped when events is NULL); MMDX_OP_SIGNAL records
+ * the hipEvent_t o.p[0] on the op's stream and MMDX_OP_WAIT makes the op's stream wait on it
+ * (cross-stream order inside a plan: e.g. weight gradients on a side stream).
  * Argument packing per op: see csrc/plan.cpp (each op forwards to the entry point of the
  * same name above/below with its i/l/f/p fields in signature order).
  * Replaces: the per-layer Python dispatch of ImageEncoderCNN's trunk (TP:279-289). */
 enum {
   MMDX_OP_EVENT = 1, MMDX_OP_NCHW2NHWC, MMDX_OP_CONV_PACK, MMDX_OP_CONV_FWD, MMDX_OP_BN_FWD,
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
-  MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD
+  MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
+  MMDX_OP_SIGNAL, MMDX_OP_WAIT
 };
 typedef struct {
-  int op, dtype;
+  int op, dtype, stream;
   int i[8];
   long l[4];
   float f[4];
@@ -139,7 +143,7 @@ typedef struct {
   mmdx_conv_desc d;
 } mmdx_plan_op;
 int mmdx_plan_run(const mmdx_plan_op* ops, int n_ops, void* const* ext, void* const* events,
-                  void* stream);
+                  void* const* streams, int n_streams);
 size_t mmdx_plan_op_size(void); /* sizeof(mmdx_plan_op): binding layout check */
 
 /* ---------------------------------------------------------------- pooling

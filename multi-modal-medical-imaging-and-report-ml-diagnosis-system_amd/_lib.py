@@ -36,14 +36,15 @@ CD = C.POINTER(ConvDesc)
 
 class PlanOp(C.Structure):
     """mmdx_plan_op (include/mmdx.h): one recorded operation of a launch plan."""
-    _fields_ = [("op", C.c_int), ("dtype", C.c_int), ("i", C.c_int * 8), ("l", C.c_long * 4),
+    _fields_ = [("op", C.c_int), ("dtype", C.c_int), ("stream", C.c_int), ("i", C.c_int * 8),
+                ("l", C.c_long * 4),
                 ("f", C.c_float * 4), ("p", C.c_void_p * 12), ("ext", C.c_int * 12),
                 ("d", ConvDesc)]
 
 
 (OP_EVENT, OP_NCHW2NHWC, OP_CONV_PACK, OP_CONV_FWD, OP_BN_FWD, OP_MAXPOOL_FWD,
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
- OP_CONV_DGRAD) = range(1, 14)
+ OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT) = range(1, 16)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -64,7 +65,7 @@ SIGNATURES = {
                           vp, i32, vp, vp, sz, vp]),
     "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp,
                           f32, vp, sz, vp]),
-    "mmdx_plan_run": (i32, [C.POINTER(PlanOp), i32, vp, vp, vp]),
+    "mmdx_plan_run": (i32, [C.POINTER(PlanOp), i32, vp, vp, vp, i32]),
     "mmdx_plan_op_size": (sz, []),
     "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,
                                vp]),

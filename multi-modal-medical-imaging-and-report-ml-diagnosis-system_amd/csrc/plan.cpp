@@ -18,17 +18,23 @@ inline void* P(const mmdx_plan_op& o, int j, void* const* ext) {
   return (char*)ext[e] + (intptr_t)o.p[j];
 }
 
+int hip_rc(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  mmdx_set_error("plan: %s: %s", what, hipGetErrorString(e));
+  return -(int)e;
+}
+
 int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* s) {
   switch (o.op) {
+    case MMDX_OP_SIGNAL:
+      return hip_rc(hipEventRecord((hipEvent_t)o.p[0], (hipStream_t)s), "hipEventRecord");
+    case MMDX_OP_WAIT:
+      return hip_rc(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)o.p[0], 0),
+                    "hipStreamWaitEvent");
     case MMDX_OP_EVENT:
-      if (events) {
-        const hipError_t e = hipEventRecord((hipEvent_t)events[o.i[0]], (hipStream_t)s);
-        if (e != hipSuccess) {
-          mmdx_set_error("plan: hipEventRecord: %s", hipGetErrorString(e));
-          return -(int)e;
-        }
-      }
-      return 0;
+      return events ? hip_rc(hipEventRecord((hipEvent_t)events[o.i[0]], (hipStream_t)s),
+                             "hipEventRecord")
+                    : 0;
     case MMDX_OP_NCHW2NHWC:
       return mmdx_nchw_to_nhwc(o.dtype, (const float*)P(o, 0, ext), o.i[0], o.i[1], o.i[2],
                                o.i[3], o.i[4], P(o, 1, ext), s);
@@ -86,13 +92,19 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
 extern "C" size_t mmdx_plan_op_size(void) { return sizeof(mmdx_plan_op); }
 
 extern "C" int mmdx_plan_run(const mmdx_plan_op* ops, int n_ops, void* const* ext,
-                             void* const* events, void* stream) {
-  if (!ops || n_ops < 0) {
-    mmdx_set_error("plan: bad op list");
+                             void* const* events, void* const* streams, int n_streams) {
+  if (!ops || n_ops < 0 || !streams || n_streams < 1) {
+    mmdx_set_error("plan: bad op list or stream table");
     return -22;
   }
   for (int k = 0; k < n_ops; ++k) {
-    const int rc = run_one(ops[k], ext, events, stream);
+    if (ops[k].stream < 0 || ops[k].stream >= n_streams) {
+      mmdx_set_error("plan: op %d names stream %d of %d", k, ops[k].stream, n_streams);
+      return -22;
+    }
+  }
+  for (int k = 0; k < n_ops; ++k) {
+    const int rc = run_one(ops[k], ext, events, streams[ops[k].stream]);
     if (rc) return rc;  // the failing op's own message stays in mmdx_last_error()
   }
   return 0;

@@ -212,9 +212,9 @@ class _OpList:
         self.ops = []
         self.conv_names = []   # per timed conv op, its tag (fwd / dgrad / wgrad)
 
-    def add(self, code, dtype=0, i=(), l=(), f=(), p=(), d=None):
+    def add(self, code, dtype=0, i=(), l=(), f=(), p=(), d=None, stream=0):
         o = L.PlanOp()
-        o.op, o.dtype = code, dtype
+        o.op, o.dtype, o.stream = code, dtype, stream
         for j, v in enumerate(i):
             o.i[j] = int(v)
         for j, v in enumerate(l):
@@ -235,11 +235,11 @@ class _OpList:
             o.d = d
         self.ops.append(o)
 
-    def timed(self, name, code, **kw):
+    def timed(self, name, code, stream=0, **kw):
         k = len(self.conv_names)
-        self.add(L.OP_EVENT, i=(2 * k,))
-        self.add(code, **kw)
-        self.add(L.OP_EVENT, i=(2 * k + 1,))
+        self.add(L.OP_EVENT, i=(2 * k,), stream=stream)
+        self.add(code, stream=stream, **kw)
+        self.add(L.OP_EVENT, i=(2 * k + 1,), stream=stream)
         self.conv_names.append(name)
 
     def freeze(self):
@@ -248,13 +248,14 @@ class _OpList:
         self.ops = None
         return self
 
-    def run(self, ext):
+    def run(self, ext, streams):
         exts = (ctypes.c_void_p * max(1, len(ext)))(*ext)
+        sts = (ctypes.c_void_p * len(streams))(*streams)
         evs = None
         if CONV_TIMER.active and self.conv_names:
             evs = CONV_TIMER.take(self.conv_names)
             evs = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
-        call("mmdx_plan_run", self.arr, self.n, exts, evs, stream())
+        call("mmdx_plan_run", self.arr, self.n, exts, evs, sts, len(streams))
 
 
 class _Arena:
@@ -269,6 +270,13 @@ class _Arena:
         self.bufs.append(t)
         return t
 
+    def event(self):
+        """A synchronisation event owned by the arena (recorded once so it exists)."""
+        e = torch.cuda.Event()
+        e.record(torch.cuda.current_stream())
+        self.bufs.append(e)
+        return e.cuda_event
+
     def busy(self):
         return self.owner is not None and self.owner() is not None
 
@@ -281,10 +289,10 @@ class _Plan:
         vec = _VEC[T]
         A = self.arena = _Arena()
         fw = _OpList()
-        ws_need = [0]
+        ws_need = [0, 0]  # per stream: 0 = main, 1 = weight-gradient side stream
 
-        def ws_for(n):
-            ws_need[0] = max(ws_need[0], int(n))
+        def ws_for(n, st=0):
+            ws_need[st] = max(ws_need[st], int(n))
 
         # ---- forward
         if in_nchw:
@@ -359,6 +367,10 @@ class _Plan:
         self.out_geom = (N, H, W, C)
 
         # ---- backward (ext: 0 = dfeats in T, 1 = gradient arena base, 2 = trunk input x0)
+        # The weight gradients (wgrad) run on a side stream: they depend on the BN backward
+        # of their unit but nothing on the critical dgrad chain depends on them, so they fill
+        # the CUs the chain's smaller launches leave idle.  The main stream joins the side
+        # stream once at the end, before the optimizer reads the gradients.
         self.bwd = None
         if keep:
             bw = _OpList()
@@ -391,9 +403,12 @@ class _Plan:
                        p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"], u["rstd"],
                           dconv, dres, g(u["bn"].weight), g(u["bn"].bias), _WS))
                 wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
-                ws_for(wsn)
-                bw.timed("wgrad", L.OP_CONV_WGRAD, dtype=dt, i=(u["cm"],), l=(wsn,), f=(0.0,),
-                         p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS), d=d)
+                ws_for(wsn, 1)
+                ev = A.event()
+                bw.add(L.OP_SIGNAL, p=(ev,), stream=0)
+                bw.add(L.OP_WAIT, p=(ev,), stream=1)
+                bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(u["cm"],), l=(wsn,),
+                         f=(0.0,), p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
                 dx = None
                 if want_dx:
                     if dx_acc is not None:
@@ -425,22 +440,33 @@ class _Plan:
             bw.add(L.OP_MAXPOOL_BWD, dt, i=(n0, h0, w0, c0, mp.kernel_size, mp.stride,
                                             mp.padding, p0), l=(q0,), p=(am, dx, da))
             unit_bwd(stem_u, da, False)
+            ev = A.event()
+            bw.add(L.OP_SIGNAL, p=(ev,), stream=1)
+            bw.add(L.OP_WAIT, p=(ev,), stream=0)
             self.bwd = bw
-        # one workspace for every op of this plan (they run in stream order)
-        ws = A.new((max(1, ws_need[0]),), torch.uint8, dev)
+        # one workspace per stream for the ops of this plan (each stream runs in order)
+        ws = [A.new((max(1, n),), torch.uint8, dev) for n in ws_need]
         for lst in (fw,) + ((self.bwd,) if self.bwd is not None else ()):
             for o in lst.ops:
                 for j in range(12):
-                    if o.p[j] == _WS_TOKEN and o.ext[j] == -1:
-                        o.p[j] = ws.data_ptr()
+                    if o.ext[j] == -1 and o.p[j] in (_WS_TOKEN, _WS2_TOKEN):
+                        o.p[j] = ws[0 if o.p[j] == _WS_TOKEN else 1].data_ptr()
         self.fwd = fw.freeze()
         if self.bwd is not None:
             self.bwd.freeze()
 
 
-# placeholder operand for the plan's shared workspace, patched once the size is known
-_WS_TOKEN = 0x1
-_WS = _WS_TOKEN
+# placeholder operands for the plan's per-stream workspaces, patched once sizes are known
+_WS_TOKEN, _WS2_TOKEN = 0x1, 0x2
+_WS, _WS2 = _WS_TOKEN, _WS2_TOKEN
+
+
+def _side_stream(trunk, dev):
+    key = "_mmdx_wgrad_stream_%d" % dev.index
+    st = trunk.__dict__.get(key)
+    if st is None:
+        st = trunk.__dict__[key] = torch.cuda.Stream(device=dev)
+    return st
 
 
 def _plans_for(trunk, key, build):
@@ -481,7 +507,7 @@ class _TrunkFn(torch.autograd.Function):
                tuple(p.data_ptr() for p in params))
         plan = _plans_for(trunk, key,
                           lambda: _Plan(trunk, N, H, W, in_nchw, cin, T, train, keep, dev))
-        plan.fwd.run([x.data_ptr()])
+        plan.fwd.run([x.data_ptr()], [stream()])
         if train:  # every BN's num_batches_tracked += 1, in one multi-tensor launch
             torch._foreach_add_([m.num_batches_tracked for m in trunk.modules()
                                  if isinstance(m, BatchNorm2d)], 1)
@@ -490,6 +516,7 @@ class _TrunkFn(torch.autograd.Function):
             plan.arena.owner = weakref.ref(tok)
             ctx.tok = tok
             ctx.plan = plan
+            ctx.trunk_ref = trunk
             ctx.x = None if in_nchw else x  # the stem's wgrad reads an NHWC input directly
         return plan.feats.clone()
 
@@ -502,9 +529,10 @@ class _TrunkFn(torch.autograd.Function):
         dev = dfeats.device
         grads = torch.empty(plan.grad_bytes // 4, dtype=torch.float32, device=dev)
         x0 = ctx.x.data_ptr() if isinstance(plan.x0, _Ext) else plan.x0.data_ptr()
-        plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0])
+        side = _side_stream(ctx.trunk_ref, dev)
+        plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0], [stream(), side.cuda_stream])
         plan.arena.owner = None
-        ctx.plan = ctx.x = ctx.tok = None
+        ctx.plan = ctx.x = ctx.tok = ctx.trunk_ref = None
         out = [None, None, None]
         for prm in trunk_params:
             if prm.requires_grad:
