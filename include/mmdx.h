@@ -80,6 +80,15 @@ int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void*
 /* dx = dgrad + beta * dx  (beta = 1 sums the residual-path gradient in the epilogue) */
 int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
                     const void* w_crsk, void* dx, float beta, void* stream);
+/* dx = dgrad (beta 0) and, in the same epilogue, the backward statistics of the BatchNorm
+ * whose output gradient dx is (its input bn_y, affine, saved mean/rstd; ReLU mask recomputed
+ * from bn_y): stat_part [C][mmdx_conv_dgrad_stat_blocks()] (sum g, sum g*xhat) per 128-row
+ * tile, for mmdx_bn_bwd.  stat_blocks == 0: the fusion does not apply to this conv. */
+int mmdx_conv_dgrad_stat_blocks(int dtype, const mmdx_conv_desc* d);
+int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const void* dy,
+                           const void* w_crsk, void* dx, const void* bn_y, const float* gamma,
+                           const float* bn_beta, const float* save_mean,
+                           const float* save_rstd, int relu, float* stat_part, void* stream);
 size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc* d);
 /* dw_kcrs (fp32, master layout, Cin = c_master) = dw_kcrs*beta + grad */
 int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void* x,
@@ -107,9 +116,13 @@ int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
  * (may be NULL), and dgamma/dbeta (fp32, accumulated with beta_acc). */
 int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
                 long rows, int C, const float* gamma, const float* bn_beta,
-                const float* save_mean, const float* save_rstd, int relu, void* dx,
+                const float* save_mean, const float* save_rstd, int relu,
+                const float* stat_part, int stat_blocks, void* dx,
                 void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                 void* workspace, size_t ws_bytes, void* stream);
+/* stat_part (optional, [C][stat_blocks] pairs (sum g, sum g*xhat)): the reduction already
+ * made by mmdx_conv_dgrad_bnstat in the epilogue that produced dy — the BN backward then
+ * skips its own pass over (dy, x).  Only for relu units without residual (y == NULL). */
 /* relu with y == NULL (a unit without residual): the ReLU mask is recomputed from x as
  * x*scale + shift > 0 with the forward's own scale/shift (gamma, bn_beta, save_mean,
  * save_rstd), so the post-activation tensor is not read. */
@@ -131,7 +144,7 @@ enum {
   MMDX_OP_EVENT = 1, MMDX_OP_NCHW2NHWC, MMDX_OP_CONV_PACK, MMDX_OP_CONV_FWD, MMDX_OP_BN_FWD,
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
-  MMDX_OP_SIGNAL, MMDX_OP_WAIT
+  MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT
 };
 typedef struct {
   int op, dtype, stream;

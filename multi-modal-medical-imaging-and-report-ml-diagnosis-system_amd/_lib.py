@@ -44,7 +44,7 @@ class PlanOp(C.Structure):
 
 (OP_EVENT, OP_NCHW2NHWC, OP_CONV_PACK, OP_CONV_FWD, OP_BN_FWD, OP_MAXPOOL_FWD,
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
- OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT) = range(1, 16)
+ OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT) = range(1, 17)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -58,13 +58,15 @@ SIGNATURES = {
     "mmdx_conv_fwd_stat_blocks": (i32, [CD]),
     "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
+    "mmdx_conv_dgrad_stat_blocks": (i32, [i32, CD]),
+    "mmdx_conv_dgrad_bnstat": (i32, [i32, CD, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]),
     "mmdx_conv_wgrad_workspace_size": (sz, [i32, CD]),
     "mmdx_conv_wgrad": (i32, [i32, CD, i32, vp, vp, vp, f32, vp, sz, vp]),
     "mmdx_bn_workspace_size": (sz, [i64, i32]),
     "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, i32, i64, vp, vp, vp, vp, f32, f32, vp, vp,
                           vp, i32, vp, vp, sz, vp]),
-    "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp,
-                          f32, vp, sz, vp]),
+    "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp,
+                          vp, vp, f32, vp, sz, vp]),
     "mmdx_plan_run": (i32, [C.POINTER(PlanOp), i32, vp, vp, vp, i32]),
     "mmdx_plan_op_size": (sz, []),
     "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,

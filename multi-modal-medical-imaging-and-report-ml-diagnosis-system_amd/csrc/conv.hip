@@ -126,10 +126,12 @@ static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32) {
 
 template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
-                     hipStream_t st, float* stats = nullptr, bool dma_ok = false) {
+                     hipStream_t st, float* stats = nullptr, bool dma_ok = false,
+                     const BnStat& bs = BnStat{}) {
   DenseK<T> sb{(const T*)w, K, N, true};
   EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
                   (float2*)stats};
+  epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
   if constexpr (DmaOk<SA>::value) {
     if (dma_ok) {
     // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
@@ -163,7 +165,7 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
 // as zeros (beta = 0) or left untouched (beta != 0).
 template <typename T>
 static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_crsk, void* dx,
-                             float beta, hipStream_t st) {
+                             float beta, hipStream_t st, BnStat bs = BnStat{}) {
   for (int a = 0; a < g.sh; ++a) {
     for (int b = 0; b < g.sw; ++b) {
       PhaseGeom ph;
@@ -182,6 +184,8 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       DgradPhaseK<T> sa{(const T*)dy, g, ph, M};
       PhaseTapK<T> sb{(const T*)w_crsk, (long)g.R * g.S * g.K, g.C, g.K, g.S, g.sh, g.sw, ph};
       EpiPhase<T> epi{(T*)dx, g.C, M, N, beta, ph.Hp, ph.Wp, g.H, g.W, a, b, g.sh, g.sw};
+      epi.bs = bs;
+      bs.tile0 += (M + 127) / 128;  // the next phase's tiles follow this phase's
       int rc = -1;
       if constexpr (sizeof(T) == 2) {
         if (dma_geom_ok(g, false)) {
@@ -209,14 +213,14 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
 
 template <typename T>
 static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
-                        float beta, hipStream_t st) {
+                        float beta, hipStream_t st, const BnStat& bs = BnStat{}) {
   const ConvGeom g = geom(d);
   if ((g.sh > 1 || g.sw > 1) && g.K % KTile<T>::BK == 0)
-    return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st);
+    return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st, bs);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
   if (g.K % KTile<T>::BK == 0)
     return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
-                        nullptr, dma_geom_ok(g, true));
+                        nullptr, dma_geom_ok(g, true), bs);
   return conv_gemm<T>(DgradK<T, false>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
 }
 
@@ -356,4 +360,44 @@ extern "C" int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master,
   if (dtype == BF16)
     return conv_wgrad_t<bf16>(d, c_master, x, dy, dw, beta, ws, ws_bytes, (hipStream_t)stream);
   return conv_wgrad_t<float>(d, c_master, x, dy, dw, beta, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// Fused consumer-BN backward statistics are produced by the LDS-DMA dgrad kernels only
+// (bf16, Kout % 64 == 0, 32-bit offsets; strided convs need every output phase reached).
+// Returns the number of 128-row partial slots, or 0 when the fusion does not apply.
+extern "C" int mmdx_conv_dgrad_stat_blocks(int dtype, const mmdx_conv_desc* d) {
+  if (dtype != BF16 || !d || d->K % 64 != 0 || d->C % 8 != 0) return 0;
+  const ConvGeom g = geom(d);
+  if (g.sh == 1 && g.sw == 1) {
+    if (!dma_geom_ok(g, true)) return 0;
+    return (int)(((long)g.N * g.H * g.W + 127) / 128);
+  }
+  if (!dma_geom_ok(g, false)) return 0;
+  long tiles = 0;
+  for (int a = 0; a < g.sh; ++a)
+    for (int b = 0; b < g.sw; ++b) {
+      const int Hp = g.H > a ? (g.H - a + g.sh - 1) / g.sh : 0;
+      const int Wp = g.W > b ? (g.W - b + g.sw - 1) / g.sw : 0;
+      const int r0 = (a + g.ph) % g.sh, s0 = (b + g.pw) % g.sw;
+      if (Hp == 0 || Wp == 0) continue;
+      if (r0 >= g.R || s0 >= g.S) return 0;  // an unreached phase: no fused statistics
+      tiles += ((long)g.N * Hp * Wp + 127) / 128;
+    }
+  return (int)tiles;
+}
+
+extern "C" int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const void* dy,
+                                      const void* w_crsk, void* dx, const void* bn_y,
+                                      const float* gamma, const float* bn_beta,
+                                      const float* save_mean, const float* save_rstd, int relu,
+                                      float* stat_part, void* stream) {
+  int rc = check_desc(d, 8);
+  if (rc) return rc;
+  const int tiles = mmdx_conv_dgrad_stat_blocks(dtype, d);
+  MMDX_CHECK_ARG(tiles > 0, "conv dgrad bnstat: fused statistics unsupported for this conv");
+  MMDX_CHECK_ARG(bn_y && save_mean && save_rstd && stat_part, "conv dgrad bnstat: null operand");
+  MMDX_CHECK_ARG(((uintptr_t)dx & 15) == 0 && ((uintptr_t)bn_y & 15) == 0,
+                 "conv dgrad bnstat: dx / y must be 16-B aligned");
+  BnStat bs{bn_y, gamma, bn_beta, save_mean, save_rstd, (float2*)stat_part, relu, tiles, 0};
+  return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, 0.f, (hipStream_t)stream, bs);
 }

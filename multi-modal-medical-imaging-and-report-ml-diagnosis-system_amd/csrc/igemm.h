@@ -632,6 +632,79 @@ struct RMajorLoader {
 // --------------------------------------------------------------------------------------
 // Epilogues. `apply4(m, n, v)` handles 4 consecutive columns n..n+3 of row m.
 // --------------------------------------------------------------------------------------
+// Statistics of a consumer BatchNorm's backward, fused into the epilogue of the dgrad that
+// produces its input gradient dout (units without a residual: their ReLU mask is recomputed
+// from the BN input y with the forward's scale/shift).  Per column n over the tile's rows:
+// (sum g, sum g*xhat), g = dout * [y*scale + shift > 0], xhat = (y - mean) * rstd — the
+// partials bn_bwd_reduce_kernel would compute, written [N][tiles] at tile0 + tm.  The dout
+// values used are the stored (rounded) ones, as the separate reduce would read them.
+struct BnStat {
+  const void* y; const float *gamma, *beta, *mean, *rstd; float2* part; int relu, tiles, tile0;
+};
+
+struct BnCoef8 { float mu[8], rs[8], sc[8], sh[8]; };
+
+__device__ __forceinline__ void bn_coef8(const BnStat& b, int n, int N, BnCoef8& c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool ok = n + j < N;
+    const float mu = ok ? b.mean[n + j] : 0.f, rs = ok ? b.rstd[n + j] : 0.f;
+    const float g = ok && b.gamma ? b.gamma[n + j] : 1.f;
+    c.mu[j] = mu;
+    c.rs[j] = rs;
+    c.sc[j] = g * rs;  // same expression order as bn_coef / bn_bwd_reduce_kernel
+    c.sh[j] = (ok && b.beta ? b.beta[n + j] : 0.f) - mu * g * rs;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void bn_acc8(const BnStat& b, long off, f32x4 lo, f32x4 hi,
+                                        const BnCoef8& c, float* sg, float* sgx) {
+  typedef __attribute__((ext_vector_type(8))) T T8;
+  const T8 yv = *(const T8*)((const T*)b.y + off);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float g = to_f(from_f<T>(j < 4 ? lo[j] : hi[j - 4]));
+    const float y = to_f(yv[j]);
+    if (b.relu && !(y * c.sc[j] + c.sh[j] > 0.f)) g = 0.f;
+    sg[j] += g;
+    sgx[j] += g * (y - c.mu[j]) * c.rs[j];
+  }
+}
+
+// Merge the per-thread column sums of the vec8 epilogue loop (threads with equal
+// threadIdx % C8 own the same 8 columns) and store the tile's partials.
+template <int BN, int NW>
+__device__ __forceinline__ void bn_stat_store(const BnStat& b, float* sg, float* sgx, float* red,
+                                              int tm, int tn, int N) {
+  constexpr int C8 = BN / 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int x = C8; x < 64; x <<= 1)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sg[j] += __shfl_xor(sg[j], x, 64);
+      sgx[j] += __shfl_xor(sgx[j], x, 64);
+    }
+  if (lane < C8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wid * BN + lane * 8 + j) * 2] = sg[j];
+      red[(wid * BN + lane * 8 + j) * 2 + 1] = sgx[j];
+    }
+  __syncthreads();
+  const int col = threadIdx.x;
+  if (col < BN && tn * BN + col < N) {
+    float a = 0.f, c = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      a += red[(w * BN + col) * 2];
+      c += red[(w * BN + col) * 2 + 1];
+    }
+    b.part[(long)(tn * BN + col) * b.tiles + b.tile0 + tm] = make_float2(a, c);
+  }
+}
+
 template <typename OutT>
 struct EpiStore {
   OutT* C; long ldc; int M, N;
@@ -641,6 +714,9 @@ struct EpiStore {
   float alpha, beta;    // C = act(alpha*acc + bias + addend) + beta*C
   OutT* preact;         // optional copy of the pre-activation value, ld = ldc
   float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [N][tiles_m]
+  BnStat bs{};          // optional fused consumer-BN backward statistics (bs.part != null)
+  static constexpr bool BNSTAT = true;
+  __device__ __forceinline__ long bn_off(int m, int n) const { return (long)m * ldc + n; }
   // Per-column (mean, M2) over this tile's valid rows, from the fp32 accumulators staged in
   // LDS (cst [BM][LDC]) — the BatchNorm statistics of a conv output without re-reading it.
   // Two passes (mean, then squared deviations) over NT/BN row slices, merged with Chan.
@@ -841,6 +917,9 @@ struct EpiPartial {
   template <int BM, int BN, int WM, int WN, int RM, int RN>
   __device__ __forceinline__ void reg_stats(const f32x4 (&)[RM][RN], float*, int, int, int,
                                             int, int) const {}
+  BnStat bs{};
+  static constexpr bool BNSTAT = false;
+  __device__ __forceinline__ long bn_off(int, int) const { return 0; }
   __device__ __forceinline__ bool vec8_ok() const { return N % 4 == 0; }
   __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
     if (m >= M) return;
@@ -856,6 +935,9 @@ template <typename OutT>
 struct EpiPhase {
   OutT* C; int ldc, M, N; float beta;
   int Hp, Wp, H, W, a, b, sh, sw;
+  BnStat bs{};
+  static constexpr bool BNSTAT = true;
+  __device__ __forceinline__ long bn_off(int m, int n) const { return pix(m) * ldc + n; }
   __device__ __forceinline__ long pix(int m) const {
     const int hw = Hp * Wp;
     const int n = m / hw, rem = m - n * hw;
@@ -1166,7 +1248,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int OP_BYTES = NS * STAGE;
   constexpr int LDC = BN + 4;
-  constexpr int EPI_BYTES = BM * LDC * 4 + WM * BN * 3 * 4;
+  constexpr int EPI_BYTES = BM * LDC * 4 + 4 * BN * 3 * 4;  // staged tile + reduction scratch
   constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
   // DMA instructions one wave issues per K tile (both operands)
   constexpr int PER_TILE = OA::INSTR + OB::INSTR;
@@ -1249,13 +1331,24 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   if constexpr (!Epi::REG_STATS) epi.template tile_stats<BM, BN, LDC>(cst, red, tm, tn);
   if (epi.vec8_ok()) {
     constexpr int C8 = BN / 8;
+    static_assert(NT % C8 == 0, "a thread's 8 columns are the same every iteration");
+    const int col = (threadIdx.x % C8) * 8;
+    const bool bst = Epi::BNSTAT && epi.bs.part != nullptr;
+    BnCoef8 bc;
+    float sg[8], sgx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+    if (bst) bn_coef8(epi.bs, tn * BN + col, N, bc);
 #pragma unroll 2
     for (int c = threadIdx.x; c < BM * C8; c += NT) {
-      const int row = c / C8, col = (c - row * C8) * 8;
+      const int row = c / C8;
       const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
       const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
-      epi.apply8_fast(tm * BM + row, tn * BN + col, lo, hi);
+      const int m = tm * BM + row, n = tn * BN + col;
+      epi.apply8_fast(m, n, lo, hi);
+      if (bst && m < M && n < N) bn_acc8<bf16>(epi.bs, epi.bn_off(m, n), lo, hi, bc, sg, sgx);
     }
+    if (bst) bn_stat_store<BN, NT / 64>(epi.bs, sg, sgx, red, tm, tn, N);
   } else {
     constexpr int C4 = BN / 4;
     for (int c = threadIdx.x; c < BM * C4; c += NT) {

@@ -435,7 +435,7 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
 template <typename T>
 static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, long rows, int C,
                     const float* gamma, const float* bbeta, const float* smean,
-                    const float* srstd, int relu,
+                    const float* srstd, int relu, const float* stat_part, int stat_blocks,
                     void* dx, void* dres, float* dgamma, float* dbeta, float beta_acc, void* ws,
                     size_t ws_bytes, hipStream_t st) {
   constexpr int VEC = Vec16<T>::N;
@@ -445,16 +445,24 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "bn bwd: workspace %zu < %zu", ws_bytes, need);
   float2* part = (float2*)ws;
   float* coef = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
-                     (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
-                     smean, srstd, relu, gamma, bbeta, part);
-  if (L.rblocks > 512)
+  int nblk = L.rblocks;
+  if (stat_part) {  // (sum g, sum g*xhat) partials already made by the dgrad epilogue
+    MMDX_CHECK_ARG(stat_blocks > 0 && relu && !y, "bn bwd: precomputed partials need a "
+                   "ReLU unit without residual");
+    part = (float2*)stat_part;
+    nblk = stat_blocks;
+  } else {
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
+                       (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
+                       smean, srstd, relu, gamma, bbeta, part);
+  }
+  if (nblk > 512)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
-                       (const float2*)part, L.rblocks, rows, C, train, gamma, bbeta, smean,
+                       (const float2*)part, nblk, rows, C, train, gamma, bbeta, smean,
                        srstd, dgamma, dbeta, beta_acc, coef);
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0,
-                       st, (const float2*)part, L.rblocks, rows, C, train, gamma, bbeta, smean,
+                       st, (const float2*)part, nblk, rows, C, train, gamma, bbeta, smean,
                        srstd, dgamma, dbeta, beta_acc, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
                      (const T*)x, (const T*)y, (const T*)dy, rows, C, smean, srstd,
@@ -660,7 +668,8 @@ extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C
 
 extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
                            long rows, int C, const float* gamma, const float* bn_beta,
-                           const float* save_mean, const float* save_rstd, int relu, void* dx,
+                           const float* save_mean, const float* save_rstd, int relu,
+                           const float* stat_part, int stat_blocks, void* dx,
                            void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                            void* ws, size_t ws_bytes, void* stream) {
   MMDX_CHECK_ARG(rows > 0 && C > 0, "bn bwd: bad args");
@@ -668,9 +677,11 @@ extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, c
   hipStream_t st = (hipStream_t)stream;
   if (dtype == BF16)
     return bn_bwd_t<bf16>(train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd, relu,
-                          dx, d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+                          stat_part, stat_blocks, dx, d_residual, dgamma, dbeta, beta_acc, ws,
+                          ws_bytes, st);
   return bn_bwd_t<float>(train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd, relu,
-                         dx, d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+                         stat_part, stat_blocks, dx, d_residual, dgamma, dbeta, beta_acc, ws,
+                         ws_bytes, st);
 }
 
 extern "C" int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual, long rows,

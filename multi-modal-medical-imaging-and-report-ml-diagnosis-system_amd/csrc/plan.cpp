@@ -68,12 +68,21 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                               o.i[1], o.i[2], o.i[3], o.i[4], o.i[5], o.i[6], o.i[7],
                               (int)o.l[0], P(o, 2, ext), s);
     case MMDX_OP_BN_BWD:
-      // i: train, C, relu; l: rows, ws_bytes; f: beta_acc
+      // i: train, C, relu, stat_blocks; l: rows, ws_bytes; f: beta_acc;
+      // p: x, y, dy, gamma, beta, mean, rstd, dx, dres, dgamma, dbeta, ws; stat_part in l[2]
       return mmdx_bn_bwd(o.dtype, o.i[0], P(o, 0, ext), P(o, 1, ext), P(o, 2, ext), o.l[0],
                          o.i[1], (const float*)P(o, 3, ext), (const float*)P(o, 4, ext),
                          (const float*)P(o, 5, ext), (const float*)P(o, 6, ext), o.i[2],
-                         P(o, 7, ext), P(o, 8, ext), (float*)P(o, 9, ext),
-                         (float*)P(o, 10, ext), o.f[0], P(o, 11, ext), (size_t)o.l[1], s);
+                         (const float*)o.l[2], o.i[3], P(o, 7, ext), P(o, 8, ext),
+                         (float*)P(o, 9, ext), (float*)P(o, 10, ext), o.f[0], P(o, 11, ext),
+                         (size_t)o.l[1], s);
+    case MMDX_OP_CONV_DGRAD_BNSTAT:
+      // i: relu; p: dy, w_crsk, dx, bn_y, gamma, beta, mean, rstd, stat_part
+      return mmdx_conv_dgrad_bnstat(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
+                                    P(o, 3, ext), (const float*)P(o, 4, ext),
+                                    (const float*)P(o, 5, ext), (const float*)P(o, 6, ext),
+                                    (const float*)P(o, 7, ext), o.i[0], (float*)P(o, 8, ext),
+                                    s);
     case MMDX_OP_CONV_WGRAD:
       // i: c_master; l: ws_bytes; f: beta
       return mmdx_conv_wgrad(o.dtype, &o.d, o.i[0], P(o, 0, ext), P(o, 1, ext),

@@ -389,7 +389,12 @@ class _Plan:
             def xref(x):
                 return _Ext(2) if isinstance(x, _Ext) else x
 
-            def unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False):
+            def unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False, stats=None,
+                         feed=None):
+                """BN(+res)(+ReLU) backward, wgrad (side stream), dgrad.  `stats`: this
+                unit's BN-backward partials, already made by the dgrad that produced `dout`;
+                `feed`: the unit whose dout this unit's dgrad produces (no residual) — its
+                partials are then made in the dgrad epilogue and returned."""
                 d = u["d"]
                 K = d.K
                 rows = d.N * d.P * d.Q
@@ -398,8 +403,9 @@ class _Plan:
                 wsn = L.lib().mmdx_bn_workspace_size(rows, K)
                 ws_for(wsn)
                 out = u["out"] if want_res else None  # no residual: mask recomputed from y
-                bw.add(L.OP_BN_BWD, dt, i=(int(train), K, int(u["relu"])), l=(rows, wsn),
-                       f=(0.0,),
+                sp, sb = stats if stats is not None else (None, 0)
+                bw.add(L.OP_BN_BWD, dt, i=(int(train), K, int(u["relu"]), sb),
+                       l=(rows, wsn, sp.data_ptr() if sp is not None else 0), f=(0.0,),
                        p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"], u["rstd"],
                           dconv, dres, g(u["bn"].weight), g(u["bn"].bias), _WS))
                 wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
@@ -409,37 +415,50 @@ class _Plan:
                 bw.add(L.OP_WAIT, p=(ev,), stream=1)
                 bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(u["cm"],), l=(wsn,),
                          f=(0.0,), p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
-                dx = None
+                dx, fed = None, None
                 if want_dx:
                     if dx_acc is not None:
                         dx, beta = dx_acc, 1.0
                     else:
                         dx, beta = A.new((d.N, d.H, d.W, d.C), T, dev), 0.0
-                    bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(beta,),
-                             p=(dconv, u["wc"], dx), d=d)
-                return dx, dres
+                    tiles = (L.lib().mmdx_conv_dgrad_stat_blocks(dt, d)
+                             if feed is not None and beta == 0.0 and feed["relu"] else 0)
+                    if tiles > 0:
+                        fed = (A.new((d.C, tiles, 2), torch.float32, dev), tiles)
+                        fb = feed["bn"]
+                        bw.timed("dgrad", L.OP_CONV_DGRAD_BNSTAT, dtype=dt, i=(1,),
+                                 p=(dconv, u["wc"], dx, feed["y"], fb.weight, fb.bias,
+                                    feed["mean"], feed["rstd"], fed[0]), d=d)
+                    else:
+                        bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(beta,),
+                                 p=(dconv, u["wc"], dx), d=d)
+                return dx, dres, fed
 
             N_, H_, W_, C_ = self.out_geom
             dx = A.new((N_, H_, W_, C_), T, dev)
             bw.add(L.OP_AVGPOOL_BWD, dt, i=(N_, H_ * W_, C_), p=(_Ext(0), dx))
             for bu, ds_u, _shape in reversed(blocks):
-                dh, dres = unit_bwd(bu[-1], dx, True, want_res=True)
-                for uu in reversed(bu[:-1]):
-                    if uu is bu[0]:
+                # unit i's dgrad produces the gradient of unit i-1's output (no residual
+                # inside a block): it also makes unit i-1's BN-backward partials
+                dh, dres, fed = unit_bwd(bu[-1], dx, True, want_res=True,
+                                         feed=bu[-2] if len(bu) > 1 else None)
+                for k in range(len(bu) - 2, -1, -1):
+                    uu = bu[k]
+                    if k == 0:
                         # d(block input) = dgrad(conv1) + identity-path grad (beta = 1)
                         if ds_u is not None:
-                            dxi, _ = unit_bwd(ds_u, dres, True)
+                            dxi, _, _ = unit_bwd(ds_u, dres, True)
                         else:
                             dxi = dres
-                        dh, _ = unit_bwd(uu, dh, True, dx_acc=dxi)
+                        dh, _, _ = unit_bwd(uu, dh, True, dx_acc=dxi, stats=fed)
                     else:
-                        dh, _ = unit_bwd(uu, dh, True)
+                        dh, _, fed = unit_bwd(uu, dh, True, stats=fed, feed=bu[k - 1])
                 dx = dh
             n0, h0, w0, c0, p0, q0 = stem_geom
             da = A.new((n0, h0, w0, c0), T, dev)
             bw.add(L.OP_MAXPOOL_BWD, dt, i=(n0, h0, w0, c0, mp.kernel_size, mp.stride,
                                             mp.padding, p0), l=(q0,), p=(am, dx, da))
-            unit_bwd(stem_u, da, False)
+            unit_bwd(stem_u, da, False)  # (no dgrad into the image)
             ev = A.event()
             bw.add(L.OP_SIGNAL, p=(ev,), stream=1)
             bw.add(L.OP_WAIT, p=(ev,), stream=0)

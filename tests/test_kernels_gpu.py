@@ -188,13 +188,13 @@ def test_batchnorm(dev, dt, train, res, relu):
     dg = torch.empty(C, device=dev)
     db = torch.empty(C, device=dev)
     L.call("mmdx_bn_bwd", dc, train, xd.data_ptr(), y.data_ptr(), dyd.data_ptr(), rows, C,
-           gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), int(relu),
+           gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), int(relu), None, 0,
            dx.data_ptr(), dres.data_ptr() if res else None, dg.data_ptr(), db.data_ptr(), 0.0,
            ws.data_ptr(), ws_n, L.stream())
     if relu and not res:  # mask recomputed from x instead of read from y: identical result
         dx2 = torch.empty_like(xd)
         L.call("mmdx_bn_bwd", dc, train, xd.data_ptr(), None, dyd.data_ptr(), rows, C,
-               gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
+               gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1, None, 0,
                dx2.data_ptr(), None, None, None, 0.0, ws.data_ptr(), ws_n, L.stream())
         assert torch.equal(dx2, dx)
     tol_dt = dt
@@ -331,3 +331,59 @@ def test_dropout_counter_rng_and_graph_replay(dev, dt):
     m2 = (static_y != 0).clone()
     assert not torch.equal(m1, m2)
     assert abs(m2.float().mean().item() - (1 - p)) < 0.005
+
+
+@pytest.mark.parametrize("cfg", [(2, 14, 14, 64, 64, 3, 1), (2, 9, 7, 64, 128, 1, 1),
+                                 (3, 15, 13, 64, 128, 3, 2), (2, 28, 28, 128, 64, 3, 2)])
+def test_dgrad_fused_bn_stats(dev, cfg):
+    """dgrad with the consumer BN's backward statistics in its epilogue, then mmdx_bn_bwd on
+    those partials == dgrad, then mmdx_bn_bwd with its own reduce pass (bf16; ragged row
+    counts; stride 2 runs as output phases).  Only the summation order differs."""
+    N, H, W, C, K, k, s = cfg
+    p = k // 2
+    dt = torch.bfloat16
+    dc = L.dtype_code(dt)
+    g = torch.Generator().manual_seed(11)
+    P, Q = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q)
+    tiles = L.lib().mmdx_conv_dgrad_stat_blocks(dc, d)
+    assert tiles > 0
+    w = (torch.randn(K, C, k, k, generator=g) * 0.1).to(dev)
+    wk = torch.empty(K, k, k, C, dtype=dt, device=dev)
+    wc = torch.empty(C, k, k, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", dc, d, C, w.data_ptr(), wk.data_ptr(), wc.data_ptr(),
+           L.stream())
+    dy = torch.randn(N, P, Q, K, generator=g).to(dev, dt)
+    y = torch.randn(N, H, W, C, generator=g).to(dev, dt)       # BN input of the consumer
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.1).to(dev)
+    mean = (torch.randn(C, generator=g) * 0.1).to(dev)
+    rstd = (torch.rand(C, generator=g) + 0.5).to(dev)
+    rows = N * H * W
+    dx_a = torch.empty(N, H, W, C, dtype=dt, device=dev)
+    part = torch.empty(C, tiles, 2, device=dev)
+    L.call("mmdx_conv_dgrad_bnstat", dc, d, dy.data_ptr(), wc.data_ptr(), dx_a.data_ptr(),
+           y.data_ptr(), gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
+           part.data_ptr(), L.stream())
+    dx_b = torch.empty_like(dx_a)
+    L.call("mmdx_conv_dgrad", dc, d, dy.data_ptr(), wc.data_ptr(), dx_b.data_ptr(), 0.0,
+           L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx_a, dx_b)
+    ws_n = L.lib().mmdx_bn_workspace_size(rows, C)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    outs = []
+    for sp, nb in ((part, tiles), (None, 0)):
+        dcv = torch.empty_like(y)
+        dg = torch.empty(C, device=dev)
+        db = torch.empty(C, device=dev)
+        L.call("mmdx_bn_bwd", dc, 1, y.data_ptr(), None, dx_a.data_ptr(), rows, C,
+               gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
+               L.ptr(sp), nb, dcv.data_ptr(), None, dg.data_ptr(), db.data_ptr(), 0.0,
+               ws.data_ptr(), ws_n, L.stream())
+        outs.append((dcv.float(), dg, db))
+    torch.cuda.synchronize()
+    (ca, ga, ba), (cb, gb, bb) = outs
+    assert (ga - gb).abs().max().item() <= 1e-4 * max(1.0, gb.abs().max().item())
+    assert (ba - bb).abs().max().item() <= 1e-4 * max(1.0, bb.abs().max().item())
+    assert (ca - cb).abs().max().item() <= 2e-2 * max(1.0, cb.abs().max().item())
