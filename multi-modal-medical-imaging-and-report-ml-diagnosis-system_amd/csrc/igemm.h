@@ -657,11 +657,11 @@ __device__ __forceinline__ void bn_coef8(const BnStat& b, int n, int N, BnCoef8&
   }
 }
 
+typedef __attribute__((ext_vector_type(8))) __bf16 bn_y8;
+
 template <typename T>
-__device__ __forceinline__ void bn_acc8(const BnStat& b, long off, f32x4 lo, f32x4 hi,
+__device__ __forceinline__ void bn_acc8(const bn_y8& yv, f32x4 lo, f32x4 hi, const BnStat& b,
                                         const BnCoef8& c, float* sg, float* sgx) {
-  typedef __attribute__((ext_vector_type(8))) T T8;
-  const T8 yv = *(const T8*)((const T*)b.y + off);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float g = to_f(from_f<T>(j < 4 ? lo[j] : hi[j - 4]));
@@ -1317,6 +1317,21 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 
   float* cst = (float*)lds_raw;
   float* red = cst + BM * LDC;
+  // fused consumer-BN backward statistics: the BN input y of this thread's output chunks is
+  // loaded now, so its latency overlaps the accumulator staging below
+  constexpr int C8 = BN / 8, ITERS = BM * C8 / NT;
+  static_assert(NT % C8 == 0 && (BM * C8) % NT == 0, "vec8 epilogue geometry");
+  const bool bst = Epi::BNSTAT && epi.bs.part != nullptr && epi.vec8_ok();
+  bn_y8 yv[ITERS];
+  if (bst) {
+    const int n = tn * BN + (threadIdx.x % C8) * 8;
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int m = tm * BM + (threadIdx.x + it * NT) / C8;
+      yv[it] = m < M && n < N ? *(const bn_y8*)((const bf16*)epi.bs.y + epi.bn_off(m, n))
+                              : bn_y8{};
+    }
+  }
   if constexpr (Epi::REG_STATS)
     epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
 #pragma unroll
@@ -1329,26 +1344,32 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
             acc[i][j][r];
   __syncthreads();
   if constexpr (!Epi::REG_STATS) epi.template tile_stats<BM, BN, LDC>(cst, red, tm, tn);
-  if (epi.vec8_ok()) {
-    constexpr int C8 = BN / 8;
-    static_assert(NT % C8 == 0, "a thread's 8 columns are the same every iteration");
+  if (bst) {  // vec8 stores + the statistics of every stored chunk (rows >= M excluded)
     const int col = (threadIdx.x % C8) * 8;
-    const bool bst = Epi::BNSTAT && epi.bs.part != nullptr;
     BnCoef8 bc;
     float sg[8], sgx[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
-    if (bst) bn_coef8(epi.bs, tn * BN + col, N, bc);
+    bn_coef8(epi.bs, tn * BN + col, N, bc);
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int row = (threadIdx.x + it * NT) / C8;
+      const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
+      const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
+      const int m = tm * BM + row, n = tn * BN + col;
+      epi.apply8_fast(m, n, lo, hi);
+      if (m < M && n < N) bn_acc8<bf16>(yv[it], lo, hi, epi.bs, bc, sg, sgx);
+    }
+    bn_stat_store<BN, NT / 64>(epi.bs, sg, sgx, red, tm, tn, N);
+  } else if (epi.vec8_ok()) {
+    const int col = (threadIdx.x % C8) * 8;
 #pragma unroll 2
     for (int c = threadIdx.x; c < BM * C8; c += NT) {
       const int row = c / C8;
       const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
       const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
-      const int m = tm * BM + row, n = tn * BN + col;
-      epi.apply8_fast(m, n, lo, hi);
-      if (bst && m < M && n < N) bn_acc8<bf16>(epi.bs, epi.bn_off(m, n), lo, hi, bc, sg, sgx);
+      epi.apply8_fast(tm * BM + row, tn * BN + col, lo, hi);
     }
-    if (bst) bn_stat_store<BN, NT / 64>(epi.bs, sg, sgx, red, tm, tn, N);
   } else {
     constexpr int C4 = BN / 4;
     for (int c = threadIdx.x; c < BM * C4; c += NT) {
