@@ -261,14 +261,22 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
         opt.zero_grad(set_to_none=True)
         main = torch.cuda.current_stream()
         side.wait_stream(main)
-        with torch.cuda.stream(side):   # text tower concurrent with the image tower
-            z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+        # image tower first: its trunk is one native plan call, so the main stream starts at
+        # once; the text tower (Python-issued) then runs concurrently on the side stream
         z_img = img(x)["embeddings"]
+        with torch.cuda.stream(side):
+            z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
         main.wait_stream(side)
         logits = fus(z_img, z_txt)["disease_logits"]
         loss = mmdx.BCEWithLogitsLoss()(logits, y)
-        # = loss.backward(), with the text tower's backward queued before the image trunk's
-        two_tower_backward(loss, z_img, z_txt, fus.parameters(), text_stream=side)
+        # = loss.backward(), with the text tower's backward queued before the image trunk's;
+        # N > 1: the text tower's and fusion head's gradients start their RCCL all-reduce
+        # (from the text stream) while the image trunk is still in its backward
+        early = None
+        if reducer is not None:
+            early = lambda: reducer.launch(list(txt.parameters()) + list(fus.parameters()))
+        two_tower_backward(loss, z_img, z_txt, fus.parameters(), text_stream=side,
+                           on_text_done=early)
         if reducer is not None:
             reducer.reduce()
         _, scale = MO.grad_norm(params, 1.0)
@@ -395,6 +403,14 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # host cost of one step issued onto an idle device (no queue back-pressure)
+    was = timer.enabled
+    timer.enabled = False
+    t1 = time.perf_counter()
+    run()
+    host_one = time.perf_counter() - t1
+    torch.cuda.synchronize()
+    timer.enabled = was
     if mode == "step":
         loss = static_loss
     if use_graph:
@@ -447,6 +463,7 @@ def main():
                    "parallelism": f"dp{world}"},
         "loss": round(float(loss.item()), 5),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
+        "host_ms_one_step_idle_device": round(host_one * 1e3, 3),
         "model_tflops": round(total_flops * samples / el / 1e12, 2),
         "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
                                           (PEAK_BF16_TFLOPS * world), 2),

@@ -20,17 +20,30 @@ BUCKET_BYTES = 64 << 20
 
 
 class GradAllReducer:
+    """Mean all-reduce of `.grad` over the ranks.
+
+    `launch(params)` starts the asynchronous all-reduce of those parameters' gradients as
+    soon as they are final — from the stream that produced them, so RCCL runs beside the
+    rest of the backward (the text tower's and fusion head's gradients while the image trunk
+    is still in its backward).  `finish()` waits for every launched collective on the
+    current stream and writes the averages back.  `reduce()` = launch(all not yet
+    launched) + finish().
+
+    Gradients that are views covering one whole flat buffer (the ResNet trunk's gradient
+    arena, resnet._TrunkFn) are reduced in place on that buffer — no pack/unpack copies;
+    the rest are packed into `bucket_bytes` buckets.
+    """
+
     def __init__(self, params, world_size: int | None = None, bucket_bytes: int = BUCKET_BYTES,
                  group=None):
         self.params = [p for p in params if p.requires_grad]
         self.world = world_size or dist.get_world_size(group)
         self.bucket_bytes = bucket_bytes
         self.group = group
-        self._plan_key = None
-        self._plan = None
-        self._flat = None
+        self._pending = []
+        self._launched = set()
 
-    def _make_plan(self, grads):
+    def _buckets(self, grads):
         plan, cur, size = [], [], 0
         # reverse parameter order ~ order in which backward produces the gradients
         for g in reversed(grads):
@@ -43,26 +56,53 @@ class GradAllReducer:
             plan.append(cur)
         return plan
 
-    def reduce(self):
-        """All-reduce (mean) every existing .grad across ranks, in place."""
-        grads = [p.grad for p in self.params if p.grad is not None]
-        if not grads or self.world == 1:
+    def launch(self, params=None):
+        """Start the all-reduce of these parameters' gradients (default: all remaining)."""
+        if self.world == 1:
             return
-        key = tuple(g.data_ptr() for g in grads)
-        if key != self._plan_key:
-            self._plan = self._make_plan(grads)
-            self._plan_key = key
-        pending = []
-        for bucket in self._plan:
+        ps = self.params if params is None else [p for p in params if p.requires_grad]
+        grads = []
+        for p in ps:
+            if id(p) in self._launched or p.grad is None:
+                continue
+            self._launched.add(id(p))
+            grads.append(p.grad)
+        # whole flat buffers first (reduced in place)
+        by_base = {}
+        for g in grads:
+            b = g._base
+            if b is not None and b.is_contiguous():
+                by_base.setdefault(id(b), (b, []))[1].append(g)
+        loose = []
+        for b, gs in by_base.values():
+            if sum(g.numel() for g in gs) == b.numel():
+                work = dist.all_reduce(b, group=self.group, async_op=True)
+                self._pending.append((None, b, work))
+            else:
+                loose += gs
+        loose += [g for g in grads if g._base is None or not g._base.is_contiguous()]
+        for bucket in self._buckets(loose):
             flat = torch._utils._flatten_dense_tensors(bucket)
             work = dist.all_reduce(flat, group=self.group, async_op=True)
-            pending.append((bucket, flat, work))
+            self._pending.append((bucket, flat, work))
+
+    def finish(self):
         inv = 1.0 / self.world
-        for bucket, flat, work in pending:
+        for bucket, flat, work in self._pending:
             work.wait()
             flat.mul_(inv)
-            for g, s in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
-                g.copy_(s)
+            if bucket is not None:
+                for g, s in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
+                    g.copy_(s)
+        self._pending = []
+        self._launched = set()
+
+    def reduce(self):
+        """All-reduce (mean) every existing .grad across ranks, in place."""
+        if self.world == 1:
+            return
+        self.launch()
+        self.finish()
 
 
 def shard_batch(batch_size: int, rank: int, world: int):

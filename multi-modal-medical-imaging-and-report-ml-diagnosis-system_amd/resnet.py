@@ -379,7 +379,7 @@ class _Plan:
             off = 0
             for prm in params:
                 self.grad_off[id(prm)] = off
-                off += (prm.numel() * 4 + 255) // 256 * 256
+                off += (prm.numel() * 4 + 15) // 16 * 16  # 16-B aligned, dense for ResNets
             self.grad_bytes = off
             self.params = params
 
