@@ -199,6 +199,30 @@ int mmdx_rows_copy(int dtype, const void* src, long src_ld, void* dst, long dst_
                    int D, void* stream);
 int mmdx_add(int dtype, long n, const void* x, const void* y, void* out, void* stream);
 
+/* ---------------------------------------------------------------- image preprocessing
+ * Batched GPU version of image_transfom_into_tensor (TP:112-119): torchvision
+ * Resize(256, antialias=True) on a PIL image (= PIL ImagingResample, bilinear filter, two
+ * fixed-point passes, horizontal first, 22-bit coefficients, uint8 clipped after each pass),
+ * CenterCrop(224), ToTensor, gray->RGB repeat, Normalize(ImageNet).  Bit-exact with the CPU
+ * transform.  pixels: the batch's decoded HWC uint8 images (JPEG decode stays on the host,
+ * PIL, TP:146) packed back to back; descs/coef: per-image geometry and PIL coefficient
+ * tables (host-computed, mmdx.preprocess); temp: >= sum of trows*out_w*c bytes;
+ * out: [B][3][out_h][out_w] fp32. */
+typedef struct {
+  long src_off;         /* byte offset of the image's HWC pixels */
+  long kh_off, kv_off;  /* int offsets into coef: per crop column / row {min, count, k[ksize]} */
+  long temp_off;        /* byte offset of the image's [trows][out_w][c] intermediate */
+  int w, h, c;          /* source width, height, channels (1 = L, 3 = RGB) */
+  int left, top;        /* crop origin in the resized image */
+  int need_h, need_v;   /* which PIL resample passes run */
+  int ksize_h, ksize_v; /* coefficients per output column / row */
+  int trow0, trows;     /* source rows the horizontal pass covers */
+} mmdx_img_desc;
+size_t mmdx_img_desc_size(void); /* sizeof(mmdx_img_desc): binding layout check */
+int mmdx_image_preprocess(const uint8_t* pixels, const mmdx_img_desc* descs, int B,
+                          const int* coef, int max_trows, int out_h, int out_w, uint8_t* temp,
+                          float* out, void* stream);
+
 /* ---------------------------------------------------------------- elementwise / norms
  * LayerNorm over the last dim D (fusion_mlp[3] TP:538, BERT LayerNorms);
  * optional residual added before the norm (BERT "Add & Norm"). */

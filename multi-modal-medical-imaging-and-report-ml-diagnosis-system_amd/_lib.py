@@ -67,6 +67,8 @@ SIGNATURES = {
                           vp, i32, vp, vp, sz, vp]),
     "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp,
                           vp, vp, f32, vp, sz, vp]),
+    "mmdx_img_desc_size": (sz, []),
+    "mmdx_image_preprocess": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp]),
     "mmdx_plan_run": (i32, [C.POINTER(PlanOp), i32, vp, vp, vp, i32]),
     "mmdx_plan_op_size": (sz, []),
     "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,

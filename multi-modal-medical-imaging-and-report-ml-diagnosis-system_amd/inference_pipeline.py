@@ -17,6 +17,7 @@ import os
 
 import torch
 
+from .preprocess import preprocess_batch
 from .training_pipeline import (DISEASES, FusionTransformerModel, ImageEncoderCNN,
                                 TextEncoderTransformer, image_transfom_into_tensor,
                                 tokenize_patient_details)
@@ -78,7 +79,10 @@ def inference(model_bundle, image_pil, patient_details, device=None, gen_kwargs=
     image_encoder = model_bundle["image_encoder"].to(dev).eval()
     text_encoder = model_bundle["text_encoder"].to(dev).eval()
 
-    x_img = image_transfom_into_tensor(image_pil).unsqueeze(0).to(dev)  # IP:174
+    if dev.type == "cuda":  # IP:174 on the GPU (bit-exact with image_transfom_into_tensor)
+        x_img = preprocess_batch([image_pil], dev)
+    else:
+        x_img = image_transfom_into_tensor(image_pil).unsqueeze(0).to(dev)
     tok = tokenize_patient_details([patient_details], max_len=96)       # IP:175
     tok = {k: v.to(dev) for k, v in tok.items()}
     z_img = image_encoder(x_img)["embeddings"]                          # IP:179
