@@ -95,6 +95,24 @@ int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void
                     const void* dy, float* dw_kcrs, float beta, void* workspace,
                     size_t ws_bytes, void* stream);
 
+/* ResNet stem (backbone.0, TP:183) straight from the NCHW fp32 image batch of
+ * image_transfom_into_tensor (TP:112-119) / mmdx_image_preprocess — no NHWC copy, no
+ * channel padding: desc->C is the image's channel count (3), the GEMM K is C*R*S in the
+ * master weight's own (c, r, s) order, rounded up to mmdx_stem_k8(d) in the packed weight.
+ * bf16 compute; Cout (desc->K) <= 64 and a multiple of 8.
+ *   pack:  w_kcrs fp32 -> w_packed [K][mmdx_stem_k8(d)] bf16 (zero tail)
+ *   fwd:   y [N,P,Q,K] bf16 NHWC, stat_part as mmdx_conv_fwd (128-row blocks)
+ *   wgrad: dw_kcrs (fp32 master layout) = beta*dw_kcrs + grad, from x (NCHW fp32) and dy */
+int mmdx_stem_k8(const mmdx_conv_desc* d);
+int mmdx_stem_pack_weight(const mmdx_conv_desc* d, const float* w_kcrs, void* w_packed,
+                          void* stream);
+int mmdx_stem_fwd(const mmdx_conv_desc* d, const float* x_nchw, const void* w_packed,
+                  void* y, float* stat_part, void* stream);
+size_t mmdx_stem_wgrad_workspace_size(const mmdx_conv_desc* d);
+int mmdx_stem_wgrad(const mmdx_conv_desc* d, const float* x_nchw, const void* dy,
+                    float* dw_kcrs, float beta, void* workspace, size_t ws_bytes,
+                    void* stream);
+
 /* ---------------------------------------------------------------- batch norm (+res)(+ReLU)
  * x, y, residual: [rows, C] (NHWC flattened).  Train mode computes batch statistics
  * (biased var for normalisation, unbiased for running_var, momentum update as
@@ -144,7 +162,8 @@ enum {
   MMDX_OP_EVENT = 1, MMDX_OP_NCHW2NHWC, MMDX_OP_CONV_PACK, MMDX_OP_CONV_FWD, MMDX_OP_BN_FWD,
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
-  MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT
+  MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PACK, MMDX_OP_STEM_FWD,
+  MMDX_OP_STEM_WGRAD
 };
 typedef struct {
   int op, dtype, stream;

@@ -401,3 +401,132 @@ extern "C" int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const 
   BnStat bs{bn_y, gamma, bn_beta, save_mean, save_rstd, (float2*)stat_part, relu, tiles, 0};
   return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, 0.f, (hipStream_t)stream, bs);
 }
+
+// ------------------------------------------------------------------------------ stem
+// conv1 of the trunk (backbone.0, TP:183) straight from the NCHW fp32 image batch that
+// image_transfom_into_tensor / mmdx_image_preprocess produce: no NHWC copy, K = 147 in the
+// weight's own (c, r, s) order (packed once per step to [Cout][K8] bf16, K8 = K rounded up to
+// 8), BN statistics from the epilogue.  bf16 only (the fp32 parity path keeps the generic
+// conv on an NHWC copy).
+namespace mmdx {
+
+static StemSrc stem_src(const mmdx_conv_desc* d, const float* x) {
+  StemSrc g;
+  g.x = x; g.N = d->N; g.C = d->C; g.H = d->H; g.W = d->W; g.R = d->R; g.S = d->S;
+  g.sh = d->stride_h; g.sw = d->stride_w; g.ph = d->pad_h; g.pw = d->pad_w;
+  g.P = d->P; g.Q = d->Q; g.M = d->N * d->P * d->Q; g.K = d->C * d->R * d->S;
+  g.inv_rs = 1.f / (float)(d->R * d->S); g.inv_s = 1.f / (float)d->S;
+  return g;
+}
+
+static int stem_check(const mmdx_conv_desc* d) {
+  MMDX_CHECK_ARG(d && d->N > 0 && d->C > 0 && d->K > 0 && d->K % 8 == 0 &&
+                     d->C * d->R * d->S <= 1024 &&
+                     d->P == (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1 &&
+                     d->Q == (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1,
+                 "stem: bad descriptor");
+  MMDX_CHECK_ARG((long)d->N * d->C * d->H * d->W < (1L << 31) &&
+                     (long)d->N * d->P * d->Q * d->K * 2 < (1L << 31),
+                 "stem: tensors must stay below 2 GiB");
+  return 0;
+}
+
+static int stem_k8(const mmdx_conv_desc* d) { return (d->C * d->R * d->S + 7) / 8 * 8; }
+
+__global__ void stem_pack_kernel(const float* __restrict__ w, int K, int KC, int K8,
+                                 bf16* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= K * K8) return;
+  const int k = i / K8, j = i - k * K8;
+  out[i] = (bf16)(j < KC ? w[(long)k * KC + j] : 0.f);
+}
+
+// stem partial slab [splits][Cout][K8] -> dw[Cout][K] (= KCRS flattening) fp32
+__global__ void stem_wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Kout,
+                                         int K8, int KC, float* __restrict__ dw, float beta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Kout * KC) return;
+  const int k = i / KC, j = i - k * KC;
+  const long slab = (long)Kout * K8;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int z = 0;
+  for (; z + 4 <= splits; z += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += ws[(long)(z + u) * slab + (long)k * K8 + j];
+  for (int u = 0; z < splits; ++z, ++u) a[u] += ws[(long)z * slab + (long)k * K8 + j];
+  const float v = (a[0] + a[1]) + (a[2] + a[3]);
+  dw[i] = beta != 0.f ? beta * dw[i] + v : v;
+}
+
+struct StemWgradPlan { int splits, kper; };
+static StemWgradPlan plan_stem_wgrad(const mmdx_conv_desc* d) {
+  const long K = (long)d->N * d->P * d->Q;
+  const long ktiles = (K + 63) / 64;
+  const int tiles = (d->K + 63) / 64 * ((stem_k8(d) + 127) / 128);
+  long s = std::max(1L, std::min((512L + tiles - 1) / tiles, ktiles / 16));
+  const long kt_per = (ktiles + s - 1) / s;
+  StemWgradPlan p;
+  p.kper = (int)(kt_per * 64);
+  p.splits = (int)((K + p.kper - 1) / p.kper);
+  return p;
+}
+
+}  // namespace mmdx
+
+extern "C" int mmdx_stem_k8(const mmdx_conv_desc* d) { return d ? stem_k8(d) : 0; }
+
+extern "C" int mmdx_stem_pack_weight(const mmdx_conv_desc* d, const float* w, void* w_packed,
+                                     void* stream) {
+  int rc = stem_check(d);
+  if (rc) return rc;
+  const int K8 = stem_k8(d), KC = d->C * d->R * d->S;
+  const int total = d->K * K8;
+  hipLaunchKernelGGL(stem_pack_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, w, d->K, KC, K8, (bf16*)w_packed);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_stem_fwd(const mmdx_conv_desc* d, const float* x_nchw, const void* w_packed,
+                             void* y, float* stat_part, void* stream) {
+  int rc = stem_check(d);
+  if (rc) return rc;
+  MMDX_CHECK_ARG(d->K <= 64, "stem fwd: Cout %d > 64", d->K);
+  const StemSrc g = stem_src(d, x_nchw);
+  const int K8 = stem_k8(d);
+  DenseK<bf16> sb{(const bf16*)w_packed, K8, d->K, true};
+  EpiStore<bf16> epi{(bf16*)y, d->K, g.M, d->K, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr,
+                     (float2*)stat_part};
+  return launch_dma_ops<128, 64, StemA<128>, DmaK<64, DenseK<bf16>>>(g, sb, epi, g.M, d->K,
+                                                                      g.K, 1, g.K,
+                                                                      (hipStream_t)stream);
+}
+
+extern "C" size_t mmdx_stem_wgrad_workspace_size(const mmdx_conv_desc* d) {
+  const StemWgradPlan p = plan_stem_wgrad(d);
+  return (size_t)p.splits * d->K * stem_k8(d) * sizeof(float);
+}
+
+extern "C" int mmdx_stem_wgrad(const mmdx_conv_desc* d, const float* x_nchw, const void* dy,
+                               float* dw, float beta, void* ws, size_t ws_bytes, void* stream) {
+  int rc = stem_check(d);
+  if (rc) return rc;
+  MMDX_CHECK_ARG(d->K <= 64, "stem wgrad: Cout %d > 64", d->K);
+  const StemWgradPlan p = plan_stem_wgrad(d);
+  const int K8 = stem_k8(d), KC = d->C * d->R * d->S;
+  const size_t need = mmdx_stem_wgrad_workspace_size(d);
+  MMDX_CHECK_ARG(ws && ws_bytes >= need, "stem wgrad: workspace %zu < %zu", ws_bytes, need);
+  const StemSrc g = stem_src(d, x_nchw);
+  const int M = d->K, Kpix = g.M;
+  DenseR<bf16> sa{(const bf16*)dy, d->K, M, true, Kpix};
+  EpiPartial epi{(float*)ws, M, K8};
+  hipStream_t st = (hipStream_t)stream;
+  rc = launch_dma_ops<64, 128, DmaR<64, DenseR<bf16>>, StemR<128>>(sa, g, epi, M, K8, Kpix,
+                                                                    p.splits, p.kper, st);
+  if (rc) return rc;
+  const int total = M * KC;
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st,
+                     (const float*)ws, p.splits, M, K8, KC, dw, beta);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}

@@ -90,6 +90,16 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_CONV_DGRAD:
       return mmdx_conv_dgrad(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext), o.f[0],
                              s);
+    case MMDX_OP_STEM_PACK:
+      return mmdx_stem_pack_weight(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext), s);
+    case MMDX_OP_STEM_FWD:
+      // p: x_nchw, w_packed, y, stat_part
+      return mmdx_stem_fwd(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
+                           (float*)P(o, 3, ext), s);
+    case MMDX_OP_STEM_WGRAD:
+      // l: ws_bytes; f: beta; p: x_nchw, dy, dw, ws
+      return mmdx_stem_wgrad(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext),
+                             (float*)P(o, 2, ext), o.f[0], P(o, 3, ext), (size_t)o.l[0], s);
     default:
       mmdx_set_error("plan: unknown op code %d", o.op);
       return -22;

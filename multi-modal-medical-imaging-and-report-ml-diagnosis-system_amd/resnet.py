@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import weakref
 
 import torch
@@ -22,6 +23,7 @@ from . import _lib as L
 from ._lib import call, ptr, stream
 
 _VEC = {torch.float32: 4, torch.bfloat16: 8}
+_STEM_DIRECT = os.environ.get("MMDX_STEM", "") == "direct"
 
 
 class _NoTimer:
@@ -295,7 +297,18 @@ class _Plan:
             ws_need[st] = max(ws_need[st], int(n))
 
         # ---- forward
-        if in_nchw:
+        stem_conv = trunk[0]
+        # MMDX_STEM=direct: the bf16 stem reads the NCHW fp32 batch itself (no NHWC copy,
+        # K = 147 unpadded).  Opt-in: its per-lane gather is latency-bound (fwd 539 us, wgrad
+        # 954 us at C4 vs 228 + 254 us for the NHWC copy + padded-C DMA path).
+        stem_direct = (_STEM_DIRECT and in_nchw and T == torch.bfloat16
+                       and stem_conv.out_channels <= 64
+                       and stem_conv.out_channels % 8 == 0 and stem_conv.in_channels == cin)
+        self.stem_direct = stem_direct
+        if stem_direct:
+            cp = cin
+            x0 = _Ext(0)
+        elif in_nchw:
             cp = vec
             x0 = A.new((N, H, W, cp), T, dev)
             fw.add(L.OP_NCHW2NHWC, dt, i=(N, cin, H, W, cp), p=(_Ext(0), x0))
@@ -305,16 +318,22 @@ class _Plan:
         self.x0 = x0
         units = []
 
-        def unit(conv, bn, relu, x, N, H, W, C, cm, res):
+        def unit(conv, bn, relu, x, N, H, W, C, cm, res, direct=False):
             d = _desc(N, H, W, C, conv)
             K, k = conv.out_channels, conv.kernel_size
-            wk = A.new((K, k, k, C), T, dev)
-            wc = A.new((C, k, k, K), T, dev) if keep else None
-            fw.add(L.OP_CONV_PACK, dt, i=(cm,), p=(conv.weight, wk, wc), d=d)
             y = A.new((N, d.P, d.Q, K), T, dev)
             nstat = L.lib().mmdx_conv_fwd_stat_blocks(d) if train else 0
             part = A.new((K, nstat, 2), torch.float32, dev) if train else None
-            fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
+            if direct:  # stem on the NCHW fp32 batch: weight packed [K][K8], no dgrad copy
+                wk = A.new((K, L.lib().mmdx_stem_k8(d)), T, dev)
+                wc = None
+                fw.add(L.OP_STEM_PACK, p=(conv.weight, wk), d=d)
+                fw.timed("fwd", L.OP_STEM_FWD, p=(x, wk, y, part), d=d)
+            else:
+                wk = A.new((K, k, k, C), T, dev)
+                wc = A.new((C, k, k, K), T, dev) if keep else None
+                fw.add(L.OP_CONV_PACK, dt, i=(cm,), p=(conv.weight, wk, wc), d=d)
+                fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
             out = A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
             mean = A.new((K,), torch.float32, dev)
@@ -326,12 +345,12 @@ class _Plan:
                    p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
                       res, out, _WS))
             u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
-                     rstd=rstd, wc=wc)
+                     rstd=rstd, wc=wc, direct=direct)
             units.append(u)
             return out, d, u
 
-        stem = trunk[0]
-        a, d, stem_u = unit(stem, trunk[1], True, x0, N, H, W, cp, 3, None)
+        a, d, stem_u = unit(stem_conv, trunk[1], True, x0, N, H, W, cp, 3, None,
+                            direct=stem_direct)
         H, W, C = d.P, d.Q, d.K
         mp = trunk[3]
         P = (H + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
@@ -408,13 +427,21 @@ class _Plan:
                        l=(rows, wsn, sp.data_ptr() if sp is not None else 0), f=(0.0,),
                        p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"], u["rstd"],
                           dconv, dres, g(u["bn"].weight), g(u["bn"].bias), _WS))
-                wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
+                if u["direct"]:
+                    wsn = L.lib().mmdx_stem_wgrad_workspace_size(d)
+                else:
+                    wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
                 ws_for(wsn, 1)
                 ev = A.event()
                 bw.add(L.OP_SIGNAL, p=(ev,), stream=0)
                 bw.add(L.OP_WAIT, p=(ev,), stream=1)
-                bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(u["cm"],), l=(wsn,),
-                         f=(0.0,), p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
+                if u["direct"]:
+                    bw.timed("wgrad", L.OP_STEM_WGRAD, stream=1, l=(wsn,), f=(0.0,),
+                             p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
+                else:
+                    bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(u["cm"],),
+                             l=(wsn,), f=(0.0,),
+                             p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
                 dx, fed = None, None
                 if want_dx:
                     if dx_acc is not None:
@@ -536,7 +563,8 @@ class _TrunkFn(torch.autograd.Function):
             ctx.tok = tok
             ctx.plan = plan
             ctx.trunk_ref = trunk
-            ctx.x = None if in_nchw else x  # the stem's wgrad reads an NHWC input directly
+            # the stem's wgrad reads the trunk input itself unless the plan converted it
+            ctx.x = x if isinstance(plan.x0, _Ext) else None
         return plan.feats.clone()
 
     @staticmethod

@@ -387,3 +387,59 @@ def test_dgrad_fused_bn_stats(dev, cfg):
     assert (ga - gb).abs().max().item() <= 1e-4 * max(1.0, gb.abs().max().item())
     assert (ba - bb).abs().max().item() <= 1e-4 * max(1.0, bb.abs().max().item())
     assert (ca - cb).abs().max().item() <= 2e-2 * max(1.0, cb.abs().max().item())
+
+
+STEMS = [  # N, C, H, W, K, k, s, p  (C = image channels: read from NCHW fp32 directly)
+    (2, 3, 32, 32, 64, 7, 2, 3),
+    (3, 3, 37, 29, 64, 7, 2, 3),   # ragged: M not a multiple of 128, odd P/Q
+    (1, 1, 20, 20, 32, 7, 2, 3),   # grayscale, K = 49
+    (2, 3, 64, 64, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", STEMS)
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_stem_direct_nchw(dev, cfg, beta):
+    """mmdx_stem_{pack_weight,fwd,wgrad} (backbone.0 on the NCHW fp32 batch, TP:183) vs
+    torch conv2d fp32 on the bf16-rounded operands; BN epilogue stats as mmdx_conv_fwd's."""
+    dt = torch.bfloat16
+    N, C, H, W, K, k, s, p = cfg
+    g = torch.Generator().manual_seed(7 + sum(cfg))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, k, k, generator=g) * 0.1
+    xb, wb = x.bfloat16().float(), w.bfloat16().float()
+    wr = wb.clone().requires_grad_(True)
+    yr = tF.conv2d(xb, wr, stride=s, padding=p)
+    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    yr.backward(dy)
+    P, Q = yr.shape[2], yr.shape[3]
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q)
+    k8 = L.lib().mmdx_stem_k8(d)
+    assert k8 == (C * k * k + 7) // 8 * 8
+    wp = torch.empty(K, k8, dtype=dt, device=dev)
+    L.call("mmdx_stem_pack_weight", d, w.to(dev).data_ptr(), wp.data_ptr(), L.stream())
+    assert torch.equal(wp[:, :C * k * k].cpu(), w.reshape(K, -1).bfloat16())
+    assert not wp[:, C * k * k:].cpu().any()
+    xd = x.to(dev).contiguous()  # fp32 NCHW; the kernel rounds to bf16 on load
+    y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
+    part = torch.empty(K, nst, 2, device=dev)
+    L.call("mmdx_stem_fwd", d, xd.data_ptr(), wp.data_ptr(), y.data_ptr(), part.data_ptr(),
+           L.stream())
+    _close(y.permute(0, 3, 1, 2), yr.detach(), dt, f"stem fwd {cfg}")
+    M = N * P * Q
+    cnt = torch.tensor([min(128, M - 128 * b) for b in range(nst)], dtype=torch.float64)
+    pm, p2 = part[..., 0].t().double().cpu(), part[..., 1].t().double().cpu()
+    mean = (pm * cnt[:, None]).sum(0) / M
+    m2 = (p2 + cnt[:, None] * (pm - mean) ** 2).sum(0)
+    yref = yr.detach().double()
+    _close(mean, yref.mean((0, 2, 3)), dt, "stem stat mean")
+    _close(m2 / M, yref.var((0, 2, 3), unbiased=False), dt, "stem stat var")
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    dw0 = torch.randn(K, C, k, k, generator=g)
+    dw = dw0.to(dev)
+    ws_n = L.lib().mmdx_stem_wgrad_workspace_size(d)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    L.call("mmdx_stem_wgrad", d, xd.data_ptr(), dyd.data_ptr(), dw.data_ptr(), beta,
+           ws.data_ptr(), ws_n, L.stream())
+    _close(dw, wr.grad + beta * dw0, dt, f"stem wgrad {cfg}")
