@@ -71,6 +71,20 @@ typedef struct {
  * Channel padding: desc->C may exceed the master's Cin (c_master); pad lanes are 0. */
 int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
                           const float* w_kcrs, void* w_krsc, void* w_crsk, void* stream);
+/* Every conv weight of a network in one launch.  items: DEVICE array of n_items, sorted by
+ * first_block; item i owns blocks [first_block_i, first_block_{i+1}) (the last runs to
+ * total_blocks), mmdx_conv_pack_blocks(K, C, R*S) of them.  Same packing as
+ * mmdx_conv_pack_weight (C = padded channels, c_master = the master's Cin). */
+typedef struct {
+  const float* w;      /* fp32 KCRS master */
+  void* krsc;          /* packed [K][R][S][C] or NULL */
+  void* crsk;          /* packed [C][R][S][K] or NULL */
+  int K, C, c_master, RS;
+  long first_block;
+} mmdx_pack_item;
+long mmdx_conv_pack_blocks(int K, int C, int RS);
+int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items, long total_blocks,
+                         void* stream);
 /* stat_part (optional, fp32 pairs [K][mmdx_conv_fwd_stat_blocks(d)], channel-major): per-channel
  * (mean, M2) of each 128-row block of the output, computed from the fp32 accumulators in
  * the GEMM epilogue — the BatchNorm batch statistics without a separate pass over y. */
@@ -163,7 +177,7 @@ enum {
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
   MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PACK, MMDX_OP_STEM_FWD,
-  MMDX_OP_STEM_WGRAD
+  MMDX_OP_STEM_WGRAD, MMDX_OP_CONV_PACK_MULTI
 };
 typedef struct {
   int op, dtype, stream;

@@ -34,6 +34,12 @@ class AdamWTensor(C.Structure):
 CD = C.POINTER(ConvDesc)
 
 
+class PackItem(C.Structure):
+    """mmdx_pack_item (include/mmdx.h): one weight of a multi-tensor pack launch."""
+    _fields_ = [("w", vp), ("krsc", vp), ("crsk", vp), ("K", C.c_int), ("C", C.c_int),
+                ("c_master", C.c_int), ("RS", C.c_int), ("first_block", C.c_long)]
+
+
 class PlanOp(C.Structure):
     """mmdx_plan_op (include/mmdx.h): one recorded operation of a launch plan."""
     _fields_ = [("op", C.c_int), ("dtype", C.c_int), ("stream", C.c_int), ("i", C.c_int * 8),
@@ -45,7 +51,7 @@ class PlanOp(C.Structure):
 (OP_EVENT, OP_NCHW2NHWC, OP_CONV_PACK, OP_CONV_FWD, OP_BN_FWD, OP_MAXPOOL_FWD,
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
  OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PACK, OP_STEM_FWD,
- OP_STEM_WGRAD) = range(1, 20)
+ OP_STEM_WGRAD, OP_CONV_PACK_MULTI) = range(1, 21)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -56,6 +62,8 @@ SIGNATURES = {
     "mmdx_gemm": (i32, [i32, i32, i32, i32, vp, i64, i32, vp, i64, i32, vp, i64, i32, vp, vp,
                         i32, f32, f32, vp, vp, sz, vp]),
     "mmdx_conv_pack_weight": (i32, [i32, CD, i32, vp, vp, vp, vp]),
+    "mmdx_conv_pack_blocks": (i64, [i32, i32, i32]),
+    "mmdx_conv_pack_multi": (i32, [i32, vp, i32, i64, vp]),
     "mmdx_conv_fwd_stat_blocks": (i32, [CD]),
     "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),

@@ -45,6 +45,39 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Cm, i
   }
 }
 
+// All conv weights of a trunk in ONE launch (mmdx_conv_pack_multi): block b packs the item
+// whose [first_block, next first_block) range holds b; PACK_PER_BLOCK elements per block in
+// KRSC order (coalesced KRSC writes).  Replaces one pack launch per conv on the critical stream.
+constexpr int PACK_PER_BLOCK = 2048;
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_multi_kernel(const mmdx_pack_item* __restrict__ it,
+                                                         int n) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = n - 1;  // last item with first_block <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (it[mid].first_block <= b) lo = mid; else hi = mid - 1;
+  }
+  const mmdx_pack_item t = it[lo];
+  const int K = t.K, C = t.C, Cm = t.c_master, RS = t.RS;
+  const long total = (long)K * RS * C;
+  const long base = (b - t.first_block) * PACK_PER_BLOCK;
+  T* krsc = (T*)t.krsc;
+  T* crsk = (T*)t.crsk;
+  for (int e = threadIdx.x; e < PACK_PER_BLOCK; e += 256) {
+    const long i = base + e;
+    if (i >= total) break;
+    const int c = (int)(i % C);
+    const long q = i / C;
+    const int rs = (int)(q % RS);
+    const int k = (int)(q / RS);
+    const float v = c < Cm ? t.w[((long)k * Cm + c) * RS + rs] : 0.f;
+    if (krsc) krsc[i] = from_f<T>(v);
+    if (crsk) crsk[((long)c * RS + rs) * K + k] = from_f<T>(v);
+  }
+}
+
 // partial[z][k][(r*S+s)*C + c] summed over z -> dw[k][c][r][s] (c < Cm), dw = beta*dw + sum
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int K, int C,
                                     int Cm, int RS, float* __restrict__ dw, float beta) {
@@ -321,6 +354,25 @@ extern "C" int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_m
   else
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, st, w, d->K,
                        c_master, d->C, d->R * d->S, (float*)krsc, (float*)crsk);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" long mmdx_conv_pack_blocks(int K, int C, int RS) {
+  return ((long)K * C * RS + PACK_PER_BLOCK - 1) / PACK_PER_BLOCK;
+}
+
+extern "C" int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items,
+                                    long total_blocks, void* stream) {
+  MMDX_CHECK_ARG(items && n_items > 0 && total_blocks > 0 && total_blocks < (1L << 31),
+                 "conv pack multi: bad item table");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    hipLaunchKernelGGL(pack_multi_kernel<bf16>, dim3((unsigned)total_blocks), dim3(256), 0, st,
+                       items, n_items);
+  else
+    hipLaunchKernelGGL(pack_multi_kernel<float>, dim3((unsigned)total_blocks), dim3(256), 0, st,
+                       items, n_items);
   MMDX_LAUNCH_CHECK();
   return 0;
 }

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
   constexpr int CPT = LSTM_RB * H / (LSTM_NW * 64);
   __shared__ __attribute__((aligned(16))) T sdg[LSTM_RB * LDG];
   __shared__ float sdh[LSTM_RB * H];
+  __builtin_amdgcn_s_setprio(3);  // latency-critical chain beside conv blocks (see coop fwd)
   const int dir = blockIdx.y;
   const int b0 = blockIdx.x * LSTM_RB;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -210,35 +211,23 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
 // REGISTERS for all L steps) and every batch row.  Per step a workgroup loads h_{t-1}
 // (B x 256) into LDS, computes its 128 gate columns with MFMA, does the cell update in
 // registers (each lane holds i, f, g, o of the same (row, unit) in the same accumulator
-// slot), publishes its h_t slice to a double-buffered exchange array, and meets the other
-// workgroups of its direction at a counter barrier (agent-scope release / acquire).
-// W_hh is read once instead of once per step per workgroup, and no gate tile goes
-// through LDS.  Outputs use the batch-partitioned kernel's layouts (same backward).
+// slot) and publishes its h_t slice for the other workgroups of its direction.
+// The h exchange is a write-through hand-off (cdna_hip_programming.md §6 Guideline 16, R1):
+// the slice goes out as 16-B `sc1` stores, every wave drains them, then ONE agent atomic add
+// signals; a consumer polls that counter and reads h with `sc1` loads (L1 bypassed), so no
+// L2 writeback / L1 invalidate fence sits on the recurrence's critical path — the release
+// fence alone cost 1.7-6.5 us per step with the image tower's dirty lines in the same L2.
+// The step's xg operands are loaded before the wait, the c / gate / h saves for the
+// backward are issued after the signal.  Outputs use the batch-partitioned kernel's layouts.
 // ---------------------------------------------------------------------------------------
 constexpr int COOP_NB = 8;                 // workgroups per direction
 constexpr int COOP_H = 256;
 constexpr int COOP_UB = COOP_H / COOP_NB;  // 32 units per workgroup
 constexpr int COOP_LDH = COOP_H + 8;       // padded h row (bf16): conflict-free b128 reads
+constexpr int COOP_SC1 = 16;               // buffer instruction aux: sc1 (write-through / L1 bypass)
 constexpr long COOP_SPIN_MAX = 1L << 26;   // bounded wait: a lost peer ends the kernel
 
-__device__ __forceinline__ void coop_barrier(unsigned* ctr, unsigned target, int* err) {
-  // every wave's stores are issued; make them visible at agent scope, then arrive
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    long spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > COOP_SPIN_MAX) { *err = 1; break; }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
+typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
 
 // RT = 16-row tiles per wave (B <= 64 * RT): 8 waves = 2 unit groups x 4 row groups.
 template <int RT>
@@ -247,7 +236,13 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     bf16* __restrict__ hout, float* __restrict__ csave, float* __restrict__ gsave,
     bf16* __restrict__ hx, unsigned* __restrict__ ctr, int* __restrict__ err) {
   constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
-  __shared__ __attribute__((aligned(16))) bf16 sh[64 * RT * COOP_LDH];
+  constexpr int NROWS = 64 * RT;
+  // [0, NROWS*COOP_LDH): h_{t-1} (MFMA A operand); then this workgroup's h_t slice [NROWS][32]
+  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * COOP_LDH + NROWS * COOP_UB];
+  bf16* sout = sh + NROWS * COOP_LDH;
+  // the recurrence is the text tower's latency-critical chain and shares its CUs with the
+  // image tower's conv blocks: its waves take issue priority over them
+  __builtin_amdgcn_s_setprio(3);
   const int dir = blockIdx.y, blk = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int ug = wid & 1, rg = wid >> 1;
@@ -268,18 +263,47 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     for (int r = 0; r < 4; ++r) creg[i][r] = 0.f;
   unsigned* myctr = ctr + dir;
   bf16* hxd = hx + (long)dir * 2 * B * H;
-  const int nrows = 64 * RT;
+  const __amdgpu_buffer_rsrc_t hrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)hxd, (short)0, 2 * B * H * 2, 0x00020000);
   for (int s = 0; s < L; ++s) {
     const int t = dir == 0 ? s : L - 1 - s;
-    // h_{t-1} -> LDS (zeros at the first step)
-    const bf16* hsrc = hxd + (long)((s + 1) & 1) * B * H;
-    for (int e = threadIdx.x; e < nrows * (H / 8); e += 512) {
+    // this step's input-projection operands: independent of h, in flight during the wait
+    float xv[RT][4][4];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
+        const float* xp = xg + (((long)min(b, B - 1) * L + t) * 2 + dir) * G4 + ucol;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xv[i][r][g] = xp[g * H];
+      }
+    // wait until every workgroup of this direction has published h_{t-1}
+    if (s > 0) {
+      if (threadIdx.x == 0) {
+        const unsigned target = (unsigned)(COOP_NB * s);
+        long spins = 0;
+        while (__hip_atomic_load(myctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > COOP_SPIN_MAX) { *err = 1; break; }
+        }
+      }
+      __syncthreads();
+      if (*(volatile int*)err) return;  // a peer never arrived: give up (results invalid)
+    }
+    // h_{t-1} -> LDS (zeros at the first step); sc1 loads: the producers' sc1 stores are
+    // visible to them without an L1 invalidate
+    const int par_in = ((s + 1) & 1) * B * H * 2;  // byte offset of the h_{t-1} buffer
+    for (int e = threadIdx.x; e < NROWS * (H / 8); e += 512) {
       const int row = e / (H / 8), c8 = e - row * (H / 8);
-      bf16x8 v{};
-      if (s > 0 && row < B) v = *(const bf16x8*)(hsrc + (long)row * H + c8 * 8);
-      *(bf16x8*)(sh + row * COOP_LDH + c8 * 8) = v;
+      coop_v4u v = {0u, 0u, 0u, 0u};
+      if (s > 0 && row < B)
+        v = __builtin_amdgcn_raw_buffer_load_b128(hrs, par_in + (row * H + c8 * 8) * 2, 0,
+                                                  COOP_SC1);
+      *(coop_v4u*)(sh + row * COOP_LDH + c8 * 8) = v;
     }
     __syncthreads();
+    float hv[RT][4], cv[RT][4], gv[RT][4][4];
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
       const int rt16 = (rg + 4 * i) * 16;  // this row tile's first row
@@ -296,29 +320,49 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = rt16 + (lane >> 4) * 4 + r;
-        if (b >= B) continue;
-        const float* xp = xg + (((long)b * L + t) * 2 + dir) * G4;
-        const float gi = sigm(acc[0][r] + xp[ucol]);
-        const float gf = sigm(acc[1][r] + xp[H + ucol]);
-        const float gg = tanhf(acc[2][r] + xp[2 * H + ucol]);
-        const float go = sigm(acc[3][r] + xp[3 * H + ucol]);
+        const float gi = sigm(acc[0][r] + xv[i][r][0]);
+        const float gf = sigm(acc[1][r] + xv[i][r][1]);
+        const float gg = tanhf(acc[2][r] + xv[i][r][2]);
+        const float go = sigm(acc[3][r] + xv[i][r][3]);
         const float c = gf * creg[i][r] + gi * gg;
         creg[i][r] = c;
         const bf16 h = from_f<bf16>(go * tanhf(c));
-        hxd[(long)(s & 1) * B * H + (long)b * H + ucol] = h;
-        hout[((long)b * L + t) * 2 * H + dir * H + ucol] = h;
-        const long sidx = ((long)dir * L + t) * B + b;
-        csave[sidx * H + ucol] = c;
-        float* gp = gsave + sidx * G4;
-        gp[ucol] = gi;
-        gp[H + ucol] = gf;
-        gp[2 * H + ucol] = gg;
-        gp[3 * H + ucol] = go;
+        hv[i][r] = (float)h;
+        cv[i][r] = c;
+        gv[i][r][0] = gi; gv[i][r][1] = gf; gv[i][r][2] = gg; gv[i][r][3] = go;
+        const int row = rt16 + (lane >> 4) * 4 + r;
+        sout[row * COOP_UB + ug * 16 + (lane & 15)] = h;
       }
     }
-    if (s + 1 < L) coop_barrier(myctr, (unsigned)(COOP_NB * (s + 1)), err);
-    if (*(volatile int*)err) return;  // a peer never arrived: give up (results invalid)
+    __syncthreads();
+    // publish h_t: 16-B sc1 stores of the [B][32] slice, drain, one agent atomic add
+    if (s + 1 < L) {
+      const int par_out = (s & 1) * B * H * 2;
+      for (int e = threadIdx.x; e < B * (COOP_UB / 8); e += 512) {
+        const int row = e / (COOP_UB / 8), c8 = e - row * (COOP_UB / 8);
+        const coop_v4u v = *(const coop_v4u*)(sout + row * COOP_UB + c8 * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, hrs, par_out + (row * H + blk * COOP_UB + c8 * 8) * 2, 0, COOP_SC1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(myctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // saves for the backward (overlap the next step's wait)
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
+        if (b >= B) continue;
+        hout[((long)b * L + t) * 2 * H + dir * H + ucol] = from_f<bf16>(hv[i][r]);
+        const long sidx = ((long)dir * L + t) * B + b;
+        csave[sidx * H + ucol] = cv[i][r];
+        float* gp = gsave + sidx * G4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) gp[g * H + ucol] = gv[i][r][g];
+      }
   }
 }
 

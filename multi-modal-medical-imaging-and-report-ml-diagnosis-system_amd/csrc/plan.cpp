@@ -100,6 +100,10 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
       // l: ws_bytes; f: beta; p: x_nchw, dy, dw, ws
       return mmdx_stem_wgrad(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext),
                              (float*)P(o, 2, ext), o.f[0], P(o, 3, ext), (size_t)o.l[0], s);
+    case MMDX_OP_CONV_PACK_MULTI:
+      // i: n_items; l: total_blocks; p: item table (device)
+      return mmdx_conv_pack_multi(o.dtype, (const mmdx_pack_item*)P(o, 0, ext), o.i[0], o.l[0],
+                                  s);
     default:
       mmdx_set_error("plan: unknown op code %d", o.op);
       return -22;

@@ -317,6 +317,7 @@ class _Plan:
             x0 = _Ext(0)
         self.x0 = x0
         units = []
+        packs = []
 
         def unit(conv, bn, relu, x, N, H, W, C, cm, res, direct=False):
             d = _desc(N, H, W, C, conv)
@@ -329,10 +330,10 @@ class _Plan:
                 wc = None
                 fw.add(L.OP_STEM_PACK, p=(conv.weight, wk), d=d)
                 fw.timed("fwd", L.OP_STEM_FWD, p=(x, wk, y, part), d=d)
-            else:
+            else:  # packed by the plan's single multi-tensor pack launch (below)
                 wk = A.new((K, k, k, C), T, dev)
                 wc = A.new((C, k, k, K), T, dev) if keep else None
-                fw.add(L.OP_CONV_PACK, dt, i=(cm,), p=(conv.weight, wk, wc), d=d)
+                packs.append((conv.weight, wk, wc, K, C, cm, k * k))
                 fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
             out = A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
@@ -381,6 +382,20 @@ class _Plan:
                     bu.append(uu)
                 blocks.append((bu, ds_u, (H, W, C)))
                 x_cur, H, W, C = h, hH, hW, hC
+        # every conv weight packed (KRSC fwd + CRSK dgrad copies) in ONE launch, first op
+        if packs:
+            items = (L.PackItem * len(packs))()
+            nb = 0
+            for j, (wm, wk, wc, K_, C_, cm_, rs) in enumerate(packs):
+                items[j] = L.PackItem(wm.data_ptr(), wk.data_ptr(),
+                                      wc.data_ptr() if wc is not None else None, K_, C_, cm_,
+                                      rs, nb)
+                nb += L.lib().mmdx_conv_pack_blocks(K_, C_, rs)
+            raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
+            tbl = A.new((raw.numel(),), torch.uint8, dev)
+            tbl.copy_(raw)
+            fw.add(L.OP_CONV_PACK_MULTI, dt, i=(len(packs),), l=(nb,), p=(tbl,))
+            fw.ops.insert(0, fw.ops.pop())
         self.feats = A.new((N, C), T, dev)
         fw.add(L.OP_AVGPOOL_FWD, dt, i=(N, H * W, C), p=(x_cur, self.feats))
         self.out_geom = (N, H, W, C)

@@ -443,3 +443,33 @@ def test_stem_direct_nchw(dev, cfg, beta):
     L.call("mmdx_stem_wgrad", d, xd.data_ptr(), dyd.data_ptr(), dw.data_ptr(), beta,
            ws.data_ptr(), ws_n, L.stream())
     _close(dw, wr.grad + beta * dw0, dt, f"stem wgrad {cfg}")
+
+
+def test_conv_pack_multi_matches_single(dev):
+    """mmdx_conv_pack_multi (all trunk weights in one launch) == one mmdx_conv_pack_weight per
+    weight, bit for bit, including channel padding (c_master < C) and a NULL CRSK output."""
+    shapes = [(64, 3, 8, 7), (256, 64, 64, 1), (128, 128, 128, 3), (24, 40, 40, 3)]
+    g = torch.Generator().manual_seed(3)
+    items = (L.PackItem * len(shapes))()
+    outs, refs, nb = [], [], 0
+    for j, (K, cm, C, k) in enumerate(shapes):
+        w = (torch.randn(K, cm, k, k, generator=g)).to(dev)
+        wk = torch.empty(K, k, k, C, dtype=torch.bfloat16, device=dev)
+        wc = torch.empty(C, k, k, K, dtype=torch.bfloat16, device=dev) if j != 1 else None
+        items[j] = L.PackItem(w.data_ptr(), wk.data_ptr(),
+                              wc.data_ptr() if wc is not None else None, K, C, cm, k * k, nb)
+        nb += L.lib().mmdx_conv_pack_blocks(K, C, k * k)
+        d = L.ConvDesc(1, 8, 8, C, K, k, k, 1, 1, k // 2, k // 2, 8, 8)
+        rk = torch.empty_like(wk)
+        rc = torch.empty_like(wc) if wc is not None else None
+        L.call("mmdx_conv_pack_weight", 1, d, cm, w.data_ptr(), rk.data_ptr(),
+               rc.data_ptr() if rc is not None else None, L.stream())
+        outs.append((w, wk, wc))
+        refs.append((rk, rc))
+    raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8).to(dev)
+    L.call("mmdx_conv_pack_multi", 1, raw.data_ptr(), len(shapes), nb, L.stream())
+    torch.cuda.synchronize()
+    for (w, wk, wc), (rk, rc) in zip(outs, refs):
+        assert torch.equal(wk, rk)
+        if wc is not None:
+            assert torch.equal(wc, rc)

@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c4")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--text-first", action="store_true")
+    ap.add_argument("--text-only", action="store_true")
     args = ap.parse_args()
     cfg = dict(bench.CONFIGS[args.config])
     dev = torch.device("cuda", 0)
@@ -44,11 +46,16 @@ def main():
         main = torch.cuda.current_stream()
         mark("start", main)
         side.wait_stream(main)
+        if args.text_first:
+            with torch.cuda.stream(side):
+                z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+                mark("txt_fwd_done", side)
         z_img = img(x)["embeddings"]
         mark("img_fwd_issued", main)
-        with torch.cuda.stream(side):
-            z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
-            mark("txt_fwd_done", side)
+        if not args.text_first:
+            with torch.cuda.stream(side):
+                z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+                mark("txt_fwd_done", side)
         main.wait_stream(side)
         logits = fus(z_img, z_txt)["disease_logits"]
         loss = mmdx.BCEWithLogitsLoss()(logits, y)
@@ -73,6 +80,19 @@ def main():
         mark("end", main)
         return loss
 
+    if args.text_only:  # the text tower alone: its uncontended forward / backward time
+        for it in range(4):
+            torch.cuda.synchronize()
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            z = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+            e[1].record()
+            z.float().sum().backward()
+            e[2].record()
+            torch.cuda.synchronize()
+            print(f"text only: fwd {e[0].elapsed_time(e[1]):.3f} ms  bwd "
+                  f"{e[1].elapsed_time(e[2]):.3f} ms")
+        return
     for _ in range(5):
         step()
     torch.cuda.synchronize()
