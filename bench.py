@@ -255,17 +255,18 @@ class StepTimer:
 def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
     import mmdx
     from mmdx import optim as MO
-    from mmdx.schedule import two_tower_backward
+    from mmdx.schedule import TwoTowerForward, two_tower_backward
+    towers = TwoTowerForward(text_stream=side)
 
     def step():
         opt.zero_grad(set_to_none=True)
         main = torch.cuda.current_stream()
         side.wait_stream(main)
-        # image tower first: its trunk is one native plan call, so the main stream starts at
-        # once; the text tower (Python-issued) then runs concurrently on the side stream
-        z_img = img(x)["embeddings"]
-        with torch.cuda.stream(side):
-            z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+        # both towers issued at once: the image trunk (one native plan call) from this
+        # thread onto the main stream, the text tower (Python-issued) from a worker thread
+        # onto the side stream
+        z_img, z_txt = towers(lambda: img(x)["embeddings"],
+                              lambda: txt(input_ids=ids, attention_mask=mask)["embeddings"])
         main.wait_stream(side)
         logits = fus(z_img, z_txt)["disease_logits"]
         loss = mmdx.BCEWithLogitsLoss()(logits, y)
@@ -392,11 +393,18 @@ def main():
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.enabled = not use_graph and os.environ.get("MMDX_BENCH_EVENTS", "1") != "0"
-    timer.reserve(400 * args.steps)
+    # Conv (dominant-family) launch durations: HIP events around every conv launch of the
+    # LAST `ev_steps` timed steps (default K/10).  Bracketing every step costs ~0.75 ms/step
+    # of event markers at C4 (316 records), which would bias `value`; the sampled steps are
+    # ordinary steps of the timed loop, so the per-launch average is the timed region's.
+    timing = not use_graph and os.environ.get("MMDX_BENCH_EVENTS", "1") != "0"
+    ev_steps = min(args.steps, max(1, int(os.environ.get("MMDX_BENCH_EVENT_STEPS",
+                                                         max(1, args.steps // 10)))))
+    timer.reserve(400 * ev_steps)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        timer.enabled = timing and i >= args.steps - ev_steps
         loss = run()
     t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (no device sync)
     torch.cuda.synchronize()
@@ -420,7 +428,7 @@ def main():
         for _ in range(3):
             eager_step()
         torch.cuda.synchronize()
-    conv_steps = 3 if use_graph else args.steps
+    conv_steps = 3 if use_graph else ev_steps
     timer.enabled = False
     if world > 1:
         t = torch.tensor([el], device=dev)
@@ -484,6 +492,7 @@ def main():
             "family_ms_per_step": round(conv_ms / conv_steps, 3),
             "family_launches_per_step": n_conv // max(1, conv_steps),
             "family_gflop_per_sample": round(conv_flops / 1e9, 3),
+            "timed_steps_with_events": conv_steps,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

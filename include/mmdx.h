@@ -74,7 +74,8 @@ int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
 /* Every conv weight of a network in one launch.  items: DEVICE array of n_items, sorted by
  * first_block; item i owns blocks [first_block_i, first_block_{i+1}) (the last runs to
  * total_blocks), mmdx_conv_pack_blocks(K, C, R*S) of them.  Same packing as
- * mmdx_conv_pack_weight (C = padded channels, c_master = the master's Cin). */
+ * mmdx_conv_pack_weight for unpadded weights: c_master must equal C (channel-padded weights
+ * use mmdx_conv_pack_weight). */
 typedef struct {
   const float* w;      /* fp32 KCRS master */
   void* krsc;          /* packed [K][R][S][C] or NULL */
@@ -109,23 +110,24 @@ int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void
                     const void* dy, float* dw_kcrs, float beta, void* workspace,
                     size_t ws_bytes, void* stream);
 
-/* ResNet stem (backbone.0, TP:183) straight from the NCHW fp32 image batch of
- * image_transfom_into_tensor (TP:112-119) / mmdx_image_preprocess — no NHWC copy, no
- * channel padding: desc->C is the image's channel count (3), the GEMM K is C*R*S in the
- * master weight's own (c, r, s) order, rounded up to mmdx_stem_k8(d) in the packed weight.
- * bf16 compute; Cout (desc->K) <= 64 and a multiple of 8.
- *   pack:  w_kcrs fp32 -> w_packed [K][mmdx_stem_k8(d)] bf16 (zero tail)
- *   fwd:   y [N,P,Q,K] bf16 NHWC, stat_part as mmdx_conv_fwd (128-row blocks)
- *   wgrad: dw_kcrs (fp32 master layout) = beta*dw_kcrs + grad, from x (NCHW fp32) and dy */
-int mmdx_stem_k8(const mmdx_conv_desc* d);
-int mmdx_stem_pack_weight(const mmdx_conv_desc* d, const float* w_kcrs, void* w_packed,
-                          void* stream);
-int mmdx_stem_fwd(const mmdx_conv_desc* d, const float* x_nchw, const void* w_packed,
-                  void* y, float* stat_part, void* stream);
-size_t mmdx_stem_wgrad_workspace_size(const mmdx_conv_desc* d);
-int mmdx_stem_wgrad(const mmdx_conv_desc* d, const float* x_nchw, const void* dy,
-                    float* dw_kcrs, float beta, void* workspace, size_t ws_bytes,
-                    void* stream);
+/* ResNet stem (backbone.0, TP:183: 7x7 / stride 2 / pad 3 over the 3-channel image) as an
+ * ordinary conv over PIXEL PAIRS (bf16 path): the NCHW fp32 batch of
+ * image_transfom_into_tensor (TP:112-119) is written once, zero-bordered, as
+ * [N][H+2p][(W+2p)/2][8] bf16 (two adjacent padded pixels x 4 channels per "pixel"); the
+ * stem is then a stride (2,1), unpadded R x ceil(S/2) conv with 8 channels (K = 224 instead of
+ * 392 for the channel-padded image, no border taps) run by mmdx_conv_fwd / mmdx_conv_wgrad
+ * with the descriptor mmdx_stem_pair_desc returns.  Needs stride 2, C <= 4, even W + 2p.
+ *   pack:  w_kcrs fp32 [K][C][R][S] -> w_packed [K][R][ceil(S/2)][8] bf16 (the pair conv's KRSC)
+ *   grad:  dw_pair fp32 [K][8][R][ceil(S/2)] (mmdx_conv_wgrad of the pair conv, c_master 8)
+ *          -> dw_kcrs (master layout) = beta * dw_kcrs + grad */
+int mmdx_stem_pair_desc(int N, int C, int H, int W, int K, int R, int S, int stride, int pad,
+                        mmdx_conv_desc* out);
+int mmdx_stem_pair_input(const float* x_nchw, int N, int C, int H, int W, int pad, void* out,
+                         void* stream);
+int mmdx_stem_pair_pack_weight(const float* w_kcrs, int K, int C, int R, int S, void* w_packed,
+                               void* stream);
+int mmdx_stem_pair_grad(const float* dw_pair, int K, int C, int R, int S, float* dw_kcrs,
+                        float beta, void* stream);
 
 /* ---------------------------------------------------------------- batch norm (+res)(+ReLU)
  * x, y, residual: [rows, C] (NHWC flattened).  Train mode computes batch statistics
@@ -176,8 +178,8 @@ enum {
   MMDX_OP_EVENT = 1, MMDX_OP_NCHW2NHWC, MMDX_OP_CONV_PACK, MMDX_OP_CONV_FWD, MMDX_OP_BN_FWD,
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
-  MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PACK, MMDX_OP_STEM_FWD,
-  MMDX_OP_STEM_WGRAD, MMDX_OP_CONV_PACK_MULTI
+  MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PAIR_INPUT,
+  MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI
 };
 typedef struct {
   int op, dtype, stream;

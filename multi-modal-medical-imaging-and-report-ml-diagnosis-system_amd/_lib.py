@@ -50,8 +50,8 @@ class PlanOp(C.Structure):
 
 (OP_EVENT, OP_NCHW2NHWC, OP_CONV_PACK, OP_CONV_FWD, OP_BN_FWD, OP_MAXPOOL_FWD,
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
- OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PACK, OP_STEM_FWD,
- OP_STEM_WGRAD, OP_CONV_PACK_MULTI) = range(1, 21)
+ OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PAIR_INPUT,
+ OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI) = range(1, 21)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -71,11 +71,10 @@ SIGNATURES = {
     "mmdx_conv_dgrad_bnstat": (i32, [i32, CD, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]),
     "mmdx_conv_wgrad_workspace_size": (sz, [i32, CD]),
     "mmdx_conv_wgrad": (i32, [i32, CD, i32, vp, vp, vp, f32, vp, sz, vp]),
-    "mmdx_stem_k8": (i32, [CD]),
-    "mmdx_stem_pack_weight": (i32, [CD, vp, vp, vp]),
-    "mmdx_stem_fwd": (i32, [CD, vp, vp, vp, vp, vp]),
-    "mmdx_stem_wgrad_workspace_size": (sz, [CD]),
-    "mmdx_stem_wgrad": (i32, [CD, vp, vp, vp, f32, vp, sz, vp]),
+    "mmdx_stem_pair_desc": (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, CD]),
+    "mmdx_stem_pair_input": (i32, [vp, i32, i32, i32, i32, i32, vp, vp]),
+    "mmdx_stem_pair_pack_weight": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "mmdx_stem_pair_grad": (i32, [vp, i32, i32, i32, i32, vp, f32, vp]),
     "mmdx_bn_workspace_size": (sz, [i64, i32]),
     "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, i32, i64, vp, vp, vp, vp, f32, f32, vp, vp,
                           vp, i32, vp, vp, sz, vp]),

@@ -1,6 +1,8 @@
 // Shared device/host helpers for the mmdx HIP library (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -65,6 +67,14 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   __syncthreads();
   return t;
 }
+
+// elementwise launch geometry: grid-stride loops over at most 8192 blocks of 256
+static inline int grid_for(long n, int per = 256) {
+  return (int)std::max<long>(1, std::min<long>((n + per - 1) / per, 8192));
+}
+
+#define GRID_STRIDE(i, n) \
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
 
 }  // namespace mmdx
 

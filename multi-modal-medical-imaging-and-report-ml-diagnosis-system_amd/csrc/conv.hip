@@ -45,14 +45,19 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Cm, i
   }
 }
 
-// All conv weights of a trunk in ONE launch (mmdx_conv_pack_multi): block b packs the item
-// whose [first_block, next first_block) range holds b; PACK_PER_BLOCK elements per block in
-// KRSC order (coalesced KRSC writes).  Replaces one pack launch per conv on the critical stream.
-constexpr int PACK_PER_BLOCK = 2048;
+// All conv weights of a trunk in ONE launch (mmdx_conv_pack_multi).  The master weight is a
+// matrix Wm[K][C*RS] (col j = c*RS + rs); CRSK is exactly Wm^T and KRSC permutes each row
+// (c, rs) -> (rs, c).  A block moves one 64 x 64 tile of Wm through LDS: coalesced fp32
+// reads along j, coalesced bf16 writes along j (KRSC, per-row permutation) and along k (CRSK,
+// transposed).  Block b belongs to the item whose [first_block, next first_block) holds it;
+// 32-bit index math (every weight < 2^31 elements).  Channel-padded weights (C > c_master)
+// keep mmdx_conv_pack_weight.
+constexpr int PACK_T = 64;
 
 template <typename T>
 __global__ __launch_bounds__(256) void pack_multi_kernel(const mmdx_pack_item* __restrict__ it,
                                                          int n) {
+  __shared__ float tile[PACK_T][PACK_T + 1];
   const long b = blockIdx.x;
   int lo = 0, hi = n - 1;  // last item with first_block <= b
   while (lo < hi) {
@@ -60,21 +65,32 @@ __global__ __launch_bounds__(256) void pack_multi_kernel(const mmdx_pack_item* _
     if (it[mid].first_block <= b) lo = mid; else hi = mid - 1;
   }
   const mmdx_pack_item t = it[lo];
-  const int K = t.K, C = t.C, Cm = t.c_master, RS = t.RS;
-  const long total = (long)K * RS * C;
-  const long base = (b - t.first_block) * PACK_PER_BLOCK;
-  T* krsc = (T*)t.krsc;
-  T* crsk = (T*)t.crsk;
-  for (int e = threadIdx.x; e < PACK_PER_BLOCK; e += 256) {
-    const long i = base + e;
-    if (i >= total) break;
-    const int c = (int)(i % C);
-    const long q = i / C;
-    const int rs = (int)(q % RS);
-    const int k = (int)(q / RS);
-    const float v = c < Cm ? t.w[((long)k * Cm + c) * RS + rs] : 0.f;
-    if (krsc) krsc[i] = from_f<T>(v);
-    if (crsk) crsk[((long)c * RS + rs) * K + k] = from_f<T>(v);
+  const int K = t.K, RS = t.RS, J = t.C * RS;
+  const int tj = (J + PACK_T - 1) / PACK_T;
+  const int local = (int)(b - t.first_block);
+  const int k0 = (local / tj) * PACK_T, j0 = (local % tj) * PACK_T;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  for (int r = ty; r < PACK_T; r += 4) {
+    const int k = k0 + r, j = j0 + tx;
+    tile[r][tx] = k < K && j < J ? t.w[(long)k * J + j] : 0.f;
+  }
+  __syncthreads();
+  if (t.krsc) {  // row k: element j = c*RS + rs -> (rs*C + c)
+    T* krsc = (T*)t.krsc;
+    for (int r = ty; r < PACK_T; r += 4) {
+      const int k = k0 + r, j = j0 + tx;
+      if (k < K && j < J) {
+        const int c = j / RS, rs = j - c * RS;
+        krsc[(long)k * J + rs * t.C + c] = from_f<T>(tile[r][tx]);
+      }
+    }
+  }
+  if (t.crsk) {  // CRSK[j][k] = Wm[k][j]
+    T* crsk = (T*)t.crsk;
+    for (int r = ty; r < PACK_T; r += 4) {
+      const int j = j0 + r, k = k0 + tx;
+      if (j < J && k < K) crsk[(long)j * K + k] = from_f<T>(tile[tx][r]);
+    }
   }
 }
 
@@ -359,7 +375,7 @@ extern "C" int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_m
 }
 
 extern "C" long mmdx_conv_pack_blocks(int K, int C, int RS) {
-  return ((long)K * C * RS + PACK_PER_BLOCK - 1) / PACK_PER_BLOCK;
+  return (long)((K + PACK_T - 1) / PACK_T) * ((C * RS + PACK_T - 1) / PACK_T);
 }
 
 extern "C" int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items,
@@ -455,130 +471,115 @@ extern "C" int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const 
 }
 
 // ------------------------------------------------------------------------------ stem
-// conv1 of the trunk (backbone.0, TP:183) straight from the NCHW fp32 image batch that
-// image_transfom_into_tensor / mmdx_image_preprocess produce: no NHWC copy, K = 147 in the
-// weight's own (c, r, s) order (packed once per step to [Cout][K8] bf16, K8 = K rounded up to
-// 8), BN statistics from the epilogue.  bf16 only (the fp32 parity path keeps the generic
-// conv on an NHWC copy).
+// ResNet stem (backbone.0, TP:183: conv 7x7 / stride 2 / pad 3, 3 -> 64 channels) as an
+// ordinary NHWC conv over PIXEL PAIRS.  The image is written once, zero-bordered, as bf16
+// [N][H+2p][(W+2p)/2][8]: a "pixel" of the pair image is two adjacent padded pixels x 4
+// channels (c = 3 is zero), one 16-B chunk.  Output column q reads padded columns 2q+s,
+// s < S, = pairs q+j, j < ceil(S/2), both parities: a stride (2, 1), unpadded R x ceil(S/2)
+// conv with 8 channels, K = 7*4*8 = 224 (vs 7*7*8 = 392 for the channel-padded image), no
+// border taps, on the same implicit-GEMM kernels (fwd + BN-stat epilogue, wgrad).  The
+// weight maps to w'[k][r][j][e*4+c] = w[k][c][r][2j+e] (0 where 2j+e >= S or c >= C).
 namespace mmdx {
 
-static StemSrc stem_src(const mmdx_conv_desc* d, const float* x) {
-  StemSrc g;
-  g.x = x; g.N = d->N; g.C = d->C; g.H = d->H; g.W = d->W; g.R = d->R; g.S = d->S;
-  g.sh = d->stride_h; g.sw = d->stride_w; g.ph = d->pad_h; g.pw = d->pad_w;
-  g.P = d->P; g.Q = d->Q; g.M = d->N * d->P * d->Q; g.K = d->C * d->R * d->S;
-  g.inv_rs = 1.f / (float)(d->R * d->S); g.inv_s = 1.f / (float)d->S;
-  return g;
-}
-
-static int stem_check(const mmdx_conv_desc* d) {
-  MMDX_CHECK_ARG(d && d->N > 0 && d->C > 0 && d->K > 0 && d->K % 8 == 0 &&
-                     d->C * d->R * d->S <= 1024 &&
-                     d->P == (d->H + 2 * d->pad_h - d->R) / d->stride_h + 1 &&
-                     d->Q == (d->W + 2 * d->pad_w - d->S) / d->stride_w + 1,
-                 "stem: bad descriptor");
-  MMDX_CHECK_ARG((long)d->N * d->C * d->H * d->W < (1L << 31) &&
-                     (long)d->N * d->P * d->Q * d->K * 2 < (1L << 31),
-                 "stem: tensors must stay below 2 GiB");
-  return 0;
-}
-
-static int stem_k8(const mmdx_conv_desc* d) { return (d->C * d->R * d->S + 7) / 8 * 8; }
-
-__global__ void stem_pack_kernel(const float* __restrict__ w, int K, int KC, int K8,
-                                 bf16* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= K * K8) return;
-  const int k = i / K8, j = i - k * K8;
-  out[i] = (bf16)(j < KC ? w[(long)k * KC + j] : 0.f);
-}
-
-// stem partial slab [splits][Cout][K8] -> dw[Cout][K] (= KCRS flattening) fp32
-__global__ void stem_wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Kout,
-                                         int K8, int KC, float* __restrict__ dw, float beta) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= Kout * KC) return;
-  const int k = i / KC, j = i - k * KC;
-  const long slab = (long)Kout * K8;
-  float a[4] = {0.f, 0.f, 0.f, 0.f};
-  int z = 0;
-  for (; z + 4 <= splits; z += 4)
+__global__ void stem_pair_input_kernel(const float* __restrict__ x, int N, int C, int H, int W,
+                                       int pad, int Hp, int W2, bf16* __restrict__ out) {
+  const long total = (long)N * Hp * W2;
+  GRID_STRIDE(i, total) {
+    const int j = (int)(i % W2);
+    const long t = i / W2;
+    const int hp = (int)(t % Hp);
+    const int n = (int)(t / Hp);
+    const int ih = hp - pad;
+    bf16x8 v;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] += ws[(long)(z + u) * slab + (long)k * K8 + j];
-  for (int u = 0; z < splits; ++z, ++u) a[u] += ws[(long)z * slab + (long)k * K8 + j];
-  const float v = (a[0] + a[1]) + (a[2] + a[3]);
-  dw[i] = beta != 0.f ? beta * dw[i] + v : v;
+    for (int e = 0; e < 2; ++e) {
+      const int iw = 2 * j + e - pad;
+      const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[e * 4 + c] = (bf16)(in && c < C ? x[(((long)n * C + c) * H + ih) * W + iw] : 0.f);
+    }
+    *(bf16x8*)(out + i * 8) = v;
+  }
 }
 
-struct StemWgradPlan { int splits, kper; };
-static StemWgradPlan plan_stem_wgrad(const mmdx_conv_desc* d) {
-  const long K = (long)d->N * d->P * d->Q;
-  const long ktiles = (K + 63) / 64;
-  const int tiles = (d->K + 63) / 64 * ((stem_k8(d) + 127) / 128);
-  long s = std::max(1L, std::min((512L + tiles - 1) / tiles, ktiles / 16));
-  const long kt_per = (ktiles + s - 1) / s;
-  StemWgradPlan p;
-  p.kper = (int)(kt_per * 64);
-  p.splits = (int)((K + p.kper - 1) / p.kper);
-  return p;
+__global__ void stem_pair_pack_kernel(const float* __restrict__ w, int K, int C, int R, int S,
+                                      int S2, bf16* __restrict__ out) {
+  const long total = (long)K * R * S2 * 8;
+  GRID_STRIDE(i, total) {
+    const int ce = (int)(i & 7), e = ce >> 2, c = ce & 3;
+    const long t = i >> 3;
+    const int j = (int)(t % S2);
+    const long t2 = t / S2;
+    const int r = (int)(t2 % R), k = (int)(t2 / R);
+    const int s = 2 * j + e;
+    out[i] = (bf16)(c < C && s < S ? w[(((long)k * C + c) * R + r) * S + s] : 0.f);
+  }
+}
+
+// wgrad of the pair conv (fp32, its own KCRS: [K][8][R][S2]) -> master dw [K][C][R][S]
+__global__ void stem_pair_grad_kernel(const float* __restrict__ dwp, int K, int C, int R, int S,
+                                      int S2, float* __restrict__ dw, float beta) {
+  const long total = (long)K * C * R * S;
+  GRID_STRIDE(i, total) {
+    const int s = (int)(i % S);
+    const long t = i / S;
+    const int r = (int)(t % R);
+    const long t2 = t / R;
+    const int c = (int)(t2 % C), k = (int)(t2 / C);
+    const float v = dwp[(((long)k * 8 + (s & 1) * 4 + c) * R + r) * S2 + (s >> 1)];
+    dw[i] = beta != 0.f ? beta * dw[i] + v : v;
+  }
 }
 
 }  // namespace mmdx
 
-extern "C" int mmdx_stem_k8(const mmdx_conv_desc* d) { return d ? stem_k8(d) : 0; }
+extern "C" int mmdx_stem_pair_desc(int N, int C, int H, int W, int K, int R, int S, int stride,
+                                   int pad, mmdx_conv_desc* out) {
+  MMDX_CHECK_ARG(out && N > 0 && C > 0 && C <= 4 && H > 0 && W > 0 && K > 0 && R > 0 && S > 0 &&
+                     pad >= 0 && stride == 2 && (W + 2 * pad) % 2 == 0 &&
+                     H + 2 * pad >= R && W + 2 * pad >= S,
+                 "stem pair: needs stride 2, C <= 4, even padded width");
+  const int Hp = H + 2 * pad, W2 = (W + 2 * pad) / 2, S2 = (S + 1) / 2;
+  mmdx_conv_desc d;
+  d.N = N; d.H = Hp; d.W = W2; d.C = 8; d.K = K; d.R = R; d.S = S2;
+  d.stride_h = stride; d.stride_w = 1; d.pad_h = 0; d.pad_w = 0;
+  d.P = (Hp - R) / stride + 1;
+  d.Q = W2 - S2 + 1;
+  MMDX_CHECK_ARG(d.Q == (W + 2 * pad - S) / stride + 1, "stem pair: output width mismatch");
+  *out = d;
+  return 0;
+}
 
-extern "C" int mmdx_stem_pack_weight(const mmdx_conv_desc* d, const float* w, void* w_packed,
-                                     void* stream) {
-  int rc = stem_check(d);
-  if (rc) return rc;
-  const int K8 = stem_k8(d), KC = d->C * d->R * d->S;
-  const int total = d->K * K8;
-  hipLaunchKernelGGL(stem_pack_kernel, dim3((total + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, w, d->K, KC, K8, (bf16*)w_packed);
+extern "C" int mmdx_stem_pair_input(const float* x_nchw, int N, int C, int H, int W, int pad,
+                                    void* out, void* stream) {
+  MMDX_CHECK_ARG(x_nchw && out && C > 0 && C <= 4 && (W + 2 * pad) % 2 == 0,
+                 "stem pair input: bad args");
+  const int Hp = H + 2 * pad, W2 = (W + 2 * pad) / 2;
+  const long total = (long)N * Hp * W2;
+  hipLaunchKernelGGL(stem_pair_input_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, x_nchw, N, C, H, W, pad, Hp, W2, (bf16*)out);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
 
-extern "C" int mmdx_stem_fwd(const mmdx_conv_desc* d, const float* x_nchw, const void* w_packed,
-                             void* y, float* stat_part, void* stream) {
-  int rc = stem_check(d);
-  if (rc) return rc;
-  MMDX_CHECK_ARG(d->K <= 64, "stem fwd: Cout %d > 64", d->K);
-  const StemSrc g = stem_src(d, x_nchw);
-  const int K8 = stem_k8(d);
-  DenseK<bf16> sb{(const bf16*)w_packed, K8, d->K, true};
-  EpiStore<bf16> epi{(bf16*)y, d->K, g.M, d->K, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr,
-                     (float2*)stat_part};
-  return launch_dma_ops<128, 64, StemA<128>, DmaK<64, DenseK<bf16>>>(g, sb, epi, g.M, d->K,
-                                                                      g.K, 1, g.K,
-                                                                      (hipStream_t)stream);
+extern "C" int mmdx_stem_pair_pack_weight(const float* w_kcrs, int K, int C, int R, int S,
+                                          void* w_packed, void* stream) {
+  MMDX_CHECK_ARG(w_kcrs && w_packed && C > 0 && C <= 4, "stem pair pack: bad args");
+  const int S2 = (S + 1) / 2;
+  const long total = (long)K * R * S2 * 8;
+  hipLaunchKernelGGL(stem_pair_pack_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, w_kcrs, K, C, R, S, S2, (bf16*)w_packed);
+  MMDX_LAUNCH_CHECK();
+  return 0;
 }
 
-extern "C" size_t mmdx_stem_wgrad_workspace_size(const mmdx_conv_desc* d) {
-  const StemWgradPlan p = plan_stem_wgrad(d);
-  return (size_t)p.splits * d->K * stem_k8(d) * sizeof(float);
-}
-
-extern "C" int mmdx_stem_wgrad(const mmdx_conv_desc* d, const float* x_nchw, const void* dy,
-                               float* dw, float beta, void* ws, size_t ws_bytes, void* stream) {
-  int rc = stem_check(d);
-  if (rc) return rc;
-  MMDX_CHECK_ARG(d->K <= 64, "stem wgrad: Cout %d > 64", d->K);
-  const StemWgradPlan p = plan_stem_wgrad(d);
-  const int K8 = stem_k8(d), KC = d->C * d->R * d->S;
-  const size_t need = mmdx_stem_wgrad_workspace_size(d);
-  MMDX_CHECK_ARG(ws && ws_bytes >= need, "stem wgrad: workspace %zu < %zu", ws_bytes, need);
-  const StemSrc g = stem_src(d, x_nchw);
-  const int M = d->K, Kpix = g.M;
-  DenseR<bf16> sa{(const bf16*)dy, d->K, M, true, Kpix};
-  EpiPartial epi{(float*)ws, M, K8};
-  hipStream_t st = (hipStream_t)stream;
-  rc = launch_dma_ops<64, 128, DmaR<64, DenseR<bf16>>, StemR<128>>(sa, g, epi, M, K8, Kpix,
-                                                                    p.splits, p.kper, st);
-  if (rc) return rc;
-  const int total = M * KC;
-  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st,
-                     (const float*)ws, p.splits, M, K8, KC, dw, beta);
+extern "C" int mmdx_stem_pair_grad(const float* dw_pair, int K, int C, int R, int S, float* dw,
+                                   float beta, void* stream) {
+  MMDX_CHECK_ARG(dw_pair && dw && C > 0 && C <= 4, "stem pair grad: bad args");
+  const long total = (long)K * C * R * S;
+  hipLaunchKernelGGL(stem_pair_grad_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, dw_pair, K, C, R, S, (S + 1) / 2, dw, beta);
   MMDX_LAUNCH_CHECK();
   return 0;
 }

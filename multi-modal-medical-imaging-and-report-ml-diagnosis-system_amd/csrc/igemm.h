@@ -1134,7 +1134,6 @@ template <int ROWS, class Src>
 struct DmaK {
   static constexpr int NW = NT / 64;
   static constexpr int INSTR = ROWS / (8 * NW);  // DMAs per wave per stage
-  static constexpr bool VALU_FILL = false;
   static constexpr int BYTES = ROWS * 128;
   static_assert(ROWS % (8 * NW) == 0, "rows per wave");
   typedef Src SrcT;
@@ -1188,7 +1187,6 @@ struct DmaR {
   static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
   static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
   static constexpr int INSTR = 64 / (KPI * NW); // DMAs per wave per stage (BK = 64)
-  static constexpr bool VALU_FILL = false;
   static constexpr int BYTES = 64 * ROWS * 2;
   static_assert(ROWS == 64 || ROWS == 128, "R-major DMA tile rows");
   typedef Src SrcT;
@@ -1292,8 +1290,6 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (OA::VALU_FILL || OB::VALU_FILL)  // LDS written by ds_write, not DMA
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NS - 1 < nt) {  // its stage was consumed in iteration t-1 by every wave
       char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
@@ -1383,132 +1379,6 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     }
   }
 }
-
-// --------------------------------------------------------------------------------------
-// ResNet stem (conv 7x7/2, 3 -> 64 channels) straight from the NCHW fp32 image batch: the
-// block builds its im2col tile in LDS with vector loads + bf16 conversion (no NHWC copy of
-// the image, no channel padding: K = C*R*S = 147 in the weight's own (c, r, s) order).
-// k = (c*R + r)*S + s; element = x[n][c][p*sh - ph + r][q*sw - pw + s] (0 outside).
-// --------------------------------------------------------------------------------------
-struct StemSrc {
-  const float* x; int N, C, H, W, R, S, sh, sw, ph, pw, P, Q, M, K;
-  float inv_rs, inv_s;  // 1/(R*S), 1/S: k < 2^16 decodes exactly as (k + 0.5) * inv
-};
-
-// decode of the 8 consecutive k of one 16-B chunk (same for every row of the tile)
-struct StemK8 { int coff[8]; int r[8], s[8]; };
-
-__device__ __forceinline__ void stem_k8(const StemSrc& g, int k, StemK8& d) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int kk = k + e;
-    const int c = (int)(((float)kk + 0.5f) * g.inv_rs), rs = kk - c * g.R * g.S;
-    const int r = (int)(((float)rs + 0.5f) * g.inv_s), sx = rs - r * g.S;
-    const bool ok = kk < g.K;
-    d.coff[e] = ok ? (c * g.H + r) * g.W + sx : 0;
-    d.r[e] = ok ? r : -(1 << 20);  // makes the bounds test fail for padding k
-    d.s[e] = sx;
-  }
-}
-
-// A operand of the stem fwd: rows = output pixels, k-major LDS image as DmaK's.
-template <int ROWS>
-struct StemA {
-  static constexpr int NW = NT / 64;
-  static constexpr int INSTR = 0;  // nothing stays in flight after issue()
-  static constexpr int BYTES = ROWS * 128;
-  static constexpr int RPT = ROWS * 8 / NT;  // rows (chunks) per thread
-  static constexpr bool VALU_FILL = true;
-  typedef StemSrc SrcT;
-  int base[RPT], ih0[RPT], iw0[RPT];  // per row: image base, top-left input coordinate
-  __device__ void init(const StemSrc& g, int row0, int lane, int wid, int) {
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int m = row0 + (int)(threadIdx.x >> 3) + i * (NT / 8);
-      const int pq = g.P * g.Q, n = m / pq, rem = m - n * pq;
-      const int p = rem / g.Q, q = rem - p * g.Q;
-      base[i] = m < g.M ? n * g.C * g.H * g.W : -1;
-      ih0[i] = p * g.sh - g.ph;
-      iw0[i] = q * g.sw - g.pw;
-    }
-  }
-  __device__ void issue(const StemSrc& g, char* stage, int k0, int, int) const {
-    const int chunk = threadIdx.x & 7;
-    StemK8 d;
-    stem_k8(g, k0 + chunk * 8, d);
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int row = (int)(threadIdx.x >> 3) + i * (NT / 8);
-      bf16x8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int ih = ih0[i] + d.r[e], iw = iw0[i] + d.s[e];
-        const bool ok = base[i] >= 0 && (unsigned)ih < (unsigned)g.H &&
-                        (unsigned)iw < (unsigned)g.W;
-        v[e] = (bf16)(ok ? g.x[base[i] + d.coff[e] + ih0[i] * g.W + iw0[i]] : 0.f);
-      }
-      *(bf16x8*)(stage + row * 128 + ((chunk ^ (row & 7)) << 4)) = v;
-    }
-  }
-  __device__ static bf16x8 frag(const char* stage, int r16, int ks, int lane) {
-    return DmaK<ROWS, DenseK<bf16>>::frag(stage, r16, ks, lane);
-  }
-};
-
-// B operand of the stem wgrad: rows = im2col columns k, K = pixels; R-major LDS image with
-// DmaR's per-k-line XOR layout (read back by ds_read_b64_tr_b16).
-template <int ROWS>
-struct StemR {
-  static constexpr int NW = NT / 64;
-  static constexpr int INSTR = 0;
-  static constexpr int BYTES = 64 * ROWS * 2;
-  static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
-  static constexpr int LPT = 64 * CPR / NT;     // k-lines (pixels) per thread
-  static constexpr bool VALU_FILL = true;
-  typedef StemSrc SrcT;
-  StemK8 d;     // this thread's 8 im2col columns (fixed per block)
-  int n[LPT], p[LPT], q[LPT];  // this thread's pixels, advanced one K tile per issue
-  int dn, dp, dq;
-  __device__ void init(const StemSrc& g, int row0, int lane, int wid, int kbeg) {
-    const int cc = threadIdx.x % CPR;
-    stem_k8(g, row0 + cc * 8, d);
-    const int pq = g.P * g.Q;
-    dn = 64 / pq; dp = (64 % pq) / g.Q; dq = (64 % pq) % g.Q;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int k = kbeg + (int)(threadIdx.x / CPR) + i * (NT / CPR);
-      n[i] = k / pq;
-      const int rem = k - n[i] * pq;
-      p[i] = rem / g.Q;
-      q[i] = rem - p[i] * g.Q;
-    }
-  }
-  __device__ void issue(const StemSrc& g, char* stage, int k0, int klim, int) {
-    const int cc = threadIdx.x % CPR;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int kl = (int)(threadIdx.x / CPR) + i * (NT / CPR);
-      const bool pix_ok = k0 + kl < klim;
-      const int ihb = p[i] * g.sh - g.ph, iwb = q[i] * g.sw - g.pw;
-      const int bse = n[i] * g.C * g.H * g.W + ihb * g.W + iwb;
-      bf16x8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int ih = ihb + d.r[e], iw = iwb + d.s[e];
-        const bool ok = pix_ok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        v[e] = (bf16)(ok ? g.x[bse + d.coff[e]] : 0.f);
-      }
-      const int sw = DmaR<ROWS, DenseR<bf16>>::sw(kl);
-      *(bf16x8*)(stage + kl * (ROWS * 2) + ((cc ^ sw) << 4)) = v;
-      q[i] += dq; p[i] += dp; n[i] += dn;  // next K tile: 64 pixels on
-      if (q[i] >= g.Q) { q[i] -= g.Q; ++p[i]; }
-      if (p[i] >= g.P) { p[i] -= g.P; ++n[i]; }
-    }
-  }
-  __device__ static bf16x8 frag(const char* stage, int r16, int ks, int lane) {
-    return DmaR<ROWS, DenseR<bf16>>::frag(stage, r16, ks, lane);
-  }
-};
 
 // Loader bundles (give the kernel template one type per operand).
 template <typename T, int ROWS, class Src>

@@ -6,13 +6,6 @@
 
 namespace mmdx {
 
-static int grid_for(long n, int per = 256) {
-  return (int)std::max<long>(1, std::min<long>((n + per - 1) / per, 8192));
-}
-
-#define GRID_STRIDE(i, n) \
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
-
 // ----------------------------------------------------------------------------- maxpool
 // Semantics of PyTorch CPU max_pool2d: padded taps are skipped, the FIRST maximum in
 // row-major window order wins (strict '>'), NaN propagates.

@@ -90,16 +90,18 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_CONV_DGRAD:
       return mmdx_conv_dgrad(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext), o.f[0],
                              s);
-    case MMDX_OP_STEM_PACK:
-      return mmdx_stem_pack_weight(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext), s);
-    case MMDX_OP_STEM_FWD:
-      // p: x_nchw, w_packed, y, stat_part
-      return mmdx_stem_fwd(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
-                           (float*)P(o, 3, ext), s);
-    case MMDX_OP_STEM_WGRAD:
-      // l: ws_bytes; f: beta; p: x_nchw, dy, dw, ws
-      return mmdx_stem_wgrad(&o.d, (const float*)P(o, 0, ext), P(o, 1, ext),
-                             (float*)P(o, 2, ext), o.f[0], P(o, 3, ext), (size_t)o.l[0], s);
+    case MMDX_OP_STEM_PAIR_INPUT:
+      // i: N, C, H, W, pad; p: x_nchw, out
+      return mmdx_stem_pair_input((const float*)P(o, 0, ext), o.i[0], o.i[1], o.i[2], o.i[3],
+                                  o.i[4], P(o, 1, ext), s);
+    case MMDX_OP_STEM_PAIR_PACK:
+      // i: K, C, R, S; p: w_kcrs, w_packed
+      return mmdx_stem_pair_pack_weight((const float*)P(o, 0, ext), o.i[0], o.i[1], o.i[2],
+                                        o.i[3], P(o, 1, ext), s);
+    case MMDX_OP_STEM_PAIR_GRAD:
+      // i: K, C, R, S; f: beta; p: dw_pair, dw_kcrs
+      return mmdx_stem_pair_grad((const float*)P(o, 0, ext), o.i[0], o.i[1], o.i[2], o.i[3],
+                                 (float*)P(o, 1, ext), o.f[0], s);
     case MMDX_OP_CONV_PACK_MULTI:
       // i: n_items; l: total_blocks; p: item table (device)
       return mmdx_conv_pack_multi(o.dtype, (const mmdx_pack_item*)P(o, 0, ext), o.i[0], o.l[0],

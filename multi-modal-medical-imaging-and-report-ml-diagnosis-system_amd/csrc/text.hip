@@ -7,8 +7,6 @@
 
 namespace mmdx {
 
-static int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
-
 constexpr int EMB_MAXE = 16;  // elements per lane: D <= 1024
 
 // One wave per token: s = word[id] + pos[l] + type[tt]; y = LN(s).  (BertEmbeddings)

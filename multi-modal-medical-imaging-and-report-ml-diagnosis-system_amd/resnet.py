@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 import weakref
 
 import torch
@@ -23,7 +22,6 @@ from . import _lib as L
 from ._lib import call, ptr, stream
 
 _VEC = {torch.float32: 4, torch.bfloat16: 8}
-_STEM_DIRECT = os.environ.get("MMDX_STEM", "") == "direct"
 
 
 class _NoTimer:
@@ -298,16 +296,19 @@ class _Plan:
 
         # ---- forward
         stem_conv = trunk[0]
-        # MMDX_STEM=direct: the bf16 stem reads the NCHW fp32 batch itself (no NHWC copy,
-        # K = 147 unpadded).  Opt-in: its per-lane gather is latency-bound (fwd 539 us, wgrad
-        # 954 us at C4 vs 228 + 254 us for the NHWC copy + padded-C DMA path).
-        stem_direct = (_STEM_DIRECT and in_nchw and T == torch.bfloat16
-                       and stem_conv.out_channels <= 64
-                       and stem_conv.out_channels % 8 == 0 and stem_conv.in_channels == cin)
-        self.stem_direct = stem_direct
-        if stem_direct:
-            cp = cin
-            x0 = _Ext(0)
+        # bf16: the stem runs as a conv over pixel pairs of the zero-bordered image
+        # (mmdx_stem_pair_*: K = 224, no border taps) instead of a channel-padded NHWC copy
+        ks, ss, ps = stem_conv.kernel_size, stem_conv.stride, stem_conv.padding
+        stem_pair = (in_nchw and T == torch.bfloat16 and ss == 2 and cin <= 4
+                     and stem_conv.in_channels == cin and (W + 2 * ps) % 2 == 0)
+        d_pair = None
+        if stem_pair:
+            d_pair = L.ConvDesc()
+            call("mmdx_stem_pair_desc", N, cin, H, W, stem_conv.out_channels, ks, ks, ss, ps,
+                 ctypes.byref(d_pair))
+            cp = 8
+            x0 = A.new((N, d_pair.H, d_pair.W, 8), T, dev)
+            fw.add(L.OP_STEM_PAIR_INPUT, i=(N, cin, H, W, ps), p=(_Ext(0), x0))
         elif in_nchw:
             cp = vec
             x0 = A.new((N, H, W, cp), T, dev)
@@ -319,22 +320,24 @@ class _Plan:
         units = []
         packs = []
 
-        def unit(conv, bn, relu, x, N, H, W, C, cm, res, direct=False):
-            d = _desc(N, H, W, C, conv)
+        def unit(conv, bn, relu, x, N, H, W, C, cm, res, pair=None):
+            d = pair if pair is not None else _desc(N, H, W, C, conv)
             K, k = conv.out_channels, conv.kernel_size
             y = A.new((N, d.P, d.Q, K), T, dev)
             nstat = L.lib().mmdx_conv_fwd_stat_blocks(d) if train else 0
             part = A.new((K, nstat, 2), torch.float32, dev) if train else None
-            if direct:  # stem on the NCHW fp32 batch: weight packed [K][K8], no dgrad copy
-                wk = A.new((K, L.lib().mmdx_stem_k8(d)), T, dev)
+            wk = A.new((K, d.R, d.S, d.C), T, dev)
+            if pair is not None:  # stem over pixel pairs: its own weight map, no dgrad copy
                 wc = None
-                fw.add(L.OP_STEM_PACK, p=(conv.weight, wk), d=d)
-                fw.timed("fwd", L.OP_STEM_FWD, p=(x, wk, y, part), d=d)
-            else:  # packed by the plan's single multi-tensor pack launch (below)
-                wk = A.new((K, k, k, C), T, dev)
+                fw.add(L.OP_STEM_PAIR_PACK, i=(K, conv.in_channels, k, k),
+                       p=(conv.weight, wk))
+            else:
                 wc = A.new((C, k, k, K), T, dev) if keep else None
-                packs.append((conv.weight, wk, wc, K, C, cm, k * k))
-                fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
+                if C == cm:  # packed by the plan's single multi-tensor pack launch (below)
+                    packs.append((conv.weight, wk, wc, K, C, cm, k * k))
+                else:  # channel-padded input (fp32 stem): its own pack
+                    fw.add(L.OP_CONV_PACK, dt, i=(cm,), p=(conv.weight, wk, wc), d=d)
+            fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
             out = A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
             mean = A.new((K,), torch.float32, dev)
@@ -346,12 +349,12 @@ class _Plan:
                    p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
                       res, out, _WS))
             u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
-                     rstd=rstd, wc=wc, direct=direct)
+                     rstd=rstd, wc=wc, pair=pair is not None)
             units.append(u)
             return out, d, u
 
         a, d, stem_u = unit(stem_conv, trunk[1], True, x0, N, H, W, cp, 3, None,
-                            direct=stem_direct)
+                            pair=d_pair)
         H, W, C = d.P, d.Q, d.K
         mp = trunk[3]
         P = (H + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
@@ -442,21 +445,23 @@ class _Plan:
                        l=(rows, wsn, sp.data_ptr() if sp is not None else 0), f=(0.0,),
                        p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"], u["rstd"],
                           dconv, dres, g(u["bn"].weight), g(u["bn"].bias), _WS))
-                if u["direct"]:
-                    wsn = L.lib().mmdx_stem_wgrad_workspace_size(d)
-                else:
-                    wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
+                wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
                 ws_for(wsn, 1)
                 ev = A.event()
                 bw.add(L.OP_SIGNAL, p=(ev,), stream=0)
                 bw.add(L.OP_WAIT, p=(ev,), stream=1)
-                if u["direct"]:
-                    bw.timed("wgrad", L.OP_STEM_WGRAD, stream=1, l=(wsn,), f=(0.0,),
-                             p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
+                cv = u["conv"]
+                if u["pair"]:  # pair-conv gradient [K][8][R][S2], mapped to the master layout
+                    dwp = A.new((d.K, d.C, d.R, d.S), torch.float32, dev)
+                    bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(d.C,), l=(wsn,),
+                             f=(0.0,), p=(xref(u["x"]), dconv, dwp, _WS2), d=d)
+                    bw.add(L.OP_STEM_PAIR_GRAD, stream=1,
+                           i=(d.K, cv.in_channels, cv.kernel_size, cv.kernel_size), f=(0.0,),
+                           p=(dwp, g(cv.weight)))
                 else:
                     bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(u["cm"],),
-                             l=(wsn,), f=(0.0,),
-                             p=(xref(u["x"]), dconv, g(u["conv"].weight), _WS2), d=d)
+                             l=(wsn,), f=(0.0,), p=(xref(u["x"]), dconv, g(cv.weight), _WS2),
+                             d=d)
                 dx, fed = None, None
                 if want_dx:
                     if dx_acc is not None:

@@ -10,7 +10,49 @@ is identical to `loss.backward()`.
 """
 from __future__ import annotations
 
+import concurrent.futures
+import threading
+
 import torch
+
+
+class TwoTowerForward:
+    """Issue the two encoder towers' forwards (TP:1000-1007 `image_encoder.encode` /
+    `text_encoder.encode`) from two host threads at once.
+
+    The image tower's host side is one native launch-plan call (the GIL is released while
+    it enqueues), the text tower's is a sequence of Python-issued ops; on one thread one of
+    them always starts late on the GPU by the other's issue time.  Here the text tower is
+    issued by a persistent worker thread onto `text_stream` while the calling thread issues
+    the image tower onto the current stream; both return their usual autograd outputs.
+    `__call__(image_fn, text_fn)` -> (image_fn(), text_fn()).  The caller makes the current
+    stream wait for `text_stream` before consuming the text output."""
+
+    def __init__(self, text_stream=None):
+        self.text_stream = text_stream
+        self._pool = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="mmdx-text")
+        self._lock = threading.Lock()
+
+    def _text(self, fn, device, grad):
+        with torch.set_grad_enabled(grad):
+            if self.text_stream is None:
+                return fn()
+            torch.cuda.set_device(device)
+            with torch.cuda.stream(self.text_stream):
+                return fn()
+
+    def __call__(self, image_fn, text_fn):
+        with self._lock:  # one step in flight per instance
+            dev = torch.cuda.current_device() if self.text_stream is not None else None
+            fut = self._pool.submit(self._text, text_fn, dev, torch.is_grad_enabled())
+            try:
+                z_img = image_fn()
+            finally:
+                z_txt = fut.result()
+            return z_img, z_txt
+
+    def close(self):
+        self._pool.shutdown(wait=True)
 
 
 def _tower(z: torch.Tensor) -> None:

@@ -389,19 +389,21 @@ def test_dgrad_fused_bn_stats(dev, cfg):
     assert (ca - cb).abs().max().item() <= 2e-2 * max(1.0, cb.abs().max().item())
 
 
-STEMS = [  # N, C, H, W, K, k, s, p  (C = image channels: read from NCHW fp32 directly)
+STEMS = [  # N, C, H, W, K, k, s, p  (C = image channels, NCHW fp32 input)
     (2, 3, 32, 32, 64, 7, 2, 3),
-    (3, 3, 37, 29, 64, 7, 2, 3),   # ragged: M not a multiple of 128, odd P/Q
-    (1, 1, 20, 20, 32, 7, 2, 3),   # grayscale, K = 49
-    (2, 3, 64, 64, 64, 3, 1, 1),
+    (3, 3, 37, 30, 64, 7, 2, 3),   # ragged: odd H, M not a multiple of 128
+    (1, 1, 20, 20, 32, 7, 2, 3),   # grayscale
+    (2, 3, 16, 18, 64, 3, 2, 1),   # even kernel half-width: S2 = 2
+    (1, 3, 224, 224, 64, 7, 2, 3),  # the ResNet stem at full resolution
 ]
 
 
 @pytest.mark.parametrize("cfg", STEMS)
 @pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_stem_direct_nchw(dev, cfg, beta):
-    """mmdx_stem_{pack_weight,fwd,wgrad} (backbone.0 on the NCHW fp32 batch, TP:183) vs
-    torch conv2d fp32 on the bf16-rounded operands; BN epilogue stats as mmdx_conv_fwd's."""
+def test_stem_pixel_pair_conv(dev, cfg, beta):
+    """backbone.0 (TP:183) as a conv over pixel pairs (mmdx_stem_pair_*: zero-bordered
+    [N][H+2p][(W+2p)/2][8] image, stride (2,1) R x ceil(S/2) conv on the generic kernels) vs
+    torch conv2d fp32 on the bf16-rounded operands: fwd, BN epilogue stats, wgrad."""
     dt = torch.bfloat16
     N, C, H, W, K, k, s, p = cfg
     g = torch.Generator().manual_seed(7 + sum(cfg))
@@ -412,22 +414,26 @@ def test_stem_direct_nchw(dev, cfg, beta):
     yr = tF.conv2d(xb, wr, stride=s, padding=p)
     dy = torch.randn(yr.shape, generator=g).bfloat16().float()
     yr.backward(dy)
-    P, Q = yr.shape[2], yr.shape[3]
-    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q)
-    k8 = L.lib().mmdx_stem_k8(d)
-    assert k8 == (C * k * k + 7) // 8 * 8
-    wp = torch.empty(K, k8, dtype=dt, device=dev)
-    L.call("mmdx_stem_pack_weight", d, w.to(dev).data_ptr(), wp.data_ptr(), L.stream())
-    assert torch.equal(wp[:, :C * k * k].cpu(), w.reshape(K, -1).bfloat16())
-    assert not wp[:, C * k * k:].cpu().any()
-    xd = x.to(dev).contiguous()  # fp32 NCHW; the kernel rounds to bf16 on load
-    y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    d = L.ConvDesc()
+    L.call("mmdx_stem_pair_desc", N, C, H, W, K, k, k, s, p, d)
+    assert (d.P, d.Q, d.C, d.S) == (yr.shape[2], yr.shape[3], 8, (k + 1) // 2)
+    xd = x.to(dev).contiguous()
+    xp = torch.empty(N, d.H, d.W, 8, dtype=dt, device=dev)
+    L.call("mmdx_stem_pair_input", xd.data_ptr(), N, C, H, W, p, xp.data_ptr(), L.stream())
+    ref_pad = tF.pad(xb, (p, p, p, p))  # [N,C,H+2p,W+2p] -> pairs of pixels x 4 channels
+    ref_pair = torch.zeros(N, d.H, 2 * d.W, 4)
+    ref_pair[..., :C] = ref_pad.permute(0, 2, 3, 1)
+    assert torch.equal(xp.float().cpu(), ref_pair.reshape(N, d.H, d.W, 8))
+    wp = torch.empty(K, d.R, d.S, 8, dtype=dt, device=dev)
+    L.call("mmdx_stem_pair_pack_weight", w.to(dev).data_ptr(), K, C, k, k, wp.data_ptr(),
+           L.stream())
+    y = torch.empty(N, d.P, d.Q, K, dtype=dt, device=dev)
     nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
     part = torch.empty(K, nst, 2, device=dev)
-    L.call("mmdx_stem_fwd", d, xd.data_ptr(), wp.data_ptr(), y.data_ptr(), part.data_ptr(),
+    L.call("mmdx_conv_fwd", 1, d, xp.data_ptr(), wp.data_ptr(), y.data_ptr(), part.data_ptr(),
            L.stream())
     _close(y.permute(0, 3, 1, 2), yr.detach(), dt, f"stem fwd {cfg}")
-    M = N * P * Q
+    M = N * d.P * d.Q
     cnt = torch.tensor([min(128, M - 128 * b) for b in range(nst)], dtype=torch.float64)
     pm, p2 = part[..., 0].t().double().cpu(), part[..., 1].t().double().cpu()
     mean = (pm * cnt[:, None]).sum(0) / M
@@ -436,19 +442,28 @@ def test_stem_direct_nchw(dev, cfg, beta):
     _close(mean, yref.mean((0, 2, 3)), dt, "stem stat mean")
     _close(m2 / M, yref.var((0, 2, 3), unbiased=False), dt, "stem stat var")
     dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    dwp = torch.empty(K, 8, d.R, d.S, device=dev)
+    ws_n = L.lib().mmdx_conv_wgrad_workspace_size(1, d)
+    ws = torch.empty(max(1, ws_n), dtype=torch.uint8, device=dev)
+    L.call("mmdx_conv_wgrad", 1, d, 8, xp.data_ptr(), dyd.data_ptr(), dwp.data_ptr(), 0.0,
+           ws.data_ptr(), ws_n, L.stream())
     dw0 = torch.randn(K, C, k, k, generator=g)
     dw = dw0.to(dev)
-    ws_n = L.lib().mmdx_stem_wgrad_workspace_size(d)
-    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
-    L.call("mmdx_stem_wgrad", d, xd.data_ptr(), dyd.data_ptr(), dw.data_ptr(), beta,
-           ws.data_ptr(), ws_n, L.stream())
+    L.call("mmdx_stem_pair_grad", dwp.data_ptr(), K, C, k, k, dw.data_ptr(), beta, L.stream())
     _close(dw, wr.grad + beta * dw0, dt, f"stem wgrad {cfg}")
+
+
+def test_stem_pixel_pair_rejects_odd_width(dev):
+    d = L.ConvDesc()
+    with pytest.raises(RuntimeError, match="even padded width"):
+        L.call("mmdx_stem_pair_desc", 1, 3, 29, 29, 64, 7, 7, 2, 3, d)
 
 
 def test_conv_pack_multi_matches_single(dev):
     """mmdx_conv_pack_multi (all trunk weights in one launch) == one mmdx_conv_pack_weight per
-    weight, bit for bit, including channel padding (c_master < C) and a NULL CRSK output."""
-    shapes = [(64, 3, 8, 7), (256, 64, 64, 1), (128, 128, 128, 3), (24, 40, 40, 3)]
+    weight, bit for bit, including ragged tiles and a NULL CRSK output."""
+    shapes = [(64, 24, 24, 7), (256, 64, 64, 1), (128, 128, 128, 3), (24, 40, 40, 3),
+              (2048, 512, 512, 1)]
     g = torch.Generator().manual_seed(3)
     items = (L.PackItem * len(shapes))()
     outs, refs, nb = [], [], 0

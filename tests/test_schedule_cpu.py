@@ -33,3 +33,32 @@ def test_two_tower_backward_matches_plain_backward():
         for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
             assert torch.equal(p.grad, q.grad), n
     assert z_img.grad is None and z_txt.grad is None
+
+
+def test_two_tower_forward_threads_match_sequential():
+    """TwoTowerForward (text tower issued from a worker thread) builds the same autograd
+    graph as issuing the towers one after the other: identical outputs and gradients."""
+    from mmdx.schedule import TwoTowerForward
+    g = torch.Generator().manual_seed(0)
+    x, ids = torch.randn(6, 12, generator=g), torch.randint(0, 50, (6, 5), generator=g)
+    y = (torch.rand(6, 3, generator=g) < 0.3).float()
+    ref = _model(2)
+    loss, _, _ = _loss(*ref, x, ids, y)
+    loss.backward()
+    mine = _model(2)
+    towers = TwoTowerForward()
+    try:
+        for _ in range(2):  # the worker thread is reused across steps
+            for p in (q for m in mine for q in m.parameters()):
+                p.grad = None
+            z_img, z_txt = towers(lambda: mine[0](x), lambda: mine[1](ids))
+            logits = mine[2](torch.cat([z_img, z_txt], -1))
+            nn.functional.binary_cross_entropy_with_logits(logits, y).backward()
+            for a, b in zip(ref, mine):
+                for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+                    assert torch.equal(p.grad, q.grad), n
+        with torch.no_grad():  # grad mode follows the caller into the worker thread
+            _, z = towers(lambda: mine[0](x), lambda: mine[1](ids))
+            assert not z.requires_grad
+    finally:
+        towers.close()
