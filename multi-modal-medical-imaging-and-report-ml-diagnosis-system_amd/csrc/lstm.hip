@@ -138,7 +138,6 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
   constexpr int CPT = LSTM_RB * H / (LSTM_NW * 64);
   __shared__ __attribute__((aligned(16))) T sdg[LSTM_RB * LDG];
   __shared__ float sdh[LSTM_RB * H];
-  __builtin_amdgcn_s_setprio(3);  // latency-critical chain beside conv blocks (see coop fwd)
   const int dir = blockIdx.y;
   const int b0 = blockIdx.x * LSTM_RB;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
