@@ -137,17 +137,24 @@ static bool use_three_stages(long blocks, int ktiles_per_block) {
   return blocks <= 256 && ktiles_per_block >= 4;
 }
 
+template <int BM, int BN, class OA, class OB, class Epi, int NS>
+static void launch_dma_ns(const typename OA::SrcT& sa, const typename OB::SrcT& sb,
+                          const Epi& epi, int M, int N, int K, int splits, int kper, int nwg,
+                          hipStream_t st) {
+  hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, NS>), dim3(nwg, 1, splits),
+                     dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+}
+
 template <int BM, int BN, class OA, class OB, class Epi>
 static int launch_dma_ops(const typename OA::SrcT& sa, const typename OB::SrcT& sb,
                           const Epi& epi, int M, int N, int K, int splits, int kper,
                           hipStream_t st) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (use_three_stages((long)nwg * splits, (kper + 63) / 64))
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3>), dim3(nwg, 1, splits),
-                       dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
-  else
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 2>), dim3(nwg, 1, splits),
-                       dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+  if (use_three_stages((long)nwg * splits, (kper + 63) / 64)) {
+    launch_dma_ns<BM, BN, OA, OB, Epi, 3>(sa, sb, epi, M, N, K, splits, kper, nwg, st);
+  } else {
+    launch_dma_ns<BM, BN, OA, OB, Epi, 2>(sa, sb, epi, M, N, K, splits, kper, nwg, st);
+  }
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -306,7 +313,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   DenseR<T> sa{(const T*)dy, g.K, M, true, K};
   const int pq = g.P * g.Q;
   Im2colR<T> sb{(const T*)x, g, N, 1.f / (float)pq, 1.f / (float)g.Q, 64 / pq, (64 % pq) / g.Q,
-                (64 % pq) % g.Q};
+                (64 % pq) % g.Q};  // lane stepping: one 64-pixel K tile per issue
   EpiPartial epi{(float*)ws, M, N};
   int rc;
   if constexpr (sizeof(T) == 2) {

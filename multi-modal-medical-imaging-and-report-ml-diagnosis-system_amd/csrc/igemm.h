@@ -1130,25 +1130,33 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, char* lds, un
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <int ROWS, class Src>
+// BK = 64: rows of 128 B (8 chunks), slot = chunk ^ (row & 7), an instruction fills 8 rows.
+// BK = 32: rows of 64 B (4 chunks), slot = chunk ^ ((row >> 1) & 3) (conflict-free for the
+// ds_read_b128 lane groups of a 16-row x 4-chunk fragment read), an instruction fills 16 rows.
+template <int ROWS, class Src, int BK_ = 64>
 struct DmaK {
+  static constexpr int BK = BK_;
   static constexpr int NW = NT / 64;
-  static constexpr int INSTR = ROWS / (8 * NW);  // DMAs per wave per stage
-  static constexpr int BYTES = ROWS * 128;
-  static_assert(ROWS % (8 * NW) == 0, "rows per wave");
+  static constexpr int CPR = BK / 8;                 // 16-B chunks per row
+  static constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
+  static constexpr int INSTR = ROWS / (RPI * NW);    // DMAs per wave per stage
+  static constexpr int BYTES = ROWS * BK * 2;
+  static_assert(BK == 64 || BK == 32, "K tile depth");
+  static_assert(ROWS % (RPI * NW) == 0, "rows per wave");
   typedef Src SrcT;
   typedef typename Src::Mask Mask;
   __amdgpu_buffer_rsrc_t rsrc;
   int off[INSTR];       // byte offset of this lane's chunk at tap 0
   Mask mask[INSTR];     // valid taps of the row
   int coff;             // element offset of this lane's logical chunk within the K tile
+  __device__ static int swz(int row) { return BK == 64 ? (row & 7) : ((row >> 1) & 3); }
   __device__ void init(const Src& s, int row0, int lane, int wid, int /*kbeg*/) {
-    const int rr = lane >> 3, slot = lane & 7;
-    coff = (slot ^ rr) * 8;  // rows of an instruction start at a multiple of 8: r & 7 == rr
+    const int rr = lane / CPR, slot = lane % CPR;
+    coff = (slot ^ swz(rr)) * 8;  // instructions start at a multiple of RPI rows
     rsrc = dma_rsrc(s.bbase(), s.bbytes());
 #pragma unroll
     for (int j = 0; j < INSTR; ++j)  // LANE_TAP sources fold the chunk offset into toff
-      off[j] = s.brow(row0 + (j * NW + wid) * 8 + rr, mask[j]) + (Src::LANE_TAP ? 0 : coff * 2);
+      off[j] = s.brow(row0 + (j * NW + wid) * RPI + rr, mask[j]) + (Src::LANE_TAP ? 0 : coff * 2);
   }
   __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) const {
     const bool kok = k0 + coff < klim;
@@ -1173,7 +1181,7 @@ struct DmaK {
   __device__ static bf16x8 frag(const char* stage, int r16, int ks, int lane) {
     const int row = r16 + (lane & 15);
     const int c = (ks >> 3) + (lane >> 4);
-    return *(const bf16x8*)(stage + row * 128 + ((c ^ (row & 7)) << 4));
+    return *(const bf16x8*)(stage + row * (BK * 2) + ((c ^ swz(row)) << 4));
   }
 };
 
@@ -1181,14 +1189,16 @@ struct DmaK {
 // [64 k][ROWS] bf16, one ROWS*2-byte line per k; a DMA instruction fills 1 KiB = KPI whole
 // k-lines.  Chunk slots are XOR-swizzled per k so the ds_read_b64_tr_b16 fragment reads (8
 // k-lines x 32 B per 32-lane group) hit every bank once.
-template <int ROWS, class Src>
+template <int ROWS, class Src, int BK_ = 64>
 struct DmaR {
+  static constexpr int BK = BK_;
   static constexpr int NW = NT / 64;
   static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
   static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
-  static constexpr int INSTR = 64 / (KPI * NW); // DMAs per wave per stage (BK = 64)
-  static constexpr int BYTES = 64 * ROWS * 2;
+  static constexpr int INSTR = BK / (KPI * NW); // DMAs per wave per stage
+  static constexpr int BYTES = BK * ROWS * 2;
   static_assert(ROWS == 64 || ROWS == 128, "R-major DMA tile rows");
+  static_assert(BK == 64 || BK == 32, "K tile depth");
   typedef Src SrcT;
   __amdgpu_buffer_rsrc_t rsrc;
   typename Src::RowState rs[INSTR];
@@ -1234,15 +1244,17 @@ struct DmaR {
   }
 };
 
-// NS operand stages (2 or 3): with NS = 3 two K tiles are in flight while one is consumed
-// (counted vmcnt); used where the grid leaves one block per CU anyway (LDS 3 x STAGE).
+// NS operand stages (2..5) of BK = OA::BK (64 or 32): NS - 1 K tiles are in flight while one
+// is consumed (counted vmcnt).  NS = 3 at BK 64 where the grid leaves one block per CU anyway;
+// BK 32 x NS 4-5 keeps two blocks per CU with twice the bytes in flight of BK 64 x NS 2.
 // Epilogue: BatchNorm tile statistics straight from the accumulators (reg_stats), fp32
 // staging through LDS, then 8 consecutive columns per lane -> one 16-B bf16 store.
 template <int BM, int BN, class OA, class OB, class Epi, int NS = 2>
 __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                           typename OB::SrcT sb, Epi epi, int M,
                                                           int N, int K, int kper) {
-  constexpr int BK = 64, WM = 2, WN = 2;
+  constexpr int BK = OA::BK, WM = 2, WN = 2;
+  static_assert(OB::BK == BK, "operand K tile depths differ");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
@@ -1252,7 +1264,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
   // DMA instructions one wave issues per K tile (both operands)
   constexpr int PER_TILE = OA::INSTR + OB::INSTR;
-  static_assert(NS == 2 || NS == 3, "stages");
+  static_assert(NS >= 2 && NS <= 5 && PER_TILE * (NS - 2) <= 63, "stages");
   __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];  // the only LDS object
 
   const int tiles_n = (N + BN - 1) / BN;
@@ -1286,7 +1298,12 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   }
   for (int t = 0; t < nt; ++t) {
     // wait for this wave's DMAs of tile t (tiles t+1 .. t+NS-2 may stay in flight)
-    if (NS == 3 && t + 1 < nt)
+    const int ahead = min(NS - 2, nt - 1 - t);
+    if (NS >= 5 && ahead >= 3)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER_TILE) : "memory");
+    else if (NS >= 4 && ahead == 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_TILE) : "memory");
+    else if (NS >= 3 && ahead == 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
