@@ -28,3 +28,31 @@ def test_preprocess_feeds_inference_path(dev):
     assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
     ref = torch.stack([mmdx.image_transfom_into_tensor(im) for im in ims])
     assert np.array_equal(x.cpu().numpy(), ref.numpy())
+
+
+def test_local_batches_feed_gpu_transform(dev, tmp_path):
+    """mmdx.data.LocalCXRBatches: host decode + GPU transform per batch
+    == the reference transform of each decoded image, labels and details in batch order."""
+    import pandas as pd
+    from mmdx import data as D
+    ims = images()
+    keys = []
+    for i, im in enumerate(ims):
+        k = f"img{i}.png"
+        im.save(tmp_path / k)
+        keys.append(k)
+    vecs = [np.eye(13)[i % 13].tolist() for i in range(len(keys))]
+    df = pd.DataFrame(dict(image_url=keys, patient_details=[f"p{i}" for i in range(len(keys))],
+                           disease_classification_vector=vecs, report=["r"] * len(keys)))
+    df = D.enforce_raw_data_columns(df)
+    it = D.LocalCXRBatches(df, str(tmp_path), batch_size=3, shuffle=True, seed=1, device=dev)
+    order = D.LocalCXRBatches(df, str(tmp_path), batch_size=3, shuffle=True, seed=1).order()
+    seen = 0
+    for x, details, y in it:
+        idx = order[seen:seen + x.shape[0]]
+        want = torch.stack([R.reference_transform(ims[i]) for i in idx])
+        assert torch.equal(x.cpu().view(torch.int32), want.view(torch.int32))
+        assert details == [f"p{i}" for i in idx]
+        assert torch.equal(y.cpu(), torch.tensor([vecs[i] for i in idx], dtype=torch.float32))
+        seen += x.shape[0]
+    assert seen == len(ims)
