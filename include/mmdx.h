@@ -95,15 +95,19 @@ int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void*
 /* dx = dgrad + beta * dx  (beta = 1 sums the residual-path gradient in the epilogue) */
 int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
                     const void* w_crsk, void* dx, float beta, void* stream);
-/* dx = dgrad (beta 0) and, in the same epilogue, the backward statistics of the BatchNorm
- * whose output gradient dx is (its input bn_y, affine, saved mean/rstd; ReLU mask recomputed
- * from bn_y): stat_part [C][mmdx_conv_dgrad_stat_blocks()] (sum g, sum g*xhat) per 128-row
- * tile, for mmdx_bn_bwd.  stat_blocks == 0: the fusion does not apply to this conv. */
+/* dx = dgrad + beta * dx and, in the same epilogue, the backward statistics of the
+ * BatchNorm whose output gradient the final dx is (its input bn_y, affine, saved mean/rstd):
+ * stat_part [C][mmdx_conv_dgrad_stat_blocks()] (sum g, sum g*xhat) per 128-row tile, for
+ * mmdx_bn_bwd.  The ReLU mask is bn_out > 0 for a residual unit (bn_out = its output
+ * relu(bn(y) + res)), else recomputed from bn_y with the forward's scale/shift (bn_out NULL).
+ * beta != 0 (accumulating a residual branch's gradient) needs a stride-1 conv.
+ * stat_blocks == 0: the fusion does not apply to this conv. */
 int mmdx_conv_dgrad_stat_blocks(int dtype, const mmdx_conv_desc* d);
 int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const void* dy,
-                           const void* w_crsk, void* dx, const void* bn_y, const float* gamma,
-                           const float* bn_beta, const float* save_mean,
-                           const float* save_rstd, int relu, float* stat_part, void* stream);
+                           const void* w_crsk, void* dx, float beta, const void* bn_y,
+                           const void* bn_out, const float* gamma, const float* bn_beta,
+                           const float* save_mean, const float* save_rstd, int relu,
+                           float* stat_part, void* stream);
 size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc* d);
 /* dw_kcrs (fp32, master layout, Cin = c_master) = dw_kcrs*beta + grad */
 int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void* x,
@@ -156,7 +160,8 @@ int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* 
                 void* workspace, size_t ws_bytes, void* stream);
 /* stat_part (optional, [C][stat_blocks] pairs (sum g, sum g*xhat)): the reduction already
  * made by mmdx_conv_dgrad_bnstat in the epilogue that produced dy — the BN backward then
- * skips its own pass over (dy, x).  Only for relu units without residual (y == NULL). */
+ * skips its own pass over (dy, x).  ReLU units only (with y = the unit's output for a
+ * residual unit, y == NULL otherwise). */
 /* relu with y == NULL (a unit without residual): the ReLU mask is recomputed from x as
  * x*scale + shift > 0 with the forward's own scale/shift (gamma, bn_beta, save_mean,
  * save_rstd), so the post-activation tensor is not read. */

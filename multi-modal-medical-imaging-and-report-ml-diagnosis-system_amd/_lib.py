@@ -68,7 +68,8 @@ SIGNATURES = {
     "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
     "mmdx_conv_dgrad_stat_blocks": (i32, [i32, CD]),
-    "mmdx_conv_dgrad_bnstat": (i32, [i32, CD, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]),
+    "mmdx_conv_dgrad_bnstat": (i32, [i32, CD, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, i32, vp,
+                                     vp]),
     "mmdx_conv_wgrad_workspace_size": (sz, [i32, CD]),
     "mmdx_conv_wgrad": (i32, [i32, CD, i32, vp, vp, vp, f32, vp, sz, vp]),
     "mmdx_stem_pair_desc": (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, CD]),

@@ -462,19 +462,24 @@ extern "C" int mmdx_conv_dgrad_stat_blocks(int dtype, const mmdx_conv_desc* d) {
 }
 
 extern "C" int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const void* dy,
-                                      const void* w_crsk, void* dx, const void* bn_y,
-                                      const float* gamma, const float* bn_beta,
-                                      const float* save_mean, const float* save_rstd, int relu,
-                                      float* stat_part, void* stream) {
+                                      const void* w_crsk, void* dx, float beta,
+                                      const void* bn_y, const void* bn_out, const float* gamma,
+                                      const float* bn_beta, const float* save_mean,
+                                      const float* save_rstd, int relu, float* stat_part,
+                                      void* stream) {
   int rc = check_desc(d, 8);
   if (rc) return rc;
   const int tiles = mmdx_conv_dgrad_stat_blocks(dtype, d);
   MMDX_CHECK_ARG(tiles > 0, "conv dgrad bnstat: fused statistics unsupported for this conv");
+  MMDX_CHECK_ARG(beta == 0.f || (d->stride_h == 1 && d->stride_w == 1),
+                 "conv dgrad bnstat: accumulation (beta != 0) needs a stride-1 conv");
   MMDX_CHECK_ARG(bn_y && save_mean && save_rstd && stat_part, "conv dgrad bnstat: null operand");
-  MMDX_CHECK_ARG(((uintptr_t)dx & 15) == 0 && ((uintptr_t)bn_y & 15) == 0,
-                 "conv dgrad bnstat: dx / y must be 16-B aligned");
-  BnStat bs{bn_y, gamma, bn_beta, save_mean, save_rstd, (float2*)stat_part, relu, tiles, 0};
-  return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, 0.f, (hipStream_t)stream, bs);
+  MMDX_CHECK_ARG(((uintptr_t)dx & 15) == 0 && ((uintptr_t)bn_y & 15) == 0 &&
+                     ((uintptr_t)bn_out & 15) == 0,
+                 "conv dgrad bnstat: dx / y / out must be 16-B aligned");
+  BnStat bs{bn_y, gamma, bn_beta, save_mean, save_rstd, (float2*)stat_part, relu, tiles, 0,
+            bn_out};
+  return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, beta, (hipStream_t)stream, bs);
 }
 
 // ------------------------------------------------------------------------------ stem

@@ -640,6 +640,7 @@ struct RMajorLoader {
 // values used are the stored (rounded) ones, as the separate reduce would read them.
 struct BnStat {
   const void* y; const float *gamma, *beta, *mean, *rstd; float2* part; int relu, tiles, tile0;
+  const void* out;  // residual unit: its output relu(bn(y) + res), the ReLU mask source
 };
 
 struct BnCoef8 { float mu[8], rs[8], sc[8], sh[8]; };
@@ -660,15 +661,58 @@ __device__ __forceinline__ void bn_coef8(const BnStat& b, int n, int N, BnCoef8&
 typedef __attribute__((ext_vector_type(8))) __bf16 bn_y8;
 
 template <typename T>
-__device__ __forceinline__ void bn_acc8(const bn_y8& yv, f32x4 lo, f32x4 hi, const BnStat& b,
-                                        const BnCoef8& c, float* sg, float* sgx) {
+__device__ __forceinline__ void bn_acc8(const bn_y8& yv, const bn_y8& ov, f32x4 lo, f32x4 hi,
+                                        const BnStat& b, const BnCoef8& c, float* sg,
+                                        float* sgx) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float g = to_f(from_f<T>(j < 4 ? lo[j] : hi[j - 4]));
     const float y = to_f(yv[j]);
-    if (b.relu && !(y * c.sc[j] + c.sh[j] > 0.f)) g = 0.f;
+    const float a = b.out ? to_f(ov[j]) : y * c.sc[j] + c.sh[j];  // the forward's ReLU input
+    if (b.relu && !(a > 0.f)) g = 0.f;
     sg[j] += g;
     sgx[j] += g * (y - c.mu[j]) * c.rs[j];
+  }
+}
+
+// The fused-statistics epilogue stores the final values itself (alpha = 1): (lo, hi) +=
+// beta * C[m][n..n+7] first, so the statistics see the accumulated gradient of a residual
+// branch (beta = 1), then a plain store.  Epi::bn_off maps (m, n) to the element offset.
+template <class Epi>
+__device__ __forceinline__ void bst_accum8(const Epi& e, int m, int n, f32x4& lo, f32x4& hi) {
+  if constexpr (Epi::BNSTAT) {
+    if (e.beta == 0.f || m >= e.M) return;
+    const long off = e.bn_off(m, n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (n + j < e.N) lo[j] += e.beta * to_f(e.C[off + j]);
+      if (n + 4 + j < e.N) hi[j] += e.beta * to_f(e.C[off + 4 + j]);
+    }
+  }
+}
+
+template <class Epi>
+__device__ __forceinline__ void bst_store8(const Epi& e, int m, int n, f32x4 lo, f32x4 hi) {
+  if constexpr (Epi::BNSTAT) {
+    if (m >= e.M) return;
+    const long off = e.bn_off(m, n);
+    typedef typename std::remove_pointer<decltype(e.C)>::type OutT;
+    if (n + 8 > e.N) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (n + j < e.N) e.C[off + j] = from_f<OutT>(lo[j]);
+        if (n + 4 + j < e.N) e.C[off + 4 + j] = from_f<OutT>(hi[j]);
+      }
+      return;
+    }
+    typedef __attribute__((ext_vector_type(8))) OutT O8;
+    O8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = from_f<OutT>(lo[j]);
+      o[j + 4] = from_f<OutT>(hi[j]);
+    }
+    *(O8*)(e.C + off) = o;
   }
 }
 
@@ -1339,14 +1383,16 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int C8 = BN / 8, ITERS = BM * C8 / NT;
   static_assert(NT % C8 == 0 && (BM * C8) % NT == 0, "vec8 epilogue geometry");
   const bool bst = Epi::BNSTAT && epi.bs.part != nullptr && epi.vec8_ok();
-  bn_y8 yv[ITERS];
+  bn_y8 yv[ITERS], ov[ITERS];
   if (bst) {
     const int n = tn * BN + (threadIdx.x % C8) * 8;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int m = tm * BM + (threadIdx.x + it * NT) / C8;
-      yv[it] = m < M && n < N ? *(const bn_y8*)((const bf16*)epi.bs.y + epi.bn_off(m, n))
-                              : bn_y8{};
+      const bool in = m < M && n < N;
+      yv[it] = in ? *(const bn_y8*)((const bf16*)epi.bs.y + epi.bn_off(m, n)) : bn_y8{};
+      ov[it] = in && epi.bs.out ? *(const bn_y8*)((const bf16*)epi.bs.out + epi.bn_off(m, n))
+                                : bn_y8{};
     }
   }
   if constexpr (Epi::REG_STATS)
@@ -1371,11 +1417,12 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int row = (threadIdx.x + it * NT) / C8;
-      const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
-      const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
+      f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
+      f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
       const int m = tm * BM + row, n = tn * BN + col;
-      epi.apply8_fast(m, n, lo, hi);
-      if (m < M && n < N) bn_acc8<bf16>(yv[it], lo, hi, epi.bs, bc, sg, sgx);
+      bst_accum8(epi, m, n, lo, hi);
+      bst_store8(epi, m, n, lo, hi);
+      if (m < M && n < N) bn_acc8<bf16>(yv[it], ov[it], lo, hi, epi.bs, bc, sg, sgx);
     }
     bn_stat_store<BN, NT / 64>(epi.bs, sg, sgx, red, tm, tn, N);
   } else if (epi.vec8_ok()) {

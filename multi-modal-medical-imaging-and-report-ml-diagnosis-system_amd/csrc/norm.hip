@@ -447,8 +447,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
   float* coef = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
   int nblk = L.rblocks;
   if (stat_part) {  // (sum g, sum g*xhat) partials already made by the dgrad epilogue
-    MMDX_CHECK_ARG(stat_blocks > 0 && relu && !y, "bn bwd: precomputed partials need a "
-                   "ReLU unit without residual");
+    MMDX_CHECK_ARG(stat_blocks > 0 && relu, "bn bwd: precomputed partials need a ReLU unit");
     part = (float2*)stat_part;
     nblk = stat_blocks;
   } else {

@@ -77,12 +77,12 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                          (float*)P(o, 9, ext), (float*)P(o, 10, ext), o.f[0], P(o, 11, ext),
                          (size_t)o.l[1], s);
     case MMDX_OP_CONV_DGRAD_BNSTAT:
-      // i: relu; p: dy, w_crsk, dx, bn_y, gamma, beta, mean, rstd, stat_part
+      // i: relu; f: beta; p: dy, w_crsk, dx, bn_y, gamma, beta, mean, rstd, stat_part, bn_out
       return mmdx_conv_dgrad_bnstat(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
-                                    P(o, 3, ext), (const float*)P(o, 4, ext),
-                                    (const float*)P(o, 5, ext), (const float*)P(o, 6, ext),
-                                    (const float*)P(o, 7, ext), o.i[0], (float*)P(o, 8, ext),
-                                    s);
+                                    o.f[0], P(o, 3, ext), P(o, 9, ext),
+                                    (const float*)P(o, 4, ext), (const float*)P(o, 5, ext),
+                                    (const float*)P(o, 6, ext), (const float*)P(o, 7, ext),
+                                    o.i[0], (float*)P(o, 8, ext), s);
     case MMDX_OP_CONV_WGRAD:
       // i: c_master; l: ws_bytes; f: beta
       return mmdx_conv_wgrad(o.dtype, &o.d, o.i[0], P(o, 0, ext), P(o, 1, ext),

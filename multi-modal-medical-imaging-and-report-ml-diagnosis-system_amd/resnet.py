@@ -468,14 +468,18 @@ class _Plan:
                         dx, beta = dx_acc, 1.0
                     else:
                         dx, beta = A.new((d.N, d.H, d.W, d.C), T, dev), 0.0
+                    # (units with a residual are not fed: their producer is conv1's dgrad
+                    # accumulating onto the identity-path gradient; the ABI supports it
+                    # (beta 1, mask from the unit's output) but its heavier epilogue measured
+                    # 0.8 ms/step slower than the separate reduce at C4)
                     tiles = (L.lib().mmdx_conv_dgrad_stat_blocks(dt, d)
                              if feed is not None and beta == 0.0 and feed["relu"] else 0)
                     if tiles > 0:
                         fed = (A.new((d.C, tiles, 2), torch.float32, dev), tiles)
                         fb = feed["bn"]
-                        bw.timed("dgrad", L.OP_CONV_DGRAD_BNSTAT, dtype=dt, i=(1,),
+                        bw.timed("dgrad", L.OP_CONV_DGRAD_BNSTAT, dtype=dt, i=(1,), f=(0.0,),
                                  p=(dconv, u["wc"], dx, feed["y"], fb.weight, fb.bias,
-                                    feed["mean"], feed["rstd"], fed[0]), d=d)
+                                    feed["mean"], feed["rstd"], fed[0], None), d=d)
                     else:
                         bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(beta,),
                                  p=(dconv, u["wc"], dx), d=d)

@@ -333,12 +333,18 @@ def test_dropout_counter_rng_and_graph_replay(dev, dt):
     assert abs(m2.float().mean().item() - (1 - p)) < 0.005
 
 
-@pytest.mark.parametrize("cfg", [(2, 14, 14, 64, 64, 3, 1), (2, 9, 7, 64, 128, 1, 1),
-                                 (3, 15, 13, 64, 128, 3, 2), (2, 28, 28, 128, 64, 3, 2)])
-def test_dgrad_fused_bn_stats(dev, cfg):
+@pytest.mark.parametrize("cfg,mode", [
+    ((2, 14, 14, 64, 64, 3, 1), "plain"), ((2, 9, 7, 64, 128, 1, 1), "plain"),
+    ((3, 15, 13, 64, 128, 3, 2), "plain"), ((2, 28, 28, 128, 64, 3, 2), "plain"),
+    ((2, 9, 7, 64, 128, 1, 1), "residual"), ((3, 15, 13, 256, 64, 1, 1), "residual"),
+    ((2, 14, 14, 64, 64, 3, 1), "residual")])
+def test_dgrad_fused_bn_stats(dev, cfg, mode):
     """dgrad with the consumer BN's backward statistics in its epilogue, then mmdx_bn_bwd on
     those partials == dgrad, then mmdx_bn_bwd with its own reduce pass (bf16; ragged row
-    counts; stride 2 runs as output phases).  Only the summation order differs."""
+    counts; stride 2 runs as output phases).  "residual": the dgrad accumulates onto the
+    identity-path gradient (beta = 1) and the consumer is a residual unit whose ReLU mask is
+    its output `out` (the bottleneck conv1 -> previous block's conv3 case).  Only the
+    summation order differs."""
     N, H, W, C, K, k, s = cfg
     p = k // 2
     dt = torch.bfloat16
@@ -360,13 +366,17 @@ def test_dgrad_fused_bn_stats(dev, cfg):
     mean = (torch.randn(C, generator=g) * 0.1).to(dev)
     rstd = (torch.rand(C, generator=g) + 0.5).to(dev)
     rows = N * H * W
-    dx_a = torch.empty(N, H, W, C, dtype=dt, device=dev)
+    residual = mode == "residual"
+    beta = 1.0 if residual else 0.0
+    out = torch.randn(N, H, W, C, generator=g).clamp(min=0).to(dev, dt) if residual else None
+    dx0 = torch.randn(N, H, W, C, generator=g).to(dev, dt)     # identity-path gradient
+    dx_a = dx0.clone()
     part = torch.empty(C, tiles, 2, device=dev)
-    L.call("mmdx_conv_dgrad_bnstat", dc, d, dy.data_ptr(), wc.data_ptr(), dx_a.data_ptr(),
-           y.data_ptr(), gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
-           part.data_ptr(), L.stream())
-    dx_b = torch.empty_like(dx_a)
-    L.call("mmdx_conv_dgrad", dc, d, dy.data_ptr(), wc.data_ptr(), dx_b.data_ptr(), 0.0,
+    L.call("mmdx_conv_dgrad_bnstat", dc, d, dy.data_ptr(), wc.data_ptr(), dx_a.data_ptr(), beta,
+           y.data_ptr(), L.ptr(out), gam.data_ptr(), bet.data_ptr(), mean.data_ptr(),
+           rstd.data_ptr(), 1, part.data_ptr(), L.stream())
+    dx_b = dx0.clone()
+    L.call("mmdx_conv_dgrad", dc, d, dy.data_ptr(), wc.data_ptr(), dx_b.data_ptr(), beta,
            L.stream())
     torch.cuda.synchronize()
     assert torch.equal(dx_a, dx_b)
@@ -377,7 +387,7 @@ def test_dgrad_fused_bn_stats(dev, cfg):
         dcv = torch.empty_like(y)
         dg = torch.empty(C, device=dev)
         db = torch.empty(C, device=dev)
-        L.call("mmdx_bn_bwd", dc, 1, y.data_ptr(), None, dx_a.data_ptr(), rows, C,
+        L.call("mmdx_bn_bwd", dc, 1, y.data_ptr(), L.ptr(out), dx_a.data_ptr(), rows, C,
                gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
                L.ptr(sp), nb, dcv.data_ptr(), None, dg.data_ptr(), db.data_ptr(), 0.0,
                ws.data_ptr(), ws_n, L.stream())
@@ -388,6 +398,15 @@ def test_dgrad_fused_bn_stats(dev, cfg):
     assert (ba - bb).abs().max().item() <= 1e-4 * max(1.0, bb.abs().max().item())
     assert (ca - cb).abs().max().item() <= 2e-2 * max(1.0, cb.abs().max().item())
 
+
+def test_dgrad_bnstat_rejects_strided_accumulation(dev):
+    d = L.ConvDesc(2, 16, 16, 64, 64, 3, 3, 2, 2, 1, 1, 8, 8)
+    z = torch.zeros(1 << 20, dtype=torch.bfloat16, device=dev)
+    f = torch.zeros(1 << 16, device=dev)
+    with pytest.raises(RuntimeError, match="stride-1"):
+        L.call("mmdx_conv_dgrad_bnstat", 1, d, z.data_ptr(), z.data_ptr(), z.data_ptr(), 1.0,
+               z.data_ptr(), None, f.data_ptr(), f.data_ptr(), f.data_ptr(), f.data_ptr(), 1,
+               f.data_ptr(), L.stream())
 
 STEMS = [  # N, C, H, W, K, k, s, p  (C = image channels, NCHW fp32 input)
     (2, 3, 32, 32, 64, 7, 2, 3),
