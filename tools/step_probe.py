@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--text-first", action="store_true")
     ap.add_argument("--text-only", action="store_true")
+    ap.add_argument("--threads", action="store_true", help="issue the towers from two threads")
     args = ap.parse_args()
     cfg = dict(bench.CONFIGS[args.config])
     dev = torch.device("cuda", 0)
@@ -33,6 +34,8 @@ def main():
     params = [p for grp in opt.param_groups for p in grp["params"]]
     x, ids, mask, y = bench.synth(cfg, cfg["batch"], dev, 1234)
     side = torch.cuda.Stream(device=dev)
+    from mmdx.schedule import TwoTowerForward
+    towers = TwoTowerForward(text_stream=side)
     marks = []
 
     def mark(name, st=None):
@@ -46,13 +49,21 @@ def main():
         main = torch.cuda.current_stream()
         mark("start", main)
         side.wait_stream(main)
-        if args.text_first:
+        if args.threads:
+            def text_fn():
+                z = txt(input_ids=ids, attention_mask=mask)["embeddings"]
+                mark("txt_fwd_done", side)
+                return z
+            z_img, z_txt = towers(lambda: img(x)["embeddings"], text_fn)
+            mark("img_fwd_issued", main)
+        elif args.text_first:
             with torch.cuda.stream(side):
                 z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
                 mark("txt_fwd_done", side)
-        z_img = img(x)["embeddings"]
-        mark("img_fwd_issued", main)
-        if not args.text_first:
+        if not args.threads:
+            z_img = img(x)["embeddings"]
+            mark("img_fwd_issued", main)
+        if not args.text_first and not args.threads:
             with torch.cuda.stream(side):
                 z_txt = txt(input_ids=ids, attention_mask=mask)["embeddings"]
                 mark("txt_fwd_done", side)
