@@ -180,6 +180,26 @@ static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32) {
   return !dgrad || (g.sh == 1 && g.sw == 1);
 }
 
+// Forward-conv epilogue without the fused consumer-BN statistics (the forward never uses
+// them): the kernel then holds no BN-input registers beside a 256-row tile's accumulators.
+template <typename T>
+struct EpiStoreFwd : EpiStore<T> {
+  static constexpr bool BNSTAT = false;
+};
+
+// 256x128 tiles (2x2 waves of 128x64, one block per CU, three operand stages): a quarter
+// fewer DMA pieces and LDS fill bytes per MFMA than 128x128, where the grid still gives
+// every CU at least two tiles.  Opt-in (MMDX_CONV_TILE=256): at one block per CU the 1x1
+// convs it reaches ran 1.3-1.5x slower than 128x128 at two blocks per CU (the epilogue of
+// one block no longer overlaps the other's K loop), C4 7550 vs 7815 samples/s.
+static bool use_tile256(long M, int N) {
+  static const int mode = [] {
+    const char* e = getenv("MMDX_CONV_TILE");
+    return e && atoi(e) == 256 ? 1 : 0;
+  }();
+  return mode && N % 128 == 0 && ((M + 255) / 256) * (long)(N / 128) >= 512;
+}
+
 template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
                      hipStream_t st, float* stats = nullptr, bool dma_ok = false,
@@ -190,6 +210,17 @@ static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K
   epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
   if constexpr (DmaOk<SA>::value) {
     if (dma_ok) {
+    if constexpr (std::is_same<SA, Im2colK<bf16, true>>::value) {
+      if (bs.part == nullptr && beta == 0.f && use_tile256(M, N)) {
+        EpiStoreFwd<T> ef;
+        static_cast<EpiStore<T>&>(ef) = epi;
+        const int nwg = ((M + 255) / 256) * (N / 128);
+        launch_dma_ns<256, 128, DmaK<256, SA>, DmaK<128, DenseK<T>>, EpiStoreFwd<T>, 3>(
+            sa, sb, ef, M, N, K, 1, K, nwg, st);
+        MMDX_LAUNCH_CHECK();
+        return 0;
+      }
+    }
     // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
     const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
     if (N <= 64 || tiles128 < 384) return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
@@ -290,8 +321,13 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   p.bn = N <= 64 ? 64 : 128;
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
   const long ktiles = (K + BK - 1) / BK;
-  // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small)
-  long s = (512 + tiles - 1) / tiles;
+  // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small);
+  // MMDX_WGRAD_BLOCKS overrides the target block count (A/B runs)
+  static const long target = [] {
+    const char* e = getenv("MMDX_WGRAD_BLOCKS");
+    return e && atol(e) > 0 ? atol(e) : 512L;
+  }();
+  long s = (target + tiles - 1) / tiles;
   s = std::max(1L, std::min(s, ktiles / 16));
   const long kt_per = (ktiles + s - 1) / s;
   p.kper = (int)(kt_per * BK);

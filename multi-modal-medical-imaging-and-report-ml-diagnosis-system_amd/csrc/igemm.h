@@ -891,11 +891,20 @@ struct EpiStore {
         mm += mm_b + d * d * n_a * f;
         n_a = tot;
       }
+      if constexpr (WTM == 128 && BM > 128) {
+        // a wave row spans exactly one 128-row slab (the layout every consumer expects):
+        // it is stored as is, no merge across wave rows
+        const int slab = tm * WM + wm, n = tn * BN + wn * WTN + j * 16 + lane;
+        if (lane < 16 && n_a > 0.f && n < N)
+          stats[(long)n * ((M + 127) / 128) + slab] = make_float2(mu, mm);
+        continue;
+      }
       if (lane < 16) {
         float* o = red + (wm * BN + wn * WTN + j * 16 + lane) * 3;
         o[0] = n_a; o[1] = mu; o[2] = mm;
       }
     }
+    if constexpr (WTM == 128 && BM > 128) return;
     __syncthreads();
     const int col = threadIdx.x;
     if (col < BN && tn * BN + col < N) {

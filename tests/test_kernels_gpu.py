@@ -136,6 +136,47 @@ def test_conv_fwd_dgrad_wgrad(dev, dt, cfg):
     _close(dw, wr.grad, dt, f"wgrad {cfg}")
 
 
+@pytest.mark.parametrize("cfg", [(21, 64, 56, 56, 256, 3, 1, 1), (11, 256, 56, 56, 512, 1, 1, 0)])
+def test_conv_fwd_tile256(dev, cfg):
+    """bf16 forward on grids large enough for the 256x128 tile (>= 512 tiles), M ragged
+    (M mod 256 = 64 / 128: the last tile's second 128-row slab is empty / partial), with
+    the per-128-row BN statistics the two wave rows store directly."""
+    N, C, H, W, K, k, s, p = cfg
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(K, C, k, k, generator=g) * 0.05).bfloat16().float()
+    yr = tF.conv2d(x, w, stride=s, padding=p)
+    P, Q = yr.shape[2], yr.shape[3]
+    M = N * P * Q
+    assert ((M + 255) // 256) * (K // 128) >= 512
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q)
+    wk = torch.empty(K, k, k, C, dtype=torch.bfloat16, device=dev)
+    wc = torch.empty(C, k, k, K, dtype=torch.bfloat16, device=dev)
+    L.call("mmdx_conv_pack_weight", 1, d, C, w.to(dev).data_ptr(), wk.data_ptr(),
+           wc.data_ptr(), L.stream())
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    y = torch.empty(N, P, Q, K, dtype=torch.bfloat16, device=dev)
+    nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
+    assert nst == (M + 127) // 128
+    part = torch.full((K, nst, 2), float("nan"), device=dev)
+    L.call("mmdx_conv_fwd", 1, d, xd.data_ptr(), wk.data_ptr(), y.data_ptr(), part.data_ptr(),
+           L.stream())
+    _close(y.permute(0, 3, 1, 2), yr, torch.bfloat16, f"fwd {cfg}")
+    assert torch.isfinite(part).all(), "a 128-row statistics slab was not written"
+    cnt = torch.tensor([min(128, M - 128 * b) for b in range(nst)], dtype=torch.float64)
+    pm, p2 = part[..., 0].t().double().cpu(), part[..., 1].t().double().cpu()
+    mean = (pm * cnt[:, None]).sum(0) / M
+    m2 = (p2 + cnt[:, None] * (pm - mean) ** 2).sum(0)
+    yref = yr.double()
+    _close(mean, yref.mean((0, 2, 3)), torch.bfloat16, "stat mean")
+    _close(m2 / M, yref.var((0, 2, 3), unbiased=False), torch.bfloat16, "stat var")
+    # per-slab check of the last two slabs (the ragged tile)
+    yt = yr.permute(0, 2, 3, 1).reshape(M, K).double()
+    for b in (nst - 2, nst - 1):
+        rows = yt[128 * b:min(M, 128 * b + 128)]
+        _close(pm[b], rows.mean(0), torch.bfloat16, f"slab {b} mean")
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("train", [1, 0])
 @pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
