@@ -368,6 +368,13 @@ def main():
     side = torch.cuda.Stream(device=dev, priority=-1 if prio in ("text", "main+text") else 0)
     from mmdx.dist import GradAllReducer
     reducer = GradAllReducer(params, world) if world > 1 else None
+    early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "1" if backend == "nccl" else "0")
+    if reducer is not None and early_tail != "0":
+        # the trunk's last-layer gradients start their all-reduce mid-backward (RCCL: the
+        # collective's stream waits on the plan's event, no host wait; gloo's CUDA path
+        # stalls the issuing host thread on it — 1.3 s/step in the one-GPU rehearsal — so
+        # the gloo rehearsal keeps it off unless asked for)
+        RN.TRUNK_GRAD_HOOK = lambda g, lo, ev: reducer.launch_region(g, lo, g.numel(), ev)
     step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
     timer = StepTimer()
     if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders

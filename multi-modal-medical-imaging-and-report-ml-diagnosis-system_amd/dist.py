@@ -42,6 +42,28 @@ class GradAllReducer:
         self.group = group
         self._pending = []
         self._launched = set()
+        self._regions = {}   # id(flat buffer) -> (lo, hi) already launched by launch_region
+        self._comm = None
+
+    def launch_region(self, buf, lo: int, hi: int, event=None):
+        """Start the all-reduce of the slice buf[lo:hi] of a flat gradient buffer once
+        `event` (a torch.cuda.Event recorded after the slice is final) has fired; the rest of
+        the buffer is reduced by the next launch().  Used for the ResNet trunk's last layer
+        (resnet.TRUNK_GRAD_HOOK): its ~60 % of the trunk's gradient bytes move over xGMI
+        while the earlier layers' backward still runs."""
+        if self.world == 1 or hi <= lo:
+            return
+        view = buf[lo:hi]
+        if event is not None and buf.is_cuda:
+            if self._comm is None:
+                self._comm = torch.cuda.Stream(device=buf.device)
+            with torch.cuda.stream(self._comm):
+                self._comm.wait_event(event)
+                work = dist.all_reduce(view, group=self.group, async_op=True)
+        else:
+            work = dist.all_reduce(view, group=self.group, async_op=True)
+        self._pending.append((None, view, work))
+        self._regions[id(buf)] = (lo, hi)
 
     def _buckets(self, grads):
         plan, cur, size = [], [], 0
@@ -76,8 +98,12 @@ class GradAllReducer:
         loose = []
         for b, gs in by_base.values():
             if sum(g.numel() for g in gs) == b.numel():
-                work = dist.all_reduce(b, group=self.group, async_op=True)
-                self._pending.append((None, b, work))
+                lo, hi = self._regions.get(id(b), (b.numel(), b.numel()))
+                for a, z in ((0, lo), (hi, b.numel())):  # what launch_region left
+                    if z > a:
+                        part = b[a:z]
+                        work = dist.all_reduce(part, group=self.group, async_op=True)
+                        self._pending.append((None, part, work))
             else:
                 loose += gs
         loose += [g for g in grads if g._base is None or not g._base.is_contiguous()]
@@ -96,6 +122,7 @@ class GradAllReducer:
                     g.copy_(s)
         self._pending = []
         self._launched = set()
+        self._regions = {}
 
     def reduce(self):
         """All-reduce (mean) every existing .grad across ranks, in place."""

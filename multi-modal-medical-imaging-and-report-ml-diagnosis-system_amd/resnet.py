@@ -409,6 +409,7 @@ class _Plan:
         # the CUs the chain's smaller launches leave idle.  The main stream joins the side
         # stream once at the end, before the optimizer reads the gradients.
         self.bwd = None
+        self.tail_event = None
         if keep:
             bw = _OpList()
             params = trunk.engine_params()
@@ -488,7 +489,18 @@ class _Plan:
             N_, H_, W_, C_ = self.out_geom
             dx = A.new((N_, H_, W_, C_), T, dev)
             bw.add(L.OP_AVGPOOL_BWD, dt, i=(N_, H_ * W_, C_), p=(_Ext(0), dx))
-            for bu, ds_u, _shape in reversed(blocks):
+            # the last layer's gradients (the arena's tail: engine_params is in forward
+            # order) are final once the side stream has run that layer's weight gradients
+            # (each waits for its unit's BN backward): the plan signals tail_event there, so
+            # a data-parallel all-reduce of the tail can run beside the rest of the backward
+            n_last = len(list(trunk)[7])
+            last_ids = {id(q) for q in trunk[7].parameters()}
+            self.grad_tail = min(o for i, o in self.grad_off.items() if i in last_ids) // 4
+            self.tail_event = None
+            for bi, (bu, ds_u, _shape) in enumerate(reversed(blocks)):
+                if bi == n_last:
+                    bw.add(L.OP_SIGNAL, p=(A.event(),), stream=1)
+                    self.tail_event = A.bufs[-1]
                 # unit i's dgrad produces the gradient of unit i-1's output (no residual
                 # inside a block): it also makes unit i-1's BN-backward partials
                 dh, dres, fed = unit_bwd(bu[-1], dx, True, want_res=True,
@@ -525,6 +537,12 @@ class _Plan:
         if self.bwd is not None:
             self.bwd.freeze()
 
+
+# TRUNK_GRAD_HOOK(grads, tail_lo, event): called right after the trunk backward is enqueued
+# with the flat fp32 gradient arena, the element offset where the last layer's gradients
+# start and the event after which grads[tail_lo:] are final (data parallelism: start their
+# all-reduce early, dist.GradAllReducer.launch_region).  None = no hook.
+TRUNK_GRAD_HOOK = None
 
 # placeholder operands for the plan's per-stream workspaces, patched once sizes are known
 _WS_TOKEN, _WS2_TOKEN = 0x1, 0x2
@@ -602,6 +620,9 @@ class _TrunkFn(torch.autograd.Function):
         x0 = ctx.x.data_ptr() if isinstance(plan.x0, _Ext) else plan.x0.data_ptr()
         side = _side_stream(ctx.trunk_ref, dev)
         plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0], [stream(), side.cuda_stream])
+        hook = TRUNK_GRAD_HOOK
+        if hook is not None and plan.tail_event is not None:
+            hook(grads, plan.grad_tail, plan.tail_event)
         plan.arena.owner = None
         ctx.plan = ctx.x = ctx.tok = ctx.trunk_ref = None
         out = [None, None, None]

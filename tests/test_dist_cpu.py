@@ -2,6 +2,7 @@
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -52,7 +53,7 @@ def test_grad_allreduce_mean_gloo():
 SHAPES2 = ((40, 3), (7,), (16,), (5, 5))
 
 
-def _worker_flat(rank, world, port, out):
+def _worker_flat(rank, world, port, out, region=False):
     """Gradients that are views of one flat buffer (the trunk's gradient arena) are reduced
     in place; the others through buckets; a subset is launched early (overlap path)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -67,6 +68,8 @@ def _worker_flat(rank, world, port, out):
     params[2].grad = torch.randn(16, generator=g)
     params[3].grad = torch.randn(5, 5, generator=g)
     red = GradAllReducer(params, world, bucket_bytes=64)
+    if region:  # the buffer's tail first (the trunk's last layer, resnet.TRUNK_GRAD_HOOK)
+        red.launch_region(flat, 100, flat.numel())
     red.launch([params[2]])
     red.reduce()
     assert params[0].grad._base is flat  # reduced in place, still the same buffer
@@ -74,12 +77,13 @@ def _worker_flat(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_grad_allreduce_flat_base_and_early_launch_gloo():
+@pytest.mark.parametrize("region", [False, True])
+def test_grad_allreduce_flat_base_and_early_launch_gloo(region):
     world = 2
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker_flat, args=(world, port, out), nprocs=world, join=True)
+    mp.spawn(_worker_flat, args=(world, port, out, region), nprocs=world, join=True)
     exp = []
     for r in range(world):
         g = torch.Generator().manual_seed(200 + r)

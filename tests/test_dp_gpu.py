@@ -45,24 +45,36 @@ def _grads(img, txt, fus, x, ids, mask, y):
     return [(n, p) for mod in (img, txt, fus) for n, p in mod.named_parameters()]
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, early):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     sys.path.insert(0, HERE)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx import resnet as RN
     from mmdx.dist import GradAllReducer, shard_batch
     from parity_util import synth_batch
     x, ids, mask, y = synth_batch(4, 16, hw=64)
     a, b = shard_batch(4, rank, world)
     img, txt, fus = _model()
+    red = GradAllReducer([p for mod in (img, txt, fus) for p in mod.parameters()], world)
+    tails = []
+    if early:  # the trunk's last layer reduced from the plan's mid-backward event
+        def hook(g, lo, ev):
+            tails.append((lo, g.numel()))
+            red.launch_region(g, lo, g.numel(), ev)
+        RN.TRUNK_GRAD_HOOK = hook
     named = _grads(img, txt, fus, x[a:b], ids[a:b], mask[a:b], y[a:b])
-    GradAllReducer([p for _, p in named], world).reduce()
+    red.reduce()
+    RN.TRUNK_GRAD_HOOK = None
+    if early:
+        assert len(tails) == 1 and 0 < tails[0][0] < tails[0][1], tails
     torch.cuda.synchronize()
     out[rank] = {n: p.grad.detach().cpu() for n, p in named if p.grad is not None}
     dist.destroy_process_group()
 
 
-def test_dp_two_ranks_match_full_batch(dev):
+@pytest.mark.parametrize("early", [False, True])
+def test_dp_two_ranks_match_full_batch(dev, early):
     from parity_util import cosine, synth_batch
     x, ids, mask, y = synth_batch(4, 16, hw=64)
     img, txt, fus = _model()
@@ -72,7 +84,7 @@ def test_dp_two_ranks_match_full_batch(dev):
     mgr = ctx.Manager()
     out = mgr.dict()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, out, early)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
