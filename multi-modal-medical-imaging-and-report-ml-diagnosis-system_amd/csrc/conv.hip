@@ -120,6 +120,92 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, in
   }
 }
 
+// The same reduction with the splits themselves spread over Z thread groups of the block
+// (Z = 1..16 by split count): a thread sums only ~splits/Z float4 partials with four
+// independent accumulators, the Z group sums meet in LDS in a fixed order (deterministic).
+// The one-thread-per-element loop above is latency-bound at high split counts (the layer1/2
+// weight gradients split 50-256 ways: 20-54 us per launch at 0.5 TB/s).  slab % 4 == 0.
+template <int Z>
+__global__ __launch_bounds__(256) void wgrad_reduce_z_kernel(const float* __restrict__ ws,
+                                                             int splits, int K, int C, int Cm,
+                                                             int RS, float* __restrict__ dw,
+                                                             float beta) {
+  constexpr int E = 256 / Z;  // float4 columns per block
+  __shared__ f32x4 red[256];
+  const long n4 = (long)K * RS * C / 4;
+  const int e = threadIdx.x % E, zg = threadIdx.x / E;
+  const int per = (splits + Z - 1) / Z;
+  const int z0 = min(splits, zg * per), z1 = min(splits, z0 + per);
+  const f32x4* w4 = (const f32x4*)ws;
+  for (long base = (long)blockIdx.x * E; base < n4; base += (long)gridDim.x * E) {
+    const long i4 = base + e;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    if (i4 < n4) {
+      int z = z0;
+      for (; z + 4 <= z1; z += 4) {
+        a0 += w4[(long)z * n4 + i4];
+        a1 += w4[(long)(z + 1) * n4 + i4];
+        a2 += w4[(long)(z + 2) * n4 + i4];
+        a3 += w4[(long)(z + 3) * n4 + i4];
+      }
+      for (; z < z1; ++z) a0 += w4[(long)z * n4 + i4];
+    }
+    red[threadIdx.x] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (zg == 0 && i4 < n4) {
+      f32x4 v = red[e];
+#pragma unroll
+      for (int q = 1; q < Z; ++q) v += red[q * E + e];
+      const long i = i4 * 4;
+      const int c = (int)(i % C);
+      const long t = i / C;
+      const int rs = (int)(t % RS), k = (int)(t / RS);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (c + j >= Cm) break;
+        const long o = ((long)k * Cm + c + j) * RS + rs;
+        dw[o] = beta != 0.f ? beta * dw[o] + v[j] : v[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static void wgrad_reduce(const float* ws, int splits, int K, int C, int Cm, int RS, float* dw,
+                         float beta, hipStream_t st) {
+  const long total = (long)K * C * RS;
+  // split groups only for the deep splits (>= 128: the stem's and layer1's weight gradients,
+  // at the end of the backward where little else runs); elsewhere the per-element loop, whose
+  // lower memory-level parallelism disturbs the concurrent dgrad/BN chain less (all-split:
+  // 0.6 % slower train step despite 2 % less isolated wgrad time).  MMDX_WGRAD_REDUCE=
+  // element | split forces one kernel (A/B runs).
+  static const int mode = [] {
+    const char* e = getenv("MMDX_WGRAD_REDUCE");
+    return !e ? 0 : e[0] == 'e' ? 1 : e[0] == 's' ? 2 : 0;
+  }();
+  const bool per_element = mode == 1 || (mode == 0 && splits < 128);
+  if (total % 4 != 0 || per_element) {
+    const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C,
+                       Cm, RS, dw, beta);
+    return;
+  }
+  const int Z = splits < 4 ? 1 : splits < 8 ? 2 : splits < 16 ? 4 : splits < 32 ? 8 : 16;
+  const long cols = total / 4;
+  const int blocks = (int)std::min<long>((cols + 256 / Z - 1) / (256 / Z), 8192);
+#define MMDX_WRZ(z)                                                                          \
+  hipLaunchKernelGGL(wgrad_reduce_z_kernel<z>, dim3(blocks), dim3(256), 0, st, ws, splits, K, \
+                     C, Cm, RS, dw, beta)
+  switch (Z) {
+    case 1: MMDX_WRZ(1); break;
+    case 2: MMDX_WRZ(2); break;
+    case 4: MMDX_WRZ(4); break;
+    case 8: MMDX_WRZ(8); break;
+    default: MMDX_WRZ(16); break;
+  }
+#undef MMDX_WRZ
+}
+
 template <typename T, int BM, int BN, class LA, class LB, class Epi>
 static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, const Epi& epi,
                   int M, int N, int K, int splits, int kper, hipStream_t st) {
@@ -371,10 +457,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
       rc = launch_dma_ops<64, 64, DmaR<64, DenseR<T>>, DmaR<64, Im2colR<T>>>(
           sa, sb, epi, M, N, K, p.splits, p.kper, st);
     if (rc) return rc;
-    const long total = (long)g.K * g.C * g.R * g.S;
-    const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
-                       p.splits, g.K, g.C, cm, g.R * g.S, dw, beta);
+    wgrad_reduce((const float*)ws, p.splits, g.K, g.C, cm, g.R * g.S, dw, beta, st);
     MMDX_LAUNCH_CHECK();
     return 0;
    }
@@ -392,10 +475,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   else
     rc = launch<T, 64, 64, A64, B64>(sa, sb, epi, M, N, K, p.splits, p.kper, st);
   if (rc) return rc;
-  const long total = (long)g.K * g.C * g.R * g.S;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
-                     p.splits, g.K, g.C, cm, g.R * g.S, dw, beta);
+  wgrad_reduce((const float*)ws, p.splits, g.K, g.C, cm, g.R * g.S, dw, beta, st);
   MMDX_LAUNCH_CHECK();
   return 0;
 }

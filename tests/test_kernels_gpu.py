@@ -175,6 +175,40 @@ def test_conv_fwd_tile256(dev, cfg):
     for b in (nst - 2, nst - 1):
         rows = yt[128 * b:min(M, 128 * b + 128)]
         _close(pm[b], rows.mean(0), torch.bfloat16, f"slab {b} mean")
+    _wgrad_check(dev, x, w, yr, g, d, cfg)
+
+
+@pytest.mark.parametrize("cfg", [(48, 64, 56, 56, 64, 1, 1, 0), (48, 64, 56, 56, 128, 1, 1, 0)])
+def test_conv_wgrad_deep_split(dev, cfg):
+    """Weight gradients split >= 128 ways over K = N*P*Q (the stem / layer1 regime): the
+    partials go through the split-group reduction (wgrad_reduce_z_kernel, Z = 16)."""
+    N, C, H, W, K, k, s, p = cfg
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(K, C, k, k, generator=g) * 0.05).bfloat16().float()
+    yr = tF.conv2d(x, w, stride=s, padding=p)
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, yr.shape[2], yr.shape[3])
+    ws_n = L.lib().mmdx_conv_wgrad_workspace_size(1, d)
+    assert ws_n >= 128 * K * C * k * k * 4, "expected >= 128 splits"
+    _wgrad_check(dev, x, w, yr, g, d, cfg)
+
+
+def _wgrad_check(dev, x, w, yr, g, d, cfg):
+    """bf16 weight gradient vs torch fp32 on the bf16-rounded operands, beta 1 then 0."""
+    N, C, H, W, K, k, s, p = cfg
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    dwr = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=s, padding=p)
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    ws_n = L.lib().mmdx_conv_wgrad_workspace_size(1, d)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    dw = torch.full((K, C, k, k), 0.5, device=dev)
+    L.call("mmdx_conv_wgrad", 1, d, C, xd.data_ptr(), dyd.data_ptr(), dw.data_ptr(), 1.0,
+           ws.data_ptr(), ws_n, L.stream())
+    _close(dw - 0.5, dwr, torch.bfloat16, "wgrad beta 1")
+    L.call("mmdx_conv_wgrad", 1, d, C, xd.data_ptr(), dyd.data_ptr(), dw.data_ptr(), 0.0,
+           ws.data_ptr(), ws_n, L.stream())
+    _close(dw, dwr, torch.bfloat16, "wgrad")
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
