@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import weakref
 
 import torch
@@ -543,6 +544,7 @@ class _Plan:
 # start and the event after which grads[tail_lo:] are final (data parallelism: start their
 # all-reduce early, dist.GradAllReducer.launch_region).  None = no hook.
 TRUNK_GRAD_HOOK = None
+_WGRAD_ON_MAIN = os.environ.get("MMDX_WGRAD_STREAM", "side") == "main"
 
 # placeholder operands for the plan's per-stream workspaces, patched once sizes are known
 _WS_TOKEN, _WS2_TOKEN = 0x1, 0x2
@@ -618,7 +620,9 @@ class _TrunkFn(torch.autograd.Function):
         dev = dfeats.device
         grads = torch.empty(plan.grad_bytes // 4, dtype=torch.float32, device=dev)
         x0 = ctx.x.data_ptr() if isinstance(plan.x0, _Ext) else plan.x0.data_ptr()
-        side = _side_stream(ctx.trunk_ref, dev)
+        # MMDX_WGRAD_STREAM=main: weight gradients in order on the main stream (A/B runs)
+        side = (torch.cuda.current_stream() if _WGRAD_ON_MAIN
+                else _side_stream(ctx.trunk_ref, dev))
         plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0], [stream(), side.cuda_stream])
         hook = TRUNK_GRAD_HOOK
         if hook is not None and plan.tail_event is not None:
