@@ -252,7 +252,7 @@ class StepTimer:
         return _Ctx()
 
 
-def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
+def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd=None):
     import mmdx
     from mmdx import optim as MO
     from mmdx.schedule import TwoTowerForward, two_tower_backward
@@ -276,7 +276,8 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side):
         early = None
         if reducer is not None:
             early = lambda: reducer.launch(list(txt.parameters()) + list(fus.parameters()))
-        two_tower_backward(loss, z_img, z_txt, fus.parameters(), text_stream=side,
+        two_tower_backward(loss, z_img, z_txt, fus.parameters(),
+                           text_stream=side if side_bwd is None else side_bwd,
                            on_text_done=early)
         if reducer is not None:
             reducer.reduce()
@@ -375,7 +376,11 @@ def main():
         # stalls the issuing host thread on it — 1.3 s/step in the one-GPU rehearsal — so
         # the gloo rehearsal keeps it off unless asked for)
         RN.TRUNK_GRAD_HOOK = lambda g, lo, ev: reducer.launch_region(g, lo, g.numel(), ev)
-    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
+    # the text tower's backward may run on its own stream at default priority
+    # (MMDX_TEXT_BWD_PRIO=low): it is off the critical path, the image backward is not
+    side_bwd = (torch.cuda.Stream(device=dev, priority=0)
+                if os.environ.get("MMDX_TEXT_BWD_PRIO", "high") == "low" else None)
+    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd)
     timer = StepTimer()
     if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders
         MF.GEMM_TIMER = timer

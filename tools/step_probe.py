@@ -33,7 +33,11 @@ def main():
     img, txt, fus, opt = bench.build(cfg, dev, torch.bfloat16)
     params = [p for grp in opt.param_groups for p in grp["params"]]
     x, ids, mask, y = bench.synth(cfg, cfg["batch"], dev, 1234)
-    side = torch.cuda.Stream(device=dev)
+    # the bench's stream priorities (MMDX_PRIO, default main+text)
+    prio = os.environ.get("MMDX_PRIO", "main+text")
+    if prio in ("main", "main+text"):
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
+    side = torch.cuda.Stream(device=dev, priority=-1 if prio in ("text", "main+text") else 0)
     from mmdx.schedule import TwoTowerForward
     towers = TwoTowerForward(text_stream=side)
     marks = []
