@@ -54,15 +54,21 @@ class GradAllReducer:
         if self.world == 1 or hi <= lo:
             return
         view = buf[lo:hi]
+        # reduced in a private copy, written back by finish() on the caller's stream: nothing
+        # else ever sees the slice half-reduced (the backward is still running when this is
+        # issued), and a backend's in-place write into a view never races a reader
         if event is not None and buf.is_cuda:
             if self._comm is None:
                 self._comm = torch.cuda.Stream(device=buf.device)
             with torch.cuda.stream(self._comm):
                 self._comm.wait_event(event)
-                work = dist.all_reduce(view, group=self.group, async_op=True)
+                tmp = view.clone()
+                work = dist.all_reduce(tmp, group=self.group, async_op=True)
+            tmp.record_stream(torch.cuda.current_stream(buf.device))
         else:
-            work = dist.all_reduce(view, group=self.group, async_op=True)
-        self._pending.append((None, view, work))
+            tmp = view.clone()
+            work = dist.all_reduce(tmp, group=self.group, async_op=True)
+        self._pending.append((None, tmp, work, view))
         self._regions[id(buf)] = (lo, hi)
 
     def _buckets(self, grads):
@@ -103,20 +109,22 @@ class GradAllReducer:
                     if z > a:
                         part = b[a:z]
                         work = dist.all_reduce(part, group=self.group, async_op=True)
-                        self._pending.append((None, part, work))
+                        self._pending.append((None, part, work, None))
             else:
                 loose += gs
         loose += [g for g in grads if g._base is None or not g._base.is_contiguous()]
         for bucket in self._buckets(loose):
             flat = torch._utils._flatten_dense_tensors(bucket)
             work = dist.all_reduce(flat, group=self.group, async_op=True)
-            self._pending.append((bucket, flat, work))
+            self._pending.append((bucket, flat, work, None))
 
     def finish(self):
         inv = 1.0 / self.world
-        for bucket, flat, work in self._pending:
+        for bucket, flat, work, dest in self._pending:
             work.wait()
             flat.mul_(inv)
+            if dest is not None:
+                dest.copy_(flat)
             if bucket is not None:
                 for g, s in zip(bucket, torch._utils._unflatten_dense_tensors(flat, bucket)):
                     g.copy_(s)
