@@ -127,6 +127,27 @@ def load_traffic(cfg_name, batch):
     return best
 
 
+def load_mfma_util(cfg_name):
+    """Per-family MFMA utilisation from the newest committed PMC pass (tools/pmc_mfma.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), dispatches serialised by
+    the profiler) for the C4 workload, or None."""
+    import glob
+    if cfg_name != "c4":
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    pct = {k: round(100 * v["mfma_util"], 1) for k, v in t.items()
+           if isinstance(v, dict) and v.get("mfma_util") is not None
+           and k in ("conv_fwd", "conv_dgrad", "conv_wgrad", "conv_all", "gemm")}
+    return {"pct": pct, "source": os.path.relpath(files[-1], ROOT)}
+
+
 def vit_flops_per_sample(layers=12, S=197, D=768, I=3072, patches=196, kpatch=768):
     """ViT-B/16 forward FLOPs of one 224x224 image (2 per MAC): patch embedding GEMM, per
     layer the QKV/out/MLP GEMMs and the two attention contractions (QK^T, PV)."""
@@ -496,6 +517,7 @@ def main():
         "model_tflops": round(total_flops * samples / el / 1e12, 2),
         "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
                                           (PEAK_BF16_TFLOPS * world), 2),
+        "mfma_util_pmc": load_mfma_util(args.config),
         "roofline": {
             "kernel": ("igemm_dma_kernel (dense GEMMs of the ViT-B/16 and BERT-base encoders, "
                        "fwd + both backward GEMMs)") if vit else
