@@ -220,7 +220,12 @@ static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, cons
 // stage costs occupancy only where there would be a second block to lose) and the K loop
 // is long enough to keep two tiles in flight.
 static bool use_three_stages(long blocks, int ktiles_per_block) {
-  return blocks <= 256 && ktiles_per_block >= 4;
+  // MMDX_NS3_BLOCKS overrides the grid limit (A/B runs; C4 step: 0 and 256 tie, 512 -3.5 %)
+  static const long limit = [] {
+    const char* e = getenv("MMDX_NS3_BLOCKS");
+    return e ? atol(e) : 256L;
+  }();
+  return blocks <= limit && ktiles_per_block >= 4;
 }
 
 template <int BM, int BN, class OA, class OB, class Epi, int NS>
@@ -266,6 +271,16 @@ static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32) {
   return !dgrad || (g.sh == 1 && g.sw == 1);
 }
 
+// 128x64 tiles when 128x128 would give fewer tiles than this (< 1.5 per CU); MMDX_TILE64_BELOW
+// overrides (A/B runs; in the C4 step 256 and 384 tie, 640 is 1.5 % slower)
+static long narrow_below() {
+  static const long v = [] {
+    const char* e = getenv("MMDX_TILE64_BELOW");
+    return e && atol(e) > 0 ? atol(e) : 384L;
+  }();
+  return v;
+}
+
 // Forward-conv epilogue without the fused consumer-BN statistics (the forward never uses
 // them): the kernel then holds no BN-input registers beside a 256-row tile's accumulators.
 template <typename T>
@@ -309,7 +324,7 @@ static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K
     }
     // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
     const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-    if (N <= 64 || tiles128 < 384) return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
+    if (N <= 64 || tiles128 < narrow_below()) return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
     return launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
     }
   }
@@ -363,7 +378,7 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       if constexpr (sizeof(T) == 2) {
         if (dma_geom_ok(g, false)) {
           const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-          if (N <= 64 || tiles128 < 384)
+          if (N <= 64 || tiles128 < narrow_below())
             rc = launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
           else
             rc = launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
