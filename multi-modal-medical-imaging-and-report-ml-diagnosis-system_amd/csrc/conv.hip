@@ -431,8 +431,13 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
     return e && atol(e) > 0 ? atol(e) : 0L;
   }();
   const long target = forced ? forced : 512L;
+  // MMDX_WGRAD_MINK: least K tiles per split (A/B runs; C4 step: 8, 16, 32 within noise)
+  static const long min_kt = [] {
+    const char* e = getenv("MMDX_WGRAD_MINK");
+    return e && atol(e) > 0 ? atol(e) : 16L;
+  }();
   long s = (target + tiles - 1) / tiles;
-  s = std::max(1L, std::min(s, ktiles / 16));
+  s = std::max(1L, std::min(s, ktiles / min_kt));
   const long kt_per = (ktiles + s - 1) / s;
   p.kper = (int)(kt_per * BK);
   p.splits = (int)((K + p.kper - 1) / p.kper);

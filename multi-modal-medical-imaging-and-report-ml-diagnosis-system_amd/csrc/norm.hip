@@ -377,6 +377,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// slab count above which a whole block (not one wave) reduces a channel's partials;
+// MMDX_FIN_WIDE overrides (A/B runs)
+static int fin_wide() {
+  static const int v = [] {
+    const char* e = getenv("MMDX_FIN_WIDE");
+    return e && atoi(e) > 0 ? atoi(e) : 512;
+  }();
+  return v;
+}
+
 // >= 4 row iterations per block so the per-channel coefficient loads are amortised
 static int grid_rows(long rows, int C, int vec) {
   // MMDX_BN_ITERS / MMDX_BN_MAXBLOCKS override the row iterations per block and the grid cap
@@ -422,7 +432,7 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
       hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                          (const T*)x, rows, C, L.ct, L.rows_per_block, part);
     }
-    if (nblk > 512)
+    if (nblk > fin_wide())
       hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
                          (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv, momentum,
                          eps, smean, srstd, scale, shift);
@@ -466,7 +476,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
                        (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
                        smean, srstd, relu, gamma, bbeta, part);
   }
-  if (nblk > 512)
+  if (nblk > fin_wide())
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
                        (const float2*)part, nblk, rows, C, train, gamma, bbeta, smean,
                        srstd, dgamma, dbeta, beta_acc, coef);
