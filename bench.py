@@ -185,8 +185,6 @@ def build(cfg, dev, dtype):
     torch.manual_seed(0)
     img = mmdx.ImageEncoderCNN(cfg["image"], 1024, 13, compute_dtype=dtype).to(dev)
     txt = mmdx.TextEncoderTransformer(cfg["text"], 512, 13, compute_dtype=dtype).to(dev)
-    if cfg["text"].startswith("bert"):
-        txt.encoder.config.attention_probs_dropout_prob = 0.0
     fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13, dropout=0.1).to(dev)
     img.unfreeze_backbone()
     txt.unfreeze_encoder()
@@ -308,32 +306,71 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
     return step
 
 
-def cpu_baseline(cfg, seconds=20.0, bs=8, threads=16):
-    """Time the CPU oracle (the reference's PyTorch-CPU path restated, oracle/ref_cpu.py)
-    on a bounded sample: fwd+bwd+AdamW steps of `bs` samples until ~`seconds` elapse."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: BASELINE.md's plan says os.cpu_count(), but on a
+    GPU box that counts the whole machine while this process gets a share of it
+    (OMP_NUM_THREADS / the affinity mask); oversubscribing that share only slows torch's
+    CPU kernels, so the share is used and both numbers are reported."""
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = int(share) if share and share.isdigit() else len(os.sched_getaffinity(0))
+    return max(1, min(n, os.cpu_count() or n))
+
+
+def cpu_baseline(cfg, bs=8, warmup=10, steps=50):
+    """Time the CPU oracle (the reference's PyTorch-CPU path restated, oracle/ref_cpu.py) per
+    BASELINE.md's plan: the reference's AdamW groups (TP:238-269 image phase 2, TP:408-432
+    text phase 2, TP:1018-1023 fusion), clip_grad_norm_(1.0), `warmup` untimed steps, then
+    the MEDIAN of `steps` timed fwd+bwd+AdamW steps of `bs` samples."""
     from oracle import ref_cpu as R
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    text = cfg["text"] if cfg["text"] != "bert-base-uncased" else "bert-base-uncased"
+    text = cfg["text"]
     model = R.RefMultimodal(cfg["image"], text, dropout=0.0)
     model.train()
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-2)
+    groups = [
+        {"params": list(model.image.backbone.parameters()), "lr": 1e-4},
+        {"params": list(model.image.proj.parameters()) +
+         list(model.image.classifier.parameters()), "lr": 5e-4},
+        {"params": list(model.text.encoder.parameters()), "lr": 2e-5},
+        {"params": list(model.text.proj.parameters()) +
+         list(model.text.classifier.parameters()), "lr": 5e-4},
+        {"params": list(model.fusion.parameters()), "lr": 5e-4},
+    ]
+    opt = torch.optim.AdamW(groups, weight_decay=1e-2)
     g = torch.Generator().manual_seed(1234)
     x = torch.rand(bs, 3, 224, 224, generator=g)
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    x = (x - mean) / std
     ids = torch.randint(1000, 30522, (bs, cfg["seq"]), generator=g)
+    ids[:, 0], ids[:, -1] = 101, 102
     mask = torch.ones(bs, cfg["seq"], dtype=torch.long)
-    y = (torch.rand(bs, 13, generator=g) < 0.15).float()
-    R.ref_train_step(model, opt, x, ids, mask, y)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+    y = (torch.rand(bs, 13, generator=torch.Generator().manual_seed(1235)) < 0.15).float()
+    for _ in range(warmup):
         R.ref_train_step(model, opt, x, ids, mask, y)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    return {"value": round(n * bs / el, 3), "unit": "samples/s", "cores": threads,
-            "kind": "port", "sample": f"{n} oracle train steps x {bs} samples "
-            f"({cfg['image']} + {text}, 224x224, L={cfg['seq']}), torch CPU fp32"}
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        R.ref_train_step(model, opt, x, ids, mask, y)
+        ts.append(time.perf_counter() - t0)
+    med = sorted(ts)[len(ts) // 2]
+    return {"value": round(bs / med, 3), "unit": "samples/s", "cores": threads,
+            "kind": "port", "cpu_model": _cpu_model(), "machine_cpus": os.cpu_count(),
+            "sample": f"median of {steps} oracle train steps (after {warmup} warm-up) x {bs} "
+                      f"samples ({cfg['image']} + {text}, 224x224, L={cfg['seq']}; "
+                      f"reference AdamW groups, clip 1.0), torch CPU fp32, {threads} threads"}
 
 
 def main():
@@ -344,7 +381,7 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch override")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-steps", type=int, default=50)
     args = ap.parse_args()
 
     cfg = dict(CONFIGS[args.config])
@@ -449,6 +486,10 @@ def main():
         loss = run()
     t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (no device sync)
     torch.cuda.synchronize()
+    if cfg["text"] == "bilstm":
+        # a cooperative recurrence that lost a peer invalidates the run: fail loudly
+        from mmdx.bilstm import check_recurrence
+        check_recurrence()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -539,7 +580,11 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        # C5's oracle (ViT-B/16 + BERT-base) takes seconds per CPU step: a shorter sample
+        heavy = cfg["image"] == "vit_b_16"
+        result["cpu_baseline"] = cpu_baseline(cfg, warmup=2 if heavy else 10,
+                                              steps=min(args.cpu_steps, 5) if heavy
+                                              else args.cpu_steps)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

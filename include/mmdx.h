@@ -331,13 +331,18 @@ int mmdx_embed_scatter(int dtype, const int64_t* ids, long n, int D, const void*
  * (BertSelfAttention: softmax(QK^T*scale + (1-mask)*(-huge)) V; mask may be NULL = ViT).
  * qkv: [B, L, 3, H, 64] (fused projection output); out: [B, L, H, 64];
  * probs saved for backward: [B, H, L, L] fp32 (NULL in inference).
- * dqkv: [B, L, 3, H, 64]; workspace holds dS ([B,H,L,roundup16(L)] compute dtype). */
+ * p_drop > 0 (training, BertSelfAttention's dropout on attention_probs): O = (P*keep/(1-p)) V
+ * with keep drawn from a counter-based hash of (seed, *counter, b, h, q, key); the saved
+ * probabilities carry keep in their sign bit (dropped: -P), so the backward needs neither
+ * RNG nor a mask.  counter (device uint64, may be NULL) is incremented after the launch.
+ * dqkv: [B, L, 3, H, 64]; workspace holds dS ([B,H,L,roundup32(L)] compute dtype). */
 int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
-                       int H, float scale, void* out, float* probs, void* stream);
+                       int H, float scale, float p_drop, uint64_t seed, uint64_t* counter,
+                       void* out, float* probs, void* stream);
 size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H);
 int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const void* dout,
-                       const int64_t* mask, int B, int L, int H, float scale, void* dqkv,
-                       void* workspace, size_t ws_bytes, void* stream);
+                       const int64_t* mask, int B, int L, int H, float scale, float p_drop,
+                       void* dqkv, void* workspace, size_t ws_bytes, void* stream);
 
 /* LSTM recurrence for one layer, both directions (build-defined C3/C4 tower).
  * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);
@@ -345,11 +350,19 @@ int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const voi
  * gates: [2, L, B, 4H] fp32 post-activation (for backward). */
 /* Workspace for the cooperative bf16 forward (H = 256, B <= 256): h exchange + counters.
  * 0 when that path does not apply (then ws may be NULL and the batch-partitioned kernel
- * runs). */
+ * runs).
+ * status: DEVICE int, caller-owned, zero-initialised and STICKY: the cooperative kernel sets
+ * it to 1 when a peer workgroup never arrives within spin_limit polls (<= 0: the default,
+ * ~2 s) — every workgroup then leaves and the outputs are invalid.  The kernel never clears
+ * it; the caller copies it to the host at a sync point and raises (bilstm.py).  A non-zero
+ * status on entry makes the kernel leave at its first wait.  debug_flags bit 0 (tests
+ * only): workgroup 0 of direction 0 never signals, forcing the timeout path.
+ * Returns -22 if the device cannot hold the cooperative grid resident. */
 size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H);
 int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
                   void* h_out, float* c_save, float* gates_save, void* workspace,
-                  size_t ws_bytes, void* stream);
+                  size_t ws_bytes, int* status, long spin_limit, int debug_flags,
+                  void* stream);
 size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H);
 int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                   const float* gates_save, const void* dh_out, int B, int L, int H,

@@ -114,10 +114,10 @@ SIGNATURES = {
     "mmdx_embed_mean_bwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp]),
     "mmdx_embed_gather": (i32, [i32, vp, i64, i32, vp, vp, vp]),
     "mmdx_embed_scatter": (i32, [i32, vp, i64, i32, vp, vp, vp]),
-    "mmdx_attention_fwd": (i32, [i32, vp, vp, i32, i32, i32, f32, vp, vp, vp]),
+    "mmdx_attention_fwd": (i32, [i32, vp, vp, i32, i32, i32, f32, f32, u64, vp, vp, vp, vp]),
     "mmdx_attention_workspace_size": (sz, [i32, i32, i32, i32]),
-    "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp, sz, vp]),
-    "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp]),
+    "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp, vp, sz, vp]),
+    "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp, i64, i32, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_fwd_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
@@ -211,6 +211,23 @@ def rng_counter(device) -> torch.Tensor:
     if t is None:
         t = _RNG_COUNTERS[key] = torch.zeros(1, dtype=torch.int64, device=device)
     return t
+
+
+def dropout_seed(base: int) -> int:
+    """Host seed of a dropout launch: the call site's constant mixed with torch's initial
+    seed and, under torch.distributed, the process rank — so data-parallel replicas draw
+    independent masks (as one process's nn.Dropout over the global batch would), while a
+    given (seed, rank) stays reproducible and graph-replayable (the per-launch counter
+    lives on the device, rng_counter)."""
+    rank = 0
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            rank = dist.get_rank()
+    except Exception:  # pragma: no cover
+        rank = 0
+    x = (base ^ (torch.initial_seed() * 0x9E3779B97F4A7C15) ^ (rank * 0xBF58476D1CE4E5B9))
+    return x & 0xFFFFFFFFFFFFFFFF
 
 
 def workspace(nbytes: int, device) -> torch.Tensor | None:

@@ -7,7 +7,10 @@ fused QKV GEMM -> attention core (MFMA, in-LDS softmax) -> out-proj GEMM -> Add&
 FFN up GEMM (+GELU epilogue) -> FFN down GEMM -> Add&LayerNorm, with a hand-sequenced
 backward whose residual gradients are summed inside GEMM epilogues (beta = 1).
 Hidden-state dropout runs on the mmdx dropout kernel in train mode; attention-probability
-dropout is not implemented (p_attn must be 0) — parity runs use p = 0 on both sides.
+dropout (BertSelfAttention's, p = config.attention_probs_dropout_prob) is fused into the
+attention kernel (counter-based hash, keep bit carried in the saved probabilities' sign).
+RNG streams cannot match torch's, so parity runs use p = 0 on both sides; the dropout
+arithmetic itself is checked against an explicit masked reference (tests/test_text_gpu.py).
 """
 from __future__ import annotations
 
@@ -71,8 +74,8 @@ def _ln_fwd(x, res, gamma, beta, eps):
 def _dropout_fwd(x, p, seed):
     y = torch.empty_like(x)
     m = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
-    call("mmdx_dropout_fwd", L.dtype_code(x.dtype), ptr(x), x.numel(), float(p), seed, 0,
-         ptr(L.rng_counter(x.device)), ptr(y), ptr(m), stream())
+    call("mmdx_dropout_fwd", L.dtype_code(x.dtype), ptr(x), x.numel(), float(p),
+         L.dropout_seed(seed), 0, ptr(L.rng_counter(x.device)), ptr(y), ptr(m), stream())
     return y, m
 
 
@@ -110,8 +113,13 @@ class _BertLayerFn(torch.autograd.Function):
         probs = (torch.empty((B, Hn, Ls, Ls), dtype=torch.float32, device=dev)
                  if keep else None)
         scale = 1.0 / math.sqrt(D // Hn)
+        # BertSelfAttention's dropout on attention_probs (train mode), fused in the kernel
+        pa = float(cfg.p_attn) if (cfg.training and keep) else 0.0
+        if pa > 0:
+            _SEED[0] += 1
         call("mmdx_attention_fwd", L.dtype_code(T), ptr(qkv), ptr(mask), B, Ls, Hn, float(scale),
-             ptr(att), ptr(probs), stream())
+             pa, L.dropout_seed(_SEED[0]) if pa > 0 else 0, ptr(L.rng_counter(dev)), ptr(att),
+             ptr(probs), stream())
         woc = F.cast(wo, T)
         a = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(att, D, True, woc, D, True, M, D, D, a, D, bias=bo, compute_dtype=T)
@@ -136,7 +144,7 @@ class _BertLayerFn(torch.autograd.Function):
         h2, xs2, mu2, rs2 = _ln_fwd(f2, h1, g2, b2, eps)
         ctx.save_for_backward(x, mask, wqkv, qkv, probs, att, woc, xs1, mu1, rs1, g1, h1, wic,
                               pre, f, wo2c, xs2, mu2, rs2, g2)
-        ctx.m1, ctx.m2, ctx.p = m1, m2, p
+        ctx.m1, ctx.m2, ctx.p, ctx.pa = m1, m2, p, pa
         ctx.dims = (B, Ls, D, Hn, I, scale)
         return h2.reshape(B, Ls, D)
 
@@ -176,7 +184,7 @@ class _BertLayerFn(torch.autograd.Function):
         n = L.lib().mmdx_attention_workspace_size(L.dtype_code(T), B, Ls, Hn)
         w = _ws(n, dev)
         call("mmdx_attention_bwd", L.dtype_code(T), ptr(qkv), ptr(probs), ptr(datt), ptr(mask),
-             B, Ls, Hn, float(scale), ptr(dqkv), ptr(w), n, stream())
+             B, Ls, Hn, float(scale), float(ctx.pa), ptr(dqkv), ptr(w), n, stream())
         dWqkv = torch.empty((3 * D, D), dtype=torch.float32, device=dev)
         F.gemm(dqkv, 3 * D, False, x, D, False, 3 * D, D, M, dWqkv, D, compute_dtype=T)
         dbqkv = F._bias_grad(dqkv, M, 3 * D, torch.empty(3 * D, dtype=torch.float32, device=dev))
@@ -335,10 +343,6 @@ class BertModel(nn.Module):
                 nn.init.zeros_(m.bias)
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, return_dict=True):
-        if self.config.attention_probs_dropout_prob > 0 and self.training:
-            raise NotImplementedError(
-                "attention-probability dropout is not fused; set "
-                "config.attention_probs_dropout_prob = 0 for training")
         T = self.compute_dtype
         L.require_device(input_ids)
         ids = input_ids.long().contiguous()
@@ -353,7 +357,9 @@ class BertModel(nn.Module):
                            self.config.layer_norm_eps, T)
         cfg = SimpleNamespace(num_attention_heads=self.config.num_attention_heads,
                               layer_norm_eps=self.config.layer_norm_eps,
-                              p_hidden=self.config.hidden_dropout_prob, training=self.training)
+                              p_hidden=self.config.hidden_dropout_prob,
+                              p_attn=self.config.attention_probs_dropout_prob,
+                              training=self.training)
         for layer in self.encoder.layer:
             h = _BertLayerFn.apply(h, mask, cfg, *layer.params())
         return _Out(last_hidden_state=h)

@@ -25,6 +25,72 @@ class _Out(SimpleNamespace):
     pass
 
 
+class RecurrenceError(RuntimeError):
+    """The cooperative LSTM recurrence lost a peer workgroup: its outputs are invalid."""
+
+
+class _CoopStatus:
+    """Sticky device status word of the cooperative forward recurrence (mmdx_lstm_fwd).
+
+    After every cooperative launch the word is copied (async, same stream) into pinned host
+    memory behind an event.  `poll()` raises RecurrenceError once a completed copy shows a
+    timeout; it never blocks unless asked, so the step keeps its asynchrony and the error
+    surfaces at the next forward (or at `check_recurrence()` — the bench calls it after the
+    timed region, the training loop at its loss sync)."""
+
+    def __init__(self, dev):
+        self.word = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+        self.ev = None
+
+    def after_launch(self):
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self.host.copy_(self.word, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def poll(self, block=False):
+        ev = self.ev
+        if ev is None:
+            return
+        if block:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        if int(self.host[0]) != 0:
+            raise RecurrenceError(
+                "mmdx BiLSTM: the cooperative recurrence timed out waiting for a peer "
+                "workgroup (mmdx_lstm_fwd status=1); the text tower's outputs and gradients "
+                "of this step are invalid")
+
+    def reset(self):
+        self.word.zero_()
+        self.host.zero_()
+        self.ev = None
+
+
+_STATUS: dict = {}
+
+
+def coop_status(dev) -> _CoopStatus:
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    st = _STATUS.get(key)
+    if st is None:
+        st = _STATUS[key] = _CoopStatus(dev)
+    return st
+
+
+def check_recurrence(block=True):
+    """Raise RecurrenceError if any cooperative LSTM launch so far lost a peer."""
+    for st in list(_STATUS.values()):
+        st.poll(block=block)
+
+
+# debug knobs of the cooperative forward (tests force the timeout path through these)
+DEBUG = {"spin_limit": 0, "flags": 0}
+
+
 def _cat_cast(ws, T, dev):
     rows = sum(w.shape[0] for w in ws)
     out = torch.empty((rows,) + tuple(ws[0].shape[1:]), dtype=T, device=dev)
@@ -57,8 +123,14 @@ class _LSTMLayerFn(torch.autograd.Function):
         gs = torch.empty((2, Ls, B, G4), dtype=torch.float32, device=dev)
         fw = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(T), B, Ls, H)
         fws = L.workspace(fw, dev)
+        status = coop_status(dev) if fw else None
+        if status is not None:
+            status.poll()  # an earlier launch that lost a peer fails this step loudly
         call("mmdx_lstm_fwd", L.dtype_code(T), ptr(xg), ptr(whh), B, Ls, H, ptr(hout), ptr(cs),
-             ptr(gs), ptr(fws), fw, stream())
+             ptr(gs), ptr(fws), fw, ptr(status.word) if status else None,
+             int(DEBUG["spin_limit"]), int(DEBUG["flags"]), stream())
+        if status is not None:
+            status.after_launch()
         ctx.save_for_backward(x, wih, whh, hout, cs, gs)
         ctx.H = H
         return hout

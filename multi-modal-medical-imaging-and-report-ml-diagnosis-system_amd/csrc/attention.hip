@@ -6,6 +6,12 @@
 // Backward: kernel A per query block: dP = dO V^T, dS = P o (dP - rowsum(P o dP)),
 // dQ = scale dS K; kernel B per key block, streaming query chunks: dV = P^T dO,
 // dK = scale dS^T Q.  Additive key mask as BertSelfAttention (large negative on pads).
+// Attention-probability dropout (BertSelfAttention's dropout on attention_probs, train
+// mode): P' = P * keep / (1 - p) feeds O = P' V; keep comes from a counter-based hash of
+// (seed, device launch counter, b, h, q, key).  The saved probabilities carry the keep bit
+// in their sign (P >= 0: a dropped element is saved as -P), so the backward needs no RNG
+// and no mask tensor: dV = P'^T dO, dP = keep * (dO V^T) / (1 - p),
+// dS = P o (dP - rowsum(P o dP)).
 #include <algorithm>
 
 #include "igemm.h"
@@ -62,9 +68,17 @@ __device__ __forceinline__ void load_rows_T(T* dst, int ld, const T* src, long s
   }
 }
 
+__device__ __forceinline__ uint32_t attn_hash64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
 template <typename T>
 __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask,
-                                int L, int H, float scale, T* __restrict__ out,
+                                int L, int H, float scale, float p_drop, uint64_t seed,
+                                const uint64_t* __restrict__ ctr, T* __restrict__ out,
                                 float* __restrict__ probs) {
   typedef MfmaOp<T> Op;
   constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
@@ -127,6 +141,11 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
   for (int r = 0; r < 4; ++r) sum[r] = 1.f / rowgroup_sum(sum[r]);
   __syncthreads();  // every wave is done reading K: P may overwrite it
   float* prow = probs ? probs + (((long)b * H + h) * L) * L : nullptr;
+  const bool drop = p_drop > 0.f;
+  const float keep_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
+  const uint64_t rbase = drop ? seed * 0x9E3779B97F4A7C15ULL + (ctr ? ctr[0] << 32 : 0ull) +
+                                    (((uint64_t)b * H + h) * L) * (uint64_t)L
+                              : 0ull;
 #pragma unroll
   for (int j = 0; j < MAXKT; ++j) {
     if (j >= nkt) continue;
@@ -135,9 +154,14 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
     for (int r = 0; r < 4; ++r) {
       const int rl = wid * 16 + (lane >> 4) * 4 + r;
       const float p = s[j][r] * sum[r];
-      Ps[rl * LDV + key] = from_f<T>(p);
       const int q = q0 + rl;
-      if (prow && q < L && key < L) prow[(long)q * L + key] = p;
+      bool keep = true;
+      if (drop) {
+        const float u = (attn_hash64(rbase + (uint64_t)q * L + key) >> 8) * (1.f / 16777216.f);
+        keep = u >= p_drop;
+      }
+      Ps[rl * LDV + key] = from_f<T>(keep ? p * keep_scale : 0.f);
+      if (prow && q < L && key < L) prow[(long)q * L + key] = keep ? p : -p;
     }
   }
   __syncthreads();
@@ -167,7 +191,8 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
 template <typename T>
 __global__ void attn_bwd_q_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
                                   const T* __restrict__ dout, int L, int H, float scale,
-                                  T* __restrict__ dS_g, T* __restrict__ dqkv) {
+                                  float keep_scale, T* __restrict__ dS_g,
+                                  T* __restrict__ dqkv) {
   typedef MfmaOp<T> Op;
   constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
   constexpr int LDQ = HD + PAD;
@@ -211,7 +236,10 @@ __global__ void attn_bwd_q_kernel(const T* __restrict__ qkv, const float* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = q0 + wid * 16 + (lane >> 4) * 4 + r;
-      pv[j][r] = (q < L && key < L) ? prow[(long)q * L + key] : 0.f;
+      const float v = (q < L && key < L) ? prow[(long)q * L + key] : 0.f;
+      // dP = keep * dP' / (1 - p); dropped elements are saved with the sign bit set
+      s[j][r] = __builtin_signbitf(v) ? 0.f : s[j][r] * keep_scale;
+      pv[j][r] = fabsf(v);
       dot[r] += pv[j][r] * s[j][r];
     }
   }
@@ -263,7 +291,7 @@ constexpr int QC = 32;
 template <typename T>
 __global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
                                    const T* __restrict__ dout, const T* __restrict__ dS_g, int L,
-                                   int H, float scale, T* __restrict__ dqkv) {
+                                   int H, float scale, float keep_scale, T* __restrict__ dqkv) {
   typedef MfmaOp<T> Op;
   constexpr int NW = AttnCfg<T>::NW, KB = NW * 16, PAD = Vec16<T>::N;
   constexpr int LDC = QC + PAD;
@@ -287,7 +315,8 @@ __global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __res
       const int kk = i / QC, qq = i - kk * QC;
       const int key = k0 + kk, q = qc + qq;
       const bool ok = key < L && q < L;
-      Pt[kk * LDC + qq] = from_f<T>(ok ? pb[(long)q * L + key] : 0.f);
+      const float v = ok ? pb[(long)q * L + key] : 0.f;
+      Pt[kk * LDC + qq] = from_f<T>(__builtin_signbitf(v) ? 0.f : v * keep_scale);  // P'
       dSt[kk * LDC + qq] = ok ? dsb[(long)q * LP + key] : from_f<T>(0.f);
     }
     load_rows_T<T>(dOt, LDC, dout + ((long)b * L + qc) * H * HD + h * HD, (long)H * HD, QC,
@@ -333,9 +362,16 @@ static size_t fwd_smem(int L) {
 
 using namespace mmdx;
 
+__global__ void attn_counter_incr_kernel(uint64_t* c) { c[0] += 1; }
+
 extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
-                                  int H, float scale, void* out, float* probs, void* stream) {
+                                  int H, float scale, float p_drop, uint64_t seed,
+                                  uint64_t* counter, void* out, float* probs, void* stream) {
   MMDX_CHECK_ARG(B > 0 && H > 0 && L > 0 && L <= 16 * MAXKT, "attention: L=%d > 256", L);
+  MMDX_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "attention: dropout p=%g out of range",
+                 (double)p_drop);
+  MMDX_CHECK_ARG(p_drop == 0.f || probs,
+                 "attention: dropout needs the saved probabilities (training)");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == BF16) {
     constexpr int QB = AttnCfg<bf16>::NW * 16;
@@ -344,7 +380,7 @@ extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mas
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     hipLaunchKernelGGL(attn_fwd_kernel<bf16>, dim3((L + QB - 1) / QB, H, B),
                        dim3(AttnCfg<bf16>::NW * 64), sm, st, (const bf16*)qkv, mask, L, H, scale,
-                       (bf16*)out, probs);
+                       p_drop, seed, (const uint64_t*)counter, (bf16*)out, probs);
   } else {
     constexpr int QB = AttnCfg<float>::NW * 16;
     const size_t sm = fwd_smem<float>(L);
@@ -353,8 +389,10 @@ extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mas
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     hipLaunchKernelGGL(attn_fwd_kernel<float>, dim3((L + QB - 1) / QB, H, B),
                        dim3(AttnCfg<float>::NW * 64), sm, st, (const float*)qkv, mask, L, H,
-                       scale, (float*)out, probs);
+                       scale, p_drop, seed, (const uint64_t*)counter, (float*)out, probs);
   }
+  if (p_drop > 0.f && counter)
+    hipLaunchKernelGGL(attn_counter_incr_kernel, dim3(1), dim3(1), 0, st, counter);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -366,10 +404,12 @@ extern "C" size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H) 
 
 extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs,
                                   const void* dout, const int64_t* mask, int B, int L, int H,
-                                  float scale, void* dqkv, void* ws, size_t ws_bytes,
-                                  void* stream) {
+                                  float scale, float p_drop, void* dqkv, void* ws,
+                                  size_t ws_bytes, void* stream) {
   (void)mask;  // encoded in probs (masked keys have p = 0)
-  MMDX_CHECK_ARG(L <= 16 * MAXKT && probs, "attention bwd: bad args");
+  MMDX_CHECK_ARG(L <= 16 * MAXKT && probs && p_drop >= 0.f && p_drop < 1.f,
+                 "attention bwd: bad args");
+  const float keep_scale = 1.f / (1.f - p_drop);
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_attention_workspace_size(dtype, B, L, H),
                  "attention bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
@@ -382,10 +422,10 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);                  \
     hipLaunchKernelGGL(attn_bwd_q_kernel<T>, dim3((L + QB - 1) / QB, H, B),                    \
                        dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, probs,                \
-                       (const T*)dout, L, H, scale, (T*)ws, (T*)dqkv);                         \
+                       (const T*)dout, L, H, scale, keep_scale, (T*)ws, (T*)dqkv);             \
     hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((L + QB - 1) / QB, H, B),                   \
                        dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs, (const T*)dout, \
-                       (const T*)ws, L, H, scale, (T*)dqkv);                                   \
+                       (const T*)ws, L, H, scale, keep_scale, (T*)dqkv);                       \
   }
   if (dtype == BF16) ATTN_BWD(bf16) else ATTN_BWD(float)
 #undef ATTN_BWD

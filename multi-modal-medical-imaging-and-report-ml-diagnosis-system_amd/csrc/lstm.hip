@@ -7,6 +7,7 @@
 // the cell update runs from an fp32 LDS image of G.  Input projections (x W_ih^T + b) for
 // all steps are one large GEMM outside this kernel; so are dW_ih, dX and the bias grads.
 #include <algorithm>
+#include <atomic>
 
 #include "igemm.h"
 #include "../../include/mmdx.h"
@@ -224,7 +225,8 @@ constexpr int COOP_H = 256;
 constexpr int COOP_UB = COOP_H / COOP_NB;  // 32 units per workgroup
 constexpr int COOP_LDH = COOP_H + 8;       // padded h row (bf16): conflict-free b128 reads
 constexpr int COOP_SC1 = 16;               // buffer instruction aux: sc1 (write-through / L1 bypass)
-constexpr long COOP_SPIN_MAX = 1L << 26;   // bounded wait: a lost peer ends the kernel
+constexpr long COOP_SPIN_MAX = 1L << 26;   // default bounded wait (~2 s): a lost peer ends the kernel
+constexpr int COOP_DEBUG_DROP_PEER = 1;    // debug flag: workgroup 0 of direction 0 never signals
 
 typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
 
@@ -233,7 +235,8 @@ template <int RT>
 __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     const float* __restrict__ xg, const bf16* __restrict__ whh, int B, int L,
     bf16* __restrict__ hout, float* __restrict__ csave, float* __restrict__ gsave,
-    bf16* __restrict__ hx, unsigned* __restrict__ ctr, int* __restrict__ err) {
+    bf16* __restrict__ hx, unsigned* __restrict__ ctr, int* __restrict__ status, long spin_max,
+    int debug) {
   constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
   constexpr int NROWS = 64 * RT;
   // [0, NROWS*COOP_LDH): h_{t-1} (MFMA A operand); then this workgroup's h_t slice [NROWS][32]
@@ -277,18 +280,29 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) xv[i][r][g] = xp[g * H];
       }
-    // wait until every workgroup of this direction has published h_{t-1}
+    // wait until every workgroup of this direction has published h_{t-1}.  The wait is
+    // bounded: a peer that never arrives (not co-resident, lost) makes the waiter set the
+    // sticky status word and every workgroup leave, so the grid always drains; the host
+    // reads the status word and raises (bilstm.py, mmdx_lstm_fwd's contract).
     if (s > 0) {
       if (threadIdx.x == 0) {
         const unsigned target = (unsigned)(COOP_NB * s);
         long spins = 0;
         while (__hip_atomic_load(myctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > COOP_SPIN_MAX) { *err = 1; break; }
+          ++spins;
+          if (spins > spin_max) {
+            __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          // another workgroup already gave up: stop waiting for it
+          if ((spins & 255) == 0 &&
+              __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+            break;
         }
       }
       __syncthreads();
-      if (*(volatile int*)err) return;  // a peer never arrived: give up (results invalid)
+      if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
     }
     // h_{t-1} -> LDS (zeros at the first step); sc1 loads: the producers' sc1 stores are
     // visible to them without an L1 invalidate
@@ -345,7 +359,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0)
+      if (threadIdx.x == 0 && !((debug & COOP_DEBUG_DROP_PEER) && blk == 0 && dir == 0))
         __hip_atomic_fetch_add(myctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // saves for the backward (overlap the next step's wait)
@@ -406,31 +420,63 @@ static bool coop_ok(int dtype, int B, int H) { return dtype == BF16 && H == COOP
 extern "C" size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H) {
   (void)L;
   if (!coop_ok(dtype, B, H)) return 0;
-  // h exchange [2 dir][2 parity][B][H] bf16 + 2 counters + error flag
+  // h exchange [2 dir][2 parity][B][H] bf16 + 2 counters
   return (size_t)2 * 2 * B * H * 2 + 256;
+}
+
+// The cooperative forward needs its 2 x COOP_NB workgroups resident at once: one per CU
+// (~148 KB of LDS each) on distinct CUs.  Checked once per device and kernel variant: the
+// device must have at least that many CUs and the kernel must fit one block per CU.  The
+// other streams' blocks cannot starve it: they always finish, and the spinning workgroups
+// hold at most 2 x COOP_NB of the 256 CUs.
+template <int RT>
+static bool coop_resident(hipStream_t st) {
+  static std::atomic<int> ok[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  int v = ok[dev].load(std::memory_order_relaxed);
+  if (v == 0) {
+    int per_cu = 0, cus = 0;
+    const bool q =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_fwd_coop_kernel<RT>, 512,
+                                                     0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+    v = (q && per_cu >= 1 && cus >= 2 * COOP_NB) ? 1 : -1;
+    ok[dev].store(v, std::memory_order_relaxed);
+  }
+  (void)st;
+  return v > 0;
 }
 
 extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
                              void* h_out, float* c_save, float* gates_save, void* ws,
-                             size_t ws_bytes, void* stream) {
+                             size_t ws_bytes, int* status, long spin_limit, int debug_flags,
+                             void* stream) {
   MMDX_CHECK_ARG(B > 0 && L > 0 && c_save && gates_save, "lstm fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   const size_t need = mmdx_lstm_fwd_workspace_size(dtype, B, L, H);
   if (need && ws && ws_bytes >= need) {
+    MMDX_CHECK_ARG(status, "lstm fwd: the cooperative path needs a device status word");
     bf16* hx = (bf16*)ws;
     unsigned* ctr = (unsigned*)((char*)ws + (size_t)2 * 2 * B * H * 2);
-    int* err = (int*)(ctr + 4);
+    const long spin_max = spin_limit > 0 ? spin_limit : COOP_SPIN_MAX;
     hipMemsetAsync(ctr, 0, 64, st);
     const dim3 grid(COOP_NB, 2);
+#define COOP_LAUNCH(RT)                                                                      \
+  do {                                                                                       \
+    MMDX_CHECK_ARG(coop_resident<RT>(st),                                                    \
+                   "lstm fwd: the cooperative recurrence cannot be co-resident here");       \
+    hipLaunchKernelGGL(lstm_fwd_coop_kernel<RT>, grid, dim3(512), 0, st, (const float*)xg,   \
+                       (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr,   \
+                       status, spin_max, debug_flags);                                       \
+  } while (0)
     if (B <= 64)
-      hipLaunchKernelGGL(lstm_fwd_coop_kernel<1>, grid, dim3(512), 0, st, (const float*)xg,
-                         (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr, err);
+      COOP_LAUNCH(1);
     else if (B <= 128)
-      hipLaunchKernelGGL(lstm_fwd_coop_kernel<2>, grid, dim3(512), 0, st, (const float*)xg,
-                         (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr, err);
+      COOP_LAUNCH(2);
     else
-      hipLaunchKernelGGL(lstm_fwd_coop_kernel<4>, grid, dim3(512), 0, st, (const float*)xg,
-                         (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr, err);
+      COOP_LAUNCH(4);
+#undef COOP_LAUNCH
     MMDX_LAUNCH_CHECK();
     return 0;
   }

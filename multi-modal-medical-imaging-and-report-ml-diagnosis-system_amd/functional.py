@@ -240,7 +240,7 @@ def dropout(x, p, training):
         return x
     # the device counter (L.rng_counter) advances per launch; the host seed stays fixed so
     # the call is graph-replayable
-    return _DropoutFn.apply(x, p, _DROPOUT_SEED[0], 0)
+    return _DropoutFn.apply(x, p, L.dropout_seed(_DROPOUT_SEED[0]), 0)
 
 
 # ----------------------------------------------------------------------------- BCE

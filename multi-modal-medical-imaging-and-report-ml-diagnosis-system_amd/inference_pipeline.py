@@ -9,7 +9,8 @@ SURVEY §8(f)): it is generated only when the bundle's fusion model carries one,
 `load_model_bundle(path)` rebuilds the bundle from a local `model_bundle.pt` written by the
 reference's save path (TP:773-796: keys cfg, fusion_state, image_state, text_state,
 t5_tokenizer_name, bert_tokenizer_name, version), with the same key validation and errors
-as the Django loader (VW:196-204).  Loading uses weights_only=True.
+as the Django loader (VW:196-204).  Loading uses weights_only=True.  `save_model_bundle`
+writes the same dict (atomically, TP:792-794), so bundles move both ways.
 """
 from __future__ import annotations
 
@@ -26,6 +27,29 @@ BUNDLE_KEYS = ("cfg", "fusion_state", "image_state", "text_state", "t5_tokenizer
                "bert_tokenizer_name", "version")
 
 
+def _text_model_name(raw):
+    """The text architecture comes from cfg["text_encoder"]["hf_model_name"] (TP:701, the
+    text encoder's model_name); the tokenizer name is only the fallback (same value in the
+    reference's writer, TP:788)."""
+    tc = (raw["cfg"] or {}).get("text_encoder", {}) or {}
+    return tc.get("hf_model_name") or raw.get("bert_tokenizer_name") or "bert-base-uncased"
+
+
+def _load_fusion_state(fusion, state):
+    """Strict on every disease-branch key (fusion_mlp, disease_head, cond_proj): a mismatch
+    raises instead of leaving randomly initialised heads (VW:221 loads strictly).  The T5
+    `report_model.*` keys are loaded when the model carries a report head, else set aside."""
+    has_t5 = getattr(fusion, "report_model", None) is not None
+    fs = {k: v for k, v in state.items() if has_t5 or not k.startswith("report_model.")}
+    res = fusion.load_state_dict(fs, strict=False)
+    bad = [k for k in list(res.missing_keys) + list(res.unexpected_keys)
+           if not k.startswith("report_model.")]
+    if bad or (has_t5 and res.missing_keys):
+        raise RuntimeError(f"fusion_state does not match the fusion model: "
+                           f"missing {list(res.missing_keys)}, unexpected "
+                           f"{list(res.unexpected_keys)}")
+
+
 def load_model_bundle(path: str, device="cuda", compute_dtype=torch.float32):
     if not os.path.exists(path):
         raise FileNotFoundError(f"Model bundle not found at {path}")  # VW:178
@@ -35,19 +59,17 @@ def load_model_bundle(path: str, device="cuda", compute_dtype=torch.float32):
         raise ValueError(f"Bundle missing keys: {missing}")  # VW:204
     cfg = raw["cfg"] or {}
     fc = cfg.get("fusion", {}) or {}
-    d_img = fc.get("d_img", 1024)
-    d_txt = fc.get("d_txt", 512)  # VW:209 fallback (IP:74 uses 1024)
+    d_img = fc.get("d_img") or 1024
+    d_txt = fc.get("d_txt") or 512  # VW:209 fallback (IP:74 uses 1024)
     fusion = FusionTransformerModel(d_img=d_img, d_txt=d_txt,
-                                    d_fuse_hidden=fc.get("d_fuse_hidden", 1024),
-                                    n_disease=fc.get("n_disease", 13),
-                                    n_cond_tokens=fc.get("n_cond_tokens", 4))
-    fs = {k: v for k, v in raw["fusion_state"].items() if not k.startswith("report_model.")}
-    fusion.load_state_dict(fs, strict=False)
+                                    d_fuse_hidden=fc.get("d_fuse_hidden") or 1024,
+                                    n_disease=fc.get("n_disease") or 13,
+                                    n_cond_tokens=fc.get("n_cond_tokens") or 4)
+    _load_fusion_state(fusion, raw["fusion_state"])
     backbone = ((cfg.get("image_encoder", {}) or {}).get("backbone")) or "resnet50"
     image = ImageEncoderCNN(backbone, d_img, compute_dtype=compute_dtype)
     image.load_state_dict(raw["image_state"])
-    text = TextEncoderTransformer(raw["bert_tokenizer_name"] or "bert-base-uncased", d_txt,
-                                  compute_dtype=compute_dtype)
+    text = TextEncoderTransformer(_text_model_name(raw), d_txt, compute_dtype=compute_dtype)
     text.load_state_dict(raw["text_state"])
     arts = cfg.get("artifacts", {}) or {}
     return {
@@ -61,6 +83,78 @@ def load_model_bundle(path: str, device="cuda", compute_dtype=torch.float32):
         "class_names": arts.get("class_names", DISEASES),
         "thresholds": arts.get("thresholds", [0.5] * len(DISEASES)),
     }
+
+
+def bundle_config(fusion_model, image_encoder, text_encoder, artifacts=None,
+                  hf_model_name=None):
+    """The `configuration` dict of TP:682-720 (JSON-safe), built from the live modules."""
+    from datetime import datetime, timezone
+    rm = getattr(fusion_model, "report_model", None)
+    bert_name = getattr(text_encoder, "model_name", None) or "bert-base-uncased"
+    cfg = {
+        "saved_at": datetime.now(timezone.utc).replace(tzinfo=None).isoformat() + "Z",
+        "fusion": {
+            "d_img": getattr(fusion_model, "d_img", None),
+            "d_txt": getattr(fusion_model, "d_txt", None),
+            "d_fuse_hidden": getattr(fusion_model, "d_fuse_hidden", None),
+            "n_disease": getattr(fusion_model, "n_disease", None),
+            "n_cond_tokens": getattr(fusion_model, "n_cond", None),
+            "decoder_hidden": rm.config.d_model if rm is not None else None,
+        },
+        "report_head": {"hf_model_name": hf_model_name or (
+            getattr(rm.config, "_name_or_path", None) if rm is not None else None)},
+        "text_encoder": {"hf_model_name": bert_name,
+                         "d_txt": getattr(fusion_model, "d_txt", None),
+                         "pooling": getattr(text_encoder, "pooling", "masked_mean"),
+                         "max_len": 96},
+        "image_encoder": {"backbone": getattr(image_encoder, "backbone_name", None),
+                          "d_img": getattr(fusion_model, "d_img", None),
+                          "img_size": 224,
+                          "normalize": {"mean": [0.485, 0.456, 0.406],
+                                        "std": [0.229, 0.224, 0.225]}},
+        "notes": "Fusion MLP + disease head (BCEWithLogits) + T5 report head (CE).",
+    }
+    if artifacts:
+        cfg["artifacts"] = artifacts
+    return cfg
+
+
+def save_model_bundle(fusion_model, image_encoder, text_encoder, model_dir, version=1,
+                      artifacts=None, hf_model_name=None, timestamped_copy=True):
+    """Write `model_bundle.pt` exactly as the reference's local save does (TP:773-796):
+    keys cfg, fusion_state, image_state, text_state, t5_tokenizer_name,
+    bert_tokenizer_name, version; written to a .tmp file and moved into place with
+    os.replace (atomic, TP:792-794), plus a timestamped copy (TP:779-780, TP:795).  The
+    registry upload around it (TP:650-771) is out of scope.  State dicts are saved from
+    CPU copies in the reference's layout (NCHW fp32 — the modules store it that way).
+    Returns the path of the latest bundle."""
+    import shutil
+    from datetime import datetime, timezone
+    from pathlib import Path
+    d = Path(model_dir)
+    d.mkdir(parents=True, exist_ok=True)
+    cfg = bundle_config(fusion_model, image_encoder, text_encoder, artifacts, hf_model_name)
+
+    def cpu_state(m):
+        return {k: v.detach().cpu() for k, v in m.state_dict().items()}
+
+    bundle = {
+        "cfg": cfg,
+        "fusion_state": cpu_state(fusion_model),
+        "image_state": cpu_state(image_encoder),
+        "text_state": cpu_state(text_encoder),
+        "t5_tokenizer_name": cfg["report_head"]["hf_model_name"],
+        "bert_tokenizer_name": cfg["text_encoder"]["hf_model_name"],
+        "version": version,
+    }
+    latest = d / "model_bundle.pt"
+    tmp = latest.with_suffix(".pt.tmp")
+    torch.save(bundle, tmp)
+    os.replace(tmp, latest)
+    if timestamped_copy:
+        stamp = datetime.now(timezone.utc).strftime("%Y%m%dT%H%M%SZ")
+        shutil.copyfile(latest, d / f"model_bundle_{stamp}.pt")
+    return str(latest)
 
 
 @torch.no_grad()

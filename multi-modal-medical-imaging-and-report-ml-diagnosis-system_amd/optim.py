@@ -21,9 +21,18 @@ from ._lib import call, ptr, stream
 
 CHUNK = 1 << 16  # elements per workgroup descriptor
 
-# Pinned staging buffers cannot be allocated while a stream is capturing a graph, so every
-# eagerly built table leaves a spare of its size behind for a later capture to take.
+# Pinned staging buffers cannot be allocated while a stream is capturing a graph, so the
+# eager path keeps a few spares (at most _MAX_SPARES, the largest kept) for a later capture.
 _PINNED_SPARES: list = []
+_MAX_SPARES = 4
+
+
+def _reserve_spare(nbytes: int):
+    if sum(t.numel() >= nbytes for t in _PINNED_SPARES) >= 2:  # AdamW + grad-norm tables
+        return
+    _PINNED_SPARES.append(torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+    _PINNED_SPARES.sort(key=lambda t: -t.numel())
+    del _PINNED_SPARES[_MAX_SPARES:]
 
 
 def _pinned(nbytes: int) -> torch.Tensor:
@@ -33,8 +42,7 @@ def _pinned(nbytes: int) -> torch.Tensor:
                 return _PINNED_SPARES.pop(i)
         raise RuntimeError("mmdx AdamW: no pinned staging buffer reserved for graph capture; "
                            "run one eager step before capturing")
-    while sum(t.numel() >= nbytes for t in _PINNED_SPARES) < 2:  # AdamW + grad-norm tables
-        _PINNED_SPARES.append(torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+    _reserve_spare(nbytes)
     return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
 
 
@@ -75,7 +83,19 @@ class _Plan:
         self.events = [None] * self.RING
         self.k = 0
         self.last = None
-        _PINNED_SPARES.append(torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True))
+        self.hyper = (tuple(lrs), tuple(wds))
+        _reserve_spare(self.nbytes)
+
+    def set_hyper(self, lrs, wds):
+        """A learning-rate / weight-decay change (scheduler, param_group edit) rewrites the
+        table's lr/wd columns in place; the next upload ships them."""
+        hyper = (tuple(lrs), tuple(wds))
+        if hyper == self.hyper:
+            return
+        self.hyper = hyper
+        self.desc["lr"] = np.asarray(lrs, dtype=np.float32)[self.tidx]
+        self.desc["wd"] = np.asarray(wds, dtype=np.float32)[self.tidx]
+        self.last = None
 
     def upload(self, grads):
         gp = np.fromiter((g.data_ptr() for g in grads), dtype=np.uint64, count=len(grads))
@@ -102,12 +122,17 @@ class _Plan:
 
 
 def _plan_for(cache: dict, params, ms, vs, lrs, wds, device):
-    key = (tuple(map(id, params)), tuple(lrs), tuple(wds))
+    """The table is keyed on the storage the kernel writes (p, exp_avg, exp_avg_sq data
+    pointers): a load_state_dict that swaps in new moment tensors, or a moved parameter,
+    builds a new table; lr/wd changes only rewrite two columns (_Plan.set_hyper)."""
+    key = (tuple(p.data_ptr() for p in params), tuple(m.data_ptr() for m in ms),
+           tuple(v.data_ptr() for v in vs), tuple(p.numel() for p in params))
     plan = cache.get(key)
     if plan is None:
         if len(cache) > 8:
             cache.clear()
         plan = cache[key] = _Plan(params, ms, vs, lrs, wds, device)
+    plan.set_hyper(lrs, wds)
     return plan
 
 
@@ -120,6 +145,29 @@ class AdamW(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self._tables = {}
         self._step_t = None
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict, then re-bind the fused kernel: the loaded
+        exp_avg / exp_avg_sq tensors replace the old ones (new descriptor table) and the
+        shared device step counter restarts from the loaded 'step'."""
+        super().load_state_dict(state_dict)
+        self._tables.clear()
+        self._step_t = None
+        step = None
+        for st in self.state.values():
+            if "step" in st:
+                step = float(st["step"].item() if torch.is_tensor(st["step"]) else st["step"])
+                break
+        if step is not None:
+            dev = next((st["exp_avg"].device for st in self.state.values() if "exp_avg" in st),
+                       None)
+            self._step_t = torch.full((1,), step, dtype=torch.float32, device=dev)
+            for st in self.state.values():
+                if "exp_avg" in st:
+                    st["step"] = self._step_t
+                    for k in ("exp_avg", "exp_avg_sq"):
+                        if not st[k].is_contiguous():
+                            st[k] = st[k].contiguous()
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: torch.Tensor | None = None):
@@ -146,6 +194,8 @@ class AdamW(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p,
                                                         memory_format=torch.contiguous_format)
+                    if self._step_t is not None:
+                        st["step"] = self._step_t
                 g = p.grad
                 if not g.is_contiguous():
                     g = p.grad = g.contiguous()

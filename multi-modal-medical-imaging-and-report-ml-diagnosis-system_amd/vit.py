@@ -137,7 +137,7 @@ class _VitBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(D // heads)
         att = torch.empty((M, D), dtype=T, device=dev)
         call("mmdx_attention_fwd", L.dtype_code(T), ptr(qkv), None, N, S, heads, float(scale),
-             ptr(att), ptr(probs), stream())
+             0.0, 0, None, ptr(att), ptr(probs), stream())
         woc = F.cast(w_out, T)
         o = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(att, D, True, woc, D, True, M, D, D, o, D, bias=b_out, compute_dtype=T)
@@ -188,7 +188,7 @@ class _VitBlockFn(torch.autograd.Function):
         n = L.lib().mmdx_attention_workspace_size(L.dtype_code(T), N, S, heads)
         w = L.workspace(n, dev)
         call("mmdx_attention_bwd", L.dtype_code(T), ptr(qkv), ptr(probs), ptr(datt), None, N, S,
-             heads, float(scale), ptr(dqkv), ptr(w), n, stream())
+             heads, float(scale), 0.0, ptr(dqkv), ptr(w), n, stream())
         dWqkv = torch.empty((3 * D, D), dtype=torch.float32, device=dev)
         F.gemm(dqkv, 3 * D, False, u1, D, False, 3 * D, D, M, dWqkv, D, compute_dtype=T)
         dbqkv = _colsum(dqkv, M, 3 * D)

@@ -64,3 +64,16 @@ def cosine(a, b):
     a = a.detach().double().cpu().flatten()
     b = b.detach().double().cpu().flatten()
     return (a @ b / (a.norm() * b.norm()).clamp(min=1e-30)).item()
+
+
+def norm_ratio(a, b):
+    """|a| / |b| (fp64): cosine ignores magnitude, so the grad checks pair it with this."""
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a.norm() / b.norm().clamp(min=1e-300)).item()
+
+
+def grad_report(mine: dict, ref: dict):
+    """{name: (1 - cos, |norm ratio - 1|)} over the tensors both sides have."""
+    return {n: (1.0 - cosine(mine[n], ref[n]), abs(norm_ratio(mine[n], ref[n]) - 1.0))
+            for n in ref}

@@ -1,7 +1,8 @@
 """DP parity on one GPU (SURVEY §8(e) check (i)): two ranks (gloo, both on cuda:0), each
 with half of the batch, all-reduce-averaged gradients == single-process full-batch
 gradients, with BatchNorm in eval mode so per-replica statistics do not enter.
-fp32 path; tolerance 1 - cosine <= 1e-6 per tensor (reduction order only)."""
+fp32 path; tolerance per tensor (reduction order only): 1 - cosine <= 1e-6 and the norm
+ratio |g|/|g_ref| within 1e-5 of 1 (cosine alone would miss a lost or doubled 1/world)."""
 import os
 import socket
 import sys
@@ -75,7 +76,7 @@ def _worker(rank, world, port, out, early):
 
 @pytest.mark.parametrize("early", [False, True])
 def test_dp_two_ranks_match_full_batch(dev, early):
-    from parity_util import cosine, synth_batch
+    from parity_util import cosine, norm_ratio, synth_batch
     x, ids, mask, y = synth_batch(4, 16, hw=64)
     img, txt, fus = _model()
     ref = {n: p.grad.detach().cpu() for n, p in _grads(img, txt, fus, x, ids, mask, y)
@@ -96,3 +97,5 @@ def test_dp_two_ranks_match_full_batch(dev, early):
         for n in ref:
             c = cosine(g[n], ref[n])
             assert 1 - c <= 1e-6, f"rank {r} {n}: 1-cos {1 - c:.2e}"
+            nr = norm_ratio(g[n], ref[n])
+            assert abs(nr - 1) <= 1e-5, f"rank {r} {n}: norm ratio {nr:.7f}"

@@ -83,6 +83,20 @@ def _nhwc(x, cp, dt):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cfg", CONVS)
 def test_conv_fwd_dgrad_wgrad(dev, dt, cfg):
+    _conv_case(dev, dt, cfg)
+
+
+# production M: the C4 batch (N = 128) at layer1's 56x56 (M = 401,408 rows), the 3x3 and
+# the 1x1 expansion, plus layer2's strided 1x1 downsample (M = 100,352) — the exact launch
+# geometry of the benched step (grid sizes, split-K depth of the wgrad, BN stat blocks)
+@pytest.mark.parametrize("cfg", [(128, 64, 56, 56, 64, 3, 1, 1), (128, 64, 56, 56, 256, 1, 1, 0),
+                                 (128, 256, 56, 56, 512, 1, 2, 0)])
+def test_conv_production_m(dev, cfg):
+    torch.set_num_threads(16)
+    _conv_case(dev, torch.bfloat16, cfg)
+
+
+def _conv_case(dev, dt, cfg):
     N, C, H, W, K, k, s, p = cfg
     vec = 4 if dt == torch.float32 else 8
     cp = (C + vec - 1) // vec * vec

@@ -3,7 +3,9 @@
 Stated tolerances: fp32 logits max-abs <= 1e-4*max(1,|ref|), loss rel <= 1e-5.
 Gradients are judged against the oracle run in fp64 (the fp32 oracle itself is only
 ~0.9992-cosine-accurate on deep BatchNorm grads of ResNet-50 at 2x2 final spatial size):
-1 - cos(mmdx, oracle64) <= max(5e-4, 8 * (1 - cos(oracle32, oracle64))) for every tensor
+1 - cos(mmdx, oracle64) <= max(5e-4, 8 * (1 - cos(oracle32, oracle64))) for every tensor,
+and | |g|/|g64| - 1 | <= max(1e-3, 8x the fp32 oracle's own norm error) (cosine is blind to
+a uniformly scaled gradient)
 (both fp32 paths accumulate K up to 4608 in different orders; a wrong kernel gives 1-cos >> 1e-2).
 bf16 path: logits max-abs <= 5e-2*max(1,|ref|).
 """
@@ -13,7 +15,7 @@ import torch
 
 import mmdx
 from oracle import ref_cpu as R
-from parity_util import build_pair, cosine, mmdx_forward, rel_err, synth_batch
+from parity_util import build_pair, cosine, mmdx_forward, norm_ratio, rel_err, synth_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -55,6 +57,9 @@ def test_train_step_parity_fp32(dev, arch, text):
             own = 1.0 - cosine(gr[n], g64[n])
             c = 1.0 - cosine(gm[n], g64[n])
             assert c <= max(5e-4, 8 * own), f"grad {n}: 1-cos {c:.2e} (oracle32 {own:.2e})"
+            own_r = abs(norm_ratio(gr[n], g64[n]) - 1.0)
+            r = abs(norm_ratio(gm[n], g64[n]) - 1.0)
+            assert r <= max(1e-3, 8 * own_r), f"grad {n}: |norm ratio-1| {r:.2e} ({own_r:.2e})"
     # BN running statistics follow the train-mode update
     rm = dict(img.named_buffers())
     for n, b in ref.image.named_buffers():

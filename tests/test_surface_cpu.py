@@ -148,3 +148,65 @@ def test_vit_b_16_tower_keys_match_torchvision_layout():
     assert "backbone.encoder.layers.encoder_layer_11.self_attention.in_proj_weight" in m.state_dict()
     assert sum(p.numel() for p in m.backbone.parameters()) == 85798656
     assert m.backbone.feat_dim == 768 and m.proj.in_features == 768
+
+
+def test_save_model_bundle_roundtrip(tmp_path):
+    """save_model_bundle writes TP:773-796's dict atomically (no .tmp left behind, plus a
+    timestamped copy) and load_model_bundle reads it back bit-identically."""
+    from mmdx.inference_pipeline import load_model_bundle, save_model_bundle
+    torch.manual_seed(0)
+    img = mmdx.ImageEncoderCNN("resnet18", 1024, 13)
+    txt = mmdx.TextEncoderTransformer("embed-mean", 512, 13)
+    fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13)
+    path = save_model_bundle(fus, img, txt, tmp_path, version=7,
+                             artifacts={"class_names": mmdx.DISEASES, "thresholds": [0.4] * 13})
+    files = sorted(p.name for p in tmp_path.iterdir())
+    assert "model_bundle.pt" in files and not any(f.endswith(".tmp") for f in files)
+    assert any(f.startswith("model_bundle_") and f.endswith("Z.pt") for f in files)
+    raw = torch.load(path, weights_only=True)
+    assert list(raw) == ["cfg", "fusion_state", "image_state", "text_state",
+                         "t5_tokenizer_name", "bert_tokenizer_name", "version"]
+    cfg = raw["cfg"]
+    assert cfg["fusion"] == {"d_img": 1024, "d_txt": 512, "d_fuse_hidden": 1024, "n_disease": 13,
+                             "n_cond_tokens": 4, "decoder_hidden": None}
+    assert cfg["text_encoder"]["hf_model_name"] == "embed-mean" == raw["bert_tokenizer_name"]
+    assert cfg["image_encoder"]["backbone"] == "resnet18"
+    b = load_model_bundle(path, device="cpu")
+    assert b["version"] == 7 and b["thresholds"] == [0.4] * 13
+    for mine, ref in ((b["image_encoder"], img), (b["text_encoder"], txt),
+                      (b["fusion_model"], fus)):
+        sd, rsd = mine.state_dict(), ref.state_dict()
+        assert set(sd) == set(rsd)
+        for k in rsd:
+            assert torch.equal(sd[k], rsd[k]), k
+
+
+def test_bundle_fusion_state_strict(tmp_path):
+    """report_model.* keys (a reference bundle with its T5 head) load without a T5 head;
+    any other fusion-key mismatch raises instead of running random heads.  The text
+    architecture comes from cfg, not from bert_tokenizer_name."""
+    from mmdx.inference_pipeline import load_model_bundle
+    torch.manual_seed(0)
+    img = mmdx.ImageEncoderCNN("resnet18", 1024, 13)
+    txt = mmdx.TextEncoderTransformer("embed-mean", 512, 13)
+    fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13)
+    fs = dict(fus.state_dict())
+    fs["report_model.shared.weight"] = torch.zeros(4, 4)
+    bundle = {"cfg": {"fusion": {"d_img": 1024, "d_txt": 512},
+                      "image_encoder": {"backbone": "resnet18"},
+                      "text_encoder": {"hf_model_name": "embed-mean"}},
+              "fusion_state": fs, "image_state": img.state_dict(),
+              "text_state": txt.state_dict(), "t5_tokenizer_name": "t5-small",
+              "bert_tokenizer_name": "bert-base-uncased", "version": 3}
+    ok = tmp_path / "ok.pt"
+    torch.save(bundle, ok)
+    b = load_model_bundle(str(ok), device="cpu")
+    assert b["text_encoder"].model_name == "embed-mean"
+    assert torch.equal(b["fusion_model"].disease_head.weight, fus.disease_head.weight)
+    fs2 = dict(fs)
+    fs2["disease_head.weight_renamed"] = fs2.pop("disease_head.weight")
+    bundle["fusion_state"] = fs2
+    bad = tmp_path / "bad.pt"
+    torch.save(bundle, bad)
+    with pytest.raises(RuntimeError):
+        load_model_bundle(str(bad), device="cpu")
