@@ -396,11 +396,9 @@ def main():
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
     if world > 1:
+        from mmdx.dist import init_distributed
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        init_distributed(backend, local)   # RCCL async errors / timeouts fail the job fast
     dev = torch.device("cuda", local)
     dtype = torch.bfloat16
 
@@ -429,11 +427,11 @@ def main():
     reducer = GradAllReducer(params, world) if world > 1 else None
     early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "1" if backend == "nccl" else "0")
     if reducer is not None and early_tail != "0":
-        # the trunk's last-layer gradients start their all-reduce mid-backward (RCCL: the
-        # collective's stream waits on the plan's event, no host wait; gloo's CUDA path
-        # stalls the issuing host thread on it — 1.3 s/step in the one-GPU rehearsal — so
-        # the gloo rehearsal keeps it off unless asked for)
-        RN.TRUNK_GRAD_HOOK = lambda g, lo, ev: reducer.launch_region(g, lo, g.numel(), ev)
+        # the trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward, each from
+        # its own plan event (RCCL: the comm stream waits on the event, no host wait; gloo's
+        # CUDA path stalls the issuing host thread on it — 1.3 s/step in the one-GPU
+        # rehearsal — so the gloo rehearsal keeps it off unless asked for)
+        RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
     # the text tower's backward may run on its own stream at default priority
     # (MMDX_TEXT_BWD_PRIO=low): it is off the critical path, the image backward is not
     side_bwd = (torch.cuda.Stream(device=dev, priority=0)

@@ -13,6 +13,8 @@ runs after the all-reduce, so every rank clips identically.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -35,22 +37,35 @@ class GradAllReducer:
     """
 
     def __init__(self, params, world_size: int | None = None, bucket_bytes: int = BUCKET_BYTES,
-                 group=None):
+                 group=None, bucket_dtype: torch.dtype | None = None):
         self.params = [p for p in params if p.requires_grad]
         self.world = world_size or dist.get_world_size(group)
         self.bucket_bytes = bucket_bytes
         self.group = group
+        # packed buckets may travel in bf16 (MMDX_DP_BUCKET_DTYPE=bf16: half the xGMI bytes
+        # for C5's ~800 MB of per-tensor gradients; RCCL sums in bf16, the mean is taken in
+        # fp32 after the cast back).  The trunk arena always reduces in fp32.
+        if bucket_dtype is None and os.environ.get("MMDX_DP_BUCKET_DTYPE", "fp32") == "bf16":
+            bucket_dtype = torch.bfloat16
+        self.bucket_dtype = bucket_dtype
         self._pending = []
         self._launched = set()
-        self._regions = {}   # id(flat buffer) -> (lo, hi) already launched by launch_region
+        self._regions = {}   # id(flat buffer) -> [(lo, hi)] already launched by launch_region
         self._comm = None
+
+    def trunk_hook(self, grads, regions):
+        """resnet.TRUNK_GRAD_HOOK: start the all-reduce of each layer's slice of the trunk's
+        gradient arena from that layer's plan event (layers 4, 3, 2 in backward order)."""
+        for lo, hi, ev in regions:
+            self.launch_region(grads, lo, hi, ev)
 
     def launch_region(self, buf, lo: int, hi: int, event=None):
         """Start the all-reduce of the slice buf[lo:hi] of a flat gradient buffer once
         `event` (a torch.cuda.Event recorded after the slice is final) has fired; the rest of
-        the buffer is reduced by the next launch().  Used for the ResNet trunk's last layer
-        (resnet.TRUNK_GRAD_HOOK): its ~60 % of the trunk's gradient bytes move over xGMI
-        while the earlier layers' backward still runs."""
+        the buffer is reduced by the next launch().  Used for the ResNet trunk's layers 4..2
+        (resnet.TRUNK_GRAD_HOOK): ~90 % of the trunk's gradient bytes move over xGMI while
+        the earlier layers' backward still runs.  With RCCL the host never waits: the comm
+        stream waits on the event, the collectives queue on it in issue order."""
         if self.world == 1 or hi <= lo:
             return
         view = buf[lo:hi]
@@ -69,7 +84,7 @@ class GradAllReducer:
             tmp = view.clone()
             work = dist.all_reduce(tmp, group=self.group, async_op=True)
         self._pending.append((None, tmp, work, view))
-        self._regions[id(buf)] = (lo, hi)
+        self._regions.setdefault(id(buf), []).append((lo, hi))
 
     def _buckets(self, grads):
         plan, cur, size = [], [], 0
@@ -104,17 +119,17 @@ class GradAllReducer:
         loose = []
         for b, gs in by_base.values():
             if sum(g.numel() for g in gs) == b.numel():
-                lo, hi = self._regions.get(id(b), (b.numel(), b.numel()))
-                for a, z in ((0, lo), (hi, b.numel())):  # what launch_region left
-                    if z > a:
-                        part = b[a:z]
-                        work = dist.all_reduce(part, group=self.group, async_op=True)
-                        self._pending.append((None, part, work, None))
+                for a, z in _complement(self._regions.get(id(b), []), b.numel()):
+                    part = b[a:z]   # what launch_region left
+                    work = dist.all_reduce(part, group=self.group, async_op=True)
+                    self._pending.append((None, part, work, None))
             else:
                 loose += gs
         loose += [g for g in grads if g._base is None or not g._base.is_contiguous()]
         for bucket in self._buckets(loose):
             flat = torch._utils._flatten_dense_tensors(bucket)
+            if self.bucket_dtype is not None and flat.dtype != self.bucket_dtype:
+                flat = flat.to(self.bucket_dtype)
             work = dist.all_reduce(flat, group=self.group, async_op=True)
             self._pending.append((bucket, flat, work, None))
 
@@ -122,6 +137,8 @@ class GradAllReducer:
         inv = 1.0 / self.world
         for bucket, flat, work, dest in self._pending:
             work.wait()
+            if flat.dtype != torch.float32:
+                flat = flat.float()
             flat.mul_(inv)
             if dest is not None:
                 dest.copy_(flat)
@@ -138,6 +155,34 @@ class GradAllReducer:
             return
         self.launch()
         self.finish()
+
+
+def _complement(intervals, n):
+    """[0, n) minus the union of the half-open `intervals`, as sorted (a, z) pieces."""
+    out, cur = [], 0
+    for lo, hi in sorted(intervals):
+        if lo > cur:
+            out.append((cur, lo))
+        cur = max(cur, hi)
+    if cur < n:
+        out.append((cur, n))
+    return out
+
+
+def init_distributed(backend: str, local_rank: int, timeout_s: float = 300.0):
+    """init_process_group with fail-fast semantics for the data-parallel step:
+    RCCL's async errors are polled by torch's ProcessGroupNCCL watchdog
+    (ncclCommGetAsyncError); TORCH_NCCL_ASYNC_ERROR_HANDLING=1 makes it tear the process
+    down on an error or on a collective exceeding `timeout_s`, so a lost peer ends the job
+    with a non-zero exit instead of hanging the node."""
+    from datetime import timedelta
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=timedelta(seconds=timeout_s))
+    else:
+        dist.init_process_group(backend, timeout=timedelta(seconds=timeout_s))
 
 
 def shard_batch(batch_size: int, rank: int, world: int):

@@ -411,6 +411,7 @@ class _Plan:
         # stream once at the end, before the optimizer reads the gradients.
         self.bwd = None
         self.tail_event = None
+        self.grad_regions = []
         if keep:
             bw = _OpList()
             params = trunk.engine_params()
@@ -490,18 +491,37 @@ class _Plan:
             N_, H_, W_, C_ = self.out_geom
             dx = A.new((N_, H_, W_, C_), T, dev)
             bw.add(L.OP_AVGPOOL_BWD, dt, i=(N_, H_ * W_, C_), p=(_Ext(0), dx))
-            # the last layer's gradients (the arena's tail: engine_params is in forward
-            # order) are final once the side stream has run that layer's weight gradients
-            # (each waits for its unit's BN backward): the plan signals tail_event there, so
-            # a data-parallel all-reduce of the tail can run beside the rest of the backward
-            n_last = len(list(trunk)[7])
-            last_ids = {id(q) for q in trunk[7].parameters()}
-            self.grad_tail = min(o for i, o in self.grad_off.items() if i in last_ids) // 4
+            # Per-layer gradient regions for data parallelism.  engine_params is in forward
+            # order, so layer k's gradients are one contiguous slice of the arena and layers
+            # 4, 3, 2 are its tail.  A layer's gradients are final once the side stream has
+            # run that layer's weight gradients (each waits for its unit's BN backward, which
+            # also writes the BN parameter gradients on the main stream): the plan signals
+            # one event on the side stream right after each layer's last wgrad, so the
+            # all-reduce of layer 4 runs beside layers 3..1's backward, layer 3's beside
+            # layers 2..1's, and so on.  The stem + layer 1 (the arena's head) are reduced
+            # after the backward.  self.grad_regions: [(lo, hi, event)] in backward order.
+            layer_lo = []
+            for li in range(4, 8):
+                ids_ = {id(q) for q in trunk[li].parameters()}
+                layer_lo.append(min(o for i, o in self.grad_off.items() if i in ids_) // 4)
+            layer_hi = layer_lo[1:] + [self.grad_bytes // 4]
+            n_blocks = [len(list(trunk[li])) for li in range(4, 8)]
+            # block index (reversed order) at which layer li's backward is fully enqueued
+            done_at = {}
+            acc = 0
+            for li in (3, 2, 1):           # layer4, layer3, layer2 (indices into layer_lo)
+                acc += n_blocks[li]
+                done_at[acc] = li
+            self.grad_regions = []
+            self.grad_tail = layer_lo[3]
             self.tail_event = None
             for bi, (bu, ds_u, _shape) in enumerate(reversed(blocks)):
-                if bi == n_last:
+                if bi in done_at:
+                    li = done_at[bi]
                     bw.add(L.OP_SIGNAL, p=(A.event(),), stream=1)
-                    self.tail_event = A.bufs[-1]
+                    self.grad_regions.append((layer_lo[li], layer_hi[li], A.bufs[-1]))
+                    if li == 3:
+                        self.tail_event = A.bufs[-1]
                 # unit i's dgrad produces the gradient of unit i-1's output (no residual
                 # inside a block): it also makes unit i-1's BN-backward partials
                 dh, dres, fed = unit_bwd(bu[-1], dx, True, want_res=True,
@@ -539,10 +559,10 @@ class _Plan:
             self.bwd.freeze()
 
 
-# TRUNK_GRAD_HOOK(grads, tail_lo, event): called right after the trunk backward is enqueued
-# with the flat fp32 gradient arena, the element offset where the last layer's gradients
-# start and the event after which grads[tail_lo:] are final (data parallelism: start their
-# all-reduce early, dist.GradAllReducer.launch_region).  None = no hook.
+# TRUNK_GRAD_HOOK(grads, regions): called right after the trunk backward is enqueued with the
+# flat fp32 gradient arena and [(lo, hi, event)] for layers 4, 3, 2 (backward order): after
+# `event` fires, grads[lo:hi] is final (data parallelism: start that slice's all-reduce
+# early, dist.GradAllReducer.launch_region).  None = no hook.
 TRUNK_GRAD_HOOK = None
 _WGRAD_ON_MAIN = os.environ.get("MMDX_WGRAD_STREAM", "side") == "main"
 
@@ -625,8 +645,8 @@ class _TrunkFn(torch.autograd.Function):
                 else _side_stream(ctx.trunk_ref, dev))
         plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0], [stream(), side.cuda_stream])
         hook = TRUNK_GRAD_HOOK
-        if hook is not None and plan.tail_event is not None:
-            hook(grads, plan.grad_tail, plan.tail_event)
+        if hook is not None and plan.grad_regions:
+            hook(grads, plan.grad_regions)
         plan.arena.owner = None
         ctx.plan = ctx.x = ctx.tok = ctx.trunk_ref = None
         out = [None, None, None]

@@ -53,7 +53,7 @@ def test_grad_allreduce_mean_gloo():
 SHAPES2 = ((40, 3), (7,), (16,), (5, 5))
 
 
-def _worker_flat(rank, world, port, out, region=False):
+def _worker_flat(rank, world, port, out, region=0):
     """Gradients that are views of one flat buffer (the trunk's gradient arena) are reduced
     in place; the others through buckets; a subset is launched early (overlap path)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -68,8 +68,10 @@ def _worker_flat(rank, world, port, out, region=False):
     params[2].grad = torch.randn(16, generator=g)
     params[3].grad = torch.randn(5, 5, generator=g)
     red = GradAllReducer(params, world, bucket_bytes=64)
-    if region:  # the buffer's tail first (the trunk's last layer, resnet.TRUNK_GRAD_HOOK)
+    if region == 1:  # the buffer's tail first (the trunk's last layer)
         red.launch_region(flat, 100, flat.numel())
+    elif region == 2:  # per-layer slices in backward order (resnet.TRUNK_GRAD_HOOK)
+        red.trunk_hook(flat, [(100, 127, None), (60, 100, None), (30, 60, None)])
     red.launch([params[2]])
     red.reduce()
     assert params[0].grad._base is flat  # reduced in place, still the same buffer
@@ -77,7 +79,7 @@ def _worker_flat(rank, world, port, out, region=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("region", [False, True])
+@pytest.mark.parametrize("region", [0, 1, 2])
 def test_grad_allreduce_flat_base_and_early_launch_gloo(region):
     world = 2
     port = _free_port()
@@ -94,3 +96,45 @@ def test_grad_allreduce_flat_base_and_early_launch_gloo(region):
     for r in range(world):
         for got, want in zip(out[r], mean):
             assert torch.allclose(got, want, atol=1e-6)
+
+
+def test_complement_of_launched_regions():
+    from mmdx.dist import _complement
+    assert _complement([], 10) == [(0, 10)]
+    assert _complement([(7, 10), (3, 7)], 10) == [(0, 3)]
+    assert _complement([(2, 4), (6, 8)], 10) == [(0, 2), (4, 6), (8, 10)]
+    assert _complement([(0, 10)], 10) == []
+
+
+def _worker_bf16(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx.dist import GradAllReducer
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in SHAPES2]
+    g = torch.Generator().manual_seed(300 + rank)
+    for p in params:
+        p.grad = torch.randn(p.shape, generator=g)
+    red = GradAllReducer(params, world, bucket_bytes=64, bucket_dtype=torch.bfloat16)
+    red.reduce()
+    out[rank] = [p.grad.clone() for p in params]
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_bf16_buckets_gloo():
+    """MMDX_DP_BUCKET_DTYPE=bf16: packed buckets travel in bf16; the fp32 mean is recovered
+    to bf16 precision (rel 1e-2) and the grads stay fp32."""
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_bf16, args=(world, port, out), nprocs=world, join=True)
+    exp = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(300 + r)
+        exp.append([torch.randn(s, generator=g) for s in SHAPES2])
+    mean = [(a + b) / 2 for a, b in zip(*exp)]
+    for r in range(world):
+        for got, want in zip(out[r], mean):
+            assert got.dtype == torch.float32
+            assert (got - want).abs().max() <= 1e-2 * want.abs().max() + 1e-2

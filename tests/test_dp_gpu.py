@@ -59,16 +59,18 @@ def _worker(rank, world, port, out, early):
     img, txt, fus = _model()
     red = GradAllReducer([p for mod in (img, txt, fus) for p in mod.parameters()], world)
     tails = []
-    if early:  # the trunk's last layer reduced from the plan's mid-backward event
-        def hook(g, lo, ev):
-            tails.append((lo, g.numel()))
-            red.launch_region(g, lo, g.numel(), ev)
+    if early:  # layers 4, 3, 2 reduced from the plan's mid-backward events
+        def hook(g, regions):
+            tails.extend((lo, hi, g.numel()) for lo, hi, _ in regions)
+            red.trunk_hook(g, regions)
         RN.TRUNK_GRAD_HOOK = hook
     named = _grads(img, txt, fus, x[a:b], ids[a:b], mask[a:b], y[a:b])
     red.reduce()
     RN.TRUNK_GRAD_HOOK = None
-    if early:
-        assert len(tails) == 1 and 0 < tails[0][0] < tails[0][1], tails
+    if early:  # three contiguous slices ending at the arena's end, in backward order
+        assert len(tails) == 3, tails
+        assert tails[0][1] == tails[0][2] and tails[1][1] == tails[0][0], tails
+        assert tails[2][1] == tails[1][0] and 0 < tails[2][0] < tails[2][1], tails
     torch.cuda.synchronize()
     out[rank] = {n: p.grad.detach().cpu() for n, p in named if p.grad is not None}
     dist.destroy_process_group()

@@ -385,6 +385,54 @@ def test_adamw_matches_torch(dev):
         assert torch.allclose(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6)
 
 
+def test_adamw_state_roundtrip_and_lr_change(dev):
+    """the fused AdamW must follow torch.optim.AdamW across (i) a
+    state_dict() -> load_state_dict() into a NEW optimizer (new exp_avg / exp_avg_sq storage,
+    step restored) and (ii) an lr / weight-decay change through param_groups mid-run."""
+    g = torch.Generator().manual_seed(9)
+    shapes = [(300, 70), (70,), (5, 3)]
+    ps = [torch.randn(s, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [torch.nn.Parameter(p.to(dev)) for p in ps]
+    o_ref = torch.optim.AdamW([{"params": ref[:2], "lr": 5e-4}, {"params": ref[2:], "lr": 1e-3}],
+                              weight_decay=1e-2)
+    o_mine = mmdx.AdamW([{"params": mine[:2], "lr": 5e-4}, {"params": mine[2:], "lr": 1e-3}],
+                        weight_decay=1e-2)
+
+    def step(o_r, o_m):
+        grads = [torch.randn(s, generator=g) for s in shapes]
+        for p, gr in zip(ref, grads):
+            p.grad = gr.clone()
+        for p, gr in zip(mine, grads):
+            p.grad = gr.to(dev)
+        o_r.step()
+        o_m.step()
+
+    for _ in range(2):
+        step(o_ref, o_mine)
+    import io
+    buf = io.BytesIO()
+    torch.save(o_mine.state_dict(), buf)   # a checkpoint: fresh storage on load
+    buf.seek(0)
+    sd = torch.load(buf, weights_only=True)
+    o_mine2 = mmdx.AdamW([{"params": mine[:2], "lr": 5e-4}, {"params": mine[2:], "lr": 1e-3}],
+                         weight_decay=1e-2)
+    o_mine2.load_state_dict(sd)
+    for st in o_mine2.state.values():   # the loaded moments are new storage
+        assert all(st[k].data_ptr() != o_mine.state[p][k].data_ptr()
+                   for p in mine if p in o_mine.state for k in ("exp_avg",))
+    step(o_ref, o_mine2)
+    for gr_r, gr_m in zip(o_ref.param_groups, o_mine2.param_groups):
+        gr_r["lr"] *= 0.5
+        gr_m["lr"] *= 0.5
+        gr_r["weight_decay"] = gr_m["weight_decay"] = 0.05
+    for _ in range(2):
+        step(o_ref, o_mine2)
+    for a, b in zip(mine, ref):
+        assert torch.allclose(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6)
+    assert float(o_mine2.state[mine[0]]["step"].item()) == 5.0
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_dropout_counter_rng_and_graph_replay(dev, dt):
     """nn.Dropout semantics (TP:538): keep rate 1-p, kept values scaled by 1/(1-p), backward
