@@ -413,16 +413,13 @@ def main():
             for p in list(img.parameters()) + list(txt.parameters()) + list(fus.parameters()):
                 dist.broadcast(p, 0)
     B = cfg["batch"]
-    # Stream priorities (MMDX_PRIO): "main" issues the step on a high-priority stream (the
-    # dgrad chain, BN and the heads) so the trunk's weight-gradient stream (default priority)
-    # fills the CUs it leaves; "main+text" raises the text tower's stream too; "text" only
-    # the text tower's; "0" = all default priority.  Measured at C4 (2 x 40 steps each):
-    # main+text 7866, text 7822, main 7781, 0 7805 samples/s -> main+text is the default.
-    prio = os.environ.get("MMDX_PRIO", "main+text")
-    if prio in ("main", "main+text"):
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
+    # Stream priorities: the step is issued on a high-priority stream (the dgrad chain, BN
+    # and the heads) and the text tower's stream is high priority too, so the trunk's
+    # weight-gradient stream (default priority) fills the CUs they leave.  Measured at C4
+    # (2 x 40 steps each): main+text 7866, text only 7822, main only 7781, none 7805.
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
-    side = torch.cuda.Stream(device=dev, priority=-1 if prio in ("text", "main+text") else 0)
+    side = torch.cuda.Stream(device=dev, priority=-1)
     from mmdx.dist import GradAllReducer
     reducer = GradAllReducer(params, world) if world > 1 else None
     early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "1" if backend == "nccl" else "0")
@@ -432,11 +429,7 @@ def main():
         # CUDA path stalls the issuing host thread on it — 1.3 s/step in the one-GPU
         # rehearsal — so the gloo rehearsal keeps it off unless asked for)
         RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
-    # the text tower's backward may run on its own stream at default priority
-    # (MMDX_TEXT_BWD_PRIO=low): it is off the critical path, the image backward is not
-    side_bwd = (torch.cuda.Stream(device=dev, priority=0)
-                if os.environ.get("MMDX_TEXT_BWD_PRIO", "high") == "low" else None)
-    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd)
+    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
     timer = StepTimer()
     if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders
         MF.GEMM_TIMER = timer
@@ -446,34 +439,13 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # Launch mode.  Default "0": eager launches from the host (the two towers overlap on two
-    # streams).  "step" (MMDX_GRAPH=step): the whole step captured into one hipGraph and
-    # replayed — measured slower on ROCm 7 (the replay runs the two stream branches one after
-    # the other: 26.8 vs 22.5 ms/step at C4), so it is opt-in.  N>1 always eager.
-    mode = os.environ.get("MMDX_GRAPH", "0")
-    if world > 1:
-        mode = "0"
-    use_graph = mode != "0"
-    run = step
-    eager_step = step
-    static_loss = None
-    if mode == "step":
-        graph = torch.cuda.CUDAGraph()
-        opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(graph):
-            static_loss = step()
-        torch.cuda.synchronize()
-        run = graph.replay
-        for _ in range(2):
-            run()
-        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     # Conv (dominant-family) launch durations: HIP events around every conv launch of the
     # LAST `ev_steps` timed steps (default K/10).  Bracketing every step costs ~0.75 ms/step
     # of event markers at C4 (316 records), which would bias `value`; the sampled steps are
     # ordinary steps of the timed loop, so the per-launch average is the timed region's.
-    timing = not use_graph and os.environ.get("MMDX_BENCH_EVENTS", "1") != "0"
+    timing = os.environ.get("MMDX_BENCH_EVENTS", "1") != "0"
     ev_steps = min(args.steps, max(1, int(os.environ.get("MMDX_BENCH_EVENT_STEPS",
                                                          max(1, args.steps // 10)))))
     timer.reserve(400 * ev_steps)
@@ -481,7 +453,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         timer.enabled = timing and i >= args.steps - ev_steps
-        loss = run()
+        loss = step()
     t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (no device sync)
     torch.cuda.synchronize()
     if cfg["text"] == "bilstm":
@@ -495,20 +467,11 @@ def main():
     was = timer.enabled
     timer.enabled = False
     t1 = time.perf_counter()
-    run()
+    step()
     host_one = time.perf_counter() - t1
     torch.cuda.synchronize()
     timer.enabled = was
-    if mode == "step":
-        loss = static_loss
-    if use_graph:
-        # conv kernel durations for the roofline: HIP events around each conv launch in a few
-        # eager steps after the timed region (same kernels as the replayed graph)
-        timer.enabled = True
-        for _ in range(3):
-            eager_step()
-        torch.cuda.synchronize()
-    conv_steps = 3 if use_graph else ev_steps
+    conv_steps = ev_steps
     timer.enabled = False
     if world > 1:
         t = torch.tensor([el], device=dev)
@@ -544,8 +507,8 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
-        "launch": "hipgraph-step" if mode == "step" else "eager",
-        "stream_priority": os.environ.get("MMDX_PRIO", "main+text"),
+        "launch": "eager",
+        "stream_priority": "main+text",
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,
                    "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,

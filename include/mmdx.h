@@ -92,6 +92,15 @@ int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items, lo
 int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d);
 int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
                   void* y, float* stat_part, void* stream);
+/* Eval-mode conv + BatchNorm2d (running statistics) (+residual) (+ReLU) in one launch:
+ * y = act(conv(x, w) * s + t + residual), s = gamma / sqrt(running_var + eps),
+ * t = beta - running_mean * s, applied in the conv epilogue on the fp32 accumulators.
+ * Replaces conv + bn_apply for the backbone in eval mode (TP:206 freeze_backbone, TP:1000
+ * encoders in eval, IP:170 inference).  residual may be NULL. */
+int mmdx_conv_fwd_bn_eval(int dtype, const mmdx_conv_desc* d, const void* x,
+                          const void* w_krsc, void* y, const float* gamma, const float* beta,
+                          const float* running_mean, const float* running_var, float eps,
+                          const void* residual, int relu, void* stream);
 /* dx = dgrad + beta * dx  (beta = 1 sums the residual-path gradient in the epilogue) */
 int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
                     const void* w_crsk, void* dx, float beta, void* stream);
@@ -184,7 +193,8 @@ enum {
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
   MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PAIR_INPUT,
-  MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI
+  MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI,
+  MMDX_OP_CONV_FWD_BNEVAL
 };
 typedef struct {
   int op, dtype, stream;

@@ -51,7 +51,7 @@ class PlanOp(C.Structure):
 (OP_EVENT, OP_NCHW2NHWC, OP_CONV_PACK, OP_CONV_FWD, OP_BN_FWD, OP_MAXPOOL_FWD,
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
  OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PAIR_INPUT,
- OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI) = range(1, 21)
+ OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL) = range(1, 22)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -66,6 +66,7 @@ SIGNATURES = {
     "mmdx_conv_pack_multi": (i32, [i32, vp, i32, i64, vp]),
     "mmdx_conv_fwd_stat_blocks": (i32, [CD]),
     "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
+    "mmdx_conv_fwd_bn_eval": (i32, [i32, CD, vp, vp, vp, vp, vp, vp, vp, f32, vp, i32, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
     "mmdx_conv_dgrad_stat_blocks": (i32, [i32, CD]),
     "mmdx_conv_dgrad_bnstat": (i32, [i32, CD, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, i32, vp,

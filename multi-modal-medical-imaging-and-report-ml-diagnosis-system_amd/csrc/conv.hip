@@ -177,13 +177,8 @@ static void wgrad_reduce(const float* ws, int splits, int K, int C, int Cm, int 
   // split groups only for the deep splits (>= 128: the stem's and layer1's weight gradients,
   // at the end of the backward where little else runs); elsewhere the per-element loop, whose
   // lower memory-level parallelism disturbs the concurrent dgrad/BN chain less (all-split:
-  // 0.6 % slower train step despite 2 % less isolated wgrad time).  MMDX_WGRAD_REDUCE=
-  // element | split forces one kernel (A/B runs).
-  static const int mode = [] {
-    const char* e = getenv("MMDX_WGRAD_REDUCE");
-    return !e ? 0 : e[0] == 'e' ? 1 : e[0] == 's' ? 2 : 0;
-  }();
-  const bool per_element = mode == 1 || (mode == 0 && splits < 128);
+  // 0.6 % slower train step despite 2 % less isolated wgrad time).
+  const bool per_element = splits < 128;
   if (total % 4 != 0 || per_element) {
     const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C,
@@ -220,12 +215,8 @@ static int launch(const typename LA::SrcT& sa, const typename LB::SrcT& sb, cons
 // stage costs occupancy only where there would be a second block to lose) and the K loop
 // is long enough to keep two tiles in flight.
 static bool use_three_stages(long blocks, int ktiles_per_block) {
-  // MMDX_NS3_BLOCKS overrides the grid limit (A/B runs; C4 step: 0 and 256 tie, 512 -3.5 %)
-  static const long limit = [] {
-    const char* e = getenv("MMDX_NS3_BLOCKS");
-    return e ? atol(e) : 256L;
-  }();
-  return blocks <= limit && ktiles_per_block >= 4;
+  // grid limit measured in the C4 step: 0 and 256 tie, 512 is 3.5 % slower
+  return blocks <= 256 && ktiles_per_block >= 4;
 }
 
 template <int BM, int BN, class OA, class OB, class Epi, int NS>
@@ -271,61 +262,21 @@ static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32) {
   return !dgrad || (g.sh == 1 && g.sw == 1);
 }
 
-// 128x64 tiles when 128x128 would give fewer tiles than this (< 1.5 per CU); MMDX_TILE64_BELOW
-// overrides (A/B runs; in the C4 step 256 and 384 tie, 640 is 1.5 % slower)
-static long narrow_below() {
-  static const long v = [] {
-    const char* e = getenv("MMDX_TILE64_BELOW");
-    return e && atol(e) > 0 ? atol(e) : 384L;
-  }();
-  return v;
-}
+// 128x64 tiles when 128x128 would give fewer tiles than this (< 1.5 per CU); measured in the
+// C4 step: 256 and 384 tie, 640 is 1.5 % slower
+constexpr long kNarrowBelow = 384;
 
-// Forward-conv epilogue without the fused consumer-BN statistics (the forward never uses
-// them): the kernel then holds no BN-input registers beside a 256-row tile's accumulators.
-template <typename T>
-struct EpiStoreFwd : EpiStore<T> {
-  static constexpr bool BNSTAT = false;
-};
-
-// 256x128 tiles (2x2 waves of 128x64, one block per CU, three operand stages): a quarter
-// fewer DMA pieces and LDS fill bytes per MFMA than 128x128, where the grid still gives
-// every CU at least two tiles.  Opt-in (MMDX_CONV_TILE=256): at one block per CU the 1x1
-// convs it reaches ran 1.3-1.5x slower than 128x128 at two blocks per CU (the epilogue of
-// one block no longer overlaps the other's K loop), C4 7550 vs 7815 samples/s.
-static bool use_tile256(long M, int N) {
-  static const int mode = [] {
-    const char* e = getenv("MMDX_CONV_TILE");
-    return e && atoi(e) == 256 ? 1 : 0;
-  }();
-  return mode && N % 128 == 0 && ((M + 255) / 256) * (long)(N / 128) >= 512;
-}
-
-template <typename T, class SA>
-static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
-                     hipStream_t st, float* stats = nullptr, bool dma_ok = false,
-                     const BnStat& bs = BnStat{}) {
+template <typename T, class SA, class Epi>
+static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int N, int K,
+                         hipStream_t st, bool dma_ok) {
   DenseK<T> sb{(const T*)w, K, N, true};
-  EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
-                  (float2*)stats};
-  epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
   if constexpr (DmaOk<SA>::value) {
     if (dma_ok) {
-    if constexpr (std::is_same<SA, Im2colK<bf16, true>>::value) {
-      if (bs.part == nullptr && beta == 0.f && use_tile256(M, N)) {
-        EpiStoreFwd<T> ef;
-        static_cast<EpiStore<T>&>(ef) = epi;
-        const int nwg = ((M + 255) / 256) * (N / 128);
-        launch_dma_ns<256, 128, DmaK<256, SA>, DmaK<128, DenseK<T>>, EpiStoreFwd<T>, 3>(
-            sa, sb, ef, M, N, K, 1, K, nwg, st);
-        MMDX_LAUNCH_CHECK();
-        return 0;
-      }
-    }
-    // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
-    const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-    if (N <= 64 || tiles128 < narrow_below()) return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
-    return launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
+      // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
+      const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+      if (N <= 64 || tiles128 < kNarrowBelow)
+        return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
+      return launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
     }
   }
   if (N <= 64)
@@ -333,6 +284,16 @@ static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K
                                                                             1, K, st);
   return launch<T, 128, 128, KLoad<T, 128, SA>, KLoad<T, 128, DenseK<T>>>(sa, sb, epi, M, N, K,
                                                                             1, K, st);
+}
+
+template <typename T, class SA>
+static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
+                     hipStream_t st, float* stats = nullptr, bool dma_ok = false,
+                     const BnStat& bs = BnStat{}) {
+  EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
+                  (float2*)stats};
+  epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
+  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok);
 }
 
 template <typename T>
@@ -347,6 +308,26 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
   const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
   Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
   return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64));
+}
+
+template <typename T>
+static int conv_fwd_bn_eval_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
+                              const float* gamma, const float* beta, const float* rmean,
+                              const float* rvar, float eps, const void* res, int relu,
+                              hipStream_t st) {
+  const ConvGeom g = geom(d);
+  const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
+  EpiBnEval<T> epi;
+  static_cast<EpiStore<T>&>(epi) =
+      EpiStore<T>{(T*)y, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr, nullptr};
+  epi.gamma = gamma; epi.beta_bn = beta; epi.rmean = rmean; epi.rvar = rvar; epi.eps = eps;
+  epi.res = (const T*)res; epi.relu = relu != 0;
+  if (g.C % KTile<T>::BK == 0)
+    return conv_gemm_epi<T>(Im2colK<T, true>{(const T*)x, g, M}, w, epi, M, N, K, st,
+                            dma_geom_ok(g, false));
+  const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
+  Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
+  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, pow2 && dma_geom_ok(g, false, 64));
 }
 
 // Strided dgrad as sh*sw phase GEMMs (see DgradPhaseK); phases no tap reaches are written
@@ -378,7 +359,7 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       if constexpr (sizeof(T) == 2) {
         if (dma_geom_ok(g, false)) {
           const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-          if (N <= 64 || tiles128 < narrow_below())
+          if (N <= 64 || tiles128 < kNarrowBelow)
             rc = launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
           else
             rc = launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
@@ -422,20 +403,12 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   p.bn = N <= 64 ? 64 : 128;
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
   const long ktiles = (K + BK - 1) / BK;
-  // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small);
-  // MMDX_WGRAD_BLOCKS overrides (A/B runs).  ~4 per CU for the 3x3 convs of layer3/4 ran
-  // 4-12 % faster in isolation but 0.2 % slower in the train step (more blocks contending
-  // with the dgrad chain), so one target serves every shape.
-  static const long forced = [] {
-    const char* e = getenv("MMDX_WGRAD_BLOCKS");
-    return e && atol(e) > 0 ? atol(e) : 0L;
-  }();
-  const long target = forced ? forced : 512L;
-  // MMDX_WGRAD_MINK: least K tiles per split (A/B runs; C4 step: 8, 16, 32 within noise)
-  static const long min_kt = [] {
-    const char* e = getenv("MMDX_WGRAD_MINK");
-    return e && atol(e) > 0 ? atol(e) : 16L;
-  }();
+  // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small).
+  // Measured: 256 / 384 / 768 / 1024-block targets lose to 512 in the C4 step; ~4 per CU for
+  // the 3x3 convs of layer3/4 ran 4-12 % faster in isolation but 0.2 % slower in the train
+  // step (more blocks contending with the dgrad chain); 8 / 16 / 32 least K tiles tie.
+  const long target = 512L;
+  const long min_kt = 16L;
   long s = (target + tiles - 1) / tiles;
   s = std::max(1L, std::min(s, ktiles / min_kt));
   const long kt_per = (ktiles + s - 1) / s;
@@ -550,6 +523,22 @@ extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,
   MMDX_CHECK_ARG((long)d->N * d->P * d->Q < (1L << 31), "conv fwd: too many pixels");
   if (dtype == BF16) return conv_fwd_t<bf16>(d, x, w, y, stat_part, (hipStream_t)stream);
   return conv_fwd_t<float>(d, x, w, y, stat_part, (hipStream_t)stream);
+}
+
+extern "C" int mmdx_conv_fwd_bn_eval(int dtype, const mmdx_conv_desc* d, const void* x,
+                                     const void* w, void* y, const float* gamma,
+                                     const float* beta, const float* running_mean,
+                                     const float* running_var, float eps, const void* residual,
+                                     int relu, void* stream) {
+  int rc = check_desc(d, dtype == BF16 ? 8 : 4);
+  if (rc) return rc;
+  MMDX_CHECK_ARG(gamma && beta && running_mean && running_var, "conv fwd bn-eval: null BN");
+  MMDX_CHECK_ARG((long)d->N * d->P * d->Q < (1L << 31), "conv fwd: too many pixels");
+  if (dtype == BF16)
+    return conv_fwd_bn_eval_t<bf16>(d, x, w, y, gamma, beta, running_mean, running_var, eps,
+                                    residual, relu, (hipStream_t)stream);
+  return conv_fwd_bn_eval_t<float>(d, x, w, y, gamma, beta, running_mean, running_var, eps,
+                                   residual, relu, (hipStream_t)stream);
 }
 
 extern "C" int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,

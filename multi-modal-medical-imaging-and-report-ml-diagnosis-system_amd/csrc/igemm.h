@@ -947,6 +947,64 @@ struct EpiStore {
   }
 };
 
+// Eval-mode BatchNorm folded into the producing conv (TP:206 / TP:1000 / IP:170: the
+// backbone in eval mode normalises with running statistics, an affine map per channel):
+// C = act(acc * scale[n] + shift[n] (+ res[m][n])), scale = gamma * rsqrt(var + eps),
+// shift = beta - mean * scale, computed in the epilogue from the BN's own tensors (no fold
+// kernel, no re-packed weights, fp32 math on the fp32 accumulators).  Replaces the conv
+// store + bn_apply pass of the eval forward.
+template <typename OutT>
+struct EpiBnEval : EpiStore<OutT> {
+  static constexpr bool BNSTAT = false;
+  const float *gamma, *beta_bn, *rmean, *rvar;
+  float eps;
+  const OutT* res;  // residual [M][ldc] or null
+  bool relu;
+  __device__ __forceinline__ void coef(int n, float& sc, float& sh) const {
+    sc = gamma[n] * rsqrtf(rvar[n] + eps);
+    sh = beta_bn[n] - rmean[n] * sc;
+  }
+  __device__ __forceinline__ float fin(float v, int n, long off) const {
+    float sc, sh;
+    coef(n, sc, sh);
+    v = v * sc + sh;
+    if (res) v += to_f(res[off]);
+    return relu ? fmaxf(v, 0.f) : v;
+  }
+  __device__ __forceinline__ bool vec8_ok() const {
+    return this->ldc % 8 == 0 && ((uintptr_t)this->C & 15) == 0 && ((uintptr_t)res & 15) == 0;
+  }
+  __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
+    if (m >= this->M) return;
+    const long off = (long)m * this->ldc + n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (n + j < this->N) this->C[off + j] = from_f<OutT>(fin(v[j], n + j, off + j));
+  }
+  __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
+    if (m >= this->M) return;
+    if (n + 8 > this->N) {
+      apply4(m, n, lo);
+      if (n + 4 < this->N) apply4(m, n + 4, hi);
+      return;
+    }
+    const long off = (long)m * this->ldc + n;
+    typedef __attribute__((ext_vector_type(8))) OutT O8;
+    O8 r{};
+    if (res) r = *(const O8*)(res + off);
+    O8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sc, sh;
+      coef(n + j, sc, sh);
+      float v = (j < 4 ? lo[j] : hi[j - 4]) * sc + sh;
+      if (res) v += to_f(r[j]);
+      o[j] = from_f<OutT>(relu ? fmaxf(v, 0.f) : v);
+    }
+    *(O8*)(this->C + off) = o;
+  }
+};
+
 // Raw fp32 partial for split-K: ws[z][M][N].
 struct EpiPartial {
   float* ws; int M, N;

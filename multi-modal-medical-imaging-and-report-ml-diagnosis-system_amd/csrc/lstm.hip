@@ -460,7 +460,7 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
     bf16* hx = (bf16*)ws;
     unsigned* ctr = (unsigned*)((char*)ws + (size_t)2 * 2 * B * H * 2);
     const long spin_max = spin_limit > 0 ? spin_limit : COOP_SPIN_MAX;
-    hipMemsetAsync(ctr, 0, 64, st);
+    (void)hipMemsetAsync(ctr, 0, 64, st);
     const dim3 grid(COOP_NB, 2);
 #define COOP_LAUNCH(RT)                                                                      \
   do {                                                                                       \

@@ -377,29 +377,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
-// slab count above which a whole block (not one wave) reduces a channel's partials;
-// MMDX_FIN_WIDE overrides (A/B runs; C4 step: 128 and 512 tie, 2048 -1.6 %)
-static int fin_wide() {
-  static const int v = [] {
-    const char* e = getenv("MMDX_FIN_WIDE");
-    return e && atoi(e) > 0 ? atoi(e) : 512;
-  }();
-  return v;
-}
+// slab count above which a whole block (not one wave) reduces a channel's partials
+// (C4 step: 128 and 512 tie, 2048 -1.6 %)
+static int fin_wide() { return 512; }
 
 // >= 4 row iterations per block so the per-channel coefficient loads are amortised
 static int grid_rows(long rows, int C, int vec) {
-  // MMDX_BN_ITERS / MMDX_BN_MAXBLOCKS override the row iterations per block and the grid cap
-  // (A/B runs; C4 step: 2 and 4 iterations tie, 8 is 0.5 % slower; cap 8192 beat 4096 in
-  // 4 of 4 paired runs, +0.3 %, 2048 -1 %, 16384 no better)
-  static const long per = [] {
-    const char* e = getenv("MMDX_BN_ITERS");
-    return e && atol(e) > 0 ? atol(e) : 4L;
-  }();
-  static const long cap = [] {
-    const char* e = getenv("MMDX_BN_MAXBLOCKS");
-    return e && atol(e) > 0 ? atol(e) : 8192L;
-  }();
+  // row iterations per block and grid cap, measured in the C4 step: 2 and 4 iterations tie,
+  // 8 is 0.5 % slower; cap 8192 beat 4096 in 4 of 4 paired runs (+0.3 %), 2048 -1 %
+  const long per = 4L;
+  const long cap = 8192L;
   const RowTile rt = row_tile(C, vec);
   const long iters = (rows + rt.rpi - 1) / rt.rpi;
   return (int)std::max<long>(1, std::min<long>((iters + per - 1) / per, cap));

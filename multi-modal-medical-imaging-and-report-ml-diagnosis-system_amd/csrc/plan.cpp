@@ -44,6 +44,12 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_CONV_FWD:
       return mmdx_conv_fwd(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
                            (float*)P(o, 3, ext), s);
+    case MMDX_OP_CONV_FWD_BNEVAL:
+      // i: relu; f: eps; p: x, w, y, gamma, beta, running_mean, running_var, residual
+      return mmdx_conv_fwd_bn_eval(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
+                                   (const float*)P(o, 3, ext), (const float*)P(o, 4, ext),
+                                   (const float*)P(o, 5, ext), (const float*)P(o, 6, ext),
+                                   o.f[0], P(o, 7, ext), o.i[0], s);
     case MMDX_OP_BN_FWD:
       // i: train, C, stat_blocks, relu; l: rows, stat_rows, ws_bytes; f: momentum, eps
       return mmdx_bn_fwd(o.dtype, o.i[0], P(o, 0, ext), o.l[0], o.i[1],

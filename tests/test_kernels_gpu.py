@@ -151,10 +151,9 @@ def _conv_case(dev, dt, cfg):
 
 
 @pytest.mark.parametrize("cfg", [(21, 64, 56, 56, 256, 3, 1, 1), (11, 256, 56, 56, 512, 1, 1, 0)])
-def test_conv_fwd_tile256(dev, cfg):
-    """bf16 forward on grids large enough for the 256x128 tile (>= 512 tiles), M ragged
-    (M mod 256 = 64 / 128: the last tile's second 128-row slab is empty / partial), with
-    the per-128-row BN statistics the two wave rows store directly."""
+def test_conv_fwd_large_ragged(dev, cfg):
+    """bf16 forward on large grids (>= 512 256-row tiles), M ragged (M mod 256 = 64 / 128:
+    the last 128-row slabs are partial), with the per-128-row BN statistics slabs."""
     N, C, H, W, K, k, s, p = cfg
     g = torch.Generator().manual_seed(7)
     x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
@@ -644,3 +643,44 @@ def test_conv_pack_multi_matches_single(dev):
         assert torch.equal(wk, rk)
         if wc is not None:
             assert torch.equal(wc, rc)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg,res,relu", [((2, 64, 14, 14, 256, 1, 1, 0), True, True),
+                                          ((3, 64, 15, 15, 64, 3, 2, 1), False, True),
+                                          ((2, 128, 9, 9, 512, 3, 1, 1), True, False)])
+def test_conv_fwd_bn_eval(dev, dt, cfg, res, relu):
+    """Eval-mode conv + BatchNorm (running stats) (+residual) (+ReLU) in one launch
+    (mmdx_conv_fwd_bn_eval) vs torch: relu(bn_eval(conv(x, w)) + res)."""
+    N, C, H, W, K, k, s, p = cfg
+    g = torch.Generator().manual_seed(sum(cfg) + res)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, k, k, generator=g) * 0.1
+    gamma, beta = torch.randn(K, generator=g), torch.randn(K, generator=g)
+    rm, rv = torch.randn(K, generator=g) * 0.3, torch.rand(K, generator=g) + 0.5
+    if dt == torch.bfloat16:
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    y = tF.conv2d(x, w, stride=s, padding=p)
+    y = tF.batch_norm(y, rm, rv, gamma, beta, training=False, eps=1e-5)
+    P, Q = y.shape[2], y.shape[3]
+    r = torch.randn(N, K, P, Q, generator=g)
+    if dt == torch.bfloat16:
+        r = r.bfloat16().float()
+    if res:
+        y = y + r
+    if relu:
+        y = y.clamp(min=0)
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q)
+    dc = L.dtype_code(dt)
+    wk = torch.empty(K, k, k, C, dtype=dt, device=dev)
+    wc = torch.empty(C, k, k, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", dc, d, C, w.to(dev).data_ptr(), wk.data_ptr(),
+           wc.data_ptr(), L.stream())
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    rd = r.permute(0, 2, 3, 1).contiguous().to(dev, dt)
+    out = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    bn = [t.to(dev) for t in (gamma, beta, rm, rv)]
+    L.call("mmdx_conv_fwd_bn_eval", dc, d, xd.data_ptr(), wk.data_ptr(), out.data_ptr(),
+           *[t.data_ptr() for t in bn], 1e-5, rd.data_ptr() if res else None, int(relu),
+           L.stream())
+    _close(out.permute(0, 3, 1, 2), y, dt, f"bn-eval {cfg}")
