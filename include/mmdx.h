@@ -349,6 +349,14 @@ int mmdx_embed_scatter(int dtype, const int64_t* ids, long n, int D, const void*
 int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
                        int H, float scale, float p_drop, uint64_t seed, uint64_t* counter,
                        void* out, float* probs, void* stream);
+/* As mmdx_attention_fwd, plus an additive fp32 score bias [H][L][L] shared by the batch
+ * (T5's relative position bias; NULL = none) and a causal mask (key > query masked). */
+int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* mask, const float* bias,
+                          int causal, int B, int L, int H, float scale, float p_drop,
+                          uint64_t seed, uint64_t* counter, void* out, float* probs,
+                          void* stream);
+/* The backward leaves dS (the score gradient = the bias gradient) in the workspace as
+ * [B][H][L][roundup32(L)] compute dtype, for mmdx_t5_position_bias_bwd. */
 size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H);
 int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const void* dout,
                        const int64_t* mask, int B, int L, int H, float scale, float p_drop,
@@ -378,6 +386,56 @@ int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c
                   const float* gates_save, const void* dh_out, int B, int L, int H,
                   void* dxg, float* dw_hh, void* workspace, size_t ws_bytes,
                   void* stream);
+
+/* ---------------------------------------------------------------- T5 report head
+ * (TP:545-618 cond_proj + T5ForConditionalGeneration, TP:983-991 /
+ * TP:1049-1053 teacher-forced CE, IP:190-196 beam generate).  transformers' T5 arithmetic:
+ * T5LayerNorm (RMSNorm, no mean / bias), unscaled self-attention with a relative-position
+ * bias and a causal mask (mmdx_attention_fwd_ex), cross-attention over the K condition
+ * tokens, ReLU FFN, tied lm_head on d_model^-0.5-scaled states, CE with ignore_index -100.
+ * rmsnorm: y = w * x * rsqrt(mean(x^2) + eps); save_rstd [rows] fp32.
+ * rmsnorm_bwd: dx = (grad) + beta * dx (beta = 1 adds onto a residual gradient);
+ * dw (+)= dw_beta * dw + sum_rows dy * x * rstd (dw may be NULL). */
+int mmdx_rmsnorm_fwd(int dtype, const void* x, long rows, int D, const float* w, float eps,
+                     void* y, float* save_rstd, void* stream);
+size_t mmdx_rmsnorm_workspace_size(long rows, int D);
+int mmdx_rmsnorm_bwd(int dtype, const void* x, const void* dy, long rows, int D,
+                     const float* w, const float* save_rstd, void* dx, float beta, float* dw,
+                     float dw_beta, void* workspace, size_t ws_bytes, void* stream);
+/* bias[h][q][k] = table[bucket(q - k)][h], table [num_buckets][H] (relative_attention_bias
+ * .weight), causal (decoder) buckets of T5Attention._relative_position_bucket. */
+int mmdx_t5_position_bias(const float* table, int H, int L, int num_buckets, int max_distance,
+                          float* bias, void* stream);
+/* dtable (+)= bucketed sum over batch and cells of dscores [B][H][L][ld] (compute dtype). */
+int mmdx_t5_position_bias_bwd(int dtype, const void* dscores, int B, int H, int L, int ld,
+                              int num_buckets, int max_distance, float* dtable, float beta,
+                              void* stream);
+/* Cross-attention over Lk <= 16 keys (the K condition tokens), head dim 64, no mask:
+ * q rows [B][Lq] of ldq elements (head h at h*64); kv [B][Lk][2][H][64] (k then v);
+ * out [B][Lq][H][64]; probs [B][H][Lq][Lk] fp32 (dropout keep bit in the sign, as
+ * mmdx_attention_fwd).  dq rows of lddq elements; dkv like kv. */
+int mmdx_xattn_fwd(int dtype, const void* q, long ldq, const void* kv, int B, int Lq, int Lk,
+                   int H, float scale, float p_drop, uint64_t seed, uint64_t* counter,
+                   void* out, float* probs, void* stream);
+size_t mmdx_xattn_workspace_size(int B, int Lq, int Lk, int H);
+int mmdx_xattn_bwd(int dtype, const void* q, long ldq, const void* kv, const float* probs,
+                   const void* dout, int B, int Lq, int Lk, int H, float scale, float p_drop,
+                   void* dq, long lddq, void* dkv, void* workspace, size_t ws_bytes,
+                   void* stream);
+/* CrossEntropyLoss(ignore_index=-100) mean over the rows whose target is in [0, V):
+ * loss, count (device scalars).  The workspace keeps per-row log-sum-exp for the backward:
+ * dlogits = (softmax - onehot) * dloss / count (dloss device scalar or NULL = 1). */
+size_t mmdx_cross_entropy_workspace_size(long rows);
+int mmdx_cross_entropy_fwd(const float* logits, const int64_t* targets, long rows, long V,
+                           float* loss, float* count, void* workspace, size_t ws_bytes,
+                           void* stream);
+int mmdx_cross_entropy_bwd(int dtype, const float* logits, const int64_t* targets, long rows,
+                           long V, const float* dloss, const float* count,
+                           const void* workspace, void* dlogits, void* stream);
+/* row-wise log_softmax (beam search scores) */
+int mmdx_log_softmax(const float* logits, long rows, long V, float* out, void* stream);
+/* dx = dy * (y > 0) (T5 DenseReluDense backward from the ReLU output) */
+int mmdx_relu_bwd(int dtype, const void* y, const void* dy, long n, void* dx, void* stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.AdamW (decoupled weight decay) over every tensor of every param group in

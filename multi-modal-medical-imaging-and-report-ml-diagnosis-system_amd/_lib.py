@@ -116,6 +116,8 @@ SIGNATURES = {
     "mmdx_embed_gather": (i32, [i32, vp, i64, i32, vp, vp, vp]),
     "mmdx_embed_scatter": (i32, [i32, vp, i64, i32, vp, vp, vp]),
     "mmdx_attention_fwd": (i32, [i32, vp, vp, i32, i32, i32, f32, f32, u64, vp, vp, vp, vp]),
+    "mmdx_attention_fwd_ex": (i32, [i32, vp, vp, vp, i32, i32, i32, i32, f32, f32, u64, vp, vp,
+                                    vp, vp]),
     "mmdx_attention_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp, vp, sz, vp]),
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp, i64, i32, vp]),
@@ -127,6 +129,21 @@ SIGNATURES = {
     "mmdx_vit_tokens_bwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),
     "mmdx_rows_copy": (i32, [i32, vp, i64, vp, i64, i64, i32, vp]),
     "mmdx_add": (i32, [i32, i64, vp, vp, vp, vp]),
+    "mmdx_rmsnorm_fwd": (i32, [i32, vp, i64, i32, vp, f32, vp, vp, vp]),
+    "mmdx_rmsnorm_workspace_size": (sz, [i64, i32]),
+    "mmdx_rmsnorm_bwd": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, f32, vp, f32, vp, sz, vp]),
+    "mmdx_t5_position_bias": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "mmdx_t5_position_bias_bwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, f32, vp]),
+    "mmdx_xattn_fwd": (i32, [i32, vp, i64, vp, i32, i32, i32, i32, f32, f32, u64, vp, vp, vp,
+                             vp]),
+    "mmdx_xattn_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_xattn_bwd": (i32, [i32, vp, i64, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i64,
+                             vp, vp, sz, vp]),
+    "mmdx_cross_entropy_workspace_size": (sz, [i64]),
+    "mmdx_cross_entropy_fwd": (i32, [vp, vp, i64, i64, vp, vp, vp, sz, vp]),
+    "mmdx_cross_entropy_bwd": (i32, [i32, vp, vp, i64, i64, vp, vp, vp, vp, vp]),
+    "mmdx_log_softmax": (i32, [vp, i64, i64, vp, vp]),
+    "mmdx_relu_bwd": (i32, [i32, vp, vp, i64, vp, vp]),
     "mmdx_adamw_multi": (i32, [i32, vp, f32, f32, f32, vp, vp, vp]),
     "mmdx_grad_norm_workspace_size": (sz, [i32]),
     "mmdx_grad_norm": (i32, [i32, vp, f32, vp, vp, vp, sz, vp]),

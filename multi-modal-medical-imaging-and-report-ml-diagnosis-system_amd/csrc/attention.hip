@@ -77,7 +77,8 @@ __device__ __forceinline__ uint32_t attn_hash64(uint64_t x) {
 
 template <typename T>
 __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask,
-                                int L, int H, float scale, float p_drop, uint64_t seed,
+                                const float* __restrict__ bias, int causal, int L, int H,
+                                float scale, float p_drop, uint64_t seed,
                                 const uint64_t* __restrict__ ctr, T* __restrict__ out,
                                 float* __restrict__ probs) {
   typedef MfmaOp<T> Op;
@@ -121,7 +122,12 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
     const float madd = key < L ? (mask && mask[(long)b * L + key] == 0 ? MASK_NEG : 0.f) : -INFINITY;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      s[j][r] = s[j][r] * scale + madd;
+      const int q = q0 + wid * 16 + (lane >> 4) * 4 + r;
+      float v = s[j][r] * scale + madd;
+      // additive score bias [H][L][L] (T5 relative position bias) and causal mask
+      if (bias && key < L && q < L) v += bias[((long)h * L + q) * L + key];
+      if (causal && key > q && key < L) v = MASK_NEG;
+      s[j][r] = v;
       mx[r] = fmaxf(mx[r], s[j][r]);
     }
   }
@@ -364,9 +370,10 @@ using namespace mmdx;
 
 __global__ void attn_counter_incr_kernel(uint64_t* c) { c[0] += 1; }
 
-extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
-                                  int H, float scale, float p_drop, uint64_t seed,
-                                  uint64_t* counter, void* out, float* probs, void* stream) {
+extern "C" int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* mask,
+                                     const float* bias, int causal, int B, int L, int H,
+                                     float scale, float p_drop, uint64_t seed,
+                                     uint64_t* counter, void* out, float* probs, void* stream) {
   MMDX_CHECK_ARG(B > 0 && H > 0 && L > 0 && L <= 16 * MAXKT, "attention: L=%d > 256", L);
   MMDX_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "attention: dropout p=%g out of range",
                  (double)p_drop);
@@ -379,8 +386,8 @@ extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mas
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     hipLaunchKernelGGL(attn_fwd_kernel<bf16>, dim3((L + QB - 1) / QB, H, B),
-                       dim3(AttnCfg<bf16>::NW * 64), sm, st, (const bf16*)qkv, mask, L, H, scale,
-                       p_drop, seed, (const uint64_t*)counter, (bf16*)out, probs);
+                       dim3(AttnCfg<bf16>::NW * 64), sm, st, (const bf16*)qkv, mask, bias, causal, L,
+                       H, scale, p_drop, seed, (const uint64_t*)counter, (bf16*)out, probs);
   } else {
     constexpr int QB = AttnCfg<float>::NW * 16;
     const size_t sm = fwd_smem<float>(L);
@@ -388,13 +395,20 @@ extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mas
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<float>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     hipLaunchKernelGGL(attn_fwd_kernel<float>, dim3((L + QB - 1) / QB, H, B),
-                       dim3(AttnCfg<float>::NW * 64), sm, st, (const float*)qkv, mask, L, H,
-                       scale, p_drop, seed, (const uint64_t*)counter, (float*)out, probs);
+                       dim3(AttnCfg<float>::NW * 64), sm, st, (const float*)qkv, mask, bias, causal,
+                       L, H, scale, p_drop, seed, (const uint64_t*)counter, (float*)out, probs);
   }
   if (p_drop > 0.f && counter)
     hipLaunchKernelGGL(attn_counter_incr_kernel, dim3(1), dim3(1), 0, st, counter);
   MMDX_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mask, int B, int L,
+                                  int H, float scale, float p_drop, uint64_t seed,
+                                  uint64_t* counter, void* out, float* probs, void* stream) {
+  return mmdx_attention_fwd_ex(dtype, qkv, mask, nullptr, 0, B, L, H, scale, p_drop, seed,
+                               counter, out, probs, stream);
 }
 
 extern "C" size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H) {

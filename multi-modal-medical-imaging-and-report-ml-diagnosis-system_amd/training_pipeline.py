@@ -392,34 +392,47 @@ class FusionTransformerModel(nn.Module):
         h = drop(h)
         return ln(h)
 
+    def _t5(self):
+        if self.report_model is None:
+            raise NotImplementedError(
+                "no T5 report head attached: build the fusion model with with_report_head=True, "
+                "init_t5_from_config=True or t5_assets_dir (TP:561-569)")
+        head = getattr(self, "_t5_head", None)
+        if head is None or head.m is not self.report_model:
+            from .t5 import T5Head
+            head = self._t5_head = T5Head(self.report_model)
+        return head
+
     def forward(self, z_img, z_txt, report_input_ids=None, report_attention_mask=None,
                 report_labels=None):  # TP:584-610
         z_fuse = self._fuse(z_img, z_txt)
         disease_logits = self.disease_head(z_fuse, out_dtype=torch.float32)
         gen = None
         if (report_input_ids is not None) or (report_labels is not None):
-            if self.report_model is None:
-                raise NotImplementedError(
-                    "T5 report generation is outside the mmdx hot path; build the fusion "
-                    "model with with_report_head=True / t5_assets_dir to attach it")
-            enc = self._make_encoder_outputs(z_fuse)
-            gen = self.report_model(encoder_outputs=enc, labels=report_labels, return_dict=True)
+            # T5 decoder conditioned on K tokens from z_fuse, teacher-forced CE on the labels
+            # (TP:595-604; report_input_ids / mask are accepted and unused, as in the reference)
+            head = self._t5()
+            enc = self._make_encoder_outputs(z_fuse).last_hidden_state
+            loss, logits = head.forward(enc, labels=report_labels, T=z_fuse.dtype)
+            gen = SimpleNamespace(loss=loss, logits=logits)
         return {"z_fuse": z_fuse, "disease_logits": disease_logits, "gen": gen}
 
     def _make_encoder_outputs(self, z_fuse):  # TP:574-578
         from transformers.modeling_outputs import BaseModelOutput
         B = z_fuse.size(0)
         cond = self.cond_proj[0](z_fuse, act=L.ACT_GELU)
-        cond = cond.view(B, self.n_cond, self.h_dec).float()
+        cond = cond.view(B, self.n_cond, self.h_dec)
         return BaseModelOutput(last_hidden_state=cond)
 
     @torch.no_grad()
     def generate(self, z_img, z_txt, **gen_kwargs):  # TP:613-618
-        if self.report_model is None:
-            raise NotImplementedError("T5 report head not attached (outside the hot path)")
+        """Beam-search report token ids (the reference's report_model.generate kwargs:
+        num_beams, max_new_tokens, min_new_tokens, no_repeat_ngram_size, length_penalty,
+        early_stopping, eos_token_id, pad_token_id) on the mmdx T5 decoder."""
+        head = self._t5()
         z_fuse = self._fuse(z_img, z_txt)
-        return self.report_model.generate(encoder_outputs=self._make_encoder_outputs(z_fuse),
-                                          **gen_kwargs)
+        enc = self._make_encoder_outputs(z_fuse).last_hidden_state
+        return head.generate(enc, T=z_fuse.dtype, **gen_kwargs)
 
 
 def _build_t5(model_name, init_from_config, assets_dir):
@@ -429,6 +442,10 @@ def _build_t5(model_name, init_from_config, assets_dir):
         return None
     if assets_dir:
         return T5ForConditionalGeneration.from_pretrained(assets_dir, local_files_only=True)
-    # t5-small geometry without any download
-    cfg = T5Config(d_model=512, d_ff=2048, num_layers=6, num_heads=8, vocab_size=32128)
+    # t5-small geometry (its config.json values) without any download
+    cfg = T5Config(d_model=512, d_ff=2048, d_kv=64, num_layers=6, num_decoder_layers=6,
+                   num_heads=8, vocab_size=32128, relative_attention_num_buckets=32,
+                   relative_attention_max_distance=128, dropout_rate=0.1,
+                   layer_norm_epsilon=1e-6, feed_forward_proj="relu", decoder_start_token_id=0,
+                   eos_token_id=1, pad_token_id=0, tie_word_embeddings=True)
     return T5ForConditionalGeneration(cfg)

@@ -40,3 +40,30 @@ def test_inference_matches_oracle(dev):
     for j in range(13):
         if abs(probs[j].item() - 0.5) > 1e-4:
             assert out["disease_vector"][j] == int(vec[j])
+
+
+def test_inference_with_t5_report_head(dev):
+    """IP:190-196 on the mmdx T5 decoder: a bundle whose fusion model carries the report head
+    beam-generates report token ids (no T5 tokenizer ships offline, so report_text stays ""
+    and the ids come back as report_ids); the disease branch is unchanged by the head."""
+    from mmdx.inference_pipeline import inference
+    import mmdx
+    _, img, txt, fus0 = build_pair("resnet18", "embed-mean")
+    torch.manual_seed(3)
+    fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13, dropout=0.0, init_t5_from_config=True)
+    sd = {k: v for k, v in fus0.state_dict().items()}
+    fus.load_state_dict(sd, strict=False)
+    pil = Image.open(os.path.join(GOLD, "e1.jpg")).convert("RGB")
+    with open(os.path.join(GOLD, "patient_details.json")) as f:
+        text = json.load(f)["e1.jpg"]
+    base = {"image_encoder": img, "text_encoder": txt, "class_names": mmdx.DISEASES,
+            "thresholds": [0.5] * 13, "version": 1, "t5_tok": None}
+    out0 = inference(dict(base, fusion_model=fus0), pil, text, device="cuda")
+    out = inference(dict(base, fusion_model=fus), pil, text, device="cuda",
+                    gen_kwargs={"max_new_tokens": 10, "min_new_tokens": 4})
+    assert out["report_generated"] and out["report_text"] == ""
+    ids = out["report_ids"]
+    assert ids[0] == 0 and 5 <= len(ids) <= 11
+    assert 1 not in ids[1:5]            # min_new_tokens: no EOS among the first 4 new tokens
+    for c in mmdx.DISEASES:
+        assert abs(out["disease_probs"][c] - out0["disease_probs"][c]) <= 1e-6

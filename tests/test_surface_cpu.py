@@ -200,7 +200,7 @@ def test_bundle_fusion_state_strict(tmp_path):
               "bert_tokenizer_name": "bert-base-uncased", "version": 3}
     ok = tmp_path / "ok.pt"
     torch.save(bundle, ok)
-    b = load_model_bundle(str(ok), device="cpu")
+    b = load_model_bundle(str(ok), device="cpu", with_report_head=False)
     assert b["text_encoder"].model_name == "embed-mean"
     assert torch.equal(b["fusion_model"].disease_head.weight, fus.disease_head.weight)
     fs2 = dict(fs)
@@ -209,4 +209,23 @@ def test_bundle_fusion_state_strict(tmp_path):
     bad = tmp_path / "bad.pt"
     torch.save(bundle, bad)
     with pytest.raises(RuntimeError):
-        load_model_bundle(str(bad), device="cpu")
+        load_model_bundle(str(bad), device="cpu", with_report_head=False)
+
+
+def test_bundle_with_t5_report_head_roundtrip(tmp_path):
+    """A bundle written with the T5 report head (report_model.*: the reference's
+    FusionTransformerModel state, TP:783-791) loads into the mmdx fusion model with its T5
+    head, every key strictly, bit-identical."""
+    from mmdx.inference_pipeline import load_model_bundle, save_model_bundle
+    torch.manual_seed(0)
+    img = mmdx.ImageEncoderCNN("resnet18", 1024, 13)
+    txt = mmdx.TextEncoderTransformer("embed-mean", 512, 13)
+    fus = mmdx.FusionTransformerModel(1024, 512, 1024, 13, init_t5_from_config=True)
+    path = save_model_bundle(fus, img, txt, tmp_path, version=2, timestamped_copy=False)
+    b = load_model_bundle(path, device="cpu")
+    f2 = b["fusion_model"]
+    assert f2.report_model is not None
+    sd, rsd = f2.state_dict(), fus.state_dict()
+    assert set(sd) == set(rsd)
+    for k in rsd:
+        assert torch.equal(sd[k], rsd[k]), k
