@@ -12,7 +12,9 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmmdx_hip.so")
+# MMDX_LIB_PATH: an alternative build of the same library (A/B measurements of two builds
+# in one GPU session); the product path loads the in-tree lib/libmmdx_hip.so
+LIB_PATH = os.environ.get("MMDX_LIB_PATH") or os.path.join(_HERE, "lib", "libmmdx_hip.so")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2

@@ -58,9 +58,12 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--filter", default="", help="substring of the shape string to run")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--lib", default="", help="alternative libmmdx_hip.so (A/B builds)")
     a = ap.parse_args()
     import mmdx
     from mmdx import _lib as L
+    if a.lib:
+        L.LIB_PATH = os.path.abspath(a.lib)
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16
     dc = L.dtype_code(dt)
