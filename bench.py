@@ -400,7 +400,8 @@ def main():
         torch.cuda.set_device(local)
         init_distributed(backend, local)   # RCCL async errors / timeouts fail the job fast
     dev = torch.device("cuda", local)
-    dtype = torch.bfloat16
+    # C5 is specified as "fp16 MFMA" (BASELINE.json); C2-C4 compute in bf16 (fp32 masters)
+    dtype = torch.float16 if cfg["image"] == "vit_b_16" else torch.bfloat16
 
     import mmdx
     from mmdx import resnet as RN
@@ -504,7 +505,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp16" if dtype == torch.float16 else "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
         "launch": "eager",

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # in one GPU session); the product path loads the in-tree lib/libmmdx_hip.so
 LIB_PATH = os.environ.get("MMDX_LIB_PATH") or os.path.join(_HERE, "lib", "libmmdx_hip.so")
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
 vp, i32, i64, f32, sz, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_size_t, C.c_uint64
@@ -217,7 +217,9 @@ def dtype_code(dt: torch.dtype) -> int:
         return F32
     if dt == torch.bfloat16:
         return BF16
-    raise TypeError(f"mmdx kernels compute in float32 or bfloat16, got {dt}")
+    if dt == torch.float16:
+        return F16   # the C5 path (GEMM, attention, norms, ViT / BERT kernels)
+    raise TypeError(f"mmdx kernels compute in float32, bfloat16 or float16, got {dt}")
 
 
 _RNG_COUNTERS: dict = {}

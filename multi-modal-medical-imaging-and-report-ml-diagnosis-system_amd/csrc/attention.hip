@@ -26,6 +26,7 @@ constexpr float MASK_NEG = -1e30f;
 template <typename T> struct AttnCfg;
 template <> struct AttnCfg<bf16> { static constexpr int NW = 4; };   // 64 query rows / block
 template <> struct AttnCfg<float> { static constexpr int NW = 2; };  // 32 query rows / block
+template <> struct AttnCfg<f16> { static constexpr int NW = 4; };
 
 __device__ __forceinline__ float rowgroup_max(float v) {
 #pragma unroll
@@ -380,24 +381,16 @@ extern "C" int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* 
   MMDX_CHECK_ARG(p_drop == 0.f || probs,
                  "attention: dropout needs the saved probabilities (training)");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == BF16) {
-    constexpr int QB = AttnCfg<bf16>::NW * 16;
-    const size_t sm = fwd_smem<bf16>(L);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL(attn_fwd_kernel<bf16>, dim3((L + QB - 1) / QB, H, B),
-                       dim3(AttnCfg<bf16>::NW * 64), sm, st, (const bf16*)qkv, mask, bias, causal, L,
-                       H, scale, p_drop, seed, (const uint64_t*)counter, (bf16*)out, probs);
-  } else {
-    constexpr int QB = AttnCfg<float>::NW * 16;
-    const size_t sm = fwd_smem<float>(L);
-    MMDX_CHECK_ARG(sm <= 160 * 1024, "attention fp32: L=%d needs %zu B LDS", L, sm);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<float>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, dim3((L + QB - 1) / QB, H, B),
-                       dim3(AttnCfg<float>::NW * 64), sm, st, (const float*)qkv, mask, bias, causal,
-                       L, H, scale, p_drop, seed, (const uint64_t*)counter, (float*)out, probs);
-  }
+  MMDX_DISPATCH(dtype, {
+    constexpr int QB = AttnCfg<T>::NW * 16;
+    const size_t sm = fwd_smem<T>(L);
+    MMDX_CHECK_ARG(sm <= 160 * 1024, "attention: L=%d needs %zu B LDS", L, sm);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3((L + QB - 1) / QB, H, B),
+                       dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, mask, bias, causal, L,
+                       H, scale, p_drop, seed, (const uint64_t*)counter, (T*)out, probs);
+  });
   if (p_drop > 0.f && counter)
     hipLaunchKernelGGL(attn_counter_incr_kernel, dim3(1), dim3(1), 0, st, counter);
   MMDX_LAUNCH_CHECK();
@@ -413,7 +406,7 @@ extern "C" int mmdx_attention_fwd(int dtype, const void* qkv, const int64_t* mas
 
 extern "C" size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H) {
   const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
-  return (size_t)B * H * L * LP * (dtype == BF16 ? 2 : 4);
+  return (size_t)B * H * L * LP * (dtype == F32 ? 4 : 2);
 }
 
 extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs,
@@ -441,7 +434,7 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
                        dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs, (const T*)dout, \
                        (const T*)ws, L, H, scale, keep_scale, (T*)dqkv);                       \
   }
-  if (dtype == BF16) ATTN_BWD(bf16) else ATTN_BWD(float)
+  if (dtype == BF16) ATTN_BWD(bf16) else if (dtype == F16) ATTN_BWD(f16) else ATTN_BWD(float)
 #undef ATTN_BWD
   MMDX_LAUNCH_CHECK();
   return 0;

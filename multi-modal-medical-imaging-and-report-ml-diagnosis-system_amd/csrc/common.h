@@ -9,7 +9,9 @@
 namespace mmdx {
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
@@ -17,21 +19,40 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
-enum Dtype { F32 = 0, BF16 = 1 };
+enum Dtype { F32 = 0, BF16 = 1, F16 = 2 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 constexpr int WAVE = 64;
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+__device__ __forceinline__ float to_f(f16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);
 template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> __device__ __forceinline__ f16 from_f<f16>(float x) { return (f16)x; }
 
 // 16-byte vector of T: 8 bf16 or 4 f32.
 template <typename T> struct Vec16;
 template <> struct Vec16<bf16> { static constexpr int N = 8; typedef bf16x8 type; };
 template <> struct Vec16<float> { static constexpr int N = 4; typedef f32x4 type; };
+template <> struct Vec16<f16> { static constexpr int N = 8; typedef f16x8 type; };
+
+// The element-type dispatch of every C-ABI entry: `dtype` (MMDX_F32 / _BF16 / _F16) picks T
+// for the statement(s).  One macro for the whole library.
+#define MMDX_DISPATCH(dtype, ...)                  \
+  do {                                             \
+    if ((dtype) == ::mmdx::BF16) {                 \
+      typedef ::mmdx::bf16 T;                      \
+      __VA_ARGS__;                                 \
+    } else if ((dtype) == ::mmdx::F16) {           \
+      typedef ::mmdx::f16 T;                       \
+      __VA_ARGS__;                                 \
+    } else {                                       \
+      typedef float T;                             \
+      __VA_ARGS__;                                 \
+    }                                              \
+  } while (0)
 
 // exact (erf) GELU as torch.nn.GELU() default / BERT "gelu"
 __device__ __forceinline__ float gelu_erf(float x) {

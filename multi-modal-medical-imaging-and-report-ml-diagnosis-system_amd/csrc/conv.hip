@@ -479,6 +479,7 @@ using namespace mmdx;
 
 extern "C" int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
                                      const float* w, void* krsc, void* crsk, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_pack_weight: fp16 is the C5 path only");
   MMDX_CHECK_ARG(d && c_master > 0 && c_master <= d->C, "conv pack: bad channels");
   const long total = (long)d->K * d->R * d->S * d->C;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
@@ -499,6 +500,7 @@ extern "C" long mmdx_conv_pack_blocks(int K, int C, int RS) {
 
 extern "C" int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items,
                                     long total_blocks, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_pack_multi: fp16 is the C5 path only");
   MMDX_CHECK_ARG(items && n_items > 0 && total_blocks > 0 && total_blocks < (1L << 31),
                  "conv pack multi: bad item table");
   hipStream_t st = (hipStream_t)stream;
@@ -518,6 +520,7 @@ extern "C" int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d) {
 
 extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,
                              const void* w, void* y, float* stat_part, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_fwd: fp16 is the C5 path only");
   int rc = check_desc(d, dtype == BF16 ? 8 : 4);
   if (rc) return rc;
   MMDX_CHECK_ARG((long)d->N * d->P * d->Q < (1L << 31), "conv fwd: too many pixels");
@@ -530,6 +533,7 @@ extern "C" int mmdx_conv_fwd_bn_eval(int dtype, const mmdx_conv_desc* d, const v
                                      const float* beta, const float* running_mean,
                                      const float* running_var, float eps, const void* residual,
                                      int relu, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_fwd_bn_eval: fp16 is the C5 path only");
   int rc = check_desc(d, dtype == BF16 ? 8 : 4);
   if (rc) return rc;
   MMDX_CHECK_ARG(gamma && beta && running_mean && running_var, "conv fwd bn-eval: null BN");
@@ -543,6 +547,7 @@ extern "C" int mmdx_conv_fwd_bn_eval(int dtype, const mmdx_conv_desc* d, const v
 
 extern "C" int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* dy,
                                const void* w_crsk, void* dx, float beta, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_dgrad: fp16 is the C5 path only");
   int rc = check_desc(d, dtype == BF16 ? 8 : 4);
   if (rc) return rc;
   if (dtype == BF16) return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, beta, (hipStream_t)stream);
@@ -557,6 +562,7 @@ extern "C" size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc
 extern "C" int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master,
                                const void* x, const void* dy, float* dw, float beta,
                                void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_wgrad: fp16 is the C5 path only");
   int rc = check_desc(d, dtype == BF16 ? 8 : 4);
   if (rc) return rc;
   MMDX_CHECK_ARG(c_master > 0 && c_master <= d->C, "conv wgrad: bad c_master");
@@ -595,6 +601,7 @@ extern "C" int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const 
                                       const float* bn_beta, const float* save_mean,
                                       const float* save_rstd, int relu, float* stat_part,
                                       void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_dgrad_bnstat: fp16 is the C5 path only");
   int rc = check_desc(d, 8);
   if (rc) return rc;
   const int tiles = mmdx_conv_dgrad_stat_blocks(dtype, d);

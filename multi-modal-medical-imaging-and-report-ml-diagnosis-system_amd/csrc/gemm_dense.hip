@@ -11,7 +11,7 @@ struct SplitPlan { int bm, bn, splits, kper; };
 // Tile + split-K choice; shared by the workspace query and the launch so both agree.
 static SplitPlan plan_dense(int dtype, int M, int N, int K) {
   SplitPlan p;
-  const int BK = dtype == BF16 ? KTile<bf16>::BK : KTile<float>::BK;
+  const int BK = dtype == F32 ? KTile<float>::BK : KTile<bf16>::BK;
   p.bm = M <= 64 ? 64 : 128;
   p.bn = N <= 64 ? 64 : 128;
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
@@ -56,7 +56,7 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
   if constexpr (!AK) sa.vrows = K;  // R-major: k runs over the leading-dimension rows
   if constexpr (!BKm) sb.vrows = K;
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if constexpr (std::is_same<T, bf16>::value) {
+  if constexpr (sizeof(T) == 2) {
     // LDS-DMA kernel when every 16-B chunk is either wholly inside or wholly outside the
     // operand: k-major needs K % 8 == 0, row-major needs its row count % 8 == 0
     const long abytes = (long)(AK ? M : K) * lda * 2, bbytes = (long)(BKm ? N : K) * ldb * 2;
@@ -67,11 +67,11 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
       typedef typename std::conditional<BKm, DmaK<BN, SB>, DmaR<BN, SB>>::type OB;
       // three operand stages where the grid leaves one block per CU and K is long
       if ((long)nwg * splits <= 256 && kper >= 256)
-        hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3>), dim3(nwg, 1, splits),
-                           dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+        hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3, T>),
+                           dim3(nwg, 1, splits), dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
       else
-        hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 2>), dim3(nwg, 1, splits),
-                           dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
+        hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 2, T>),
+                           dim3(nwg, 1, splits), dim3(NT), 0, st, sa, sb, epi, M, N, K, kper);
       MMDX_LAUNCH_CHECK();
       return 0;
     }
@@ -110,7 +110,7 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
                       const float* addend, int act,
                       float alpha, float beta, void* preact, void* ws, size_t ws_bytes,
                       hipStream_t st) {
-  const SplitPlan p = plan_dense(sizeof(T) == 2 ? BF16 : F32, M, N, K);
+  const SplitPlan p = plan_dense(sizeof(T) == 2 ? BF16 : F32, M, N, K);  // BF16 = any 16-bit
   MMDX_CHECK_ARG(lda >= (ak ? K : M) && ldb >= (bk ? K : N) && ldc >= N,
                  "mmdx_gemm: leading dimension too small");
   EpiStore<OutT> epi{(OutT*)C, ldc, M, N, bias, addend, act, alpha, beta, (OutT*)preact};
@@ -149,7 +149,16 @@ extern "C" int mmdx_gemm(int dtype, int M, int N, int K, const void* A, long lda
     return gemm_typed<float, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
                                     addend, act, alpha, beta, preact, workspace, ws_bytes, st);
   }
+  if (dtype == F16) {
+    if (c_dtype == F32)
+      return gemm_typed<f16, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
+                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+    MMDX_CHECK_ARG(c_dtype == F16, "mmdx_gemm: fp16 compute writes fp16 or fp32");
+    return gemm_typed<f16, f16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
+                                addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+  }
   MMDX_CHECK_ARG(dtype == BF16, "mmdx_gemm: bad dtype %d", dtype);
+  MMDX_CHECK_ARG(c_dtype == F32 || c_dtype == BF16, "mmdx_gemm: bf16 compute writes bf16/fp32");
   if (c_dtype == F32)
     return gemm_typed<bf16, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st);

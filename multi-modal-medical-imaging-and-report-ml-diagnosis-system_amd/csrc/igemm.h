@@ -38,6 +38,15 @@ template <> struct MfmaOp<bf16> {
   }
   __device__ __forceinline__ static frag_t ld(const bf16* p) { return *(const bf16x8*)p; }
 };
+template <> struct MfmaOp<f16> {
+  static constexpr int KS = 32;
+  static constexpr int FRAG = 8;
+  typedef f16x8 frag_t;
+  __device__ __forceinline__ static f32x4 mma(frag_t a, frag_t b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  __device__ __forceinline__ static frag_t ld(const f16* p) { return *(const f16x8*)p; }
+};
 template <> struct MfmaOp<float> {
   static constexpr int KS = 4;
   static constexpr int FRAG = 1;
@@ -50,6 +59,7 @@ template <> struct MfmaOp<float> {
 
 template <typename T> struct KTile;               // K depth of one LDS stage
 template <> struct KTile<bf16> { static constexpr int BK = 64; };
+template <> struct KTile<f16> { static constexpr int BK = 64; };
 template <> struct KTile<float> { static constexpr int BK = 32; };
 
 // Generic per-K-tile context: just the tile origin and the split's k bound.
@@ -1387,7 +1397,7 @@ struct DmaR {
 // BK 32 x NS 4-5 keeps two blocks per CU with twice the bytes in flight of BK 64 x NS 2.
 // Epilogue: BatchNorm tile statistics straight from the accumulators (reg_stats), fp32
 // staging through LDS, then 8 consecutive columns per lane -> one 16-B bf16 store.
-template <int BM, int BN, class OA, class OB, class Epi, int NS = 2>
+template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16>
 __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                           typename OB::SrcT sb, Epi epi, int M,
                                                           int N, int K, int kper) {
@@ -1465,8 +1475,16 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < RN; ++j) {
+          // the LDS-DMA path moves 16-bit elements; the MFMA reads them as ET
+          if constexpr (std::is_same<ET, f16>::value)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                __builtin_bit_cast(f16x8, af[i]), __builtin_bit_cast(f16x8, bfr[j]), acc[i][j],
+                0, 0, 0);
+          else
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

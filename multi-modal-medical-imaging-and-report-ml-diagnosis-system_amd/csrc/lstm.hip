@@ -452,6 +452,7 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
                              void* h_out, float* c_save, float* gates_save, void* ws,
                              size_t ws_bytes, int* status, long spin_limit, int debug_flags,
                              void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_lstm_fwd: fp16 is the C5 path only");
   MMDX_CHECK_ARG(B > 0 && L > 0 && c_save && gates_save, "lstm fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   const size_t need = mmdx_lstm_fwd_workspace_size(dtype, B, L, H);
@@ -494,6 +495,7 @@ extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
 extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                              const float* gates_save, const void* dh_out, int B, int L, int H,
                              void* dxg, float* dw_hh, void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_lstm_bwd: fp16 is the C5 path only");
   MMDX_CHECK_ARG(H == 128 || H == 256, "lstm bwd: hidden size %d unsupported", H);
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_lstm_workspace_size(dtype, B, L, H),
                  "lstm bwd: workspace too small");

@@ -228,21 +228,12 @@ __global__ void bce_bwd_kernel(const float* __restrict__ z, const float* __restr
 
 using namespace mmdx;
 
-#define DISPATCH_T(dtype, ...)          \
-  do {                                 \
-    if ((dtype) == BF16) {             \
-      typedef bf16 T;                  \
-      __VA_ARGS__;                     \
-    } else {                           \
-      typedef float T;                 \
-      __VA_ARGS__;                     \
-    }                                  \
-  } while (0)
+#define DISPATCH_T(dtype, ...) MMDX_DISPATCH(dtype, __VA_ARGS__)
 
 extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int k,
                                 int s, int p, void* y, uint8_t* argmax, int P, int Q,
                                 void* stream) {
-  const int VEC = dtype == BF16 ? 8 : 4;
+  const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(C % VEC == 0 && k * k <= 255 && argmax, "maxpool: bad args");
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "maxpool: inconsistent output size");
@@ -257,7 +248,7 @@ extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, i
 extern "C" int mmdx_maxpool_bwd(int dtype, const uint8_t* argmax, const void* dy, int N, int H,
                                 int W, int C, int k, int s, int p, int P, int Q, void* dx,
                                 void* stream) {
-  const int VEC = dtype == BF16 ? 8 : 4;
+  const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(C % VEC == 0, "maxpool bwd: bad C");
   const long total = (long)N * H * W * (C / VEC);
   DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total)), dim3(256),
@@ -306,6 +297,12 @@ extern "C" int mmdx_cast(int dst, int src, const void* x, long n, void* y, void*
   else if (dst == F32 && src == F32)
     hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st,
                        (const float*)x, n, (float*)y);
+  else if (dst == F16 && src == F32)
+    hipLaunchKernelGGL((cast_kernel<f16, float>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const float*)x, n, (f16*)y);
+  else if (dst == F32 && src == F16)
+    hipLaunchKernelGGL((cast_kernel<float, f16>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const f16*)x, n, (float*)y);
   else
     hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid_for(n)), dim3(256), 0, st,
                        (const bf16*)x, n, (bf16*)y);

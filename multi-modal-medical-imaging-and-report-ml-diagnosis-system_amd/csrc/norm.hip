@@ -659,6 +659,7 @@ extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C
                            float* running_var, float momentum, float eps, float* save_mean,
                            float* save_rstd, const void* residual, int relu, void* y,
                            void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_fwd: fp16 is the C5 path only");
   MMDX_CHECK_ARG(rows > 0 && C > 0 && save_mean && save_rstd, "bn fwd: bad args");
   MMDX_CHECK_ARG(!stat_part || (stat_blocks > 0 && stat_rows > 0 &&
                                 (long)stat_blocks * stat_rows >= rows),
@@ -679,6 +680,7 @@ extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, c
                            const float* stat_part, int stat_blocks, void* dx,
                            void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                            void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_bwd: fp16 is the C5 path only");
   MMDX_CHECK_ARG(rows > 0 && C > 0, "bn bwd: bad args");
   MMDX_CHECK_ARG(!(relu && !y && d_residual), "bn bwd: a residual unit needs its output y");
   hipStream_t st = (hipStream_t)stream;
@@ -695,19 +697,14 @@ extern "C" int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual
                                   int D, const float* gamma, const float* beta, float eps,
                                   void* y, void* sum_out, float* save_mean, float* save_rstd,
                                   void* stream) {
-  const int VEC = dtype == BF16 ? 8 : 4;
+  const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC && gamma && beta,
                  "layernorm: D=%d unsupported", D);
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (int)((rows + 3) / 4);
-  if (dtype == BF16)
-    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)x,
-                       (const bf16*)residual, rows, D, gamma, beta, eps, (bf16*)y,
-                       (bf16*)sum_out, save_mean, save_rstd);
-  else
-    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)x,
-                       (const float*)residual, rows, D, gamma, beta, eps, (float*)y,
-                       (float*)sum_out, save_mean, save_rstd);
+  MMDX_DISPATCH(dtype, hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(blocks), dim3(256), 0, st,
+                                          (const T*)x, (const T*)residual, rows, D, gamma, beta,
+                                          eps, (T*)y, (T*)sum_out, save_mean, save_rstd));
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -721,21 +718,16 @@ extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, l
                                   const float* gamma, const float* save_mean,
                                   const float* save_rstd, void* dx, float* dgamma, float* dbeta,
                                   float beta_acc, void* ws, size_t ws_bytes, void* stream) {
-  const int VEC = dtype == BF16 ? 8 : 4;
+  const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC, "layernorm bwd: D=%d", D);
   const long nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_layernorm_workspace_size(rows, D),
                  "layernorm bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = 8 * (size_t)D * sizeof(float);
-  if (dtype == BF16)
-    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nblk), dim3(256), shm, st, (const bf16*)xsum,
-                       (const bf16*)dy, rows, D, gamma, save_mean, save_rstd, (bf16*)dx,
-                       (float*)ws);
-  else
-    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), shm, st,
-                       (const float*)xsum, (const float*)dy, rows, D, gamma, save_mean,
-                       save_rstd, (float*)dx, (float*)ws);
+  MMDX_DISPATCH(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nblk), dim3(256), shm, st,
+                                          (const T*)xsum, (const T*)dy, rows, D, gamma,
+                                          save_mean, save_rstd, (T*)dx, (float*)ws));
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, st,
                      (const float*)ws, (int)nblk, D, dgamma, dbeta, beta_acc);
   MMDX_LAUNCH_CHECK();

@@ -430,18 +430,11 @@ __global__ void relu_bwd_kernel(const T* __restrict__ y, const T* __restrict__ d
 
 using namespace mmdx;
 
-#define T5_DISPATCH(dtype, ...)   \
-  if (dtype == BF16) {            \
-    typedef bf16 T;               \
-    __VA_ARGS__;                  \
-  } else {                        \
-    typedef float T;              \
-    __VA_ARGS__;                  \
-  }
+#define T5_DISPATCH(dtype, ...) MMDX_DISPATCH(dtype, __VA_ARGS__)
 
 extern "C" int mmdx_rmsnorm_fwd(int dtype, const void* x, long rows, int D, const float* w,
                                 float eps, void* y, float* save_rstd, void* stream) {
-  const int VEC = dtype == BF16 ? 8 : 4;
+  const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * RMS_MAXV * VEC && w,
                  "rmsnorm: D=%d unsupported", D);
   T5_DISPATCH(dtype, hipLaunchKernelGGL(rms_fwd_kernel<T>, dim3((rows + 3) / 4), dim3(256), 0,
@@ -459,7 +452,7 @@ extern "C" int mmdx_rmsnorm_bwd(int dtype, const void* x, const void* dy, long r
                                 const float* w, const float* save_rstd, void* dx, float beta,
                                 float* dw, float dw_beta, void* ws, size_t ws_bytes,
                                 void* stream) {
-  const int VEC = dtype == BF16 ? 8 : 4;
+  const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * RMS_MAXV * VEC, "rmsnorm bwd: D=%d", D);
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_rmsnorm_workspace_size(rows, D),
                  "rmsnorm bwd: workspace too small");

@@ -190,16 +190,7 @@ __global__ void scatter_kernel(const int64_t* __restrict__ ids, long n, int D,
 
 using namespace mmdx;
 
-#define DISPATCH_T(dtype, ...) \
-  do {                        \
-    if ((dtype) == BF16) {    \
-      typedef bf16 T;         \
-      __VA_ARGS__;            \
-    } else {                  \
-      typedef float T;        \
-      __VA_ARGS__;            \
-    }                         \
-  } while (0)
+#define DISPATCH_T(dtype, ...) MMDX_DISPATCH(dtype, __VA_ARGS__)
 
 extern "C" int mmdx_embed_ln_fwd(int dtype, const int64_t* ids, const int64_t* tt, int B, int L,
                                  int D, const float* word, const float* pos, const float* type,

@@ -98,16 +98,7 @@ __global__ void add_kernel(long n, const T* __restrict__ x, const T* __restrict_
 
 using namespace mmdx;
 
-#define VIT_DISPATCH(dtype, ...)        \
-  do {                                  \
-    if ((dtype) == BF16) {              \
-      typedef bf16 T;                   \
-      __VA_ARGS__;                      \
-    } else {                            \
-      typedef float T;                  \
-      __VA_ARGS__;                      \
-    }                                   \
-  } while (0)
+#define VIT_DISPATCH(dtype, ...) MMDX_DISPATCH(dtype, __VA_ARGS__)
 
 extern "C" int mmdx_patchify(int dtype, const float* x, int N, int C, int H, int W, int p,
                              void* out, void* stream) {

@@ -21,7 +21,7 @@ import torch.nn as nn
 from . import _lib as L
 from ._lib import call, ptr, stream
 
-_VEC = {torch.float32: 4, torch.bfloat16: 8}
+_VEC = {torch.float32: 4, torch.bfloat16: 8, torch.float16: 8}
 
 
 class _NoTimer:

@@ -40,8 +40,9 @@ _DEFAULT_DTYPE = [torch.float32]
 
 def set_compute_dtype(dtype: torch.dtype):
     """Process-wide default compute dtype for newly built towers (fp32 parity / bf16 speed)."""
-    if dtype not in (torch.float32, torch.bfloat16):
-        raise TypeError("compute dtype must be torch.float32 or torch.bfloat16")
+    if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        raise TypeError("compute dtype must be torch.float32, torch.bfloat16 or torch.float16 "
+                        "(float16: the ViT / BERT towers, C5)")
     _DEFAULT_DTYPE[0] = dtype
 
 

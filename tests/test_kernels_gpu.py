@@ -13,7 +13,7 @@ from mmdx import functional as F
 
 pytestmark = pytest.mark.gpu
 
-TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
+TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3}
 
 
 def _close(out, ref, dt, what=""):
@@ -24,7 +24,7 @@ def _close(out, ref, dt, what=""):
     assert err <= TOL[dt], f"{what}: rel err {err:.3e} > {TOL[dt]}"
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K", [(64, 13, 1024), (200, 1024, 1536), (13, 1024, 64),
                                    (1000, 96, 40), (37, 130, 1000), (8192, 768, 768)])
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
@@ -40,8 +40,8 @@ def test_gemm(dev, dt, M, N, K, ak, bk):
     F.gemm(Ad, K if ak else M, ak, Bd, K if bk else N, bk, M, N, K, C, N,
            bias=bias.to(dev), compute_dtype=dt)
     torch.cuda.synchronize()
-    if dt == torch.bfloat16:
-        ref = A.bfloat16().float() @ B.bfloat16().float().T + bias
+    if dt != torch.float32:
+        ref = A.to(dt).float() @ B.to(dt).float().T + bias
     _close(C, ref, dt, f"gemm {M}x{N}x{K} ak={ak} bk={bk}")
 
 

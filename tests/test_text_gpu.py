@@ -24,14 +24,14 @@ def _ref_attention(q, k, v, mask, scale):
     return torch.einsum("bhlm,bmhd->blhd", p, v)
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,Ls,H", [(2, 128, 12), (3, 37, 2), (2, 197, 4), (1, 256, 1)])
 @pytest.mark.parametrize("masked", [True, False])
 def test_attention(dev, dt, B, Ls, H, masked):
     g = torch.Generator().manual_seed(B * Ls + H)
     qkv = torch.randn(B, Ls, 3, H, 64, generator=g)
-    if dt == torch.bfloat16:
-        qkv = qkv.bfloat16().float()
+    if dt != torch.float32:
+        qkv = qkv.to(dt).float()
     mask = None
     if masked:
         lens = torch.randint(1, Ls + 1, (B,), generator=g)
@@ -40,8 +40,8 @@ def test_attention(dev, dt, B, Ls, H, masked):
     qr = qkv.clone().requires_grad_(True)
     o = _ref_attention(qr[:, :, 0], qr[:, :, 1], qr[:, :, 2], mask, scale)
     do = torch.randn(o.shape, generator=g)
-    if dt == torch.bfloat16:
-        do = do.bfloat16().float()
+    if dt != torch.float32:
+        do = do.to(dt).float()
     o.backward(do)
     dc = L.dtype_code(dt)
     qd = qkv.to(dev, dt).contiguous()
@@ -139,7 +139,7 @@ def test_bert_layers_parity_fp32(dev):
         assert 1 - c <= 1e-5, f"{n}: cos {c}"
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_text_encoder_transformer_bert(dev, dt):
     torch.manual_seed(1)
     ref = R.RefTextEncoderTransformer("bert-base-uncased", bert_layers=2, dropout=0.0)

@@ -12,7 +12,7 @@ from parity_util import cosine, rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_vit_trunk_parity(dev, dt):
     torch.manual_seed(0)
     ref = R.RefVitTrunk(layers=2)
@@ -28,13 +28,16 @@ def test_vit_trunk_parity(dev, dt):
     f = mine(x.to(dev))
     assert tuple(f.shape) == (2, 768)
     assert rel_err(f, f_ref) <= (1e-4 if dt == torch.float32 else 5e-2)
-    if dt != torch.float32:
+    if dt == torch.bfloat16:
         return
     f.float().backward(dy.to(dev))
     gm = dict(mine.named_parameters())
     bad = []
+    # fp16 (C5's "fp16 MFMA"): gradients 1 - cos <= 1e-2 against the fp32 oracle
+    tol = 1e-4 if dt == torch.float32 else 1e-2
     for n, p in ref.named_parameters():
+        assert torch.isfinite(gm[n].grad).all(), n
         c = cosine(gm[n].grad, p.grad)
-        if 1 - c > 1e-4:
+        if 1 - c > tol:
             bad.append((n, 1 - c))
     assert not bad, bad
