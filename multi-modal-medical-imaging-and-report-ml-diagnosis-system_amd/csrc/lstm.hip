@@ -239,9 +239,11 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     int debug) {
   constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
   constexpr int NROWS = 64 * RT;
-  // [0, NROWS*COOP_LDH): h_{t-1} (MFMA A operand); then this workgroup's h_t slice [NROWS][32]
-  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * COOP_LDH + NROWS * COOP_UB];
+  // [0, NROWS*COOP_LDH): h_{t-1} (MFMA A operand); then this workgroup's h_t slice [NROWS][32];
+  // then one int: the poller's verdict, broadcast to the workgroup
+  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * COOP_LDH + NROWS * COOP_UB + 8];
   bf16* sout = sh + NROWS * COOP_LDH;
+  int* sgiveup = (int*)(sout + NROWS * COOP_UB);
   // the recurrence is the text tower's latency-critical chain and shares its CUs with the
   // image tower's conv blocks: its waves take issue priority over them
   __builtin_amdgcn_s_setprio(3);
@@ -288,32 +290,55 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       if (threadIdx.x == 0) {
         const unsigned target = (unsigned)(COOP_NB * s);
         long spins = 0;
+        int giveup = 0;
         while (__hip_atomic_load(myctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
           __builtin_amdgcn_s_sleep(1);
           ++spins;
           if (spins > spin_max) {
             __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            giveup = 1;
             break;
           }
           // another workgroup already gave up: stop waiting for it
           if ((spins & 255) == 0 &&
-              __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+              __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            giveup = 1;
             break;
+          }
         }
+        *sgiveup = giveup;  // through LDS: no second memory round trip on the chain
       }
       __syncthreads();
-      if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+      if (*sgiveup) return;
     }
     // h_{t-1} -> LDS (zeros at the first step); sc1 loads: the producers' sc1 stores are
     // visible to them without an L1 invalidate
-    const int par_in = ((s + 1) & 1) * B * H * 2;  // byte offset of the h_{t-1} buffer
-    for (int e = threadIdx.x; e < NROWS * (H / 8); e += 512) {
-      const int row = e / (H / 8), c8 = e - row * (H / 8);
-      coop_v4u v = {0u, 0u, 0u, 0u};
-      if (s > 0 && row < B)
-        v = __builtin_amdgcn_raw_buffer_load_b128(hrs, par_in + (row * H + c8 * 8) * 2, 0,
-                                                  COOP_SC1);
-      *(coop_v4u*)(sh + row * COOP_LDH + c8 * 8) = v;
+    // All of a thread's chunks are requested before any is written to LDS: one memory round
+    // trip per batch of COOP_HB loads instead of one per chunk (a predicated load-then-store
+    // loop compiles to a vmcnt(0) wait per chunk).  Rows >= B read out of the buffer's range
+    // and come back as zeros.
+    // Thread t moves rows (t >> 5) + 16 i, chunk t & 31: one base offset, the rest constants
+    // (so nothing per chunk is kept live across steps).
+    constexpr int HCH = NROWS * (H / 8) / 512;     // 16-B chunks per thread
+    constexpr int HB = HCH < 8 ? HCH : 8;
+    const int hrow = threadIdx.x >> 5;
+    bf16* hdst = sh + hrow * COOP_LDH + (threadIdx.x & 31) * 8;
+    if (s > 0) {
+      const unsigned hsrc = (unsigned)(((s + 1) & 1) * B * H * 2 +  // the h_{t-1} buffer
+                                       (hrow * H + (threadIdx.x & 31) * 8) * 2);
+#pragma unroll
+      for (int i0 = 0; i0 < HCH; i0 += HB) {
+        coop_v4u v[HB];
+#pragma unroll
+        for (int i = 0; i < HB; ++i)
+          v[i] = __builtin_amdgcn_raw_buffer_load_b128(
+              hrs, hrow + 16 * (i0 + i) < B ? hsrc + (i0 + i) * 16 * H * 2 : DMA_OOB, 0, COOP_SC1);
+#pragma unroll
+        for (int i = 0; i < HB; ++i) *(coop_v4u*)(hdst + (i0 + i) * 16 * COOP_LDH) = v[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < HCH; ++i) *(coop_v4u*)(hdst + i * 16 * COOP_LDH) = coop_v4u{0u, 0u, 0u, 0u};
     }
     __syncthreads();
     float hv[RT][4], cv[RT][4], gv[RT][4][4];

@@ -70,6 +70,10 @@ CONVS = [  # N, C, H, W, K, k, s, p
     (2, 64, 14, 14, 256, 1, 2, 0),
     (2, 3, 32, 32, 64, 7, 2, 3),
     (1, 128, 9, 9, 512, 3, 2, 1),
+    # small grids with C, K multiples of 128: 128-deep K tiles (fwd and stride-1 dgrad)
+    (2, 256, 14, 14, 256, 3, 1, 1),
+    (3, 128, 7, 7, 128, 3, 1, 1),
+    (2, 512, 7, 7, 1024, 1, 1, 0),
 ]
 
 
@@ -87,10 +91,12 @@ def test_conv_fwd_dgrad_wgrad(dev, dt, cfg):
 
 
 # production M: the C4 batch (N = 128) at layer1's 56x56 (M = 401,408 rows), the 3x3 and
-# the 1x1 expansion, plus layer2's strided 1x1 downsample (M = 100,352) — the exact launch
-# geometry of the benched step (grid sizes, split-K depth of the wgrad, BN stat blocks)
+# the 1x1 expansion, layer2's strided 1x1 downsample (M = 100,352) and the layer3 / layer4
+# 3x3s (128-deep K tiles) — the exact launch geometry of the benched step (grid sizes,
+# split-K depth of the wgrad, BN stat blocks)
 @pytest.mark.parametrize("cfg", [(128, 64, 56, 56, 64, 3, 1, 1), (128, 64, 56, 56, 256, 1, 1, 0),
-                                 (128, 256, 56, 56, 512, 1, 2, 0)])
+                                 (128, 256, 56, 56, 512, 1, 2, 0),
+                                 (128, 512, 7, 7, 512, 3, 1, 1), (128, 256, 14, 14, 256, 3, 1, 1)])
 def test_conv_production_m(dev, cfg):
     torch.set_num_threads(16)
     _conv_case(dev, torch.bfloat16, cfg)

@@ -59,6 +59,9 @@ def main():
     ap.add_argument("--filter", default="", help="substring of the shape string to run")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--lib", default="", help="alternative libmmdx_hip.so (A/B builds)")
+    ap.add_argument("--ref-gemm", action="store_true",
+                    help="also time torch.matmul (hipBLASLt) on the same M x N x K in bf16: "
+                         "what a tuned explicit GEMM of that size reaches (no im2col)")
     a = ap.parse_args()
     import mmdx
     from mmdx import _lib as L
@@ -124,15 +127,32 @@ def main():
                      gbs=round(nbytes[name] / ms / 1e6, 1),
                      bound="mfma" if F / PEAK_F > nbytes[name] / PEAK_B else "hbm",
                      frac=round(bound / ms, 3))
+            if a.ref_gemm:
+                M_, N_, K_ = (int(v) for v in r["M_N_K"].split("x"))
+                ga = torch.randn(M_, K_, device=dev).to(dt)
+                gb = torch.randn(N_, K_, device=dev).to(dt)
+                for _ in range(3):
+                    torch.matmul(ga, gb.t())
+                torch.cuda.synchronize()
+                s0.record()
+                for _ in range(a.reps):
+                    torch.matmul(ga, gb.t())
+                s1.record()
+                torch.cuda.synchronize()
+                r["ref_gemm_us"] = round(s0.elapsed_time(s1) / a.reps * 1e3, 1)
+                tot["ref_" + name] += r["ref_gemm_us"] * 1e-3 * info["count"]
+                del ga, gb
             rows.append(r)
             tot[name] += ms * info["count"]
             tot["bound_" + name] += bound * info["count"]
             print(f"{r['tag']:10s} {r['shape']:26s} {name:5s} x{r['count']} {r['M_N_K']:22s} "
                   f"{r['us']:8.1f}us {r['tflops']:7.1f}TF {r['gbs']:7.1f}GB/s {r['bound']} "
-                  f"frac {r['frac']:.3f}", flush=True)
+                  f"frac {r['frac']:.3f}" + (f"  hipblaslt {r['ref_gemm_us']:7.1f}us"
+                                             if a.ref_gemm else ""), flush=True)
     for name in ("fwd", "dgrad", "wgrad"):
         print(f"TOTAL {name}: {tot[name]:.3f} ms/step, roofline {tot['bound_' + name]:.3f} ms "
-              f"(frac {tot['bound_' + name] / max(tot[name], 1e-9):.3f})")
+              f"(frac {tot['bound_' + name] / max(tot[name], 1e-9):.3f})"
+              + (f", hipBLASLt same-size GEMMs {tot['ref_' + name]:.3f} ms" if a.ref_gemm else ""))
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"batch": B, "rows": rows, "totals_ms": dict(tot)}, f, indent=1)

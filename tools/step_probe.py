@@ -23,7 +23,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--text-first", action="store_true")
     ap.add_argument("--text-only", action="store_true")
+    ap.add_argument("--image-only", action="store_true")
     ap.add_argument("--threads", action="store_true", help="issue the towers from two threads")
+    ap.add_argument("--bwd-thread", action="store_true",
+                    help="issue the text backward from a worker thread, concurrently with "
+                         "the image trunk's backward")
     args = ap.parse_args()
     cfg = dict(bench.CONFIGS[args.config])
     dev = torch.device("cuda", 0)
@@ -79,15 +83,23 @@ def main():
         loss.backward(inputs=[z_img, z_txt] + head, retain_graph=True)
         mark("head_bwd", main)
         side.wait_stream(main)
+
+        def text_bwd():
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(side):
+                g = z_txt.grad
+                z_txt.backward(g)
+                z_txt.grad = None
+                mark("txt_bwd_done", side)
+        fut = towers._pool.submit(text_bwd) if args.bwd_thread else None
         g = z_img.grad
         z_img.backward(g)
         z_img.grad = None
         mark("img_bwd_issued", main)
-        with torch.cuda.stream(side):
-            g = z_txt.grad
-            z_txt.backward(g)
-            z_txt.grad = None
-            mark("txt_bwd_done", side)
+        if fut is None:
+            text_bwd()
+        else:
+            fut.result()
         main.wait_stream(side)
         mark("joined", main)
         _, scale = MO.grad_norm(params, 1.0)
@@ -95,6 +107,19 @@ def main():
         mark("end", main)
         return loss
 
+    if args.image_only:  # the image tower alone (its wgrad stream still concurrent)
+        for it in range(6):
+            torch.cuda.synchronize()
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            z = img(x)["embeddings"]
+            e[1].record()
+            z.float().sum().backward()
+            e[2].record()
+            torch.cuda.synchronize()
+            print(f"image only: fwd {e[0].elapsed_time(e[1]):.3f} ms  bwd "
+                  f"{e[1].elapsed_time(e[2]):.3f} ms")
+        return
     if args.text_only:  # the text tower alone: its uncontended forward / backward time
         for it in range(4):
             torch.cuda.synchronize()
