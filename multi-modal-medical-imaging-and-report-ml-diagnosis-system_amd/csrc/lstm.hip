@@ -19,12 +19,18 @@ constexpr int LSTM_NW = 8;    // waves per workgroup
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// acc[j] += A[16 rows][K] (LDS, row base a_row = &A[lane&15][(lane>>4)*FRAG]) x
-//           Bg^T, Bg rows = output columns (row base b_row = &Bg[col0 + lane&15][(lane>>4)*FRAG],
-//           tile j at +j*16 rows), K contiguous in global (L2-resident weights).
+// acc[j] += A[16 rows][K] (LDS, row base a_row = &A[lane&15][(lane>>4)*FRAG]) x B fragments
+//           streamed from global (L2-resident weights): this lane's fragment of tile j at
+//           k-step ks is at b + j*TS + ks*KSTR.  Row-major Bg^T (rows = output columns):
+//           b = &Bg[col0 + lane&15][(lane>>4)*FRAG], TS = 16*ldb, KSTR = KS.  Fragment-packed
+//           (lstm_pack_whh_kernel): TS = (K/KS)*64*FRAG, KSTR = 64*FRAG — one contiguous 1 KiB
+//           per wave instruction.
 // The weight stream is software-pipelined D k-steps deep (D*TILES fragments in flight).
+// Short contractions are unrolled completely, so every fragment's wait is an exact vmcnt
+// (a rolled loop with the refill under a branch compiled to vmcnt(0) at each iteration:
+// one full L2 round trip per D k-steps instead of a full pipeline).
 template <typename T, int TILES, int K, int D>
-__device__ __forceinline__ void rowblock_mfma(const T* a_row, const T* b_row, long ldb,
+__device__ __forceinline__ void rowblock_mfma(const T* a_row, const T* b_row, long ts, int kstr,
                                               f32x4* acc) {
   typedef MfmaOp<T> Op;
   constexpr int NKS = K / Op::KS;
@@ -33,20 +39,28 @@ __device__ __forceinline__ void rowblock_mfma(const T* a_row, const T* b_row, lo
 #pragma unroll
   for (int d = 0; d < D; ++d)
 #pragma unroll
-    for (int j = 0; j < TILES; ++j) buf[d][j] = Op::ld(b_row + (long)j * 16 * ldb + d * Op::KS);
+    for (int j = 0; j < TILES; ++j) buf[d][j] = Op::ld(b_row + (long)j * ts + d * kstr);
+  auto kstep = [&](int ks, int d) {
+    const typename Op::frag_t af = Op::ld(a_row + ks * Op::KS);
+#pragma unroll
+    for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, buf[d][j], acc[j]);
+    if (ks + D < NKS) {
+#pragma unroll
+      for (int j = 0; j < TILES; ++j)
+        buf[d][j] = Op::ld(b_row + (long)j * ts + (ks + D) * kstr);
+    }
+    // keep the refill at this k-step: the scheduler otherwise sinks it next to its use and
+    // the pipeline collapses to ~2 k-steps in flight
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (NKS <= 64) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) kstep(ks, ks % D);
+  } else {
 #pragma unroll 1
-  for (int g = 0; g < NKS; g += D) {
+    for (int g = 0; g < NKS; g += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int ks = g + d;
-      const typename Op::frag_t af = Op::ld(a_row + ks * Op::KS);
-#pragma unroll
-      for (int j = 0; j < TILES; ++j) acc[j] = Op::mma(af, buf[d][j], acc[j]);
-      if (ks + D < NKS) {
-#pragma unroll
-        for (int j = 0; j < TILES; ++j)
-          buf[d][j] = Op::ld(b_row + (long)j * 16 * ldb + (ks + D) * Op::KS);
-      }
+      for (int d = 0; d < D; ++d) kstep(g + d, d);
     }
   }
 }
@@ -85,7 +99,12 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
     f32x4 acc[TILES];
 #pragma unroll
     for (int j = 0; j < TILES; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    rowblock_mfma<T, TILES, H, LstmDepth<T, H>::F>(a_row, b_row, H, acc);
+    // the weight operand is re-streamed every step: an opaque zero offset keeps the compiler
+    // from hoisting W_hh's fragments out of the step loop (they do not fit in VGPRs); an
+    // offset, not the pointer, so the loads stay global (not flat) loads
+    int zero = 0;
+    asm volatile("" : "+s"(zero));
+    rowblock_mfma<T, TILES, H, LstmDepth<T, H>::F>(a_row, b_row + zero, 16L * H, Op::KS, acc);
 #pragma unroll
     for (int j = 0; j < TILES; ++j)
 #pragma unroll
@@ -126,10 +145,11 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
 }
 
 // Recurrent backward.  dG (pre-activation gate grads) -> dxg [B][L][2][4H] (T) and the
-// shifted hidden states hprev [2][B*L][H] (T) for the dW_hh GEMM.
+// shifted hidden states hprev [2][B*L][H] (T) for the dW_hh GEMM.  whp: W_hh in the
+// fragment-packed layout of lstm_pack_whh_kernel.
 template <typename T, int H>
 __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
-    const T* __restrict__ whhT, const T* __restrict__ hout, const float* __restrict__ csave,
+    const T* __restrict__ whp, const T* __restrict__ hout, const float* __restrict__ csave,
     const float* __restrict__ gsave, const T* __restrict__ dhout, int B, int L,
     T* __restrict__ dxg, T* __restrict__ hprev) {
   typedef MfmaOp<T> Op;
@@ -142,7 +162,7 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
   const int dir = blockIdx.y;
   const int b0 = blockIdx.x * LSTM_RB;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const T* WT = whhT + (long)dir * H * G4;  // [H][4H]
+  constexpr int NKS = G4 / Op::KS;           // k-steps of the dh contraction
   float dcn[CPT];
 #pragma unroll
   for (int i = 0; i < CPT; ++i) dcn[i] = 0.f;
@@ -150,11 +170,36 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
   __syncthreads();
   const int col0 = wid * TILES * 16;
   const T* a_row = sdg + (lane & 15) * LDG + (lane >> 4) * Op::FRAG;
-  const T* b_row = WT + (long)(col0 + (lane & 15)) * G4 + (lane >> 4) * Op::FRAG;
+  constexpr long TS = (long)NKS * 64 * Op::FRAG;  // one 16-column tile, all k-steps
+  const T* b_row = whp + ((long)dir * (H / 16) + col0 / 16) * TS + lane * Op::FRAG;
   for (int s = L - 1; s >= 0; --s) {
     const int t = dir == 0 ? s : L - 1 - s;
     const int tp = dir == 0 ? t - 1 : t + 1;  // previous step in forward order
     const bool has_prev = s > 0;
+    // every global operand of this step's CPT elements is requested first (rows past B read
+    // row B-1 and are discarded), then the cell math, then the stores: one memory round trip
+    // per step instead of two per element
+    float gv[CPT][4], cv[CPT], cpv[CPT], dhv[CPT];
+    T hpv[CPT];
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int e = threadIdx.x + i * LSTM_NW * 64;
+      const int row = e / H, u = e - row * H;
+      const int b = min(b0 + row, B - 1);
+      const long sidx = ((long)dir * L + t) * B + b;
+      const float* gp = gsave + sidx * G4;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gv[i][g] = gp[g * H + u];
+      cv[i] = csave[sidx * H + u];
+      dhv[i] = to_f(dhout[((long)b * L + t) * 2 * H + dir * H + u]);
+      if (has_prev) {
+        cpv[i] = csave[(((long)dir * L + tp) * B + b) * H + u];
+        hpv[i] = hout[((long)b * L + tp) * 2 * H + dir * H + u];
+      } else {
+        cpv[i] = 0.f;
+        hpv[i] = from_f<T>(0.f);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int e = threadIdx.x + i * LSTM_NW * 64;
@@ -162,17 +207,14 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
       const int b = b0 + row;
       float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
       if (b < B) {
-        const long sidx = ((long)dir * L + t) * B + b;
-        const float* gp = gsave + sidx * G4;
-        const float gi = gp[u], gf = gp[H + u], gg = gp[2 * H + u], go = gp[3 * H + u];
-        const float c = csave[sidx * H + u];
-        const float cp = has_prev ? csave[(((long)dir * L + tp) * B + b) * H + u] : 0.f;
-        const float dh = to_f(dhout[((long)b * L + t) * 2 * H + dir * H + u]) + sdh[row * H + u];
+        const float gi = gv[i][0], gf = gv[i][1], gg = gv[i][2], go = gv[i][3];
+        const float c = cv[i];
+        const float dh = dhv[i] + sdh[row * H + u];
         const float tc = tanhf(c);
         const float dc = dh * go * (1.f - tc * tc) + dcn[i];
         const float d_o = dh * tc;
         dgi = dc * gg * gi * (1.f - gi);
-        dgf = dc * cp * gf * (1.f - gf);
+        dgf = dc * cpv[i] * gf * (1.f - gf);
         dgg = dc * gi * (1.f - gg * gg);
         dgo = d_o * go * (1.f - go);
         dcn[i] = dc * gf;
@@ -181,8 +223,7 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
         dp[H + u] = from_f<T>(dgf);
         dp[2 * H + u] = from_f<T>(dgg);
         dp[3 * H + u] = from_f<T>(dgo);
-        hprev[((long)dir * B * L + (long)b * L + t) * H + u] =
-            has_prev ? hout[((long)b * L + tp) * 2 * H + dir * H + u] : from_f<T>(0.f);
+        hprev[((long)dir * B * L + (long)b * L + t) * H + u] = hpv[i];
       }
       sdg[row * LDG + u] = from_f<T>(dgi);
       sdg[row * LDG + H + u] = from_f<T>(dgf);
@@ -194,7 +235,10 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
     f32x4 acc[TILES];
 #pragma unroll
     for (int j = 0; j < TILES; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    rowblock_mfma<T, TILES, G4, LstmDepth<T, H>::B>(a_row, b_row, G4, acc);
+    int zero = 0;  // (see lstm_fwd_kernel: no hoisting of W_hh^T's fragments)
+    asm volatile("" : "+s"(zero));
+    rowblock_mfma<T, TILES, G4, LstmDepth<T, H>::B>(a_row, b_row + zero, TS, 64 * Op::FRAG,
+                                                    acc);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < TILES; ++j)
@@ -404,16 +448,25 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
   }
 }
 
+// W_hh [2][4H][H] -> the backward's B-operand fragments, [2][H/16][4H/KS][64 lanes][FRAG]:
+// lane l of k-step ks of column tile c holds W_hh[ks*KS + (l>>4)*FRAG + e][16c + (l&15)],
+// so every streaming load of the recurrence is one contiguous 1 KiB per wave.
 template <typename T>
-__global__ void transpose_whh_kernel(const T* __restrict__ w, int H, T* __restrict__ wt) {
-  const int G4 = 4 * H;
+__global__ void lstm_pack_whh_kernel(const T* __restrict__ w, int H, T* __restrict__ wp) {
+  typedef MfmaOp<T> Op;
+  const int G4 = 4 * H, nks = G4 / Op::KS;
   const long total = 2L * G4 * H;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int d = (int)(i / ((long)G4 * H));
-    const long r = i - (long)d * G4 * H;
-    const int g = (int)(r / H), u = (int)(r - (long)g * H);
-    wt[(long)d * G4 * H + (long)u * G4 + g] = w[i];
+    const int e = (int)(i % Op::FRAG);
+    long r = i / Op::FRAG;
+    const int l = (int)(r % 64);
+    r /= 64;
+    const int ks = (int)(r % nks);
+    r /= nks;
+    const int c = (int)(r % (H / 16)), d = (int)(r / (H / 16));
+    const int u = 16 * c + (l & 15), j = ks * Op::KS + (l >> 4) * Op::FRAG + e;
+    wp[i] = w[((long)d * G4 + j) * H + u];
   }
 }
 
@@ -512,7 +565,7 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
 
 extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
   const size_t es = dtype == BF16 ? 2 : 4;
-  // transposed W_hh + shifted hidden states + dW_hh GEMM split-K scratch
+  // fragment-packed W_hh + shifted hidden states + dW_hh GEMM split-K scratch
   return 2 * (size_t)4 * H * H * es + 2 * (size_t)B * L * H * es +
          2 * mmdx_gemm_workspace_size(dtype, 4 * H, H, B * L) + 256;
 }
@@ -527,7 +580,7 @@ extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, con
   hipStream_t st = (hipStream_t)stream;
   const size_t es = dtype == BF16 ? 2 : 4;
   char* w = (char*)ws;
-  void* whhT = w;
+  void* whp = w;
   w += 2 * (size_t)4 * H * H * es;
   void* hprev = w;
   w += 2 * (size_t)B * L * H * es;
@@ -537,10 +590,10 @@ extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, con
   const long tw = 2L * 4 * H * H;
   const int tb = (int)std::min<long>((tw + 255) / 256, 4096);
 #define LSTM_BWD(T, HH)                                                                         \
-  hipLaunchKernelGGL(transpose_whh_kernel<T>, dim3(tb), dim3(256), 0, st, (const T*)w_hh, HH,  \
-                     (T*)whhT);                                                                 \
+  hipLaunchKernelGGL(lstm_pack_whh_kernel<T>, dim3(tb), dim3(256), 0, st, (const T*)w_hh, HH,  \
+                     (T*)whp);                                                                  \
   hipLaunchKernelGGL((lstm_bwd_kernel<T, HH>), grid, dim3(LSTM_NW * 64), 0, st,                 \
-                     (const T*)whhT, (const T*)h_out, c_save, gates_save, (const T*)dh_out, B, \
+                     (const T*)whp, (const T*)h_out, c_save, gates_save, (const T*)dh_out, B,  \
                      L, (T*)dxg, (T*)hprev)
   if (dtype == BF16) {
     if (H == 256) { LSTM_BWD(bf16, 256); } else { LSTM_BWD(bf16, 128); }

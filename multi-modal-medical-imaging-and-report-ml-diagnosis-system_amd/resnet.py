@@ -321,7 +321,9 @@ class _Plan:
         packs = []
         fold = not train and not keep   # eval-mode BN folded into the conv epilogue
 
-        def unit(conv, bn, relu, x, N, H, W, C, cm, res, pair=None):
+        def unit(conv, bn, relu, x, N, H, W, C, cm, res, pair=None, st=0, join=None):
+            """conv + BN(+res)(+ReLU) on stream `st`; `join`: an event the main stream
+            waits for before the first op that reads `res` (the downsample branch)."""
             d = pair if pair is not None else _desc(N, H, W, C, conv)
             K, k = conv.out_channels, conv.kernel_size
             y = A.new((N, d.P, d.Q, K), T, dev)
@@ -342,24 +344,29 @@ class _Plan:
                 # eval forward without a backward (inference, frozen phase 1): BN on running
                 # statistics (+residual)(+ReLU) applied in the conv epilogue; y is never
                 # materialised and no bn_apply pass runs
-                fw.timed("fwd", L.OP_CONV_FWD_BNEVAL, dtype=dt, i=(int(relu),), f=(bn.eps,),
+                if join is not None:
+                    fw.add(L.OP_WAIT, p=(join,), stream=st)
+                fw.timed("fwd", L.OP_CONV_FWD_BNEVAL, stream=st, dtype=dt, i=(int(relu),),
+                         f=(bn.eps,),
                          p=(x, wk, y, bn.weight, bn.bias, bn.running_mean, bn.running_var, res),
                          d=d)
                 u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=None, out=y,
                          mean=None, rstd=None, wc=wc, pair=pair is not None)
                 units.append(u)
                 return y, d, u
-            fw.timed("fwd", L.OP_CONV_FWD, dtype=dt, p=(x, wk, y, part), d=d)
+            fw.timed("fwd", L.OP_CONV_FWD, stream=st, dtype=dt, p=(x, wk, y, part), d=d)
             out = A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
             mean = A.new((K,), torch.float32, dev)
             rstd = A.new((K,), torch.float32, dev)
             wsn = L.lib().mmdx_bn_workspace_size(rows, K)
-            ws_for(wsn)
+            ws_for(wsn, st)
+            if join is not None:
+                fw.add(L.OP_WAIT, p=(join,), stream=st)
             fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, 128, wsn),
-                   f=(bn.momentum, bn.eps),
+                   f=(bn.momentum, bn.eps), stream=st,
                    p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
-                      res, out, _WS))
+                      res, out, _WS2 if st else _WS))
             u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
                      rstd=rstd, wc=wc, pair=pair is not None)
             units.append(u)
@@ -384,15 +391,30 @@ class _Plan:
                 bu = []
                 h, hH, hW, hC = x_in, H, W, C
                 ds_u = None
-                if blk.downsample is not None:
+                ds_done = None
+                if blk.downsample is not None and not DS_SIDE_STREAM:
                     idn, _, ds_u = unit(blk.downsample[0], blk.downsample[1], False, x_in, N, H,
                                         W, C, C, None)
+                elif blk.downsample is not None:
+                    # the downsample branch (conv + BN) runs on the side stream beside the
+                    # block's conv1 / conv2 / conv3; the main stream joins it right before
+                    # the residual BN apply that reads it (the side stream is idle in the
+                    # forward: it carries the weight gradients in the backward)
+                    ev_in = A.event()
+                    fw.add(L.OP_SIGNAL, p=(ev_in,), stream=0)
+                    fw.add(L.OP_WAIT, p=(ev_in,), stream=1)
+                    idn, _, ds_u = unit(blk.downsample[0], blk.downsample[1], False, x_in, N, H,
+                                        W, C, C, None, st=1)
+                    ds_done = A.event()
+                    fw.add(L.OP_SIGNAL, p=(ds_done,), stream=1)
                 else:
                     idn = x_in
                 specs = blk.units()
                 for i, (conv, bn, relu) in enumerate(specs):
-                    res = idn if i == len(specs) - 1 else None
-                    h, dd, uu = unit(conv, bn, relu, h, N, hH, hW, hC, hC, res)
+                    last = i == len(specs) - 1
+                    res = idn if last else None
+                    h, dd, uu = unit(conv, bn, relu, h, N, hH, hW, hC, hC, res,
+                                     join=ds_done if last else None)
                     hH, hW, hC = dd.P, dd.Q, dd.K
                     bu.append(uu)
                 blocks.append((bu, ds_u, (H, W, C)))
@@ -576,6 +598,10 @@ class _Plan:
 # early, dist.GradAllReducer.launch_region).  None = no hook.
 TRUNK_GRAD_HOOK = None
 
+# Downsample branch of the forward on the side stream (False: in order on the main stream;
+# read when a plan is built — for A/B runs, tools/step_probe.py --ds-main).
+DS_SIDE_STREAM = True
+
 # placeholder operands for the plan's per-stream workspaces, patched once sizes are known
 _WS_TOKEN, _WS2_TOKEN = 0x1, 0x2
 _WS, _WS2 = _WS_TOKEN, _WS2_TOKEN
@@ -627,7 +653,8 @@ class _TrunkFn(torch.autograd.Function):
                tuple(p.data_ptr() for p in params))
         plan = _plans_for(trunk, key,
                           lambda: _Plan(trunk, N, H, W, in_nchw, cin, T, train, keep, dev))
-        plan.fwd.run([x.data_ptr()], [stream()])
+        # the downsample branches run on the side stream (joined inside the plan)
+        plan.fwd.run([x.data_ptr()], [stream(), _side_stream(trunk, dev).cuda_stream])
         if train:  # every BN's num_batches_tracked += 1, in one multi-tensor launch
             torch._foreach_add_([m.num_batches_tracked for m in trunk.modules()
                                  if isinstance(m, BatchNorm2d)], 1)

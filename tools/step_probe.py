@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--text-first", action="store_true")
     ap.add_argument("--text-only", action="store_true")
     ap.add_argument("--image-only", action="store_true")
+    ap.add_argument("--ds-main", action="store_true",
+                    help="downsample branch in order on the main stream (A/B)")
     ap.add_argument("--threads", action="store_true", help="issue the towers from two threads")
     ap.add_argument("--bwd-thread", action="store_true",
                     help="issue the text backward from a worker thread, concurrently with "
@@ -33,6 +35,8 @@ def main():
     dev = torch.device("cuda", 0)
     import mmdx
     from mmdx import optim as MO
+    if args.ds_main:
+        mmdx.resnet.DS_SIDE_STREAM = False
     from mmdx.schedule import two_tower_backward
     img, txt, fus, opt = bench.build(cfg, dev, torch.bfloat16)
     params = [p for grp in opt.param_groups for p in grp["params"]]
