@@ -95,6 +95,125 @@ __global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ am, const T* __re
   }
 }
 
+// The ResNet stem pool (3x3, stride 2): the nine window loads of a thread are all issued
+// before the first compare (the generic loop above compiles to one load-compare round trip
+// per tap) and the argmax bytes go out as one 8-byte (bf16 / fp16) or 4-byte (fp32) store.
+// Same window order, tie rule and NaN rule as maxpool_fwd_kernel.
+template <int VEC> struct ArgPack;
+template <> struct ArgPack<8> { typedef unsigned long long type; };
+template <> struct ArgPack<4> { typedef unsigned type; };
+
+template <typename T>
+__global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C,
+                                      int p, T* __restrict__ y, uint8_t* __restrict__ am, int P,
+                                      int Q) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  typedef typename ArgPack<VEC>::type A;
+  const int cv = C / VEC;
+  const long total = (long)N * P * Q * cv;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % cv) * VEC;
+    long t = i / cv;
+    const int q = (int)(t % Q); t /= Q;
+    const int pp = (int)(t % P);
+    const int n = (int)(t / P);
+    V v[9];
+    bool ok[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int ih = pp * 2 - p + r;
+#pragma unroll
+      for (int ss = 0; ss < 3; ++ss) {
+        const int iw = q * 2 - p + ss;
+        ok[r * 3 + ss] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        v[r * 3 + ss] = ok[r * 3 + ss] ? *(const V*)(x + (((long)n * H + ih) * W + iw) * C + c)
+                                       : V{};
+      }
+    }
+    float best[VEC];
+    int arg[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { best[j] = -INFINITY; arg[j] = -1; }
+#pragma unroll
+    for (int w9 = 0; w9 < 9; ++w9) {
+      if (!ok[w9]) continue;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float f = to_f(v[w9][j]);
+        if (arg[j] < 0 || f > best[j] || (f != f && best[j] == best[j])) {
+          best[j] = f;
+          arg[j] = w9;
+        }
+      }
+    }
+    V o;
+    A packed = 0;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      o[j] = from_f<T>(best[j]);
+      packed |= (A)(uint8_t)arg[j] << (8 * j);
+    }
+    *(A*)(am + i * VEC) = packed;
+    *(V*)(y + i * VEC) = o;
+  }
+}
+
+// Backward of the 3x3 / stride-2 pool: an input pixel lies in at most 2 x 2 windows; their
+// dy vectors and packed argmax bytes are loaded together, summed in the generic kernel's
+// window order.
+template <typename T>
+__global__ void maxpool3s2_bwd_kernel(const uint8_t* __restrict__ am, const T* __restrict__ dy,
+                                      int N, int H, int W, int C, int p, int P, int Q,
+                                      T* __restrict__ dx) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  typedef typename ArgPack<VEC>::type A;
+  const int cv = C / VEC;
+  const long total = (long)N * H * W * cv;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % cv) * VEC;
+    long t = i / cv;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const int ph = (h + p) >> 1, qw = (w + p) >> 1;  // the last window that can hold (h, w)
+    V g[2][2];
+    A a[2][2];
+    bool ok[2][2];
+#pragma unroll
+    for (int dp = 0; dp < 2; ++dp) {
+      const int pp = ph - 1 + dp, r = h + p - 2 * pp;  // ascending pp, as the generic kernel
+#pragma unroll
+      for (int dq = 0; dq < 2; ++dq) {
+        const int q = qw - 1 + dq, ss = w + p - 2 * q;
+        ok[dp][dq] = pp >= 0 && pp < P && q >= 0 && q < Q && r >= 0 && r < 3 && ss >= 0 &&
+                     ss < 3;
+        const long o = (((long)n * P + pp) * Q + q) * C + c;
+        g[dp][dq] = ok[dp][dq] ? *(const V*)(dy + o) : V{};
+        a[dp][dq] = ok[dp][dq] ? *(const A*)(am + o) : (A)0;
+      }
+    }
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int dp = 0; dp < 2; ++dp)
+#pragma unroll
+      for (int dq = 0; dq < 2; ++dq) {
+        if (!ok[dp][dq]) continue;
+        const int tap = (h + p - 2 * (ph - 1 + dp)) * 3 + (w + p - 2 * (qw - 1 + dq));
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+          if ((int)((a[dp][dq] >> (8 * j)) & 0xff) == tap) acc[j] += to_f(g[dp][dq][j]);
+      }
+    V out;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) out[j] = from_f<T>(acc[j]);
+    *(V*)(dx + i * VEC) = out;
+  }
+}
+
 // ----------------------------------------------------------------------------- avgpool
 template <typename T>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, int N, int HW, int C,
@@ -238,9 +357,14 @@ extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, i
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "maxpool: inconsistent output size");
   const long total = (long)N * P * Q * (C / VEC);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total)), dim3(256),
-                                       0, (hipStream_t)stream, (const T*)x, N, H, W, C, k, s, p,
-                                       (T*)y, argmax, P, Q));
+  if (k == 3 && s == 2)
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool3s2_fwd_kernel<T>, dim3(grid_for(total)),
+                                         dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W,
+                                         C, p, (T*)y, argmax, P, Q));
+  else
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total)),
+                                         dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W,
+                                         C, k, s, p, (T*)y, argmax, P, Q));
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -251,9 +375,14 @@ extern "C" int mmdx_maxpool_bwd(int dtype, const uint8_t* argmax, const void* dy
   const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(C % VEC == 0, "maxpool bwd: bad C");
   const long total = (long)N * H * W * (C / VEC);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total)), dim3(256),
-                                       0, (hipStream_t)stream, argmax, (const T*)dy, N, H, W, C,
-                                       k, s, p, P, Q, (T*)dx));
+  if (k == 3 && s == 2 && p <= 1)
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool3s2_bwd_kernel<T>, dim3(grid_for(total)),
+                                         dim3(256), 0, (hipStream_t)stream, argmax,
+                                         (const T*)dy, N, H, W, C, p, P, Q, (T*)dx));
+  else
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total)),
+                                         dim3(256), 0, (hipStream_t)stream, argmax,
+                                         (const T*)dy, N, H, W, C, k, s, p, P, Q, (T*)dx));
   MMDX_LAUNCH_CHECK();
   return 0;
 }

@@ -300,15 +300,18 @@ def test_batchnorm(dev, dt, train, res, relu):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_pools(dev, dt):
+@pytest.mark.parametrize("hwp", [(12, 11, 1), (16, 16, 1), (13, 14, 0), (112, 112, 1)])
+def test_pools(dev, dt, hwp):
+    """3x3 / stride-2 max pool (the stem's, specialised kernels) fwd + bwd, ties included."""
     g = torch.Generator().manual_seed(4)
-    N, C, H, W = 2, 64, 12, 11
+    H, W, pad = hwp
+    N, C = (2, 64) if H < 100 else (4, 64)
     x = torch.randn(N, C, H, W, generator=g)
     x[:, :, :4, :4] = 0.0  # ties, as after ReLU
     if dt == torch.bfloat16:
         x = x.bfloat16().float()
     xr = x.clone().requires_grad_(True)
-    yr = tF.max_pool2d(xr, 3, 2, 1)
+    yr = tF.max_pool2d(xr, 3, 2, pad)
     dy = torch.randn(yr.shape, generator=g)
     if dt == torch.bfloat16:
         dy = dy.bfloat16().float()
@@ -318,12 +321,12 @@ def test_pools(dev, dt):
     y = torch.empty(N, P, Q, C, dtype=dt, device=dev)
     am = torch.empty(N, P, Q, C, dtype=torch.uint8, device=dev)
     dc = L.dtype_code(dt)
-    L.call("mmdx_maxpool_fwd", dc, xd.data_ptr(), N, H, W, C, 3, 2, 1, y.data_ptr(),
+    L.call("mmdx_maxpool_fwd", dc, xd.data_ptr(), N, H, W, C, 3, 2, pad, y.data_ptr(),
            am.data_ptr(), P, Q, L.stream())
     _close(y.permute(0, 3, 1, 2), yr.detach(), dt, "maxpool fwd")
     dyd = dy.permute(0, 2, 3, 1).contiguous().to(dev, dt)
     dx = torch.empty_like(xd)
-    L.call("mmdx_maxpool_bwd", dc, am.data_ptr(), dyd.data_ptr(), N, H, W, C, 3, 2, 1, P, Q,
+    L.call("mmdx_maxpool_bwd", dc, am.data_ptr(), dyd.data_ptr(), N, H, W, C, 3, 2, pad, P, Q,
            dx.data_ptr(), L.stream())
     _close(dx.permute(0, 3, 1, 2), xr.grad, dt, "maxpool bwd")
     f = torch.empty(N, C, dtype=dt, device=dev)
