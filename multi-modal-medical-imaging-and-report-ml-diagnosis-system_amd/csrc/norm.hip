@@ -122,6 +122,26 @@ __device__ __forceinline__ float slab_sum(int nblk, int sub, float* red, F f) {
   else return block_sum<256>(v, red);
 }
 
+// slab_sum over slabs already held in registers (vals[j] = slab sub + TPC*j): the same
+// accumulator assignment and order as slab_sum, so the result is bit-identical, but the
+// channel's slabs are read from memory once for both passes of the finalize.
+template <int TPC, int PER, class F>
+__device__ __forceinline__ float slab_sum_regs(const float2* vals, int nblk, int sub, float* red,
+                                               F f) {
+  float a4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int b = sub + TPC * j;
+    if (b < nblk) a4[j & 3] += f(b, vals[j]);
+  }
+  const float v = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  if constexpr (TPC == 64) return wave_sum(v);
+  else return block_sum<256>(v, red);
+}
+
+// slabs per thread held in registers by the finalize kernels (more: two passes over memory)
+constexpr int FIN_PER = 16;
+
 // TPC = threads per channel: 64 (one wave; few slabs) or 256 (whole block; thousands of
 // slabs, e.g. the 3136 per-128-row slabs of a layer1 conv at batch 128)
 template <int TPC>
@@ -136,14 +156,31 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   if (c >= C) return;  // uniform per wave (TPC = 64) or per block (TPC = 256)
   const long last = rows - (long)(nblk - 1) * rpb;  // rows of the final (short) slab
   const float2* pc = part + (long)c * nblk;          // this channel's slabs, contiguous
-  const float mean = slab_sum<TPC>(nblk, sub, red, [&](int b) {
-    return (b == nblk - 1 ? (float)last : (float)rpb) * pc[b].x;
-  }) / (float)rows;
-  const float m2 = slab_sum<TPC>(nblk, sub, red, [&](int b) {
-    const float2 p = pc[b];
-    const float d = p.x - mean;
-    return p.y + (b == nblk - 1 ? (float)last : (float)rpb) * d * d;
-  });
+  float mean, m2;
+  if (nblk <= TPC * FIN_PER) {  // one read of the slabs (all loads in flight together)
+    float2 v[FIN_PER];
+#pragma unroll
+    for (int j = 0; j < FIN_PER; ++j) {
+      const int b = sub + TPC * j;
+      v[j] = b < nblk ? pc[b] : make_float2(0.f, 0.f);
+    }
+    mean = slab_sum_regs<TPC, FIN_PER>(v, nblk, sub, red, [&](int b, float2 p) {
+      return (b == nblk - 1 ? (float)last : (float)rpb) * p.x;
+    }) / (float)rows;
+    m2 = slab_sum_regs<TPC, FIN_PER>(v, nblk, sub, red, [&](int b, float2 p) {
+      const float d = p.x - mean;
+      return p.y + (b == nblk - 1 ? (float)last : (float)rpb) * d * d;
+    });
+  } else {
+    mean = slab_sum<TPC>(nblk, sub, red, [&](int b) {
+      return (b == nblk - 1 ? (float)last : (float)rpb) * pc[b].x;
+    }) / (float)rows;
+    m2 = slab_sum<TPC>(nblk, sub, red, [&](int b) {
+      const float2 p = pc[b];
+      const float d = p.x - mean;
+      return p.y + (b == nblk - 1 ? (float)last : (float)rpb) * d * d;
+    });
+  }
   const int lane = sub;
   if (lane != 0) return;
   const float var = m2 / (float)rows;
@@ -319,8 +356,20 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
   const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
   if (c >= C) return;
   const float2* pc = part + (long)c * nblk;  // this channel's slabs, contiguous
-  const float sg = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].x; });
-  const float sgx = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].y; });
+  float sg, sgx;
+  if (nblk <= TPC * FIN_PER) {  // one read of the slabs for both sums
+    float2 v[FIN_PER];
+#pragma unroll
+    for (int j = 0; j < FIN_PER; ++j) {
+      const int b = sub + TPC * j;
+      v[j] = b < nblk ? pc[b] : make_float2(0.f, 0.f);
+    }
+    sg = slab_sum_regs<TPC, FIN_PER>(v, nblk, sub, red, [](int, float2 p) { return p.x; });
+    sgx = slab_sum_regs<TPC, FIN_PER>(v, nblk, sub, red, [](int, float2 p) { return p.y; });
+  } else {
+    sg = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].x; });
+    sgx = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].y; });
+  }
   if (sub != 0) return;
   if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
   if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;
