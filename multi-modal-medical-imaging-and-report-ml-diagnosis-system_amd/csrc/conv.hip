@@ -256,9 +256,11 @@ template <> struct DmaOk<DgradK<bf16, true>> { static constexpr bool value = tru
 template <> struct DmaOk<Im2colK<bf16, false>> { static constexpr bool value = true; };
 
 // buffer-DMA preconditions: 32-bit byte offsets (< 2 GiB) and a 32-bit tap-validity mask
-static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32) {
+static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32, long rows = 0) {
   const long xb = (long)g.N * g.H * g.W * g.C * 2, yb = (long)g.N * g.P * g.Q * g.K * 2;
   if (xb >= (1L << 31) || yb >= (1L << 31) || g.R * g.S > max_taps) return false;
+  // the k-major gathers decode their rows by float reciprocal (fdivu): rows < 2^22
+  if (rows >= (1L << 22) - 256) return false;
   return !dgrad || (g.sh == 1 && g.sw == 1);
 }
 
@@ -303,11 +305,11 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
-                        dma_geom_ok(g, false));
+                        dma_geom_ok(g, false, 32, M));
   // channel count a power of two: the LDS-DMA kernel decodes each lane's tap itself
   const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
   Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
-  return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64));
+  return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64, M));
 }
 
 template <typename T>
@@ -324,10 +326,10 @@ static int conv_fwd_bn_eval_t(const mmdx_conv_desc* d, const void* x, const void
   epi.res = (const T*)res; epi.relu = relu != 0;
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm_epi<T>(Im2colK<T, true>{(const T*)x, g, M}, w, epi, M, N, K, st,
-                            dma_geom_ok(g, false));
+                            dma_geom_ok(g, false, 32, M));
   const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
   Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
-  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, pow2 && dma_geom_ok(g, false, 64));
+  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, pow2 && dma_geom_ok(g, false, 64, M));
 }
 
 // Strided dgrad as sh*sw phase GEMMs (see DgradPhaseK); phases no tap reaches are written
@@ -357,7 +359,7 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       bs.tile0 += (M + 127) / 128;  // the next phase's tiles follow this phase's
       int rc = -1;
       if constexpr (sizeof(T) == 2) {
-        if (dma_geom_ok(g, false)) {
+        if (dma_geom_ok(g, false, 32, M)) {
           const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
           if (N <= 64 || tiles128 < kNarrowBelow)
             rc = launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
@@ -389,7 +391,7 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
   if (g.K % KTile<T>::BK == 0)
     return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
-                        nullptr, dma_geom_ok(g, true), bs);
+                        nullptr, dma_geom_ok(g, true, 32, M), bs);
   return conv_gemm<T>(DgradK<T, false>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
 }
 
@@ -430,8 +432,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu", ws_bytes, need);
   DenseR<T> sa{(const T*)dy, g.K, M, true, K};
   const int pq = g.P * g.Q;
-  Im2colR<T> sb{(const T*)x, g, N, 1.f / (float)pq, 1.f / (float)g.Q, 64 / pq, (64 % pq) / g.Q,
-                (64 % pq) % g.Q};  // lane stepping: one 64-pixel K tile per issue
+  const Im2colR<T> sb = make_im2colr<T>((const T*)x, g, N);  // one 64-pixel K tile per issue
   EpiPartial epi{(float*)ws, M, N};
   int rc;
   if constexpr (sizeof(T) == 2) {
@@ -578,10 +579,11 @@ extern "C" int mmdx_conv_dgrad_stat_blocks(int dtype, const mmdx_conv_desc* d) {
   if (dtype != BF16 || !d || d->K % 64 != 0 || d->C % 8 != 0) return 0;
   const ConvGeom g = geom(d);
   if (g.sh == 1 && g.sw == 1) {
-    if (!dma_geom_ok(g, true)) return 0;
+    if (!dma_geom_ok(g, true, 32, (long)g.N * g.H * g.W)) return 0;
     return (int)(((long)g.N * g.H * g.W + 127) / 128);
   }
-  if (!dma_geom_ok(g, false)) return 0;
+  // every phase has at most N*H*W rows: this check passing implies each phase's launch passes
+  if (!dma_geom_ok(g, false, 32, (long)g.N * g.H * g.W)) return 0;
   long tiles = 0;
   for (int a = 0; a < g.sh; ++a)
     for (int b = 0; b < g.sw; ++b) {

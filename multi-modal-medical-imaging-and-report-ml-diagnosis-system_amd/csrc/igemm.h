@@ -65,6 +65,30 @@ template <> struct KTile<float> { static constexpr int BK = 32; };
 // Generic per-K-tile context: just the tile origin and the split's k bound.
 struct KCtx { int k0, klim; };
 
+// a / b for 0 <= a < 2^22, b >= 1 (uniform): float reciprocal estimate + one correction
+// step (the estimate is within 1 of the quotient) — ~8 VALU instead of the ~30 of an integer
+// division; the LDS-DMA prologue decodes every row it loads with it.
+__device__ __forceinline__ int fdivu(int a, int b) {
+  int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
+  const int r = a - q * b;
+  q += (r >= b) - (r < 0);
+  return q;
+}
+
+// Bit mask of the valid filter taps (bit r*S + s) for r in [rlo, rhi) x s in [slo, shi),
+// bounds clamped to [0, R) x [0, S) (R*S <= 32): two bit ranges and R shifted copies instead of
+// an R*S loop of bounds tests.
+__device__ __forceinline__ unsigned tap_mask(int rlo, int rhi, int slo, int shi, int R, int S) {
+  rlo = max(rlo, 0); rhi = min(rhi, R);
+  slo = max(slo, 0); shi = min(shi, S);
+  if (rhi <= rlo || shi <= slo) return 0u;
+  const unsigned sb = (unsigned)((1ull << shi) - (1ull << slo));
+  const unsigned rb = (unsigned)((1ull << rhi) - (1ull << rlo));
+  unsigned m = 0u;
+  for (int r = 0; r < R; ++r) m |= ((rb >> r) & 1u) ? sb << (r * S) : 0u;
+  return m;
+}
+
 // --------------------------------------------------------------------------------------
 // Operand sources.  `row(r)` -> per-row state (computed once per block), `ktile(k0,klim)`
 // -> per-K-tile state (scalar, once per tile), `load(rs, kt, off)` -> one 16-B vector:
@@ -140,11 +164,15 @@ struct DenseR {
   }
   __device__ const void* bbase() const { return base; }
   __device__ unsigned bbytes() const { return (unsigned)((long)vrows * ld * sizeof(T)); }
-  static constexpr bool STEP = false;
-  struct Lane {};
-  __device__ Lane lane_at(int) const { return Lane{}; }
-  __device__ void lane_step(Lane&) const {}
-  __device__ int roff_at(RowState rs, const Lane&, int k, int klim) const { return roff(rs, k, klim); }
+  // LDS-DMA lane state: element offset k*ld of this lane's k-line, stepped one 64-deep K tile
+  // per issue (an add instead of a multiply per DMA; the operand is < 2 GiB)
+  static constexpr bool STEP = true;
+  struct Lane { int koff; };
+  __device__ Lane lane_at(int k) const { return Lane{k * (int)ld}; }
+  __device__ void lane_step(Lane& l) const { l.koff += (int)ld << 6; }
+  __device__ int roff_at(RowState rs, const Lane& l, int k, int klim) const {
+    return rs >= 0 && k < klim ? (l.koff + rs) * (int)sizeof(T) : -1;
+  }
   // byte offset of the 8 rows from rs at k, or -1 (zeros)
   __device__ int roff(RowState rs, int k, int klim) const {
     return rs >= 0 && k < klim ? (int)(((long)k * ld + rs) * sizeof(T)) : -1;
@@ -225,16 +253,13 @@ struct Im2colK {
   static constexpr bool LANE_TAP = !FAST;
   __device__ int brow(int m, Mask& mask) const {
     const int pq = g.P * g.Q;
-    const int n = m / pq, rem = m - n * pq;
-    const int p = rem / g.Q, q = rem - p * g.Q;
+    const int n = fdivu(m, pq), rem = m - n * pq;
+    const int p = fdivu(rem, g.Q), q = rem - p * g.Q;
     const int ih0 = p * g.sh - g.ph, iw0 = q * g.sw - g.pw;
     if constexpr (FAST) {
       mask = 0u;
       if (m >= M) return 0;
-      for (int r = 0; r < g.R; ++r)
-        for (int s = 0; s < g.S; ++s)
-          if ((unsigned)(ih0 + r) < (unsigned)g.H && (unsigned)(iw0 + s) < (unsigned)g.W)
-            mask |= 1u << (r * g.S + s);
+      mask = tap_mask(-ih0, g.H - ih0, -iw0, g.W - iw0, g.R, g.S);
     } else {
       mask = m < M ? (int)(((unsigned)ih0 << 16) | ((unsigned)iw0 & 0xffffu)) : (int)0x80008000;
       if (m >= M) return 0;
@@ -337,12 +362,10 @@ struct DgradK {
     mask = 0u;
     if (m >= M) return 0;
     const int hw = g.H * g.W;
-    const int n = m / hw, rem = m - n * hw;
-    const int h = rem / g.W, w = rem - h * g.W;
-    for (int r = 0; r < g.R; ++r)
-      for (int s = 0; s < g.S; ++s)
-        if ((unsigned)(h + g.ph - r) < (unsigned)g.P && (unsigned)(w + g.pw - s) < (unsigned)g.Q)
-          mask |= 1u << (r * g.S + s);
+    const int n = fdivu(m, hw), rem = m - n * hw;
+    const int h = fdivu(rem, g.W), w = rem - h * g.W;
+    // valid taps: 0 <= h + ph - r < P, 0 <= w + pw - s < Q
+    mask = tap_mask(h + g.ph - g.P + 1, h + g.ph + 1, w + g.pw - g.Q + 1, w + g.pw + 1, g.R, g.S);
     return (int)((((long)n * g.P + h + g.ph) * g.Q + w + g.pw) * g.K * (long)sizeof(T));
   }
   __device__ void btile(int k0, int& toff, int& tap) const {
@@ -412,12 +435,11 @@ struct DgradPhaseK {
     mask = 0u;
     if (m >= M) return 0;
     const int hw = ph.Hp * ph.Wp;
-    const int n = m / hw, rem = m - n * hw;
-    const int i = rem / ph.Wp, j = rem - i * ph.Wp;
-    for (int u = 0; u < ph.ntr; ++u)
-      for (int v = 0; v < ph.nts; ++v)
-        if ((unsigned)(i + ph.dr0 - u) < (unsigned)g.P && (unsigned)(j + ph.ds0 - v) < (unsigned)g.Q)
-          mask |= 1u << (u * ph.nts + v);
+    const int n = fdivu(m, hw), rem = m - n * hw;
+    const int i = fdivu(rem, ph.Wp), j = rem - i * ph.Wp;
+    // valid taps: 0 <= i + dr0 - u < P, 0 <= j + ds0 - v < Q
+    mask = tap_mask(i + ph.dr0 - g.P + 1, i + ph.dr0 + 1, j + ph.ds0 - g.Q + 1, j + ph.ds0 + 1,
+                    ph.ntr, ph.nts);
     return (int)((((long)n * g.P + i) * g.Q + j) * g.K * (long)sizeof(T));
   }
   __device__ void btile(int k0, int& toff, int& tap) const {
@@ -473,16 +495,21 @@ template <typename T>
 struct Im2colR {
   const T* x; ConvGeom g; int Rows; float inv_pq, inv_q;  // 1/(P*Q), 1/Q for roff()
   int dn, dp, dq;  // one 64-pixel K tile = dn*P*Q + dp*Q + dq pixels (lane stepping)
-  struct RowState { int r, s, c; };
+  // lane stepping in input coordinates (set by the host, im2colr_steps): one K tile moves a
+  // lane's window origin (ih0, iw0) by (dp*sh, dq*sw) and its element offset by doff; a q
+  // (p) wrap moves it by (sh, -Q*sw) (-P*sh) and the offset by wq (wp)
+  int dih, diw, doff, qlim, qspan, wq, plim, pspan, wp;
+  struct RowState { int r, s, c, toff; };  // toff = element offset of tap (r, s), channel c
   typedef KCtx KT;
   typedef typename Vec16<T>::type V;
   __device__ RowState row(int row) const {
     RowState rs;
-    if (row >= Rows) { rs.r = -1; rs.s = rs.c = 0; return rs; }
+    if (row >= Rows) { rs.r = -1; rs.s = rs.c = rs.toff = 0; return rs; }
     const int tap = row / g.C;
     rs.c = row - tap * g.C;
     rs.r = tap / g.S;
     rs.s = tap - rs.r * g.S;
+    rs.toff = (rs.r * g.W + rs.s) * g.C + rs.c;
     return rs;
   }
   __device__ KT ktile(int k0, int klim) const { return KT{k0, klim}; }
@@ -508,30 +535,40 @@ struct Im2colR {
   }
   __device__ const void* bbase() const { return x; }
   __device__ unsigned bbytes() const { return (unsigned)((long)g.N * g.H * g.W * g.C * sizeof(T)); }
-  // LDS-DMA lane state: (n, p, q) of this lane's pixel, advanced one K tile per issue
+  // LDS-DMA lane state: the window origin (ih0, iw0) of this lane's pixel and the element
+  // offset of (n, ih0, iw0, 0), advanced one K tile per issue with adds and two wrap selects
+  // (no multiplies in the K loop; the tensor is < 2 GiB, so 32-bit offsets)
   static constexpr bool STEP = true;
-  struct Lane { int n, p, q; };
+  struct Lane { int ih0, iw0, off; };
   __device__ Lane lane_at(int k) const {
     const int pq = g.P * g.Q;
+    int n = (int)((float)k * inv_pq);
+    int rem = k - n * pq;
+    if (rem < 0) { --n; rem += pq; } else if (rem >= pq) { ++n; rem -= pq; }
+    int p = (int)((float)rem * inv_q);
+    int q = rem - p * g.Q;
+    if (q < 0) { --p; q += g.Q; } else if (q >= g.Q) { ++p; q -= g.Q; }
     Lane l;
-    l.n = (int)((float)k * inv_pq);
-    int rem = k - l.n * pq;
-    if (rem < 0) { --l.n; rem += pq; } else if (rem >= pq) { ++l.n; rem -= pq; }
-    l.p = (int)((float)rem * inv_q);
-    l.q = rem - l.p * g.Q;
-    if (l.q < 0) { --l.p; l.q += g.Q; } else if (l.q >= g.Q) { ++l.p; l.q -= g.Q; }
+    l.ih0 = p * g.sh - g.ph;
+    l.iw0 = q * g.sw - g.pw;
+    l.off = ((n * g.H + l.ih0) * g.W + l.iw0) * g.C;
     return l;
   }
   __device__ void lane_step(Lane& l) const {
-    l.q += dq; l.p += dp; l.n += dn;
-    if (l.q >= g.Q) { l.q -= g.Q; ++l.p; }
-    if (l.p >= g.P) { l.p -= g.P; ++l.n; }
+    l.iw0 += diw; l.ih0 += dih; l.off += doff;
+    const bool wq_ = l.iw0 >= qlim;
+    l.iw0 -= wq_ ? qspan : 0;
+    l.ih0 += wq_ ? g.sh : 0;
+    l.off += wq_ ? wq : 0;
+    const bool wp_ = l.ih0 >= plim;
+    l.ih0 -= wp_ ? pspan : 0;
+    l.off += wp_ ? wp : 0;
   }
   __device__ int roff_at(const RowState& rs, const Lane& l, int k, int klim) const {
-    if (rs.r < 0 || k >= klim) return -1;
-    const int ih = l.p * g.sh - g.ph + rs.r, iw = l.q * g.sw - g.pw + rs.s;
-    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return -1;
-    return (int)(((((long)l.n * g.H + ih) * g.W + iw) * g.C + rs.c) * (long)sizeof(T));
+    const int ih = l.ih0 + rs.r, iw = l.iw0 + rs.s;
+    const bool ok = rs.r >= 0 && k < klim && (unsigned)ih < (unsigned)g.H &&
+                    (unsigned)iw < (unsigned)g.W;
+    return ok ? (l.off + rs.toff) * (int)sizeof(T) : -1;
   }
   // pixel k -> (n, p, q) by float reciprocals (k < 2^23: one correction step is exact)
   __device__ int roff(const RowState& rs, int k, int klim) const {
@@ -548,6 +585,30 @@ struct Im2colR {
     return (int)(((((long)n * g.H + ih) * g.W + iw) * g.C + rs.c) * (long)sizeof(T));
   }
 };
+
+// Host: the wgrad im2col^T operand with its per-K-tile lane-stepping constants (64 pixels).
+template <typename T>
+inline Im2colR<T> make_im2colr(const T* x, const ConvGeom& g, int rows) {
+  Im2colR<T> s{};
+  s.x = x; s.g = g; s.Rows = rows;
+  const int pq = g.P * g.Q;
+  s.inv_pq = 1.f / (float)pq;
+  s.inv_q = 1.f / (float)g.Q;
+  s.dn = 64 / pq;
+  s.dp = (64 % pq) / g.Q;
+  s.dq = (64 % pq) % g.Q;
+  const int HWC = g.H * g.W * g.C, WC = g.W * g.C;
+  s.dih = s.dp * g.sh;
+  s.diw = s.dq * g.sw;
+  s.doff = s.dn * HWC + s.dih * WC + s.diw * g.C;
+  s.qlim = g.Q * g.sw - g.pw;
+  s.qspan = g.Q * g.sw;
+  s.wq = -s.qspan * g.C + g.sh * WC;
+  s.plim = g.P * g.sh - g.ph;
+  s.pspan = g.P * g.sh;
+  s.wp = -s.pspan * WC + HWC;
+  return s;
+}
 
 // --------------------------------------------------------------------------------------
 // Tile loaders (global -> registers -> LDS) and MFMA fragment reads from their LDS image.
@@ -867,9 +928,19 @@ struct EpiStore {
   __device__ __forceinline__ void reg_stats(const f32x4 (&acc)[RM][RN], float* red, int tm,
                                             int tn, int wm, int wn, int lane) const {
     if (!stats) return;
+    // a full tile (every block but the last row of tiles) takes the branch-free instance: all
+    // counts are the same power of two, so the masks, the divisions and the count shuffles
+    // fold to constants — the same float operations on the same values (bit-identical)
+    if (M - tm * BM >= BM)
+      reg_stats_t<BM, BN, WM, WN, RM, RN, true>(acc, red, tm, tn, wm, wn, lane);
+    else
+      reg_stats_t<BM, BN, WM, WN, RM, RN, false>(acc, red, tm, tn, wm, wn, lane);
+  }
+  template <int BM, int BN, int WM, int WN, int RM, int RN, bool FULL>
+  __device__ __forceinline__ void reg_stats_t(const f32x4 (&acc)[RM][RN], float* red, int tm,
+                                              int tn, int wm, int wn, int lane) const {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     const int rows_valid = min(BM, M - tm * BM);
-    const bool full = rows_valid == BM;
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
       float cnt = 0.f, s = 0.f;
@@ -877,27 +948,28 @@ struct EpiStore {
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool ok = full || wm * WTM + i * 16 + (lane >> 4) * 4 + r < rows_valid;
+          const bool ok = FULL || wm * WTM + i * 16 + (lane >> 4) * 4 + r < rows_valid;
           cnt += ok ? 1.f : 0.f;
           s += ok ? acc[i][j][r] : 0.f;
         }
+      if constexpr (FULL) cnt = (float)(RM * 4);
       const float mean = cnt > 0.f ? s / cnt : 0.f;
       float m2 = 0.f;
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool ok = full || wm * WTM + i * 16 + (lane >> 4) * 4 + r < rows_valid;
+          const bool ok = FULL || wm * WTM + i * 16 + (lane >> 4) * 4 + r < rows_valid;
           const float d = acc[i][j][r] - mean;
           m2 += ok ? d * d : 0.f;
         }
       float n_a = cnt, mu = mean, mm = m2;
 #pragma unroll
       for (int x = 16; x <= 32; x <<= 1) {
-        const float n_b = __shfl_xor(n_a, x, 64), mu_b = __shfl_xor(mu, x, 64),
-                    mm_b = __shfl_xor(mm, x, 64);
+        const float n_b = FULL ? n_a : __shfl_xor(n_a, x, 64);
+        const float mu_b = __shfl_xor(mu, x, 64), mm_b = __shfl_xor(mm, x, 64);
         const float tot = n_a + n_b;
-        const float d = mu_b - mu, f = tot > 0.f ? n_b / tot : 0.f;
+        const float d = mu_b - mu, f = FULL ? 0.5f : (tot > 0.f ? n_b / tot : 0.f);
         mu += d * f;
         mm += mm_b + d * d * n_a * f;
         n_a = tot;
@@ -923,10 +995,11 @@ struct EpiStore {
 #pragma unroll
       for (int q = 0; q < WM; ++q) {
         const float* o = red + (q * BN + col) * 3;
-        const float nb = o[0], mb = o[1], m2b = o[2];
+        const float nb = FULL ? (float)WTM : o[0], mb = o[1], m2b = o[2];
         if (nb == 0.f) continue;
         if (nn == 0.f) { nn = nb; mu = mb; mm = m2b; continue; }
-        const float tot = nn + nb, d = mb - mu, f = nb / tot;
+        // full tiles: equal counts, f = nb / (q + 1) nb exactly
+        const float tot = nn + nb, d = mb - mu, f = FULL ? 1.f / (float)(q + 1) : nb / tot;
         mu += d * f;
         mm += m2b + d * d * nn * f;
         nn = tot;
@@ -1284,6 +1357,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, char* lds, un
 template <int ROWS, class Src, int BK_ = 64>
 struct DmaK {
   static constexpr int BK = BK_;
+  static constexpr bool RMAJOR = false;
   static constexpr int NW = NT / 64;
   static constexpr int CPR = BK / 8;                 // 16-B chunks per row
   static constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
@@ -1340,6 +1414,8 @@ struct DmaK {
 template <int ROWS, class Src, int BK_ = 64>
 struct DmaR {
   static constexpr int BK = BK_;
+  static constexpr bool RMAJOR = true;
+  static_assert(!Src::STEP || BK == 64, "lane stepping advances one 64-deep K tile");
   static constexpr int NW = NT / 64;
   static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
   static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
@@ -1402,6 +1478,10 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                           typename OB::SrcT sb, Epi epi, int M,
                                                           int N, int K, int kper) {
   constexpr int BK = OA::BK, WM = 2, WN = 2;
+  // fragments-first K loop (below): measured on the C4 conv shapes, 5-13 % faster for the
+  // R-major (weight-gradient) operands and most 128-wide tiles, mixed on the 128x64 k-major
+  // tiles (three blocks per CU there already cover the LDS latency)
+  constexpr bool FRAG_FIRST = BN == 128 || OA::RMAJOR;
   static_assert(OB::BK == BK, "operand K tile depths differ");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
@@ -1424,7 +1504,9 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   const int kbeg = zsplit * kper;
   const int kend = min(K, kbeg + kper);
   const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wave index as a scalar: the LDS-DMA destinations (M0) and fragment bases become SALU math
+  const int lane = threadIdx.x & 63,
+            wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int wm = wid / WN, wn = wid % WN;
 
   OA oa;
@@ -1458,13 +1540,46 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    const char* as = lds_raw + (t % NS) * STAGE;
+    const char* bs = as + OA::BYTES;
+    if constexpr (FRAG_FIRST) {
+      // every fragment of the tile is requested before the next tile's DMAs are issued, so
+      // the LDS read latency runs under the DMA issue instead of in front of the MFMAs
+      constexpr int KS = BK / 32;
+      bf16x8 af[KS][RM], bfr[KS][RN];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[s][i] = OA::frag(as, wm * WTM + i * 16, s * 32, lane);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[s][j] = OB::frag(bs, wn * WTN + j * 16, s * 32, lane);
+      }
+      if (t + NS - 1 < nt) {
+        char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
+        oa.issue(sa, st, kbeg + (t + NS - 1) * BK, kend, wid);
+        ob.issue(sb, st + OA::BYTES, kbeg + (t + NS - 1) * BK, kend, wid);
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            if constexpr (std::is_same<ET, f16>::value)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                  __builtin_bit_cast(f16x8, af[s][i]), __builtin_bit_cast(f16x8, bfr[s][j]),
+                  acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j],
+                                                                   acc[i][j], 0, 0, 0);
+          }
+      continue;
+    }
     if (t + NS - 1 < nt) {  // its stage was consumed in iteration t-1 by every wave
       char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
       oa.issue(sa, st, kbeg + (t + NS - 1) * BK, kend, wid);
       ob.issue(sb, st + OA::BYTES, kbeg + (t + NS - 1) * BK, kend, wid);
     }
-    const char* as = lds_raw + (t % NS) * STAGE;
-    const char* bs = as + OA::BYTES;
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 32) {
       bf16x8 af[RM], bfr[RN];
