@@ -254,6 +254,7 @@ template <class S> struct DmaOk { static constexpr bool value = false; };
 template <> struct DmaOk<Im2colK<bf16, true>> { static constexpr bool value = true; };
 template <> struct DmaOk<DgradK<bf16, true>> { static constexpr bool value = true; };
 template <> struct DmaOk<Im2colK<bf16, false>> { static constexpr bool value = true; };
+template <> struct DmaOk<DenseK<bf16>> { static constexpr bool value = true; };
 
 // buffer-DMA preconditions: 32-bit byte offsets (< 2 GiB) and a 32-bit tap-validity mask
 static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32, long rows = 0) {
@@ -262,6 +263,11 @@ static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32, long r
   // the k-major gathers decode their rows by float reciprocal (fdivu): rows < 2^22
   if (rows >= (1L << 22) - 256) return false;
   return !dgrad || (g.sh == 1 && g.sw == 1);
+}
+
+// 1x1, stride 1, no padding: the implicit GEMM's gathers are plain dense matrices over NHWC
+static bool is_pointwise(const ConvGeom& g) {
+  return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
 }
 
 // 128x64 tiles when 128x128 would give fewer tiles than this (< 1.5 per CU); measured in the
@@ -303,6 +309,9 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
                       float* stats, hipStream_t st) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
+  if (g.C % KTile<T>::BK == 0 && is_pointwise(g))  // x itself is the [M][C] A operand
+    return conv_gemm<T>(DenseK<T>{(const T*)x, g.C, M, true}, w, y, M, N, K, 0.f, st, stats,
+                        dma_geom_ok(g, false, 32, M));
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
                         dma_geom_ok(g, false, 32, M));
@@ -324,6 +333,9 @@ static int conv_fwd_bn_eval_t(const mmdx_conv_desc* d, const void* x, const void
       EpiStore<T>{(T*)y, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr, nullptr};
   epi.gamma = gamma; epi.beta_bn = beta; epi.rmean = rmean; epi.rvar = rvar; epi.eps = eps;
   epi.res = (const T*)res; epi.relu = relu != 0;
+  if (g.C % KTile<T>::BK == 0 && is_pointwise(g))
+    return conv_gemm_epi<T>(DenseK<T>{(const T*)x, g.C, M, true}, w, epi, M, N, K, st,
+                            dma_geom_ok(g, false, 32, M));
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm_epi<T>(Im2colK<T, true>{(const T*)x, g, M}, w, epi, M, N, K, st,
                             dma_geom_ok(g, false, 32, M));
@@ -389,6 +401,9 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
   if ((g.sh > 1 || g.sw > 1) && g.K % KTile<T>::BK == 0)
     return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st, bs);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
+  if (g.K % KTile<T>::BK == 0 && is_pointwise(g))  // dY itself is the [M][K] A operand
+    return conv_gemm<T>(DenseK<T>{(const T*)dy, g.K, M, true}, w_crsk, dx, M, N, K, beta, st,
+                        nullptr, dma_geom_ok(g, true, 32, M), bs);
   if (g.K % KTile<T>::BK == 0)
     return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
                         nullptr, dma_geom_ok(g, true, 32, M), bs);
@@ -419,6 +434,22 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   return p;
 }
 
+template <typename T, class SB>
+static int wgrad_dma(const WgradPlan& p, const DenseR<T>& sa, const SB& sb, const EpiPartial& epi,
+                     int M, int N, int K, hipStream_t st) {
+  if (p.bm == 128 && p.bn == 128)
+    return launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, SB>>(sa, sb, epi, M, N, K,
+                                                                        p.splits, p.kper, st);
+  if (p.bm == 128)
+    return launch_dma_ops<128, 64, DmaR<128, DenseR<T>>, DmaR<64, SB>>(sa, sb, epi, M, N, K,
+                                                                      p.splits, p.kper, st);
+  if (p.bn == 128)
+    return launch_dma_ops<64, 128, DmaR<64, DenseR<T>>, DmaR<128, SB>>(sa, sb, epi, M, N, K,
+                                                                      p.splits, p.kper, st);
+  return launch_dma_ops<64, 64, DmaR<64, DenseR<T>>, DmaR<64, SB>>(sa, sb, epi, M, N, K,
+                                                                  p.splits, p.kper, st);
+}
+
 template <typename T>
 static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const void* dy,
                         float* dw, float beta, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -431,25 +462,18 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   const size_t need = (size_t)p.splits * M * N * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu", ws_bytes, need);
   DenseR<T> sa{(const T*)dy, g.K, M, true, K};
-  const int pq = g.P * g.Q;
   const Im2colR<T> sb = make_im2colr<T>((const T*)x, g, N);  // one 64-pixel K tile per issue
   EpiPartial epi{(float*)ws, M, N};
   int rc;
   if constexpr (sizeof(T) == 2) {
    if (dma_geom_ok(g, false, 1 << 30) && K < (1 << 23)) {
-    // LDS-DMA wgrad: both operands R-major (M = Kout and N = R*S*C are multiples of 8)
-    if (p.bm == 128 && p.bn == 128)
-      rc = launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, Im2colR<T>>>(
-          sa, sb, epi, M, N, K, p.splits, p.kper, st);
-    else if (p.bm == 128)
-      rc = launch_dma_ops<128, 64, DmaR<128, DenseR<T>>, DmaR<64, Im2colR<T>>>(
-          sa, sb, epi, M, N, K, p.splits, p.kper, st);
-    else if (p.bn == 128)
-      rc = launch_dma_ops<64, 128, DmaR<64, DenseR<T>>, DmaR<128, Im2colR<T>>>(
-          sa, sb, epi, M, N, K, p.splits, p.kper, st);
+    // LDS-DMA wgrad: both operands R-major (M = Kout and N = R*S*C are multiples of 8).  A
+    // 1x1 / stride-1 / unpadded conv's im2col^T is x^T itself: a dense R-major operand
+    // (no window decode or tap tests)
+    if (is_pointwise(g))
+      rc = wgrad_dma<T>(p, sa, DenseR<T>{(const T*)x, g.C, N, true, K}, epi, M, N, K, st);
     else
-      rc = launch_dma_ops<64, 64, DmaR<64, DenseR<T>>, DmaR<64, Im2colR<T>>>(
-          sa, sb, epi, M, N, K, p.splits, p.kper, st);
+      rc = wgrad_dma<T>(p, sa, sb, epi, M, N, K, st);
     if (rc) return rc;
     wgrad_reduce((const float*)ws, p.splits, g.K, g.C, cm, g.R * g.S, dw, beta, st);
     MMDX_LAUNCH_CHECK();

@@ -143,7 +143,9 @@ struct DenseR {
   typedef int RowState;
   typedef KCtx KT;
   typedef typename Vec16<T>::type V;
-  __device__ RowState row(int r) const { return r < R ? r : -1; }
+  // an out-of-range row is a large negative marker: its DMA offsets stay negative (= zeros)
+  // without a per-DMA row test
+  __device__ RowState row(int r) const { return r < R ? r : -(1 << 30); }
   __device__ KT ktile(int k0, int klim) const { return KT{k0, klim}; }
   __device__ V load(RowState rs, const KT& kt, int off) const {
     constexpr int VEC = Vec16<T>::N;
@@ -170,8 +172,10 @@ struct DenseR {
   struct Lane { int koff; };
   __device__ Lane lane_at(int k) const { return Lane{k * (int)ld}; }
   __device__ void lane_step(Lane& l) const { l.koff += (int)ld << 6; }
+  template <bool CHECK_K>
   __device__ int roff_at(RowState rs, const Lane& l, int k, int klim) const {
-    return rs >= 0 && k < klim ? (l.koff + rs) * (int)sizeof(T) : -1;
+    const int o = (l.koff + rs) * (int)sizeof(T);  // < 0 for an out-of-range row
+    return CHECK_K && k >= klim ? -1 : o;
   }
   // byte offset of the 8 rows from rs at k, or -1 (zeros)
   __device__ int roff(RowState rs, int k, int klim) const {
@@ -564,9 +568,11 @@ struct Im2colR {
     l.ih0 -= wp_ ? pspan : 0;
     l.off += wp_ ? wp : 0;
   }
+  template <bool CHECK_K>
   __device__ int roff_at(const RowState& rs, const Lane& l, int k, int klim) const {
+    // an out-of-range row has r = -1: ih = ih0 - 1 may still be valid, so it is tested
     const int ih = l.ih0 + rs.r, iw = l.iw0 + rs.s;
-    const bool ok = rs.r >= 0 && k < klim && (unsigned)ih < (unsigned)g.H &&
+    const bool ok = rs.r >= 0 && (!CHECK_K || k < klim) && (unsigned)ih < (unsigned)g.H &&
                     (unsigned)iw < (unsigned)g.W;
     return ok ? (l.off + rs.toff) * (int)sizeof(T) : -1;
   }
@@ -1444,9 +1450,16 @@ struct DmaR {
   }
   // called once per K tile, in order (k0 = kbeg, kbeg + 64, ...)
   __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) {
+    if (k0 + BK <= klim)  // uniform: every k-line of the tile is inside the split
+      issue_t<false>(s, stage, k0, klim, wid);
+    else
+      issue_t<true>(s, stage, k0, klim, wid);
+  }
+  template <bool CHECK_K>
+  __device__ void issue_t(const Src& s, char* stage, int k0, int klim, int wid) {
 #pragma unroll
     for (int j = 0; j < INSTR; ++j) {
-      const int o = s.roff_at(rs[j], ln[j], k0 + kr[j], klim);
+      const int o = s.template roff_at<CHECK_K>(rs[j], ln[j], k0 + kr[j], klim);
       dma16(rsrc, stage + (j * NW + wid) * 1024, o >= 0 ? (unsigned)o : DMA_OOB);
       if constexpr (Src::STEP) s.lane_step(ln[j]);
     }
