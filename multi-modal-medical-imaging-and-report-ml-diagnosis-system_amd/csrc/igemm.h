@@ -134,6 +134,11 @@ struct DenseK {
     return r < R ? (int)((long)r * ld * sizeof(T)) : 0;
   }
   __device__ void btile(int k0, int& toff, int& tap) const { toff = k0 * (int)sizeof(T); tap = 0; }
+  // K-tile iterator (DmaK): k = (u * T2 + v) * Cblk + c0; here one block spanning all of K
+  __device__ void tdims(int& cblk, int& t2) const { cblk = 1 << 30; t2 = 1; }
+  __device__ void tmap(int, int, int c0, int& toff, int& tap) const {
+    toff = c0 * (int)sizeof(T); tap = 0;
+  }
 };
 
 // Dense, rows contiguous: element (r, k) at base[k*ld + r].
@@ -286,6 +291,12 @@ struct Im2colK {
     const int c0 = k0 - tap * g.C, r = tap / g.S, s = tap - r * g.S;
     toff = ((r * g.W + s) * g.C + c0) * (int)sizeof(T);
   }
+  // K-tile iterator: (u, v) = filter tap (r, s), c0 = channel block
+  __device__ void tdims(int& cblk, int& t2) const { cblk = g.C; t2 = g.S; }
+  __device__ void tmap(int r, int s, int c0, int& toff, int& tap) const {
+    toff = ((r * g.W + s) * g.C + c0) * (int)sizeof(T);
+    tap = r * g.S + s;
+  }
 };
 
 // conv dgrad A operand: rows = input pixels (n,h,w), k = (r, s, kout) with kout contiguous.
@@ -377,6 +388,11 @@ struct DgradK {
     const int kb = k0 - tap * g.K, r = tap / g.S, s = tap - r * g.S;
     toff = (kb - (r * g.Q + s) * g.K) * (int)sizeof(T);
   }
+  __device__ void tdims(int& cblk, int& t2) const { cblk = g.K; t2 = g.S; }
+  __device__ void tmap(int r, int s, int kb, int& toff, int& tap) const {
+    toff = (kb - (r * g.Q + s) * g.K) * (int)sizeof(T);
+    tap = r * g.S + s;
+  }
 };
 
 // Strided-conv dgrad, one output phase (a, b) = (h mod sh, w mod sw) at a time: only the
@@ -451,6 +467,11 @@ struct DgradPhaseK {
     const int kb = k0 - tap * g.K, u = tap / ph.nts, v = tap - u * ph.nts;
     toff = (((ph.dr0 - u) * g.Q + (ph.ds0 - v)) * g.K + kb) * (int)sizeof(T);
   }
+  __device__ void tdims(int& cblk, int& t2) const { cblk = g.K; t2 = ph.nts; }
+  __device__ void tmap(int u, int v, int kb, int& toff, int& tap) const {
+    toff = (((ph.dr0 - u) * g.Q + (ph.ds0 - v)) * g.K + kb) * (int)sizeof(T);
+    tap = u * ph.nts + v;
+  }
 };
 
 // B operand of the phase dgrad: packed CRSK weights, k = (phase tap t, kout).
@@ -489,6 +510,11 @@ struct PhaseTapK {
   __device__ void btile(int k0, int& toff, int& tap) const {
     const int t = k0 / K, kb = k0 - t * K;
     const int u = t / ph.nts, v = t - u * ph.nts;
+    toff = (((ph.r0 + sh * u) * S + (ph.s0 + sw * v)) * K + kb) * (int)sizeof(T);
+    tap = 0;
+  }
+  __device__ void tdims(int& cblk, int& t2) const { cblk = K; t2 = ph.nts; }
+  __device__ void tmap(int u, int v, int kb, int& toff, int& tap) const {
     toff = (((ph.r0 + sh * u) * S + (ph.s0 + sw * v)) * K + kb) * (int)sizeof(T);
     tap = 0;
   }
@@ -1377,16 +1403,27 @@ struct DmaK {
   int off[INSTR];       // byte offset of this lane's chunk at tap 0
   Mask mask[INSTR];     // valid taps of the row
   int coff;             // element offset of this lane's logical chunk within the K tile
+  // uniform K-tile iterator: the K tiles are issued in order, so the tile's filter tap is
+  // stepped (k = (tu * tT + tv) * tC + tc0) instead of divided out of k0 every tile
+  int tc0, tv, tu, tC, tT;
   __device__ static int swz(int row) { return BK == 64 ? (row & 7) : ((row >> 1) & 3); }
-  __device__ void init(const Src& s, int row0, int lane, int wid, int /*kbeg*/) {
+  __device__ void init(const Src& s, int row0, int lane, int wid, int kbeg) {
     const int rr = lane / CPR, slot = lane % CPR;
     coff = (slot ^ swz(rr)) * 8;  // instructions start at a multiple of RPI rows
+    if constexpr (!Src::LANE_TAP) {
+      s.tdims(tC, tT);
+      const int tap = kbeg / tC;
+      tc0 = kbeg - tap * tC;
+      tu = tap / tT;
+      tv = tap - tu * tT;
+    }
     rsrc = dma_rsrc(s.bbase(), s.bbytes());
 #pragma unroll
     for (int j = 0; j < INSTR; ++j)  // LANE_TAP sources fold the chunk offset into toff
       off[j] = s.brow(row0 + (j * NW + wid) * RPI + rr, mask[j]) + (Src::LANE_TAP ? 0 : coff * 2);
   }
-  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) const {
+  // called once per K tile, in order (k0 = kbeg, kbeg + BK, ...)
+  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) {
     const bool kok = k0 + coff < klim;
     if constexpr (Src::LANE_TAP) {  // this lane's chunk has its own tap
       int toff, r, sx;
@@ -1399,7 +1436,12 @@ struct DmaK {
       return;
     }
     int toff, tap;
-    s.btile(k0, toff, tap);  // one tap for the whole K tile (uniform)
+    s.tmap(tu, tv, tc0, toff, tap);  // one tap for the whole K tile (uniform)
+    tc0 += BK;                       // C % BK == 0 (FAST sources): a tap ends on a tile edge
+    if (tc0 >= tC) {
+      tc0 = 0;
+      if (++tv == tT) { tv = 0; ++tu; }
+    }
 #pragma unroll
     for (int j = 0; j < INSTR; ++j) {
       const bool ok = kok && ((mask[j] >> tap) & 1u);
