@@ -395,7 +395,10 @@ def main():
     backend = os.environ.get("MMDX_DIST_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # MMDX_DP_REHEARSE=1 under torch.distributed.run with one rank: the full data-parallel
+    # path (RCCL process group, comm stream, mid-backward trunk all-reduces) on one GPU
+    dp = world > 1 or os.environ.get("MMDX_DP_REHEARSE", "0") == "1"
+    if dp:
         from mmdx.dist import init_distributed
         torch.cuda.set_device(local)
         init_distributed(backend, local)   # RCCL async errors / timeouts fail the job fast
@@ -409,7 +412,7 @@ def main():
     img, txt, fus, opt = build(cfg, dev, dtype)
     vit = cfg["image"] == "vit_b_16"
     params = [p for grp in opt.param_groups for p in grp["params"]]
-    if world > 1:  # identical initial weights on every rank (broadcast from rank 0)
+    if dp:  # identical initial weights on every rank (broadcast from rank 0)
         with torch.no_grad():
             for p in list(img.parameters()) + list(txt.parameters()) + list(fus.parameters()):
                 dist.broadcast(p, 0)
@@ -422,7 +425,7 @@ def main():
     x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
     side = torch.cuda.Stream(device=dev, priority=-1)
     from mmdx.dist import GradAllReducer
-    reducer = GradAllReducer(params, world) if world > 1 else None
+    reducer = GradAllReducer(params, world, rehearse=dp) if dp else None
     early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "1" if backend == "nccl" else "0")
     if reducer is not None and early_tail != "0":
         # the trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward, each from
@@ -440,7 +443,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     # Conv (dominant-family) launch durations: HIP events around every conv launch of the
     # LAST `ev_steps` timed steps (default K/10).  Bracketing every step costs ~0.75 ms/step
@@ -461,7 +464,7 @@ def main():
         # a cooperative recurrence that lost a peer invalidates the run: fail loudly
         from mmdx.bilstm import check_recurrence
         check_recurrence()
-    if world > 1:
+    if dp:
         dist.barrier()
     el = time.perf_counter() - t0
     # host cost of one step issued onto an idle device (no queue back-pressure)
@@ -474,7 +477,7 @@ def main():
     timer.enabled = was
     conv_steps = ev_steps
     timer.enabled = False
-    if world > 1:
+    if dp:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
@@ -513,7 +516,8 @@ def main():
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,
                    "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}" + ("-rccl-rehearsal" if dp and world == 1
+                                                  else "")},
         "loss": round(float(loss.item()), 5),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "host_ms_one_step_idle_device": round(host_one * 1e3, 3),
@@ -549,7 +553,7 @@ def main():
                                               else args.cpu_steps)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

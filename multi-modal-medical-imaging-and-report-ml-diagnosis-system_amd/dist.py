@@ -37,9 +37,12 @@ class GradAllReducer:
     """
 
     def __init__(self, params, world_size: int | None = None, bucket_bytes: int = BUCKET_BYTES,
-                 group=None, bucket_dtype: torch.dtype | None = None):
+                 group=None, bucket_dtype: torch.dtype | None = None, rehearse: bool = False):
         self.params = [p for p in params if p.requires_grad]
         self.world = world_size or dist.get_world_size(group)
+        # rehearse: run every collective even in a 1-rank group (RCCL on one GPU exercises
+        # the comm stream, the plan events and the write-back of the multi-GPU path)
+        self.active = self.world > 1 or rehearse
         self.bucket_bytes = bucket_bytes
         self.group = group
         # packed buckets may travel in bf16 (MMDX_DP_BUCKET_DTYPE=bf16: half the xGMI bytes
@@ -66,7 +69,7 @@ class GradAllReducer:
         (resnet.TRUNK_GRAD_HOOK): ~90 % of the trunk's gradient bytes move over xGMI while
         the earlier layers' backward still runs.  With RCCL the host never waits: the comm
         stream waits on the event, the collectives queue on it in issue order."""
-        if self.world == 1 or hi <= lo:
+        if not self.active or hi <= lo:
             return
         view = buf[lo:hi]
         # reduced in a private copy, written back by finish() on the caller's stream: nothing
@@ -101,7 +104,7 @@ class GradAllReducer:
 
     def launch(self, params=None):
         """Start the all-reduce of these parameters' gradients (default: all remaining)."""
-        if self.world == 1:
+        if not self.active:
             return
         ps = self.params if params is None else [p for p in params if p.requires_grad]
         grads = []
@@ -151,7 +154,7 @@ class GradAllReducer:
 
     def reduce(self):
         """All-reduce (mean) every existing .grad across ranks, in place."""
-        if self.world == 1:
+        if not self.active:
             return
         self.launch()
         self.finish()
