@@ -159,6 +159,8 @@ int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
                 float* save_mean, float* save_rstd,
                 const void* residual, int relu, void* y,
                 void* workspace, size_t ws_bytes, void* stream);
+/* y == NULL (train): statistics only — save_mean/save_rstd and the running-stat update, no
+ * apply pass (the consumer normalises on the fly, e.g. mmdx_maxpool_bn_fwd). */
 /* dy: grad w.r.t. y; y: forward output (ReLU mask source).  Writes dx, d_residual
  * (may be NULL), and dgamma/dbeta (fp32, accumulated with beta_acc). */
 int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
@@ -174,6 +176,19 @@ int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* 
 /* relu with y == NULL (a unit without residual): the ReLU mask is recomputed from x as
  * x*scale + shift > 0 with the forward's own scale/shift (gamma, bn_beta, save_mean,
  * save_rstd), so the post-activation tensor is not read. */
+
+/* The stem's BN backward reading its upstream gradient straight from the 3x3 / stride-2
+ * pool's output gradient dy_pooled [N][P][Q][C] and argmax (mmdx_maxpool_fwd /
+ * mmdx_maxpool_bn_fwd): dL/d(pool input) is gathered on the fly (rounded to the compute dtype,
+ * as mmdx_maxpool_bwd stores it), so the result equals mmdx_maxpool_bwd followed by
+ * mmdx_bn_bwd (y == NULL, no residual) without materialising the [N][H][W][C] gradient.
+ * x: the stem conv's raw output [N][H][W][C]. */
+int mmdx_bn_bwd_pool(int dtype, int train, const void* x, const uint8_t* argmax,
+                     const void* dy_pooled, int N, int H, int W, int C, int k, int s, int p,
+                     int P, int Q, const float* gamma, const float* bn_beta,
+                     const float* save_mean, const float* save_rstd, int relu, void* dx,
+                     float* dgamma, float* dbeta, float beta_acc, void* workspace,
+                     size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- launch plans
  * A plan is a host array of operations over caller-owned buffers, recorded once by the
@@ -194,7 +209,7 @@ enum {
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
   MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PAIR_INPUT,
   MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI,
-  MMDX_OP_CONV_FWD_BNEVAL
+  MMDX_OP_CONV_FWD_BNEVAL, MMDX_OP_MAXPOOL_BN_FWD, MMDX_OP_BN_BWD_POOL
 };
 typedef struct {
   int op, dtype, stream;
@@ -215,6 +230,17 @@ size_t mmdx_plan_op_size(void); /* sizeof(mmdx_plan_op): binding layout check */
 /* argmax: uint8 window index (r*k+s) of the first maximum, as PyTorch CPU max_pool2d */
 int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int k, int s,
                      int p, void* y, uint8_t* argmax, int P, int Q, void* stream);
+/* The stem's BN(+ReLU) fused into its 3x3 / stride-2 pool (train forward): x is the RAW stem
+ * conv output; every tap is normalised with the batch statistics mmdx_bn_fwd saved (called
+ * with y == NULL: statistics, running stats and save_mean/save_rstd only, no apply pass), as
+ * scale = gamma*rstd, shift = beta - mean*gamma*rstd, ReLU'd and rounded to the compute dtype
+ * before the compare — y and argmax are bit-identical to mmdx_bn_fwd's apply followed by
+ * mmdx_maxpool_fwd, without writing or re-reading the post-activation tensor.
+ * Replaces: backbone[1..3] (BatchNorm2d, ReLU, MaxPool2d) of the trunk, TP:183/279-281. */
+int mmdx_maxpool_bn_fwd(int dtype, const void* x, int N, int H, int W, int C, int k, int s,
+                        int p, const float* gamma, const float* beta, const float* save_mean,
+                        const float* save_rstd, int relu, void* y, uint8_t* argmax, int P, int Q,
+                        void* stream);
 int mmdx_maxpool_bwd(int dtype, const uint8_t* argmax, const void* dy, int N, int H, int W,
                      int C, int k, int s, int p, int P, int Q, void* dx, void* stream);
 int mmdx_avgpool_fwd(int dtype, const void* x, int N, int HW, int C, void* y, void* stream);

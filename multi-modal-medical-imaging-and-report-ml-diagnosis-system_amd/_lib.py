@@ -53,7 +53,8 @@ class PlanOp(C.Structure):
 (OP_EVENT, OP_NCHW2NHWC, OP_CONV_PACK, OP_CONV_FWD, OP_BN_FWD, OP_MAXPOOL_FWD,
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
  OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PAIR_INPUT,
- OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL) = range(1, 22)
+ OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL,
+ OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL) = range(1, 24)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -84,12 +85,16 @@ SIGNATURES = {
                           vp, i32, vp, vp, sz, vp]),
     "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp,
                           vp, vp, f32, vp, sz, vp]),
+    "mmdx_bn_bwd_pool": (i32, [i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
+                               i32, vp, vp, vp, vp, i32, vp, vp, vp, f32, vp, sz, vp]),
     "mmdx_img_desc_size": (sz, []),
     "mmdx_image_preprocess": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp]),
     "mmdx_plan_run": (i32, [C.POINTER(PlanOp), i32, vp, vp, vp, i32]),
     "mmdx_plan_op_size": (sz, []),
     "mmdx_maxpool_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,
                                vp]),
+    "mmdx_maxpool_bn_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
+                                  i32, vp, vp, i32, i32, vp]),
     "mmdx_maxpool_bwd": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp,
                                vp]),
     "mmdx_avgpool_fwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),

@@ -2,6 +2,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "pool.h"
 #include "../../include/mmdx.h"
 
 namespace mmdx {
@@ -99,14 +100,30 @@ __global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ am, const T* __re
 // before the first compare (the generic loop above compiles to one load-compare round trip
 // per tap) and the argmax bytes go out as one 8-byte (bf16 / fp16) or 4-byte (fp32) store.
 // Same window order, tie rule and NaN rule as maxpool_fwd_kernel.
-template <int VEC> struct ArgPack;
-template <> struct ArgPack<8> { typedef unsigned long long type; };
-template <> struct ArgPack<4> { typedef unsigned type; };
 
-template <typename T>
+//
+// BN = true: the pool reads the stem conv's RAW output and applies its train-mode BatchNorm
+// + ReLU on the fly (the stem unit's post-activation tensor is never written: its backward
+// recomputes the ReLU mask from the raw output, and nothing else reads it).  Each tap value
+// is the bf16 the separate BN-apply pass would have stored — same scale/shift expressions
+// (bn_coef_fwd), same fp32 math, rounded to T before the compare — so the pooled values and
+// argmax bytes are bit-identical to BN-apply followed by the pool.
+__device__ __forceinline__ void bn_coef_fwd(const float* gamma, const float* beta,
+                                            const float* mean, const float* rstd, int c,
+                                            float& scale, float& shift) {
+  // the expressions of bn_finalize_kernel (norm.hip): scale = g*rstd, shift = b - mean*g*rstd
+  const float g = gamma ? gamma[c] : 1.f;
+  scale = g * rstd[c];
+  shift = (beta ? beta[c] : 0.f) - mean[c] * g * rstd[c];
+}
+
+template <typename T, bool BN = false>
 __global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C,
                                       int p, T* __restrict__ y, uint8_t* __restrict__ am, int P,
-                                      int Q) {
+                                      int Q, const float* __restrict__ gamma,
+                                      const float* __restrict__ beta,
+                                      const float* __restrict__ mean,
+                                      const float* __restrict__ rstd, int relu) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   typedef typename ArgPack<VEC>::type A;
@@ -114,6 +131,11 @@ __global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int
   const long total = (long)N * P * Q * cv;
   GRID_STRIDE(i, total) {
     const int c = (int)(i % cv) * VEC;
+    float sc[VEC], sh[VEC];
+    if constexpr (BN) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) bn_coef_fwd(gamma, beta, mean, rstd, c + j, sc[j], sh[j]);
+    }
     long t = i / cv;
     const int q = (int)(t % Q); t /= Q;
     const int pp = (int)(t % P);
@@ -140,7 +162,12 @@ __global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int
       if (!ok[w9]) continue;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        const float f = to_f(v[w9][j]);
+        float f = to_f(v[w9][j]);
+        if constexpr (BN) {
+          f = f * sc[j] + sh[j];
+          if (relu) f = fmaxf(f, 0.f);
+          f = to_f(from_f<T>(f));  // the value BN-apply would have stored
+        }
         if (arg[j] < 0 || f > best[j] || (f != f && best[j] == best[j])) {
           best[j] = f;
           arg[j] = w9;
@@ -168,7 +195,7 @@ __global__ void maxpool3s2_bwd_kernel(const uint8_t* __restrict__ am, const T* _
                                       T* __restrict__ dx) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
-  typedef typename ArgPack<VEC>::type A;
+  const Pool3s2Grad<T> pg{am, dy, H, W, C, p, P, Q};
   const int cv = C / VEC;
   const long total = (long)N * H * W * cv;
   GRID_STRIDE(i, total) {
@@ -177,40 +204,7 @@ __global__ void maxpool3s2_bwd_kernel(const uint8_t* __restrict__ am, const T* _
     const int w = (int)(t % W); t /= W;
     const int h = (int)(t % H);
     const int n = (int)(t / H);
-    const int ph = (h + p) >> 1, qw = (w + p) >> 1;  // the last window that can hold (h, w)
-    V g[2][2];
-    A a[2][2];
-    bool ok[2][2];
-#pragma unroll
-    for (int dp = 0; dp < 2; ++dp) {
-      const int pp = ph - 1 + dp, r = h + p - 2 * pp;  // ascending pp, as the generic kernel
-#pragma unroll
-      for (int dq = 0; dq < 2; ++dq) {
-        const int q = qw - 1 + dq, ss = w + p - 2 * q;
-        ok[dp][dq] = pp >= 0 && pp < P && q >= 0 && q < Q && r >= 0 && r < 3 && ss >= 0 &&
-                     ss < 3;
-        const long o = (((long)n * P + pp) * Q + q) * C + c;
-        g[dp][dq] = ok[dp][dq] ? *(const V*)(dy + o) : V{};
-        a[dp][dq] = ok[dp][dq] ? *(const A*)(am + o) : (A)0;
-      }
-    }
-    float acc[VEC];
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int dp = 0; dp < 2; ++dp)
-#pragma unroll
-      for (int dq = 0; dq < 2; ++dq) {
-        if (!ok[dp][dq]) continue;
-        const int tap = (h + p - 2 * (ph - 1 + dp)) * 3 + (w + p - 2 * (qw - 1 + dq));
-#pragma unroll
-        for (int j = 0; j < VEC; ++j)
-          if ((int)((a[dp][dq] >> (8 * j)) & 0xff) == tap) acc[j] += to_f(g[dp][dq][j]);
-      }
-    V out;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) out[j] = from_f<T>(acc[j]);
-    *(V*)(dx + i * VEC) = out;
+    *(V*)(dx + i * VEC) = pg.at(n, h, w, c);
   }
 }
 
@@ -358,13 +352,33 @@ extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, i
                  "maxpool: inconsistent output size");
   const long total = (long)N * P * Q * (C / VEC);
   if (k == 3 && s == 2)
-    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool3s2_fwd_kernel<T>, dim3(grid_for(total)),
-                                         dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W,
-                                         C, p, (T*)y, argmax, P, Q));
+    DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, false>),
+                                         dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, N, H, W, C, p, (T*)y, argmax, P, Q,
+                                         (const float*)nullptr, (const float*)nullptr,
+                                         (const float*)nullptr, (const float*)nullptr, 0));
   else
     DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total)),
                                          dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W,
                                          C, k, s, p, (T*)y, argmax, P, Q));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_maxpool_bn_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                                   int k, int s, int p, const float* gamma, const float* beta,
+                                   const float* save_mean, const float* save_rstd, int relu,
+                                   void* y, uint8_t* argmax, int P, int Q, void* stream) {
+  const int VEC = dtype == F32 ? 4 : 8;
+  MMDX_CHECK_ARG(C % VEC == 0 && argmax && save_mean && save_rstd, "maxpool bn: bad args");
+  MMDX_CHECK_ARG(k == 3 && s == 2, "maxpool bn: only the 3x3 / stride-2 stem pool is fused");
+  MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
+                 "maxpool bn: inconsistent output size");
+  const long total = (long)N * P * Q * (C / VEC);
+  DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, true>), dim3(grid_for(total)),
+                                       dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W, C,
+                                       p, (T*)y, argmax, P, Q, gamma, beta, save_mean, save_rstd,
+                                       relu));
   MMDX_LAUNCH_CHECK();
   return 0;
 }

@@ -8,6 +8,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "pool.h"
 #include "../../include/mmdx.h"
 
 namespace mmdx {
@@ -275,10 +276,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
   }
 }
 
-// backward reduce: partial[c][b] = (sum g, sum g*xhat), g = dy * relu'(y)
-template <typename T>
+// backward reduce: partial[c][b] = (sum g, sum g*xhat), g = dy * relu'(y); dy row r comes
+// from the gradient source G (DenseGrad: the [rows][C] tensor; Pool3s2Grad: gathered from the
+// stem pool's output gradient and argmax, pool.h)
+template <typename T, class G>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
-    const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
+    const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
     int ct, long rpb, const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
     const float* __restrict__ gamma, const float* __restrict__ bbeta, float2* __restrict__ part) {
   typedef typename Vec16<T>::type V;
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
   if (c0 < C) {
     for (long r = r0 + ty; r < r1; r += rt) {
       const V vx = *(const V*)(x + r * C + c0);
-      const V vd = *(const V*)(dy + r * C + c0);
+      const V vd = dy.row(r, c0);
       V vy{};
       if (relu && !mask_x) vy = *(const V*)(y + r * C + c0);
 #pragma unroll
@@ -387,9 +390,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
 }
 
 // dx = a*g + b + k*xhat  ==  a*g + (b - k*mean*rstd) + (k*rstd)*x,  g = dy*relu'(y)
-template <typename T>
+template <typename T, class G>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy, long rows, int C,
+    const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ coef, int relu, const float* __restrict__ gamma,
     const float* __restrict__ bbeta, T* __restrict__ dx, T* __restrict__ dres) {
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
       const V vx = ((const V*)x)[i];
-      const V vd = ((const V*)dy)[i];
+      const V vd = dy.row(r, j * VEC);
       V vy{};
       if (relu && !mask_x) vy = ((const V*)y)[i];
       V o, og;
@@ -482,15 +485,16 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
                        beta, (const float*)rm, (const float*)rv, eps, smean, srstd, scale,
                        shift);
   }
-  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
-                     (const T*)x, (const T*)res, rows, C, (const float*)scale,
-                     (const float*)shift, relu, (T*)y);
+  if (y)  // (y == NULL: statistics only, the consumer applies the normalisation itself)
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
+                       (const T*)x, (const T*)res, rows, C, (const float*)scale,
+                       (const float*)shift, relu, (T*)y);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
 
-template <typename T>
-static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, long rows, int C,
+template <typename T, class G>
+static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long rows, int C,
                     const float* gamma, const float* bbeta, const float* smean,
                     const float* srstd, int relu, const float* stat_part, int stat_blocks,
                     void* dx, void* dres, float* dgamma, float* dbeta, float beta_acc, void* ws,
@@ -508,8 +512,8 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
     part = (float2*)stat_part;
     nblk = stat_blocks;
   } else {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
-                       (const T*)x, (const T*)y, (const T*)dy, rows, C, L.ct, L.rows_per_block,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, G>), dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0,
+                       st, (const T*)x, (const T*)y, dy, rows, C, L.ct, L.rows_per_block,
                        smean, srstd, relu, gamma, bbeta, part);
   }
   if (nblk > fin_wide())
@@ -520,8 +524,8 @@ static int bn_bwd_t(int train, const void* x, const void* y, const void* dy, lon
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0,
                        st, (const float2*)part, nblk, rows, C, train, gamma, bbeta, smean,
                        srstd, dgamma, dbeta, beta_acc, coef);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
-                     (const T*)x, (const T*)y, (const T*)dy, rows, C, smean, srstd,
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G>), dim3(grid_rows(rows, C, VEC)), dim3(256), 0,
+                     st, (const T*)x, (const T*)y, dy, rows, C, smean, srstd,
                      (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres);
   MMDX_LAUNCH_CHECK();
   return 0;
@@ -734,12 +738,37 @@ extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, c
   MMDX_CHECK_ARG(!(relu && !y && d_residual), "bn bwd: a residual unit needs its output y");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == BF16)
-    return bn_bwd_t<bf16>(train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd, relu,
-                          stat_part, stat_blocks, dx, d_residual, dgamma, dbeta, beta_acc, ws,
-                          ws_bytes, st);
-  return bn_bwd_t<float>(train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd, relu,
-                         stat_part, stat_blocks, dx, d_residual, dgamma, dbeta, beta_acc, ws,
-                         ws_bytes, st);
+    return bn_bwd_t<bf16>(train, x, y, DenseGrad<bf16>{(const bf16*)dy, C}, rows, C, gamma,
+                          bn_beta, save_mean, save_rstd, relu, stat_part, stat_blocks, dx,
+                          d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+  return bn_bwd_t<float>(train, x, y, DenseGrad<float>{(const float*)dy, C}, rows, C, gamma,
+                         bn_beta, save_mean, save_rstd, relu, stat_part, stat_blocks, dx,
+                         d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+}
+
+extern "C" int mmdx_bn_bwd_pool(int dtype, int train, const void* x, const uint8_t* argmax,
+                                const void* dy_pooled, int N, int H, int W, int C, int k, int s,
+                                int p, int P, int Q, const float* gamma, const float* bn_beta,
+                                const float* save_mean, const float* save_rstd, int relu,
+                                void* dx, float* dgamma, float* dbeta, float beta_acc, void* ws,
+                                size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_bwd_pool: fp16 is the C5 path only");
+  MMDX_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && argmax && dy_pooled,
+                 "bn bwd pool: bad args");
+  MMDX_CHECK_ARG(k == 3 && s == 2 && p <= 1, "bn bwd pool: only the 3x3 / stride-2 stem pool");
+  MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
+                 "bn bwd pool: inconsistent pool output size");
+  const long rows = (long)N * H * W;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    return bn_bwd_t<bf16>(train, x, nullptr,
+                          Pool3s2Grad<bf16>{argmax, (const bf16*)dy_pooled, H, W, C, p, P, Q},
+                          rows, C, gamma, bn_beta, save_mean, save_rstd, relu, nullptr, 0, dx,
+                          nullptr, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+  return bn_bwd_t<float>(train, x, nullptr,
+                         Pool3s2Grad<float>{argmax, (const float*)dy_pooled, H, W, C, p, P, Q},
+                         rows, C, gamma, bn_beta, save_mean, save_rstd, relu, nullptr, 0, dx,
+                         nullptr, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
 }
 
 extern "C" int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual, long rows,

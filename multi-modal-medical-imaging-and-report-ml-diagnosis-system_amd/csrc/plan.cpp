@@ -63,6 +63,23 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
       return mmdx_maxpool_fwd(o.dtype, P(o, 0, ext), o.i[0], o.i[1], o.i[2], o.i[3], o.i[4],
                               o.i[5], o.i[6], P(o, 1, ext), (uint8_t*)P(o, 2, ext), o.i[7],
                               (int)o.l[0], s);
+    case MMDX_OP_MAXPOOL_BN_FWD:
+      // i: N, H, W, C, k, s, p, P ; l: Q, relu ; p: x, y, argmax, gamma, beta, mean, rstd
+      return mmdx_maxpool_bn_fwd(o.dtype, P(o, 0, ext), o.i[0], o.i[1], o.i[2], o.i[3], o.i[4],
+                                 o.i[5], o.i[6], (const float*)P(o, 3, ext),
+                                 (const float*)P(o, 4, ext), (const float*)P(o, 5, ext),
+                                 (const float*)P(o, 6, ext), (int)o.l[1], P(o, 1, ext),
+                                 (uint8_t*)P(o, 2, ext), o.i[7], (int)o.l[0], s);
+    case MMDX_OP_BN_BWD_POOL:
+      // i: train, N, H, W, C, relu, P, Q ; l: ws_bytes, k, s, p ; f: beta_acc
+      // p: x, argmax, dy_pooled, gamma, beta, mean, rstd, dx, dgamma, dbeta, ws
+      return mmdx_bn_bwd_pool(o.dtype, o.i[0], P(o, 0, ext), (const uint8_t*)P(o, 1, ext),
+                              P(o, 2, ext), o.i[1], o.i[2], o.i[3], o.i[4], (int)o.l[1],
+                              (int)o.l[2], (int)o.l[3], o.i[6], o.i[7],
+                              (const float*)P(o, 3, ext), (const float*)P(o, 4, ext),
+                              (const float*)P(o, 5, ext), (const float*)P(o, 6, ext), o.i[5],
+                              P(o, 7, ext), (float*)P(o, 8, ext), (float*)P(o, 9, ext), o.f[0],
+                              P(o, 10, ext), (size_t)o.l[0], s);
     case MMDX_OP_AVGPOOL_FWD:
       return mmdx_avgpool_fwd(o.dtype, P(o, 0, ext), o.i[0], o.i[1], o.i[2], P(o, 1, ext), s);
     case MMDX_OP_CAST:

@@ -321,9 +321,12 @@ class _Plan:
         packs = []
         fold = not train and not keep   # eval-mode BN folded into the conv epilogue
 
-        def unit(conv, bn, relu, x, N, H, W, C, cm, res, pair=None, st=0, join=None):
+        def unit(conv, bn, relu, x, N, H, W, C, cm, res, pair=None, st=0, join=None,
+                 stats_only=False):
             """conv + BN(+res)(+ReLU) on stream `st`; `join`: an event the main stream
-            waits for before the first op that reads `res` (the downsample branch)."""
+            waits for before the first op that reads `res` (the downsample branch);
+            `stats_only`: the BN's statistics only — its consumer normalises on the fly and
+            the post-activation tensor is never written (u["out"] is None)."""
             d = pair if pair is not None else _desc(N, H, W, C, conv)
             K, k = conv.out_channels, conv.kernel_size
             y = A.new((N, d.P, d.Q, K), T, dev)
@@ -355,7 +358,7 @@ class _Plan:
                 units.append(u)
                 return y, d, u
             fw.timed("fwd", L.OP_CONV_FWD, stream=st, dtype=dt, p=(x, wk, y, part), d=d)
-            out = A.new((N, d.P, d.Q, K), T, dev)
+            out = None if stats_only else A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
             mean = A.new((K,), torch.float32, dev)
             rstd = A.new((K,), torch.float32, dev)
@@ -372,16 +375,28 @@ class _Plan:
             units.append(u)
             return out, d, u
 
-        a, d, stem_u = unit(stem_conv, trunk[1], True, x0, N, H, W, cp, 3, None,
-                            pair=d_pair)
-        H, W, C = d.P, d.Q, d.K
         mp = trunk[3]
+        # train forward: the stem's BN + ReLU run inside the 3x3/2 pool (mmdx_maxpool_bn_fwd,
+        # bit-identical to apply-then-pool) — the 112x112x64 post-activation tensor is never
+        # written or re-read; the stem's backward recomputes its ReLU mask from the raw output
+        pool_bn = train and not fold and mp.kernel_size == 3 and mp.stride == 2
+        a, d, stem_u = unit(stem_conv, trunk[1], True, x0, N, H, W, cp, 3, None,
+                            pair=d_pair, stats_only=pool_bn)
+        H, W, C = d.P, d.Q, d.K
         P = (H + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
         Q = (W + 2 * mp.padding - mp.kernel_size) // mp.stride + 1
         pooled = A.new((N, P, Q, C), T, dev)
         am = A.new((N, P, Q, C), torch.uint8, dev)
-        fw.add(L.OP_MAXPOOL_FWD, dt, i=(N, H, W, C, mp.kernel_size, mp.stride, mp.padding, P),
-               l=(Q,), p=(a, pooled, am))
+        if pool_bn:
+            bn0 = trunk[1]
+            fw.add(L.OP_MAXPOOL_BN_FWD, dt,
+                   i=(N, H, W, C, mp.kernel_size, mp.stride, mp.padding, P), l=(Q, 1),
+                   p=(stem_u["y"], pooled, am, bn0.weight, bn0.bias, stem_u["mean"],
+                      stem_u["rstd"]))
+        else:
+            fw.add(L.OP_MAXPOOL_FWD, dt,
+                   i=(N, H, W, C, mp.kernel_size, mp.stride, mp.padding, P),
+                   l=(Q,), p=(a, pooled, am))
         stem_geom = (N, H, W, C, P, Q)
         x_cur, H, W = pooled, P, Q
         blocks = []
@@ -463,7 +478,7 @@ class _Plan:
                 return _Ext(2) if isinstance(x, _Ext) else x
 
             def unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False, stats=None,
-                         feed=None):
+                         feed=None, pool=None):
                 """BN(+res)(+ReLU) backward, wgrad (side stream), dgrad.  `stats`: this
                 unit's BN-backward partials, already made by the dgrad that produced `dout`;
                 `feed`: the unit whose dout this unit's dgrad produces (no residual) — its
@@ -472,15 +487,27 @@ class _Plan:
                 K = d.K
                 rows = d.N * d.P * d.Q
                 dconv = A.new(tuple(u["y"].shape), T, dev)
+                u["dconv"] = dconv
                 dres = A.new(tuple(u["y"].shape), T, dev) if want_res else None
                 wsn = L.lib().mmdx_bn_workspace_size(rows, K)
                 ws_for(wsn)
                 out = u["out"] if want_res else None  # no residual: mask recomputed from y
                 sp, sb = stats if stats is not None else (None, 0)
-                bw.add(L.OP_BN_BWD, dt, i=(int(train), K, int(u["relu"]), sb),
-                       l=(rows, wsn, sp.data_ptr() if sp is not None else 0), f=(0.0,),
-                       p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"], u["rstd"],
-                          dconv, dres, g(u["bn"].weight), g(u["bn"].bias), _WS))
+                if pool is not None:
+                    # `dout` is the stem pool's OUTPUT gradient: the BN backward gathers
+                    # dL/d(pool input) through the pool's argmax itself (mmdx_bn_bwd_pool)
+                    am_, (pN, pH, pW, pC, pk, ps_, pp, pP, pQ) = pool
+                    bw.add(L.OP_BN_BWD_POOL, dt,
+                           i=(int(train), pN, pH, pW, pC, int(u["relu"]), pP, pQ),
+                           l=(wsn, pk, ps_, pp), f=(0.0,),
+                           p=(u["y"], am_, dout, u["bn"].weight, u["bn"].bias, u["mean"],
+                              u["rstd"], dconv, g(u["bn"].weight), g(u["bn"].bias), _WS))
+                else:
+                    bw.add(L.OP_BN_BWD, dt, i=(int(train), K, int(u["relu"]), sb),
+                           l=(rows, wsn, sp.data_ptr() if sp is not None else 0), f=(0.0,),
+                           p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"],
+                              u["rstd"], dconv, dres, g(u["bn"].weight), g(u["bn"].bias),
+                              _WS))
                 wsn = L.lib().mmdx_conv_wgrad_workspace_size(dt, d)
                 ws_for(wsn, 1)
                 ev = A.event()
@@ -561,7 +588,17 @@ class _Plan:
                                          feed=bu[-2] if len(bu) > 1 else None)
                 for k in range(len(bu) - 2, -1, -1):
                     uu = bu[k]
-                    if k == 0:
+                    if k == 0 and ds_u is not None and ds_u["d"].stride_h > 1:
+                        # d(block input) = dgrad(conv1) + dgrad(strided downsample): conv1's
+                        # dgrad writes it (beta 0), then the 1x1/2 downsample's dgrad adds
+                        # its one output phase (beta 1; the phases no tap reaches are left
+                        # alone) — instead of the downsample writing 3/4 zeros first and
+                        # conv1 re-reading the whole tensor to accumulate onto it
+                        unit_bwd(ds_u, dres, False)
+                        dh, _, _ = unit_bwd(uu, dh, True, stats=fed)
+                        bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(1.0,),
+                                 p=(ds_u["dconv"], ds_u["wc"], dh), d=ds_u["d"])
+                    elif k == 0:
                         # d(block input) = dgrad(conv1) + identity-path grad (beta = 1)
                         if ds_u is not None:
                             dxi, _, _ = unit_bwd(ds_u, dres, True)
@@ -572,10 +609,16 @@ class _Plan:
                         dh, _, fed = unit_bwd(uu, dh, True, stats=fed, feed=bu[k - 1])
                 dx = dh
             n0, h0, w0, c0, p0, q0 = stem_geom
-            da = A.new((n0, h0, w0, c0), T, dev)
-            bw.add(L.OP_MAXPOOL_BWD, dt, i=(n0, h0, w0, c0, mp.kernel_size, mp.stride,
-                                            mp.padding, p0), l=(q0,), p=(am, dx, da))
-            unit_bwd(stem_u, da, False)  # (no dgrad into the image)
+            if mp.kernel_size == 3 and mp.stride == 2 and mp.padding <= 1 and stem_u["relu"]:
+                # the pool's backward runs inside the stem BN backward: the 112x112x64
+                # gradient of the pool input is never materialised
+                unit_bwd(stem_u, dx, False, pool=(am, (n0, h0, w0, c0, mp.kernel_size,
+                                                       mp.stride, mp.padding, p0, q0)))
+            else:
+                da = A.new((n0, h0, w0, c0), T, dev)
+                bw.add(L.OP_MAXPOOL_BWD, dt, i=(n0, h0, w0, c0, mp.kernel_size, mp.stride,
+                                                mp.padding, p0), l=(q0,), p=(am, dx, da))
+                unit_bwd(stem_u, da, False)  # (no dgrad into the image)
             ev = A.event()
             bw.add(L.OP_SIGNAL, p=(ev,), stream=1)
             bw.add(L.OP_WAIT, p=(ev,), stream=0)

@@ -335,6 +335,77 @@ def test_pools(dev, dt, hwp):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hwp", [(12, 11, 1), (112, 112, 1), (13, 14, 0)])
+def test_maxpool_bn_fused(dev, dt, hwp):
+    """The stem's train-mode BN + ReLU fused into the 3x3/2 pool (mmdx_maxpool_bn_fwd) equals
+    mmdx_bn_fwd's apply followed by mmdx_maxpool_fwd BIT FOR BIT (pooled values and argmax
+    bytes; about half of every window is ReLU zeros, so the tie rule is exercised), and the
+    statistics-only BN call (y == NULL) saves the same mean / rstd / running stats."""
+    g = torch.Generator().manual_seed(11)
+    H, W, pad = hwp
+    N, C = (2, 64) if H < 100 else (8, 64)
+    rows = N * H * W
+    x = (torch.randn(rows, C, generator=g) * 2 + 0.3).to(dev, dt)
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    gam[::7] *= -1.0  # negative scales: the max is taken after the affine map
+    bet = (torch.randn(C, generator=g) * 0.2).to(dev)
+    dc = L.dtype_code(dt)
+    ws_n = L.lib().mmdx_bn_workspace_size(rows, C)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    outs = []
+    for apply in (True, False):
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        mean, rstd = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        a = torch.empty_like(x) if apply else None
+        L.call("mmdx_bn_fwd", dc, 1, x.data_ptr(), rows, C, None, 0, 0, gam.data_ptr(),
+               bet.data_ptr(), rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, mean.data_ptr(),
+               rstd.data_ptr(), None, 1, a.data_ptr() if apply else None, ws.data_ptr(), ws_n,
+               L.stream())
+        P, Q = (H + 2 * pad - 3) // 2 + 1, (W + 2 * pad - 3) // 2 + 1
+        y = torch.empty(N, P, Q, C, dtype=dt, device=dev)
+        am = torch.empty(N, P, Q, C, dtype=torch.uint8, device=dev)
+        if apply:
+            L.call("mmdx_maxpool_fwd", dc, a.data_ptr(), N, H, W, C, 3, 2, pad, y.data_ptr(),
+                   am.data_ptr(), P, Q, L.stream())
+        else:
+            L.call("mmdx_maxpool_bn_fwd", dc, x.data_ptr(), N, H, W, C, 3, 2, pad,
+                   gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1,
+                   y.data_ptr(), am.data_ptr(), P, Q, L.stream())
+        outs.append((y, am, mean, rstd, rm, rv))
+    torch.cuda.synchronize()
+    for u, v, name in zip(outs[0], outs[1], ("pooled", "argmax", "mean", "rstd", "rm", "rv")):
+        assert torch.equal(u, v), name
+    assert (outs[0][0] == 0).any()  # all-zero windows: a nine-way tie after the ReLU
+
+    # backward: mmdx_bn_bwd_pool (pool gradient gathered inside the BN backward) equals
+    # mmdx_maxpool_bwd + mmdx_bn_bwd (ReLU mask from x) bit for bit
+    y, am, mean, rstd = outs[1][:4]
+    dyp = torch.randn(y.shape, generator=g).to(dev, dt)
+    da = torch.empty_like(x)
+    L.call("mmdx_maxpool_bwd", dc, am.data_ptr(), dyp.data_ptr(), N, H, W, C, 3, 2, pad, P, Q,
+           da.data_ptr(), L.stream())
+    res = []
+    for fused in (False, True):
+        dx = torch.empty_like(x)
+        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        if fused:
+            L.call("mmdx_bn_bwd_pool", dc, 1, x.data_ptr(), am.data_ptr(), dyp.data_ptr(), N, H,
+                   W, C, 3, 2, pad, P, Q, gam.data_ptr(), bet.data_ptr(), mean.data_ptr(),
+                   rstd.data_ptr(), 1, dx.data_ptr(), dg.data_ptr(), db.data_ptr(), 0.0,
+                   ws.data_ptr(), ws_n, L.stream())
+        else:
+            L.call("mmdx_bn_bwd", dc, 1, x.data_ptr(), None, da.data_ptr(), rows, C,
+                   gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 1, None, 0,
+                   dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(), 0.0, ws.data_ptr(), ws_n,
+                   L.stream())
+        res.append((dx, dg, db))
+    torch.cuda.synchronize()
+    for u, v, name in zip(res[0], res[1], ("dx", "dgamma", "dbeta")):
+        assert torch.equal(u, v), name
+    assert res[0][0].abs().sum() > 0
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_layernorm_bce_gelu(dev, dt):
     g = torch.Generator().manual_seed(5)
     rows, D = 70, 1024
