@@ -255,6 +255,8 @@ template <> struct DmaOk<Im2colK<bf16, true>> { static constexpr bool value = tr
 template <> struct DmaOk<DgradK<bf16, true>> { static constexpr bool value = true; };
 template <> struct DmaOk<Im2colK<bf16, false>> { static constexpr bool value = true; };
 template <> struct DmaOk<DenseK<bf16>> { static constexpr bool value = true; };
+template <> struct DmaOk<PointFwdK<bf16>> { static constexpr bool value = true; };
+template <> struct DmaOk<PointDgradK<bf16>> { static constexpr bool value = true; };
 
 // buffer-DMA preconditions: 32-bit byte offsets (< 2 GiB) and a 32-bit tap-validity mask
 static bool dma_geom_ok(const ConvGeom& g, bool dgrad, int max_taps = 32, long rows = 0) {
@@ -310,8 +312,8 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
   if (g.C % KTile<T>::BK == 0 && is_pointwise(g))  // x itself is the [M][C] A operand
-    return conv_gemm<T>(DenseK<T>{(const T*)x, g.C, M, true}, w, y, M, N, K, 0.f, st, stats,
-                        dma_geom_ok(g, false, 32, M));
+    return conv_gemm<T>(PointFwdK<T>{{(const T*)x, g.C, M, true}}, w, y, M, N, K, 0.f, st,
+                        stats, dma_geom_ok(g, false, 32, M));
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
                         dma_geom_ok(g, false, 32, M));
@@ -334,7 +336,7 @@ static int conv_fwd_bn_eval_t(const mmdx_conv_desc* d, const void* x, const void
   epi.gamma = gamma; epi.beta_bn = beta; epi.rmean = rmean; epi.rvar = rvar; epi.eps = eps;
   epi.res = (const T*)res; epi.relu = relu != 0;
   if (g.C % KTile<T>::BK == 0 && is_pointwise(g))
-    return conv_gemm_epi<T>(DenseK<T>{(const T*)x, g.C, M, true}, w, epi, M, N, K, st,
+    return conv_gemm_epi<T>(PointFwdK<T>{{(const T*)x, g.C, M, true}}, w, epi, M, N, K, st,
                             dma_geom_ok(g, false, 32, M));
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm_epi<T>(Im2colK<T, true>{(const T*)x, g, M}, w, epi, M, N, K, st,
@@ -402,8 +404,8 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
     return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st, bs);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
   if (g.K % KTile<T>::BK == 0 && is_pointwise(g))  // dY itself is the [M][K] A operand
-    return conv_gemm<T>(DenseK<T>{(const T*)dy, g.K, M, true}, w_crsk, dx, M, N, K, beta, st,
-                        nullptr, dma_geom_ok(g, true, 32, M), bs);
+    return conv_gemm<T>(PointDgradK<T>{{(const T*)dy, g.K, M, true}}, w_crsk, dx, M, N, K,
+                        beta, st, nullptr, dma_geom_ok(g, true, 32, M), bs);
   if (g.K % KTile<T>::BK == 0)
     return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
                         nullptr, dma_geom_ok(g, true, 32, M), bs);
@@ -471,7 +473,8 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
     // 1x1 / stride-1 / unpadded conv's im2col^T is x^T itself: a dense R-major operand
     // (no window decode or tap tests)
     if (is_pointwise(g))
-      rc = wgrad_dma<T>(p, sa, DenseR<T>{(const T*)x, g.C, N, true, K}, epi, M, N, K, st);
+      rc = wgrad_dma<T>(p, sa, PointWgradR<T>{{(const T*)x, g.C, N, true, K}}, epi, M, N, K,
+                        st);
     else
       rc = wgrad_dma<T>(p, sa, sb, epi, M, N, K, st);
     if (rc) return rc;

@@ -141,6 +141,12 @@ struct DenseK {
   }
 };
 
+// The pointwise (1x1 / stride 1 / unpadded) conv's activation operands: plain dense
+// matrices, given their own names so a kernel trace tells the conv family's dispatches
+// (PointFwdK: x in the forward, PointDgradK: dY in the dgrad) from the Linear layers' DenseK.
+template <typename T> struct PointFwdK : DenseK<T> {};
+template <typename T> struct PointDgradK : DenseK<T> {};
+
 // Dense, rows contiguous: element (r, k) at base[k*ld + r].
 template <typename T>
 struct DenseR {
@@ -187,6 +193,9 @@ struct DenseR {
     return rs >= 0 && k < klim ? (int)(((long)k * ld + rs) * sizeof(T)) : -1;
   }
 };
+
+// x^T of a pointwise conv in its weight gradient (named apart from DenseR, see PointFwdK)
+template <typename T> struct PointWgradR : DenseR<T> {};
 
 struct ConvGeom {
   int N, H, W, C;      // input NHWC

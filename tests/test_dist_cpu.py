@@ -53,9 +53,11 @@ def test_grad_allreduce_mean_gloo():
 SHAPES2 = ((40, 3), (7,), (16,), (5, 5))
 
 
-def _worker_flat(rank, world, port, out, region=0):
+def _worker_flat(rank, world, port, out, region=0, detach=False):
     """Gradients that are views of one flat buffer (the trunk's gradient arena) are reduced
-    in place; the others through buckets; a subset is launched early (overlap path)."""
+    in place; the others through buckets; a subset is launched early (overlap path).
+    detach: the views are stored detached, as autograd's AccumulateGrad stores a view a
+    backward returns (.grad._base is None) — the arena is found by its storage."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -65,6 +67,10 @@ def _worker_flat(rank, world, port, out, region=0):
     flat = torch.randn(40 * 3 + 7, generator=g)
     params[0].grad = flat[:120].view(40, 3)
     params[1].grad = flat[120:127]
+    if detach:
+        params[0].grad = params[0].grad.detach()
+        params[1].grad = params[1].grad.detach()
+        assert params[0].grad._base is None
     params[2].grad = torch.randn(16, generator=g)
     params[3].grad = torch.randn(5, 5, generator=g)
     red = GradAllReducer(params, world, bucket_bytes=64)
@@ -73,19 +79,25 @@ def _worker_flat(rank, world, port, out, region=0):
     elif region == 2:  # per-layer slices in backward order (resnet.TRUNK_GRAD_HOOK)
         red.trunk_hook(flat, [(100, 127, None), (60, 100, None), (30, 60, None)])
     red.launch([params[2]])
-    red.reduce()
-    assert params[0].grad._base is flat  # reduced in place, still the same buffer
+    red.launch()
+    arena = {id(params[0].grad), id(params[1].grad)}
+    assert all(b is None or not arena & {id(t) for t in b} for b, *_ in red._pending), \
+        "arena gradients went through a packed bucket"
+    red.finish()
+    if not detach:
+        assert params[0].grad._base is flat  # reduced in place, still the same buffer
+    assert params[0].grad.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
     out[rank] = [p.grad.clone() for p in params]
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("region", [0, 1, 2])
-def test_grad_allreduce_flat_base_and_early_launch_gloo(region):
+@pytest.mark.parametrize("region,detach", [(0, False), (1, False), (2, False), (2, True)])
+def test_grad_allreduce_flat_base_and_early_launch_gloo(region, detach):
     world = 2
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker_flat, args=(world, port, out, region), nprocs=world, join=True)
+    mp.spawn(_worker_flat, args=(world, port, out, region, detach), nprocs=world, join=True)
     exp = []
     for r in range(world):
         g = torch.Generator().manual_seed(200 + r)

@@ -24,9 +24,9 @@ import re
 
 SIMDS = 256 * 4
 FAMILIES = [
-    ("conv_fwd", re.compile(r"igemm(_dma)?_kernel.*Im2colK")),
+    ("conv_fwd", re.compile(r"igemm(_dma)?_kernel.*(Im2colK|PointFwdK)")),
     ("conv_dgrad", re.compile(r"igemm(_dma)?_kernel.*(DgradK|DgradPhaseK|PhaseTap)")),
-    ("conv_wgrad", re.compile(r"igemm(_dma)?_kernel.*Im2colR")),
+    ("conv_wgrad", re.compile(r"igemm(_dma)?_kernel.*(Im2colR|PointWgradR)")),
     ("lstm", re.compile(r"lstm_")),
     ("gemm", re.compile(r"igemm(_dma)?_kernel|splitk")),
 ]

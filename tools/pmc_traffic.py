@@ -8,7 +8,8 @@
 FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the bytes of a wide
 coalesced read (MI355X_MICROARCH.md §HBM), so  bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
 Conv kernels are the implicit-GEMM instantiations whose operand source is an im2col/dgrad
-gather (`Im2colK`, `DgradK`, `Im2colR`) plus the split-K `wgrad_reduce_kernel`; the per-launch
+gather (`Im2colK`, `DgradK`, `Im2colR`) or a pointwise conv's dense operand (`PointFwdK`,
+`PointDgradK`, `PointWgradR`) plus the split-K `wgrad_reduce_kernel`; the per-launch
 figure divides by the number of conv CALLS (steps x --calls-per-step; steps = AdamW
 dispatches), the unit bench.py's `roofline.achieved` times.
 """
@@ -19,7 +20,7 @@ import json
 import os
 import re
 
-CONV = re.compile(r"igemm(_dma)?_kernel.*(Im2col|Dgrad|PhaseTap)")
+CONV = re.compile(r"igemm(_dma)?_kernel.*(Im2col|Dgrad|PhaseTap|PointFwdK|PointWgradR)")
 STEP = re.compile(r"adamw_kernel")
 REDUCE = re.compile(r"wgrad_reduce_kernel")
 
@@ -73,7 +74,7 @@ def main():
     out = {
         "config": a.config, "per_gpu_batch": a.batch, "dispatches": n_f, "steps": s_f,
         "calls": calls,
-        "kernels": "igemm(_dma)_kernel (Im2colK/DgradK/DgradPhaseK/Im2colR sources) + wgrad_reduce_kernel",
+        "kernels": "igemm(_dma)_kernel (Im2colK/DgradK/DgradPhaseK/Im2colR/PointFwdK/PointDgradK/PointWgradR sources) + wgrad_reduce_kernel",
         "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
         "traffic_bytes_per_launch": round(fetch + write),
         "reduce_share": round((2 * f_red + w_red) * 1024 / calls / max(1.0, fetch + write), 4),
