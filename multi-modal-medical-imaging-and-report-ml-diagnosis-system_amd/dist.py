@@ -43,6 +43,10 @@ class GradAllReducer:
         # rehearse: run every collective even in a 1-rank group (RCCL on one GPU exercises
         # the comm stream, the plan events and the write-back of the multi-GPU path)
         self.active = self.world > 1 or rehearse
+        # RCCL averages inside the collective (ncclAvg): no separate 1/world pass over the
+        # ~160 MB of fp32 gradients afterwards; gloo has no AVG (sum, then scale)
+        self._avg = (self.active and dist.is_initialized()
+                     and dist.get_backend(group) == "nccl")
         self.bucket_bytes = bucket_bytes
         self.group = group
         # packed buckets may travel in bf16 (MMDX_DP_BUCKET_DTYPE=bf16: half the xGMI bytes
@@ -82,11 +86,12 @@ class GradAllReducer:
             with torch.cuda.stream(self._comm):
                 self._comm.wait_event(event)
                 tmp = view.clone()
-                work = dist.all_reduce(tmp, group=self.group, async_op=True)
+                work = dist.all_reduce(tmp, op=self._op(tmp), group=self.group,
+                                       async_op=True)
             tmp.record_stream(torch.cuda.current_stream(buf.device))
         else:
             tmp = view.clone()
-            work = dist.all_reduce(tmp, group=self.group, async_op=True)
+            work = dist.all_reduce(tmp, op=self._op(tmp), group=self.group, async_op=True)
         self._pending.append((None, tmp, work, view))
         off = buf.storage_offset()
         self._regions.setdefault(_store_key(buf), []).append((off + lo, off + hi))
@@ -130,22 +135,31 @@ class GradAllReducer:
                 continue
             for a, z in _complement(self._regions.get(key, []), flat.numel()):
                 part = flat[a:z]   # what launch_region left
-                work = dist.all_reduce(part, group=self.group, async_op=True)
+                work = dist.all_reduce(part, op=self._op(part), group=self.group,
+                                       async_op=True)
                 self._pending.append((None, part, work, None))
         for bucket in self._buckets(loose):
             flat = torch._utils._flatten_dense_tensors(bucket)
             if self.bucket_dtype is not None and flat.dtype != self.bucket_dtype:
                 flat = flat.to(self.bucket_dtype)
-            work = dist.all_reduce(flat, group=self.group, async_op=True)
+            work = dist.all_reduce(flat, op=self._op(flat), group=self.group, async_op=True)
             self._pending.append((bucket, flat, work, None))
+
+    def _op(self, t):
+        # averaged in the collective for fp32 with RCCL; bf16 buckets sum in bf16 and take
+        # the mean in fp32 after the cast back
+        avg = self._avg and t.dtype == torch.float32
+        return dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
 
     def finish(self):
         inv = 1.0 / self.world
         for bucket, flat, work, dest in self._pending:
             work.wait()
+            averaged = self._op(flat) == dist.ReduceOp.AVG
             if flat.dtype != torch.float32:
                 flat = flat.float()
-            flat.mul_(inv)
+            if not averaged:
+                flat.mul_(inv)
             if dest is not None:
                 dest.copy_(flat)
             if bucket is not None:
