@@ -276,6 +276,7 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
     from mmdx import optim as MO
     from mmdx.schedule import TwoTowerForward, two_tower_backward
     towers = TwoTowerForward(text_stream=side)
+    text_early = os.environ.get("MMDX_DP_TEXT_EARLY", "1") != "0"
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -293,7 +294,7 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
         # N > 1: the text tower's and fusion head's gradients start their RCCL all-reduce
         # (from the text stream) while the image trunk is still in its backward
         early = None
-        if reducer is not None:
+        if reducer is not None and text_early:
             early = lambda: reducer.launch(list(txt.parameters()) + list(fus.parameters()))
         two_tower_backward(loss, z_img, z_txt, fus.parameters(),
                            text_stream=side if side_bwd is None else side_bwd,
@@ -426,12 +427,17 @@ def main():
     side = torch.cuda.Stream(device=dev, priority=-1)
     from mmdx.dist import GradAllReducer
     reducer = GradAllReducer(params, world, rehearse=dp) if dp else None
-    early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "1" if backend == "nccl" else "0")
+    # Opt-in: the trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward, each
+    # from its own plan event (RCCL: a comm stream waits on the event, no host wait).  Off by
+    # default: in the one-rank RCCL rehearsal it costs 0.43 ms/step (15.83 vs 15.40 ms) — the
+    # comm and RCCL streams' event waits share the process's 4 hardware queues with the text
+    # and weight-gradient streams and hold their work back — about what it could hide of the
+    # 94 MB trunk all-reduce at 8 GPUs.  The text tower's and fusion head's buckets still
+    # start as soon as their gradients are final (MMDX_DP_TEXT_EARLY, on: 0.08 ms here,
+    # ~66 MB of the collective hidden at N > 1).  gloo's CUDA path would stall the issuing
+    # host thread on the event (1.3 s/step in the one-GPU rehearsal).
+    early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "0")
     if reducer is not None and early_tail != "0":
-        # the trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward, each from
-        # its own plan event (RCCL: the comm stream waits on the event, no host wait; gloo's
-        # CUDA path stalls the issuing host thread on it — 1.3 s/step in the one-GPU
-        # rehearsal — so the gloo rehearsal keeps it off unless asked for)
         RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
     step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
     timer = StepTimer()
@@ -483,6 +489,22 @@ def main():
         el = t.item()
     conv_ms = sum(s.elapsed_time(e) for _, s, e in timer.pairs)
     n_conv = len(timer.pairs)
+    # wall time during which at least one timed launch was running (union of the launch
+    # intervals, all events on one device): the family's launches overlap each other (the
+    # weight-gradient stream beside the dgrad chain), so the per-launch sum above counts
+    # shared time twice; this is the extra `busy_*` figure, the contract's `frac` stays
+    busy_ms = 0.0
+    if timer.pairs:
+        ref = timer.pairs[0][1]
+        iv = sorted((ref.elapsed_time(s), ref.elapsed_time(e)) for _, s, e in timer.pairs)
+        lo, hi = iv[0]
+        for a, b in iv[1:]:
+            if a > hi:
+                busy_ms += hi - lo
+                lo, hi = a, b
+            else:
+                hi = max(hi, b)
+        busy_ms += hi - lo
     conv_flops, total_flops = model_flops_per_sample(cfg, img, txt)
 
     samples = B * world * args.steps
@@ -540,6 +562,10 @@ def main():
             "algorithmic_bytes_per_launch": (round(alg_bytes / alg_launches) if not vit
                                              else None),
             "family_ms_per_step": round(conv_ms / conv_steps, 3),
+            "busy_ms_per_step": round(busy_ms / conv_steps, 3),
+            "busy_achieved": (round(conv_tf * conv_ms / busy_ms, 2) if busy_ms > 0 else None),
+            "busy_frac": (round(conv_tf * conv_ms / busy_ms / PEAK_BF16_TFLOPS, 4)
+                          if busy_ms > 0 else None),
             "family_launches_per_step": n_conv // max(1, conv_steps),
             "family_gflop_per_sample": round(conv_flops / 1e9, 3),
             "timed_steps_with_events": conv_steps,
