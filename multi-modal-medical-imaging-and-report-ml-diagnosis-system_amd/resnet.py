@@ -400,6 +400,15 @@ class _Plan:
         stem_geom = (N, H, W, C, P, Q)
         x_cur, H, W = pooled, P, Q
         blocks = []
+        # the multi-tensor weight pack (below) runs on the side stream beside the stem (whose
+        # weights have their own pack on the main stream); the main stream joins it here,
+        # before the first conv that reads a packed weight (70 us off the critical path)
+        pack_side = len(packs) == 0
+        ev_pack_t = None
+        wait_pos = len(fw.ops)
+        if pack_side:
+            ev_pack_t = A.event()
+            fw.add(L.OP_WAIT, p=(ev_pack_t,), stream=0)
         for layer in list(trunk)[4:8]:
             for blk in layer:
                 x_in = x_cur
@@ -446,8 +455,20 @@ class _Plan:
             raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
             tbl = A.new((raw.numel(),), torch.uint8, dev)
             tbl.copy_(raw)
-            fw.add(L.OP_CONV_PACK_MULTI, dt, i=(len(packs),), l=(nb,), p=(tbl,))
-            fw.ops.insert(0, fw.ops.pop())
+            if pack_side:  # side stream: after whatever the main stream ran before the plan
+                ev_start_t = A.event()
+                fw.add(L.OP_SIGNAL, p=(ev_start_t,), stream=0)
+                fw.add(L.OP_WAIT, p=(ev_start_t,), stream=1)
+                fw.add(L.OP_CONV_PACK_MULTI, dt, i=(len(packs),), l=(nb,), p=(tbl,), stream=1)
+                fw.add(L.OP_SIGNAL, p=(ev_pack_t,), stream=1)
+                head = fw.ops[-4:]
+                del fw.ops[-4:]
+                fw.ops[0:0] = head
+            else:
+                fw.add(L.OP_CONV_PACK_MULTI, dt, i=(len(packs),), l=(nb,), p=(tbl,))
+                fw.ops.insert(0, fw.ops.pop())
+        elif pack_side:
+            del fw.ops[wait_pos]
         self.feats = A.new((N, C), T, dev)
         fw.add(L.OP_AVGPOOL_FWD, dt, i=(N, H * W, C), p=(x_cur, self.feats))
         self.out_geom = (N, H, W, C)
