@@ -101,3 +101,56 @@ def test_dp_two_ranks_match_full_batch(dev, early):
             assert 1 - c <= 1e-6, f"rank {r} {n}: 1-cos {1 - c:.2e}"
             nr = norm_ratio(g[n], ref[n])
             assert abs(nr - 1) <= 1e-5, f"rank {r} {n}: norm ratio {nr:.7f}"
+
+
+def _rccl_worker(port, out, early):
+    """One-rank RCCL group: the nccl-backend path of GradAllReducer (AVG collectives, the
+    arena found by storage and reduced in place, optional early trunk tail on a comm
+    stream, bucket unpack) must leave every gradient exactly as the local backward made it
+    (the mean over one rank is the identity)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    from mmdx import resnet as RN
+    from mmdx.dist import GradAllReducer
+    from parity_util import synth_batch
+    x, ids, mask, y = synth_batch(4, 16, hw=64)
+    img, txt, fus = _model()
+    params = [p for mod in (img, txt, fus) for p in mod.parameters()]
+    named = _grads(img, txt, fus, x, ids, mask, y)
+    ref = {n: p.grad.detach().clone() for n, p in named if p.grad is not None}
+    for p in params:
+        p.grad = None
+    red = GradAllReducer(params, 1, rehearse=True)
+    assert red._avg
+    if early:
+        RN.TRUNK_GRAD_HOOK = red.trunk_hook
+    named = _grads(img, txt, fus, x, ids, mask, y)
+    RN.TRUNK_GRAD_HOOK = None
+    trunk = {id(p.grad) for p in img.backbone.parameters() if p.grad is not None}
+    red.launch()
+    packed = sum(1 for b, *_ in red._pending if b is not None for t in b if id(t) in trunk)
+    red.finish()
+    torch.cuda.synchronize()
+    bad = [n for n, p in named if p.grad is not None and not torch.equal(p.grad, ref[n])]
+    out["packed"] = packed
+    out["bad"] = bad
+    out["n"] = len(ref)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("early", [False, True])
+def test_dp_rccl_one_rank_identity(dev, early):
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    p = ctx.Process(target=_rccl_worker, args=(_port(), out, early))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0
+    assert out["n"] > 50
+    assert out["packed"] == 0, "trunk arena gradients went through a packed bucket"
+    assert out["bad"] == [], out["bad"]
