@@ -150,3 +150,22 @@ def test_grad_allreduce_bf16_buckets_gloo():
         for got, want in zip(out[r], mean):
             assert got.dtype == torch.float32
             assert (got - want).abs().max() <= 1e-2 * want.abs().max() + 1e-2
+
+
+def test_whole_buffer_detection():
+    """The arena test of GradAllReducer.launch: gradients that tile one whole storage (as
+    detached views, the way autograd stores them) are one flat buffer; a gap, a foreign
+    tensor, a dtype mix or a single tensor is not."""
+    from mmdx.dist import _store_key, _whole_buffer
+    buf = torch.arange(12.0)
+    a, b = buf[:4].view(2, 2).detach(), buf[4:].detach()
+    flat = _whole_buffer([a, b])
+    assert flat is not None and flat.numel() == 12
+    assert flat.untyped_storage().data_ptr() == buf.untyped_storage().data_ptr()
+    flat.mul_(2)
+    assert torch.equal(buf, torch.arange(12.0) * 2)
+    assert _store_key(a) == _store_key(b)
+    assert _whole_buffer([buf[:4], buf[6:]]) is None          # 2 elements uncovered
+    assert _whole_buffer([a]) is None                          # a lone tensor: bucketed
+    c = torch.zeros(12, dtype=torch.float64)
+    assert _whole_buffer([c[:4], c[4:].float()]) is None       # not one storage / dtype
