@@ -120,22 +120,33 @@ def _rccl_worker(port, out, early):
     x, ids, mask, y = synth_batch(4, 16, hw=64)
     img, txt, fus = _model()
     params = [p for mod in (img, txt, fus) for p in mod.parameters()]
-    named = _grads(img, txt, fus, x, ids, mask, y)
-    ref = {n: p.grad.detach().clone() for n, p in named if p.grad is not None}
+    _grads(img, txt, fus, x, ids, mask, y)
+    ref = {id(p): p.grad.detach().clone() for p in params if p.grad is not None}
     for p in params:
         p.grad = None
     red = GradAllReducer(params, 1, rehearse=True)
     assert red._avg
     if early:
         RN.TRUNK_GRAD_HOOK = red.trunk_hook
-    named = _grads(img, txt, fus, x, ids, mask, y)
+    _grads(img, txt, fus, x, ids, mask, y)
     RN.TRUNK_GRAD_HOOK = None
+    trunk_p = {id(p) for p in img.backbone.parameters()}
     trunk = {id(p.grad) for p in img.backbone.parameters() if p.grad is not None}
     red.launch()
     packed = sum(1 for b, *_ in red._pending if b is not None for t in b if id(t) in trunk)
     red.finish()
     torch.cuda.synchronize()
-    bad = [n for n, p in named if p.grad is not None and not torch.equal(p.grad, ref[n])]
+    bad = []
+    for i, p in enumerate(params):
+        if p.grad is None:
+            continue
+        g, r = p.grad, ref[id(p)]
+        if id(p) in trunk_p:  # the arena: reduced in place, must be untouched bit for bit
+            ok = torch.equal(g, r)
+        else:  # (the text embedding's gradient is an atomic scatter: its bits vary per run)
+            ok = torch.allclose(g, r, rtol=1e-6, atol=1e-7)
+        if not ok:
+            bad.append(i)
     out["packed"] = packed
     out["bad"] = bad
     out["n"] = len(ref)
