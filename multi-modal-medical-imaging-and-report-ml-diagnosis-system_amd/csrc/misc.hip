@@ -129,12 +129,24 @@ __global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int
   typedef typename ArgPack<VEC>::type A;
   const int cv = C / VEC;
   const long total = (long)N * P * Q * cv;
+  // the grid stride is a multiple of cv when the block is: a thread's channel vector (and
+  // its BN coefficients) is then fixed, computed once instead of per output
+  const bool fixed_c = blockDim.x % cv == 0;
+  float sc[VEC], sh[VEC];
+  if constexpr (BN) {
+    if (fixed_c) {
+      const int c0 = (int)(threadIdx.x % cv) * VEC;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) bn_coef_fwd(gamma, beta, mean, rstd, c0 + j, sc[j], sh[j]);
+    }
+  }
   GRID_STRIDE(i, total) {
     const int c = (int)(i % cv) * VEC;
-    float sc[VEC], sh[VEC];
     if constexpr (BN) {
+      if (!fixed_c) {
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) bn_coef_fwd(gamma, beta, mean, rstd, c + j, sc[j], sh[j]);
+        for (int j = 0; j < VEC; ++j) bn_coef_fwd(gamma, beta, mean, rstd, c + j, sc[j], sh[j]);
+      }
     }
     long t = i / cv;
     const int q = (int)(t % Q); t /= Q;
@@ -184,95 +196,6 @@ __global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int
     *(A*)(am + i * VEC) = packed;
     *(V*)(y + i * VEC) = o;
   }
-}
-
-// The same pool, one block per output row (n, p): the three input rows it reads are staged
-// in LDS once (with the stem's BN + ReLU applied and rounded to T on the way in when BN),
-// then every output vector takes its nine taps from LDS.  Each input element is loaded
-// (and normalised) once instead of once per window that holds it (2.25x on average), and a
-// thread's channel vector — so its BN coefficients — is fixed (256 % (C / VEC) == 0).
-// Same values, window order, tie and NaN rules as maxpool3s2_fwd_kernel (bit-identical).
-template <typename T, bool BN>
-__global__ __launch_bounds__(256) void maxpool3s2_rows_kernel(
-    const T* __restrict__ x, int H, int W, int C, int p, T* __restrict__ y,
-    uint8_t* __restrict__ am, int P, int Q, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const float* __restrict__ mean,
-    const float* __restrict__ rstd, int relu) {
-  typedef typename Vec16<T>::type V;
-  constexpr int VEC = Vec16<T>::N;
-  typedef typename ArgPack<VEC>::type A;
-  extern __shared__ __attribute__((aligned(16))) char pool_lds[];
-  V* rows = (V*)pool_lds;  // [3][W][C / VEC]
-  const int cv = C / VEC;
-  const int n = blockIdx.x / P, pp = blockIdx.x - n * P;
-  const int j = threadIdx.x % cv;  // this thread's channel vector in both phases
-  float sc[VEC], sh[VEC];
-  if constexpr (BN) {
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) bn_coef_fwd(gamma, beta, mean, rstd, j * VEC + e, sc[e], sh[e]);
-  }
-  const int row_v = W * cv;
-  for (int i = threadIdx.x; i < 3 * row_v; i += 256) {
-    const int r = i / row_v;
-    const int ih = pp * 2 - p + r;
-    V o{};
-    if ((unsigned)ih < (unsigned)H) {
-      const V v = *(const V*)(x + ((long)n * H + ih) * (long)W * C + (long)(i - r * row_v) * VEC);
-      if constexpr (BN) {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          float f = to_f(v[e]) * sc[e] + sh[e];
-          if (relu) f = fmaxf(f, 0.f);
-          o[e] = from_f<T>(f);  // the value BN-apply would have stored
-        }
-      } else {
-        o = v;
-      }
-    }
-    rows[i] = o;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < Q * cv; i += 256) {
-    const int q = i / cv;
-    float best[VEC];
-    int arg[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) { best[e] = -INFINITY; arg[e] = -1; }
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int ih = pp * 2 - p + r;
-#pragma unroll
-      for (int ss = 0; ss < 3; ++ss) {
-        const int iw = q * 2 - p + ss;
-        if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
-        const V v = rows[(r * W + iw) * cv + j];
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float f = to_f(v[e]);
-          if (arg[e] < 0 || f > best[e] || (f != f && best[e] == best[e])) {
-            best[e] = f;
-            arg[e] = r * 3 + ss;
-          }
-        }
-      }
-    }
-    V o;
-    A packed = 0;
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      o[e] = from_f<T>(best[e]);
-      packed |= (A)(uint8_t)arg[e] << (8 * e);
-    }
-    const long oi = (((long)n * P + pp) * Q + q) * C + (long)j * VEC;
-    *(A*)(am + oi) = packed;
-    *(V*)(y + oi) = o;
-  }
-}
-
-// the row-staged pool applies: whole channel vectors per thread, three input rows in LDS
-static bool pool_rows_ok(int C, int W, int vec, int elem) {
-  const int cv = C / vec;
-  return cv > 0 && 256 % cv == 0 && 3L * W * C * elem <= 64 * 1024;
 }
 
 // Backward of the 3x3 / stride-2 pool: an input pixel lies in at most 2 x 2 windows; their
@@ -440,14 +363,7 @@ extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, i
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "maxpool: inconsistent output size");
   const long total = (long)N * P * Q * (C / VEC);
-  const int esz = dtype == F32 ? 4 : 2;
-  if (k == 3 && s == 2 && pool_rows_ok(C, W, VEC, esz))
-    DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_rows_kernel<T, false>), dim3(N * P),
-                                         dim3(256), 3 * W * C * esz, (hipStream_t)stream,
-                                         (const T*)x, H, W, C, p, (T*)y, argmax, P, Q,
-                                         (const float*)nullptr, (const float*)nullptr,
-                                         (const float*)nullptr, (const float*)nullptr, 0));
-  else if (k == 3 && s == 2)
+  if (k == 3 && s == 2)
     DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, false>),
                                          dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                                          (const T*)x, N, H, W, C, p, (T*)y, argmax, P, Q,
@@ -471,17 +387,10 @@ extern "C" int mmdx_maxpool_bn_fwd(int dtype, const void* x, int N, int H, int W
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "maxpool bn: inconsistent output size");
   const long total = (long)N * P * Q * (C / VEC);
-  const int esz = dtype == F32 ? 4 : 2;
-  if (pool_rows_ok(C, W, VEC, esz))
-    DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_rows_kernel<T, true>), dim3(N * P),
-                                         dim3(256), 3 * W * C * esz, (hipStream_t)stream,
-                                         (const T*)x, H, W, C, p, (T*)y, argmax, P, Q, gamma,
-                                         beta, save_mean, save_rstd, relu));
-  else
-    DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, true>),
-                                         dim3(grid_for(total)), dim3(256), 0,
-                                         (hipStream_t)stream, (const T*)x, N, H, W, C, p, (T*)y,
-                                         argmax, P, Q, gamma, beta, save_mean, save_rstd, relu));
+  DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, true>), dim3(grid_for(total)),
+                                       dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W, C,
+                                       p, (T*)y, argmax, P, Q, gamma, beta, save_mean, save_rstd,
+                                       relu));
   MMDX_LAUNCH_CHECK();
   return 0;
 }
