@@ -101,11 +101,13 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, in
   const long slab = (long)K * RS * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < slab;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
+    // 32-bit decode (slab < 2^31, checked by the launcher): 64-bit division is slow
+    const unsigned ui = (unsigned)i;
+    const int c = (int)(ui % (unsigned)C);
     if (c >= Cm) continue;
-    const long t = i / C;
-    const int rs = (int)(t % RS);
-    const int k = (int)(t / RS);
+    const unsigned t = ui / (unsigned)C;
+    const int rs = (int)(t % (unsigned)RS);
+    const int k = (int)(t / (unsigned)RS);
     // 8 independent partial sums keep 8 slab loads in flight (fixed order: deterministic)
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int z = 0;
@@ -156,10 +158,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce_z_kernel(const float* __rest
       f32x4 v = red[e];
 #pragma unroll
       for (int q = 1; q < Z; ++q) v += red[q * E + e];
-      const long i = i4 * 4;
-      const int c = (int)(i % C);
-      const long t = i / C;
-      const int rs = (int)(t % RS), k = (int)(t / RS);
+      const unsigned i = (unsigned)(i4 * 4);  // 32-bit decode (slab < 2^31)
+      const int c = (int)(i % (unsigned)C);
+      const unsigned t = i / (unsigned)C;
+      const int rs = (int)(t % (unsigned)RS), k = (int)(t / (unsigned)RS);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (c + j >= Cm) break;
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_z_kernel(const float* __rest
 
 static void wgrad_reduce(const float* ws, int splits, int K, int C, int Cm, int RS, float* dw,
                          float beta, hipStream_t st) {
-  const long total = (long)K * C * RS;
+  const long total = (long)K * C * RS;  // < 2^31: checked by the wgrad entry point
   // split groups only for the deep splits (>= 128: the stem's and layer1's weight gradients,
   // at the end of the backward where little else runs); elsewhere the per-element loop, whose
   // lower memory-level parallelism disturbs the concurrent dgrad/BN chain less (all-split:
@@ -460,6 +462,7 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   const int M = g.K, N = g.R * g.S * g.C;
   const long Kl = (long)g.N * g.P * g.Q;
   MMDX_CHECK_ARG(Kl < (1L << 31), "conv wgrad: N*P*Q too large");
+  MMDX_CHECK_ARG((long)M * N < (1L << 31), "conv wgrad: K*C*R*S too large");
   const int K = (int)Kl;
   const size_t need = (size_t)p.splits * M * N * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu", ws_bytes, need);
@@ -660,11 +663,12 @@ namespace mmdx {
 __global__ void stem_pair_input_kernel(const float* __restrict__ x, int N, int C, int H, int W,
                                        int pad, int Hp, int W2, bf16* __restrict__ out) {
   const long total = (long)N * Hp * W2;
-  GRID_STRIDE(i, total) {
-    const int j = (int)(i % W2);
-    const long t = i / W2;
-    const int hp = (int)(t % Hp);
-    const int n = (int)(t / Hp);
+  GRID_STRIDE(i, total) {  // 32-bit decode (total < 2^31, checked by the entry point)
+    const unsigned ui = (unsigned)i;
+    const int j = (int)(ui % (unsigned)W2);
+    const unsigned t = ui / (unsigned)W2;
+    const int hp = (int)(t % (unsigned)Hp);
+    const int n = (int)(t / (unsigned)Hp);
     const int ih = hp - pad;
     bf16x8 v;
 #pragma unroll
@@ -733,6 +737,7 @@ extern "C" int mmdx_stem_pair_input(const float* x_nchw, int N, int C, int H, in
                  "stem pair input: bad args");
   const int Hp = H + 2 * pad, W2 = (W + 2 * pad) / 2;
   const long total = (long)N * Hp * W2;
+  MMDX_CHECK_ARG(total < (1L << 31), "stem pair input: more than 2^31 pixel pairs");
   hipLaunchKernelGGL(stem_pair_input_kernel, dim3(grid_for(total)), dim3(256), 0,
                      (hipStream_t)stream, x_nchw, N, C, H, W, pad, Hp, W2, (bf16*)out);
   MMDX_LAUNCH_CHECK();

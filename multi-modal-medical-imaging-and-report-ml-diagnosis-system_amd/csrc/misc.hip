@@ -141,17 +141,20 @@ __global__ void maxpool3s2_fwd_kernel(const T* __restrict__ x, int N, int H, int
     }
   }
   GRID_STRIDE(i, total) {
-    const int c = (int)(i % cv) * VEC;
+    // 32-bit index math (total < 2^31, checked by the entry point): a 64-bit division is a
+    // long software sequence on the GPU
+    const unsigned ui = (unsigned)i, ucv = (unsigned)cv;
+    const int c = (int)(ui % ucv) * VEC;
     if constexpr (BN) {
       if (!fixed_c) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) bn_coef_fwd(gamma, beta, mean, rstd, c + j, sc[j], sh[j]);
       }
     }
-    long t = i / cv;
-    const int q = (int)(t % Q); t /= Q;
-    const int pp = (int)(t % P);
-    const int n = (int)(t / P);
+    unsigned t = ui / ucv;
+    const int q = (int)(t % (unsigned)Q); t /= (unsigned)Q;
+    const int pp = (int)(t % (unsigned)P);
+    const int n = (int)(t / (unsigned)P);
     V v[9];
     bool ok[9];
 #pragma unroll
@@ -210,12 +213,13 @@ __global__ void maxpool3s2_bwd_kernel(const uint8_t* __restrict__ am, const T* _
   const Pool3s2Grad<T> pg{am, dy, H, W, C, p, P, Q};
   const int cv = C / VEC;
   const long total = (long)N * H * W * cv;
-  GRID_STRIDE(i, total) {
-    const int c = (int)(i % cv) * VEC;
-    long t = i / cv;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+  GRID_STRIDE(i, total) {  // 32-bit index math (total < 2^31, checked by the entry point)
+    const unsigned ui = (unsigned)i, ucv = (unsigned)cv;
+    const int c = (int)(ui % ucv) * VEC;
+    unsigned t = ui / ucv;
+    const int w = (int)(t % (unsigned)W); t /= (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
     *(V*)(dx + i * VEC) = pg.at(n, h, w, c);
   }
 }
@@ -363,6 +367,7 @@ extern "C" int mmdx_maxpool_fwd(int dtype, const void* x, int N, int H, int W, i
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "maxpool: inconsistent output size");
   const long total = (long)N * P * Q * (C / VEC);
+  MMDX_CHECK_ARG((long)N * H * W * C < (1L << 31), "maxpool: more than 2^31 input elements");
   if (k == 3 && s == 2)
     DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, false>),
                                          dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
@@ -387,6 +392,7 @@ extern "C" int mmdx_maxpool_bn_fwd(int dtype, const void* x, int N, int H, int W
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "maxpool bn: inconsistent output size");
   const long total = (long)N * P * Q * (C / VEC);
+  MMDX_CHECK_ARG((long)N * H * W * C < (1L << 31), "maxpool bn: more than 2^31 input elements");
   DISPATCH_T(dtype, hipLaunchKernelGGL((maxpool3s2_fwd_kernel<T, true>), dim3(grid_for(total)),
                                        dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W, C,
                                        p, (T*)y, argmax, P, Q, gamma, beta, save_mean, save_rstd,
@@ -401,6 +407,7 @@ extern "C" int mmdx_maxpool_bwd(int dtype, const uint8_t* argmax, const void* dy
   const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(C % VEC == 0, "maxpool bwd: bad C");
   const long total = (long)N * H * W * (C / VEC);
+  MMDX_CHECK_ARG((long)N * H * W * C < (1L << 31), "maxpool bwd: more than 2^31 elements");
   if (k == 3 && s == 2 && p <= 1)
     DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool3s2_bwd_kernel<T>, dim3(grid_for(total)),
                                          dim3(256), 0, (hipStream_t)stream, argmax,

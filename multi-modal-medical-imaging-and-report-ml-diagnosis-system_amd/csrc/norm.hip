@@ -759,6 +759,7 @@ extern "C" int mmdx_bn_bwd_pool(int dtype, int train, const void* x, const uint8
   MMDX_CHECK_ARG(P == (H + 2 * p - k) / s + 1 && Q == (W + 2 * p - k) / s + 1,
                  "bn bwd pool: inconsistent pool output size");
   const long rows = (long)N * H * W;
+  MMDX_CHECK_ARG(rows < (1L << 31), "bn bwd pool: more than 2^31 rows");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == BF16)
     return bn_bwd_t<bf16>(train, x, nullptr,

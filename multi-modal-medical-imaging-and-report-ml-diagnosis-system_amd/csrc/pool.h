@@ -60,12 +60,14 @@ struct Pool3s2Grad {
     for (int j = 0; j < VEC; ++j) out[j] = from_f<T>(acc[j]);
     return out;
   }
-  // the same for NHWC row r = (n*H + h)*W + w
+  // the same for NHWC row r = (n*H + h)*W + w (rows < 2^31, checked by mmdx_bn_bwd_pool:
+  // 32-bit divisions — a 64-bit one is a long software sequence on the GPU)
   __device__ __forceinline__ V row(long r, int c) const {
-    const int w = (int)(r % W);
-    const long t = r / W;
-    const int h = (int)(t % H);
-    return at((int)(t / H), h, w, c);
+    const unsigned ur = (unsigned)r;
+    const int w = (int)(ur % (unsigned)W);
+    const unsigned t = ur / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    return at((int)(t / (unsigned)H), h, w, c);
   }
 };
 
