@@ -161,6 +161,16 @@ int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
                 void* workspace, size_t ws_bytes, void* stream);
 /* y == NULL (train): statistics only — save_mean/save_rstd and the running-stat update, no
  * apply pass (the consumer normalises on the fly, e.g. mmdx_maxpool_bn_fwd). */
+/* mmdx_bn_fwd plus, when relu_mask != NULL (relu units): one byte per 16-B channel vector of
+ * each row ([rows][C / (16 / sizeof(dtype))]), bit e set iff the stored y element e is > 0 —
+ * the ReLU mask mmdx_bn_bwd_ex reads instead of y (1 bit per element instead of 16). */
+int mmdx_bn_fwd_ex(int dtype, int train, const void* x, long rows, int C,
+                   const float* stat_part, int stat_blocks, long stat_rows,
+                   const float* gamma, const float* beta, float* running_mean,
+                   float* running_var, float momentum, float eps,
+                   float* save_mean, float* save_rstd,
+                   const void* residual, int relu, void* y, uint8_t* relu_mask,
+                   void* workspace, size_t ws_bytes, void* stream);
 /* dy: grad w.r.t. y; y: forward output (ReLU mask source).  Writes dx, d_residual
  * (may be NULL), and dgamma/dbeta (fp32, accumulated with beta_acc). */
 int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
@@ -169,6 +179,15 @@ int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* 
                 const float* stat_part, int stat_blocks, void* dx,
                 void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                 void* workspace, size_t ws_bytes, void* stream);
+/* mmdx_bn_bwd with the ReLU mask taken from relu_mask (written by mmdx_bn_fwd_ex) when it is
+ * not NULL — a residual unit's backward then reads 1 bit per element instead of its output;
+ * results are identical to mmdx_bn_bwd with y. */
+int mmdx_bn_bwd_ex(int dtype, int train, const void* x, const void* y, const void* dy,
+                   long rows, int C, const float* gamma, const float* bn_beta,
+                   const float* save_mean, const float* save_rstd, int relu,
+                   const float* stat_part, int stat_blocks, void* dx,
+                   void* d_residual, float* dgamma, float* dbeta, float beta_acc,
+                   const uint8_t* relu_mask, void* workspace, size_t ws_bytes, void* stream);
 /* stat_part (optional, [C][stat_blocks] pairs (sum g, sum g*xhat)): the reduction already
  * made by mmdx_conv_dgrad_bnstat in the epilogue that produced dy — the BN backward then
  * skips its own pass over (dy, x).  ReLU units only (with y = the unit's output for a

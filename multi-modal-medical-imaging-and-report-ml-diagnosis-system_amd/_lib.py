@@ -83,8 +83,12 @@ SIGNATURES = {
     "mmdx_bn_workspace_size": (sz, [i64, i32]),
     "mmdx_bn_fwd": (i32, [i32, i32, vp, i64, i32, vp, i32, i64, vp, vp, vp, vp, f32, f32, vp, vp,
                           vp, i32, vp, vp, sz, vp]),
+    "mmdx_bn_fwd_ex": (i32, [i32, i32, vp, i64, i32, vp, i32, i64, vp, vp, vp, vp, f32, f32, vp,
+                             vp, vp, i32, vp, vp, vp, sz, vp]),
     "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp,
                           vp, vp, f32, vp, sz, vp]),
+    "mmdx_bn_bwd_ex": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp,
+                             vp, vp, vp, f32, vp, vp, sz, vp]),
     "mmdx_bn_bwd_pool": (i32, [i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
                                i32, vp, vp, vp, vp, i32, vp, vp, vp, f32, vp, sz, vp]),
     "mmdx_img_desc_size": (sz, []),

@@ -243,13 +243,16 @@ __device__ __forceinline__ void bn_coef(const float* gamma, const float* beta, f
   shift = (beta ? beta[c] : 0.f) - mean * g * rstd;
 }
 
-// y = act(x*scale[c] + shift[c] (+ res))
+// y = act(x*scale[c] + shift[c] (+ res)); mask (optional): one byte per channel vector of a
+// row, bit e = (stored y[e] > 0) — the ReLU mask the backward of a residual unit reads
+// instead of y itself (1 bit per element instead of 16)
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res, long rows,
                                                        int C, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
-                                                       T* __restrict__ y) {
+                                                       T* __restrict__ y,
+                                                       uint8_t* __restrict__ mask) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   const RowTile rt = row_tile(C, VEC);
@@ -272,6 +275,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
         o[e] = from_f<T>(f);
       }
       ((V*)y)[i] = o;
+      if (mask) {
+        unsigned b = 0;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) b |= (to_f(o[e]) > 0.f ? 1u : 0u) << e;
+        mask[i] = (uint8_t)b;
+      }
     }
   }
 }
@@ -283,7 +292,8 @@ template <typename T, class G>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
     int ct, long rpb, const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
-    const float* __restrict__ gamma, const float* __restrict__ bbeta, float2* __restrict__ part) {
+    const float* __restrict__ gamma, const float* __restrict__ bbeta, float2* __restrict__ part,
+    const uint8_t* __restrict__ mask) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   __shared__ float s_a[BN_NT * VEC], s_b[BN_NT * VEC];
@@ -291,7 +301,9 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
   const int c0 = (blockIdx.y * ct + tx) * VEC;
   const long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
   float sg[VEC], sgx[VEC], mu[VEC], rs[VEC], sc[VEC], sh[VEC];
-  const bool mask_x = relu && !y;  // ReLU mask recomputed from x (no residual)
+  // ReLU mask source: the forward's bit mask, else y (the unit's output), else recomputed
+  // from x (no residual)
+  const bool mask_x = relu && !y && !mask;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) sg[j] = sgx[j] = mu[j] = rs[j] = sc[j] = sh[j] = 0.f;
   if (c0 < C) {
@@ -314,12 +326,15 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
       const V vx = *(const V*)(x + r * C + c0);
       const V vd = dy.row(r, c0);
       V vy{};
-      if (relu && !mask_x) vy = *(const V*)(y + r * C + c0);
+      unsigned mb = 0;
+      if (relu && mask) mb = mask[r * (C / VEC) + c0 / VEC];
+      else if (relu && !mask_x) vy = *(const V*)(y + r * C + c0);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         float g = to_f(vd[j]);
         const float a = mask_x ? to_f(vx[j]) * sc[j] + sh[j] : to_f(vy[j]);
-        if (relu && !(a > 0.f)) g = 0.f;
+        const bool pos = mask ? ((mb >> j) & 1u) != 0 : a > 0.f;
+        if (relu && !pos) g = 0.f;
         sg[j] += g;
         sgx[j] += g * (to_f(vx[j]) - mu[j]) * rs[j];
       }
@@ -395,8 +410,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ coef, int relu, const float* __restrict__ gamma,
-    const float* __restrict__ bbeta, T* __restrict__ dx, T* __restrict__ dres) {
-  const bool mask_x = relu && !y;
+    const float* __restrict__ bbeta, T* __restrict__ dx, T* __restrict__ dres,
+    const uint8_t* __restrict__ mask) {
+  const bool mask_x = relu && !y && !mask;
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   const RowTile rt = row_tile(C, VEC);
@@ -413,13 +429,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       const V vx = ((const V*)x)[i];
       const V vd = dy.row(r, j * VEC);
       V vy{};
-      if (relu && !mask_x) vy = ((const V*)y)[i];
+      unsigned mb = 0;
+      if (relu && mask) mb = mask[i];
+      else if (relu && !mask_x) vy = ((const V*)y)[i];
       V o, og;
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         float g = to_f(vd[e]);
         const float a = mask_x ? to_f(vx[e]) * sc[e] + sh[e] : to_f(vy[e]);
-        if (relu && !(a > 0.f)) g = 0.f;
+        const bool pos = mask ? ((mb >> e) & 1u) != 0 : a > 0.f;
+        if (relu && !pos) g = 0.f;
         o[e] = from_f<T>(ca[e] * g + cb[e] + ck[e] * to_f(vx[e]));
         og[e] = from_f<T>(g);
       }
@@ -449,7 +468,7 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
                     int stat_blocks, long stat_rows, const float* gamma, const float* beta,
                     float* rm, float* rv, float momentum, float eps, float* smean, float* srstd,
                     const void* res, int relu, void* y, void* ws, size_t ws_bytes,
-                    hipStream_t st) {
+                    hipStream_t st, uint8_t* mask = nullptr) {
   constexpr int VEC = Vec16<T>::N;
   MMDX_CHECK_ARG(C % VEC == 0, "bn: C=%d must be a multiple of %d", C, VEC);
   const BnLayout L = bn_layout(rows, C, VEC);
@@ -488,7 +507,7 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
   if (y)  // (y == NULL: statistics only, the consumer applies the normalisation itself)
     hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_rows(rows, C, VEC)), dim3(256), 0, st,
                        (const T*)x, (const T*)res, rows, C, (const float*)scale,
-                       (const float*)shift, relu, (T*)y);
+                       (const float*)shift, relu, (T*)y, relu ? mask : nullptr);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -498,7 +517,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
                     const float* gamma, const float* bbeta, const float* smean,
                     const float* srstd, int relu, const float* stat_part, int stat_blocks,
                     void* dx, void* dres, float* dgamma, float* dbeta, float beta_acc, void* ws,
-                    size_t ws_bytes, hipStream_t st) {
+                    size_t ws_bytes, hipStream_t st, const uint8_t* mask = nullptr) {
   constexpr int VEC = Vec16<T>::N;
   MMDX_CHECK_ARG(C % VEC == 0, "bn bwd: C=%d must be a multiple of %d", C, VEC);
   const BnLayout L = bn_layout(rows, C, VEC);
@@ -514,7 +533,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
   } else {
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, G>), dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0,
                        st, (const T*)x, (const T*)y, dy, rows, C, L.ct, L.rows_per_block,
-                       smean, srstd, relu, gamma, bbeta, part);
+                       smean, srstd, relu, gamma, bbeta, part, mask);
   }
   if (nblk > fin_wide())
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
@@ -526,7 +545,7 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
                        srstd, dgamma, dbeta, beta_acc, coef);
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G>), dim3(grid_rows(rows, C, VEC)), dim3(256), 0,
                      st, (const T*)x, (const T*)y, dy, rows, C, smean, srstd,
-                     (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres);
+                     (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres, mask);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -706,25 +725,59 @@ extern "C" size_t mmdx_bn_workspace_size(long rows, int C) {
   return (size_t)nb * C * sizeof(float2) + 5 * (size_t)C * sizeof(float);
 }
 
+extern "C" int mmdx_bn_fwd_ex(int dtype, int train, const void* x, long rows, int C,
+                              const float* stat_part, int stat_blocks, long stat_rows,
+                              const float* gamma, const float* beta, float* running_mean,
+                              float* running_var, float momentum, float eps, float* save_mean,
+                              float* save_rstd, const void* residual, int relu, void* y,
+                              uint8_t* relu_mask, void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_fwd: fp16 is the C5 path only");
+  MMDX_CHECK_ARG(rows > 0 && C > 0 && save_mean && save_rstd, "bn fwd: bad args");
+  MMDX_CHECK_ARG(!stat_part || (stat_blocks > 0 && stat_rows > 0 &&
+                                (long)stat_blocks * stat_rows >= rows),
+                 "bn fwd: bad precomputed statistics layout");
+  MMDX_CHECK_ARG(!relu_mask || (relu && y), "bn fwd: a ReLU mask needs relu and y");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    return bn_fwd_t<bf16>(train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma, beta,
+                          running_mean, running_var, momentum, eps, save_mean, save_rstd,
+                          residual, relu, y, ws, ws_bytes, st, relu_mask);
+  return bn_fwd_t<float>(train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma, beta,
+                         running_mean, running_var, momentum, eps, save_mean, save_rstd,
+                         residual, relu, y, ws, ws_bytes, st, relu_mask);
+}
+
 extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
                            const float* stat_part, int stat_blocks, long stat_rows,
                            const float* gamma, const float* beta, float* running_mean,
                            float* running_var, float momentum, float eps, float* save_mean,
                            float* save_rstd, const void* residual, int relu, void* y,
                            void* ws, size_t ws_bytes, void* stream) {
-  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_fwd: fp16 is the C5 path only");
-  MMDX_CHECK_ARG(rows > 0 && C > 0 && save_mean && save_rstd, "bn fwd: bad args");
-  MMDX_CHECK_ARG(!stat_part || (stat_blocks > 0 && stat_rows > 0 &&
-                                (long)stat_blocks * stat_rows >= rows),
-                 "bn fwd: bad precomputed statistics layout");
+  return mmdx_bn_fwd_ex(dtype, train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma,
+                        beta, running_mean, running_var, momentum, eps, save_mean, save_rstd,
+                        residual, relu, y, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int mmdx_bn_bwd_ex(int dtype, int train, const void* x, const void* y,
+                              const void* dy, long rows, int C, const float* gamma,
+                              const float* bn_beta, const float* save_mean,
+                              const float* save_rstd, int relu, const float* stat_part,
+                              int stat_blocks, void* dx, void* d_residual, float* dgamma,
+                              float* dbeta, float beta_acc, const uint8_t* relu_mask, void* ws,
+                              size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_bwd: fp16 is the C5 path only");
+  MMDX_CHECK_ARG(rows > 0 && C > 0, "bn bwd: bad args");
+  MMDX_CHECK_ARG(!(relu && !y && !relu_mask && d_residual),
+                 "bn bwd: a residual unit needs its output y or its ReLU mask");
   hipStream_t st = (hipStream_t)stream;
+  const uint8_t* mk = relu ? relu_mask : nullptr;
   if (dtype == BF16)
-    return bn_fwd_t<bf16>(train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma, beta,
-                          running_mean, running_var, momentum, eps, save_mean, save_rstd,
-                          residual, relu, y, ws, ws_bytes, st);
-  return bn_fwd_t<float>(train, x, rows, C, stat_part, stat_blocks, stat_rows, gamma, beta,
-                         running_mean, running_var, momentum, eps, save_mean, save_rstd,
-                         residual, relu, y, ws, ws_bytes, st);
+    return bn_bwd_t<bf16>(train, x, y, DenseGrad<bf16>{(const bf16*)dy, C}, rows, C, gamma,
+                          bn_beta, save_mean, save_rstd, relu, stat_part, stat_blocks, dx,
+                          d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st, mk);
+  return bn_bwd_t<float>(train, x, y, DenseGrad<float>{(const float*)dy, C}, rows, C, gamma,
+                         bn_beta, save_mean, save_rstd, relu, stat_part, stat_blocks, dx,
+                         d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st, mk);
 }
 
 extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
@@ -733,17 +786,9 @@ extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, c
                            const float* stat_part, int stat_blocks, void* dx,
                            void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                            void* ws, size_t ws_bytes, void* stream) {
-  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_bwd: fp16 is the C5 path only");
-  MMDX_CHECK_ARG(rows > 0 && C > 0, "bn bwd: bad args");
-  MMDX_CHECK_ARG(!(relu && !y && d_residual), "bn bwd: a residual unit needs its output y");
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == BF16)
-    return bn_bwd_t<bf16>(train, x, y, DenseGrad<bf16>{(const bf16*)dy, C}, rows, C, gamma,
-                          bn_beta, save_mean, save_rstd, relu, stat_part, stat_blocks, dx,
-                          d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
-  return bn_bwd_t<float>(train, x, y, DenseGrad<float>{(const float*)dy, C}, rows, C, gamma,
-                         bn_beta, save_mean, save_rstd, relu, stat_part, stat_blocks, dx,
-                         d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+  return mmdx_bn_bwd_ex(dtype, train, x, y, dy, rows, C, gamma, bn_beta, save_mean, save_rstd,
+                        relu, stat_part, stat_blocks, dx, d_residual, dgamma, dbeta, beta_acc,
+                        nullptr, ws, ws_bytes, stream);
 }
 
 extern "C" int mmdx_bn_bwd_pool(int dtype, int train, const void* x, const uint8_t* argmax,

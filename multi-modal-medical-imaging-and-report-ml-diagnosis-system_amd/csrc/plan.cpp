@@ -52,12 +52,14 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                                    o.f[0], P(o, 7, ext), o.i[0], s);
     case MMDX_OP_BN_FWD:
       // i: train, C, stat_blocks, relu; l: rows, stat_rows, ws_bytes; f: momentum, eps
-      return mmdx_bn_fwd(o.dtype, o.i[0], P(o, 0, ext), o.l[0], o.i[1],
-                         (const float*)P(o, 1, ext), o.i[2], o.l[1],
-                         (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
-                         (float*)P(o, 4, ext), (float*)P(o, 5, ext), o.f[0], o.f[1],
-                         (float*)P(o, 6, ext), (float*)P(o, 7, ext), P(o, 8, ext), o.i[3],
-                         P(o, 9, ext), P(o, 10, ext), (size_t)o.l[2], s);
+      // p[11]: optional ReLU bit mask (mmdx_bn_fwd_ex)
+      return mmdx_bn_fwd_ex(o.dtype, o.i[0], P(o, 0, ext), o.l[0], o.i[1],
+                            (const float*)P(o, 1, ext), o.i[2], o.l[1],
+                            (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
+                            (float*)P(o, 4, ext), (float*)P(o, 5, ext), o.f[0], o.f[1],
+                            (float*)P(o, 6, ext), (float*)P(o, 7, ext), P(o, 8, ext), o.i[3],
+                            P(o, 9, ext), (uint8_t*)P(o, 11, ext), P(o, 10, ext),
+                            (size_t)o.l[2], s);
     case MMDX_OP_MAXPOOL_FWD:
       // i: N, H, W, C, k, s, p, P ; l: Q
       return mmdx_maxpool_fwd(o.dtype, P(o, 0, ext), o.i[0], o.i[1], o.i[2], o.i[3], o.i[4],
@@ -92,13 +94,14 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                               (int)o.l[0], P(o, 2, ext), s);
     case MMDX_OP_BN_BWD:
       // i: train, C, relu, stat_blocks; l: rows, ws_bytes; f: beta_acc;
-      // p: x, y, dy, gamma, beta, mean, rstd, dx, dres, dgamma, dbeta, ws; stat_part in l[2]
-      return mmdx_bn_bwd(o.dtype, o.i[0], P(o, 0, ext), P(o, 1, ext), P(o, 2, ext), o.l[0],
-                         o.i[1], (const float*)P(o, 3, ext), (const float*)P(o, 4, ext),
-                         (const float*)P(o, 5, ext), (const float*)P(o, 6, ext), o.i[2],
-                         (const float*)o.l[2], o.i[3], P(o, 7, ext), P(o, 8, ext),
-                         (float*)P(o, 9, ext), (float*)P(o, 10, ext), o.f[0], P(o, 11, ext),
-                         (size_t)o.l[1], s);
+      // p: x, y, dy, gamma, beta, mean, rstd, dx, dres, dgamma, dbeta, ws; stat_part in l[2],
+      // the optional ReLU bit mask (absolute pointer) in l[3]
+      return mmdx_bn_bwd_ex(o.dtype, o.i[0], P(o, 0, ext), P(o, 1, ext), P(o, 2, ext), o.l[0],
+                            o.i[1], (const float*)P(o, 3, ext), (const float*)P(o, 4, ext),
+                            (const float*)P(o, 5, ext), (const float*)P(o, 6, ext), o.i[2],
+                            (const float*)o.l[2], o.i[3], P(o, 7, ext), P(o, 8, ext),
+                            (float*)P(o, 9, ext), (float*)P(o, 10, ext), o.f[0],
+                            (const uint8_t*)o.l[3], P(o, 11, ext), (size_t)o.l[1], s);
     case MMDX_OP_CONV_DGRAD_BNSTAT:
       // i: relu; f: beta; p: dy, w_crsk, dx, bn_y, gamma, beta, mean, rstd, stat_part, bn_out
       return mmdx_conv_dgrad_bnstat(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),

@@ -366,12 +366,16 @@ class _Plan:
             ws_for(wsn, st)
             if join is not None:
                 fw.add(L.OP_WAIT, p=(join,), stream=st)
+            # a residual unit's backward needs its ReLU mask: kept as 1 bit per element
+            # (one byte per 16-B channel vector) instead of re-reading its output
+            rmask = (A.new((rows, K // vec), torch.uint8, dev)
+                     if keep and relu and res is not None and out is not None else None)
             fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, 128, wsn),
                    f=(bn.momentum, bn.eps), stream=st,
                    p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
-                      res, out, _WS2 if st else _WS))
+                      res, out, _WS2 if st else _WS, rmask))
             u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
-                     rstd=rstd, wc=wc, pair=pair is not None)
+                     rstd=rstd, wc=wc, pair=pair is not None, rmask=rmask)
             units.append(u)
             return out, d, u
 
@@ -512,7 +516,10 @@ class _Plan:
                 dres = A.new(tuple(u["y"].shape), T, dev) if want_res else None
                 wsn = L.lib().mmdx_bn_workspace_size(rows, K)
                 ws_for(wsn)
-                out = u["out"] if want_res else None  # no residual: mask recomputed from y
+                # ReLU mask: a residual unit's bit mask from the forward (else its output);
+                # no residual: recomputed from y
+                rmask = u.get("rmask") if want_res else None
+                out = u["out"] if want_res and rmask is None else None
                 sp, sb = stats if stats is not None else (None, 0)
                 if pool is not None:
                     # `dout` is the stem pool's OUTPUT gradient: the BN backward gathers
@@ -525,7 +532,8 @@ class _Plan:
                               u["rstd"], dconv, g(u["bn"].weight), g(u["bn"].bias), _WS))
                 else:
                     bw.add(L.OP_BN_BWD, dt, i=(int(train), K, int(u["relu"]), sb),
-                           l=(rows, wsn, sp.data_ptr() if sp is not None else 0), f=(0.0,),
+                           l=(rows, wsn, sp.data_ptr() if sp is not None else 0,
+                              rmask.data_ptr() if rmask is not None else 0), f=(0.0,),
                            p=(u["y"], out, dout, u["bn"].weight, u["bn"].bias, u["mean"],
                               u["rstd"], dconv, dres, g(u["bn"].weight), g(u["bn"].bias),
                               _WS))

@@ -764,3 +764,47 @@ def test_conv_fwd_bn_eval(dev, dt, cfg, res, relu):
            *[t.data_ptr() for t in bn], 1e-5, rd.data_ptr() if res else None, int(relu),
            L.stream())
     _close(out.permute(0, 3, 1, 2), y, dt, f"bn-eval {cfg}")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_relu_bitmask(dev, dt):
+    """A residual unit's BN backward reading the forward's 1-bit ReLU mask
+    (mmdx_bn_fwd_ex / mmdx_bn_bwd_ex) equals the one reading the unit's output, bit for bit,
+    including elements that are exactly zero after the residual add."""
+    g = torch.Generator().manual_seed(5)
+    rows, C = 3000, 64
+    x = torch.randn(rows, C, generator=g).to(dev, dt)
+    r = torch.randn(rows, C, generator=g)
+    r[:100] = 0.0
+    r = r.to(dev, dt)
+    dy = torch.randn(rows, C, generator=g).to(dev, dt)
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.1).to(dev)
+    dc = L.dtype_code(dt)
+    vec = 4 if dt == torch.float32 else 8
+    ws_n = L.lib().mmdx_bn_workspace_size(rows, C)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    mean, rstd = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    y = torch.empty_like(x)
+    mask = torch.empty(rows, C // vec, dtype=torch.uint8, device=dev)
+    L.call("mmdx_bn_fwd_ex", dc, 1, x.data_ptr(), rows, C, None, 0, 0, gam.data_ptr(),
+           bet.data_ptr(), rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, mean.data_ptr(),
+           rstd.data_ptr(), r.data_ptr(), 1, y.data_ptr(), mask.data_ptr(), ws.data_ptr(), ws_n,
+           L.stream())
+    bits = ((y.view(rows, C // vec, vec).float() > 0).to(torch.int32)
+            << torch.arange(vec, device=dev, dtype=torch.int32)).sum(-1)
+    assert torch.equal(mask.to(torch.int32), bits)
+    outs = []
+    for use_mask in (False, True):
+        dx, dres = torch.empty_like(x), torch.empty_like(x)
+        dgm, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        L.call("mmdx_bn_bwd_ex", dc, 1, x.data_ptr(), None if use_mask else y.data_ptr(),
+               dy.data_ptr(), rows, C, gam.data_ptr(), bet.data_ptr(), mean.data_ptr(),
+               rstd.data_ptr(), 1, None, 0, dx.data_ptr(), dres.data_ptr(), dgm.data_ptr(),
+               dbt.data_ptr(), 0.0, mask.data_ptr() if use_mask else None, ws.data_ptr(), ws_n,
+               L.stream())
+        outs.append((dx, dres, dgm, dbt))
+    torch.cuda.synchronize()
+    for u, v, name in zip(outs[0], outs[1], ("dx", "dres", "dgamma", "dbeta")):
+        assert torch.equal(u, v), name
