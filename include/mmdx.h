@@ -117,6 +117,14 @@ int mmdx_conv_dgrad_bnstat(int dtype, const mmdx_conv_desc* d, const void* dy,
                            const void* bn_out, const float* gamma, const float* bn_beta,
                            const float* save_mean, const float* save_rstd, int relu,
                            float* stat_part, void* stream);
+/* stride-1 dgrad whose epilogue adds a masked tensor: dx = dgrad(dy) + (bit ? acc_src : 0),
+ * the bit from a 1-bit ReLU mask written by mmdx_bn_fwd_ex ([rows][C / (16 / elem)] bytes).
+ * An identity block's conv1 dgrad adds the gradient that reached the block output through
+ * the residual unit's ReLU (its dout, masked) — mmdx_bn_bwd then writes no d_residual.
+ * Equals mmdx_conv_dgrad with beta 1 onto that masked gradient, bit for bit. */
+int mmdx_conv_dgrad_accmask(int dtype, const mmdx_conv_desc* d, const void* dy,
+                            const void* w_crsk, void* dx, const void* acc_src,
+                            const uint8_t* acc_mask, void* stream);
 size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc* d);
 /* dw_kcrs (fp32, master layout, Cin = c_master) = dw_kcrs*beta + grad */
 int mmdx_conv_wgrad(int dtype, const mmdx_conv_desc* d, int c_master, const void* x,
@@ -228,7 +236,8 @@ enum {
   MMDX_OP_MAXPOOL_BWD, MMDX_OP_BN_BWD, MMDX_OP_CONV_WGRAD, MMDX_OP_CONV_DGRAD,
   MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PAIR_INPUT,
   MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI,
-  MMDX_OP_CONV_FWD_BNEVAL, MMDX_OP_MAXPOOL_BN_FWD, MMDX_OP_BN_BWD_POOL
+  MMDX_OP_CONV_FWD_BNEVAL, MMDX_OP_MAXPOOL_BN_FWD, MMDX_OP_BN_BWD_POOL,
+  MMDX_OP_CONV_DGRAD_ACCMASK
 };
 typedef struct {
   int op, dtype, stream;

@@ -54,7 +54,7 @@ class PlanOp(C.Structure):
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
  OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PAIR_INPUT,
  OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL,
- OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL) = range(1, 24)
+ OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK) = range(1, 25)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -74,6 +74,7 @@ SIGNATURES = {
     "mmdx_conv_dgrad_stat_blocks": (i32, [i32, CD]),
     "mmdx_conv_dgrad_bnstat": (i32, [i32, CD, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, i32, vp,
                                      vp]),
+    "mmdx_conv_dgrad_accmask": (i32, [i32, CD, vp, vp, vp, vp, vp, vp]),
     "mmdx_conv_wgrad_workspace_size": (sz, [i32, CD]),
     "mmdx_conv_wgrad": (i32, [i32, CD, i32, vp, vp, vp, f32, vp, sz, vp]),
     "mmdx_stem_pair_desc": (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, CD]),

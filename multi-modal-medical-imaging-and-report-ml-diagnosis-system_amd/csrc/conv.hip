@@ -301,10 +301,13 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
 template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
                      hipStream_t st, float* stats = nullptr, bool dma_ok = false,
-                     const BnStat& bs = BnStat{}) {
+                     const BnStat& bs = BnStat{}, const void* acc_src = nullptr,
+                     const uint8_t* acc_mask = nullptr) {
   EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
                   (float2*)stats};
   epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
+  epi.acc_src = (const T*)acc_src;
+  epi.acc_mask = acc_mask;
   return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok);
 }
 
@@ -400,18 +403,20 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
 
 template <typename T>
 static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
-                        float beta, hipStream_t st, const BnStat& bs = BnStat{}) {
+                        float beta, hipStream_t st, const BnStat& bs = BnStat{},
+                        const void* acc_src = nullptr, const uint8_t* acc_mask = nullptr) {
   const ConvGeom g = geom(d);
   if ((g.sh > 1 || g.sw > 1) && g.K % KTile<T>::BK == 0)
     return conv_dgrad_phases<T>(g, dy, w_crsk, dx, beta, st, bs);
   const int M = g.N * g.H * g.W, N = g.C, K = g.R * g.S * g.K;
   if (g.K % KTile<T>::BK == 0 && is_pointwise(g))  // dY itself is the [M][K] A operand
     return conv_gemm<T>(PointDgradK<T>{{(const T*)dy, g.K, M, true}}, w_crsk, dx, M, N, K,
-                        beta, st, nullptr, dma_geom_ok(g, true, 32, M), bs);
+                        beta, st, nullptr, dma_geom_ok(g, true, 32, M), bs, acc_src, acc_mask);
   if (g.K % KTile<T>::BK == 0)
     return conv_gemm<T>(DgradK<T, true>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
-                        nullptr, dma_geom_ok(g, true, 32, M), bs);
-  return conv_gemm<T>(DgradK<T, false>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st);
+                        nullptr, dma_geom_ok(g, true, 32, M), bs, acc_src, acc_mask);
+  return conv_gemm<T>(DgradK<T, false>{(const T*)dy, g, M}, w_crsk, dx, M, N, K, beta, st,
+                      nullptr, false, BnStat{}, acc_src, acc_mask);
 }
 
 struct WgradPlan { int bm, bn, splits, kper; };
@@ -583,6 +588,22 @@ extern "C" int mmdx_conv_dgrad(int dtype, const mmdx_conv_desc* d, const void* d
   if (rc) return rc;
   if (dtype == BF16) return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, beta, (hipStream_t)stream);
   return conv_dgrad_t<float>(d, dy, w_crsk, dx, beta, (hipStream_t)stream);
+}
+
+extern "C" int mmdx_conv_dgrad_accmask(int dtype, const mmdx_conv_desc* d, const void* dy,
+                                       const void* w_crsk, void* dx, const void* acc_src,
+                                       const uint8_t* acc_mask, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_dgrad_accmask: fp16 is the C5 path only");
+  int rc = check_desc(d, dtype == BF16 ? 8 : 4);
+  if (rc) return rc;
+  MMDX_CHECK_ARG(acc_src && acc_mask && d->stride_h == 1 && d->stride_w == 1,
+                 "conv dgrad accmask: needs a stride-1 conv and both accumulation operands");
+  MMDX_CHECK_ARG(((uintptr_t)acc_src & 15) == 0 && ((uintptr_t)dx & 15) == 0,
+                 "conv dgrad accmask: dx / acc_src must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    return conv_dgrad_t<bf16>(d, dy, w_crsk, dx, 0.f, st, BnStat{}, acc_src, acc_mask);
+  return conv_dgrad_t<float>(d, dy, w_crsk, dx, 0.f, st, BnStat{}, acc_src, acc_mask);
 }
 
 extern "C" size_t mmdx_conv_wgrad_workspace_size(int dtype, const mmdx_conv_desc* d) {

@@ -871,9 +871,19 @@ struct EpiStore {
   OutT* preact;         // optional copy of the pre-activation value, ld = ldc
   float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [N][tiles_m]
   BnStat bs{};          // optional fused consumer-BN backward statistics (bs.part != null)
+  // optional masked accumulation source (beta must be 0): C = acc + (bit ? acc_src : 0), bit
+  // from a 1-bit ReLU mask ([M][N / VEC] bytes, bit e of byte n / VEC = column n) — the
+  // gradient a residual unit's identity path adds, without materialising it
+  const OutT* acc_src = nullptr;
+  const uint8_t* acc_mask = nullptr;
   static constexpr bool BNSTAT = true;
   static constexpr bool SPLIT = false;
   __device__ __forceinline__ long bn_off(int m, int n) const { return (long)m * ldc + n; }
+  __device__ __forceinline__ float acc_at(int m, int n) const {
+    constexpr int VM = 16 / (int)sizeof(OutT);
+    const unsigned b = acc_mask[(long)m * (N / VM) + n / VM];
+    return (b >> (n % VM)) & 1u ? to_f(acc_src[(long)m * ldc + n]) : 0.f;
+  }
   // Per-column (mean, M2) over this tile's valid rows, from the fp32 accumulators staged in
   // LDS (cst [BM][LDC]) — the BatchNorm statistics of a conv output without re-reading it.
   // Two passes (mean, then squared deviations) over NT/BN row slices, merged with Chan.
@@ -926,6 +936,7 @@ struct EpiStore {
     if (act == ACT_RELU) v = fmaxf(v, 0.f);
     else if (act == ACT_GELU) v = gelu_erf(v);
     if (beta != 0.f) v += beta * to_f(C[off]);
+    if (acc_src) v += acc_at(m, n);
     C[off] = from_f<OutT>(v);
   }
   // Block-uniform: every 8-column chunk can take one 16-B (bf16) / 2x16-B (fp32) store.
@@ -944,7 +955,16 @@ struct EpiStore {
     const long off = (long)m * ldc + n;
     typedef __attribute__((ext_vector_type(8))) OutT O8;
     O8 o;
-    if (beta != 0.f) {
+    if (acc_src) {  // 8 columns = one mask byte (bf16) or two (fp32)
+      const O8 c = *(const O8*)(acc_src + off);
+      constexpr int VM = 16 / (int)sizeof(OutT);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned b = acc_mask[(long)m * (N / VM) + (n + j) / VM];
+        const float a = (b >> ((n + j) % VM)) & 1u ? to_f(c[j]) : 0.f;
+        o[j] = from_f<OutT>(alpha * (j < 4 ? lo[j] : hi[j - 4]) + a);
+      }
+    } else if (beta != 0.f) {
       const O8 c = *(const O8*)(C + off);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1052,7 +1072,7 @@ struct EpiStore {
     if (m >= M) return;
     const long off = (long)m * ldc + n;
     const bool fast = n + 4 <= N && (off & 3) == 0 && !bias && !addend && !preact &&
-                      act == ACT_NONE;
+                      act == ACT_NONE && !acc_src;
     if (!fast) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);

@@ -102,6 +102,10 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                             (const float*)o.l[2], o.i[3], P(o, 7, ext), P(o, 8, ext),
                             (float*)P(o, 9, ext), (float*)P(o, 10, ext), o.f[0],
                             (const uint8_t*)o.l[3], P(o, 11, ext), (size_t)o.l[1], s);
+    case MMDX_OP_CONV_DGRAD_ACCMASK:
+      // p: dy, w_crsk, dx, acc_src, acc_mask
+      return mmdx_conv_dgrad_accmask(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
+                                     P(o, 3, ext), (const uint8_t*)P(o, 4, ext), s);
     case MMDX_OP_CONV_DGRAD_BNSTAT:
       // i: relu; f: beta; p: dy, w_crsk, dx, bn_y, gamma, beta, mean, rstd, stat_part, bn_out
       return mmdx_conv_dgrad_bnstat(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),

@@ -503,7 +503,7 @@ class _Plan:
                 return _Ext(2) if isinstance(x, _Ext) else x
 
             def unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False, stats=None,
-                         feed=None, pool=None):
+                         feed=None, pool=None, no_dres=False, acc=None):
                 """BN(+res)(+ReLU) backward, wgrad (side stream), dgrad.  `stats`: this
                 unit's BN-backward partials, already made by the dgrad that produced `dout`;
                 `feed`: the unit whose dout this unit's dgrad produces (no residual) — its
@@ -513,7 +513,10 @@ class _Plan:
                 rows = d.N * d.P * d.Q
                 dconv = A.new(tuple(u["y"].shape), T, dev)
                 u["dconv"] = dconv
-                dres = A.new(tuple(u["y"].shape), T, dev) if want_res else None
+                # no_dres: the identity path's gradient is added by conv1's dgrad epilogue
+                # from (dout, ReLU bit mask) instead (mmdx_conv_dgrad_accmask)
+                dres = (A.new(tuple(u["y"].shape), T, dev) if want_res and not no_dres
+                        else None)
                 wsn = L.lib().mmdx_bn_workspace_size(rows, K)
                 ws_for(wsn)
                 # ReLU mask: a residual unit's bit mask from the forward (else its output);
@@ -566,7 +569,10 @@ class _Plan:
                     # 0.8 ms/step slower than the separate reduce at C4)
                     tiles = (L.lib().mmdx_conv_dgrad_stat_blocks(dt, d)
                              if feed is not None and beta == 0.0 and feed["relu"] else 0)
-                    if tiles > 0:
+                    if acc is not None:  # dx = dgrad + (ReLU bit ? acc_src : 0)
+                        bw.timed("dgrad", L.OP_CONV_DGRAD_ACCMASK, dtype=dt,
+                                 p=(dconv, u["wc"], dx, acc[0], acc[1]), d=d)
+                    elif tiles > 0:
                         fed = (A.new((d.C, tiles, 2), torch.float32, dev), tiles)
                         fb = feed["bn"]
                         bw.timed("dgrad", L.OP_CONV_DGRAD_BNSTAT, dtype=dt, i=(1,), f=(0.0,),
@@ -613,8 +619,14 @@ class _Plan:
                         self.tail_event = A.bufs[-1]
                 # unit i's dgrad produces the gradient of unit i-1's output (no residual
                 # inside a block): it also makes unit i-1's BN-backward partials
+                # identity block (bf16, 1-bit ReLU mask kept): conv1's dgrad adds the masked
+                # block-output gradient itself, the residual unit writes no d_residual
+                acc_id = (ds_u is None and T == torch.bfloat16 and len(bu) > 1
+                          and bu[-1].get("rmask") is not None)
                 dh, dres, fed = unit_bwd(bu[-1], dx, True, want_res=True,
-                                         feed=bu[-2] if len(bu) > 1 else None)
+                                         feed=bu[-2] if len(bu) > 1 else None,
+                                         no_dres=acc_id)
+                blk_dout = dx
                 for k in range(len(bu) - 2, -1, -1):
                     uu = bu[k]
                     if k == 0 and ds_u is not None and ds_u["d"].stride_h > 1:
@@ -627,6 +639,9 @@ class _Plan:
                         dh, _, _ = unit_bwd(uu, dh, True, stats=fed)
                         bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(1.0,),
                                  p=(ds_u["dconv"], ds_u["wc"], dh), d=ds_u["d"])
+                    elif k == 0 and acc_id:
+                        dh, _, _ = unit_bwd(uu, dh, True, stats=fed,
+                                            acc=(blk_dout, bu[-1]["rmask"]))
                     elif k == 0:
                         # d(block input) = dgrad(conv1) + identity-path grad (beta = 1)
                         if ds_u is not None:

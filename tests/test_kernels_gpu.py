@@ -808,3 +808,33 @@ def test_bn_relu_bitmask(dev, dt):
     torch.cuda.synchronize()
     for u, v, name in zip(outs[0], outs[1], ("dx", "dres", "dgamma", "dbeta")):
         assert torch.equal(u, v), name
+
+
+@pytest.mark.parametrize("cfg", [(2, 256, 14, 14, 64, 1, 1, 0), (4, 64, 56, 56, 64, 1, 1, 0),
+                                 (2, 128, 9, 9, 128, 3, 1, 1)])
+def test_conv_dgrad_accmask(dev, cfg):
+    """dgrad + (ReLU bit ? acc_src : 0) in the epilogue (mmdx_conv_dgrad_accmask) equals a
+    beta-1 dgrad onto the masked source, bit for bit (the identity block's conv1 dgrad)."""
+    dt = torch.bfloat16
+    N, C, H, W, K, k, s, p = cfg
+    g = torch.Generator().manual_seed(sum(cfg))
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, H, W)
+    dc = L.dtype_code(dt)
+    wm = (torch.randn(K, C, k, k, generator=g) * 0.1).to(dev)
+    wk = torch.empty(K, k, k, C, dtype=dt, device=dev)
+    wc = torch.empty(C, k, k, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", dc, d, C, wm.data_ptr(), wk.data_ptr(), wc.data_ptr(),
+           L.stream())
+    dy = torch.randn(N, H, W, K, generator=g).to(dev, dt)
+    src = torch.randn(N, H, W, C, generator=g).to(dev, dt)
+    pos = torch.rand(N, H, W, C, generator=g) > 0.5
+    bits = (pos.view(-1, C // 8, 8).to(torch.int32) << torch.arange(8, dtype=torch.int32)).sum(-1)
+    mask = bits.to(torch.uint8).to(dev)
+    ref = torch.where(pos.to(dev), src, torch.zeros_like(src))
+    L.call("mmdx_conv_dgrad", dc, d, dy.data_ptr(), wc.data_ptr(), ref.data_ptr(), 1.0,
+           L.stream())
+    got = torch.empty_like(src)
+    L.call("mmdx_conv_dgrad_accmask", dc, d, dy.data_ptr(), wc.data_ptr(), got.data_ptr(),
+           src.data_ptr(), mask.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
