@@ -196,6 +196,14 @@ int mmdx_bn_bwd_ex(int dtype, int train, const void* x, const void* y, const voi
                    const float* stat_part, int stat_blocks, void* dx,
                    void* d_residual, float* dgamma, float* dbeta, float beta_acc,
                    const uint8_t* relu_mask, void* workspace, size_t ws_bytes, void* stream);
+/* BN backward (no ReLU, no residual: a downsample branch's BN) whose upstream gradient is
+ * dy with a 1-bit ReLU mask applied on the fly (dy_mask from mmdx_bn_fwd_ex of the residual
+ * unit whose identity path feeds it) — equals mmdx_bn_bwd on the materialised masked dy. */
+int mmdx_bn_bwd_masked_dy(int dtype, int train, const void* x, const void* dy,
+                          const uint8_t* dy_mask, long rows, int C, const float* gamma,
+                          const float* bn_beta, const float* save_mean,
+                          const float* save_rstd, void* dx, float* dgamma, float* dbeta,
+                          float beta_acc, void* workspace, size_t ws_bytes, void* stream);
 /* stat_part (optional, [C][stat_blocks] pairs (sum g, sum g*xhat)): the reduction already
  * made by mmdx_conv_dgrad_bnstat in the epilogue that produced dy — the BN backward then
  * skips its own pass over (dy, x).  ReLU units only (with y = the unit's output for a
@@ -237,7 +245,7 @@ enum {
   MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PAIR_INPUT,
   MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI,
   MMDX_OP_CONV_FWD_BNEVAL, MMDX_OP_MAXPOOL_BN_FWD, MMDX_OP_BN_BWD_POOL,
-  MMDX_OP_CONV_DGRAD_ACCMASK
+  MMDX_OP_CONV_DGRAD_ACCMASK, MMDX_OP_BN_BWD_MASKED_DY
 };
 typedef struct {
   int op, dtype, stream;

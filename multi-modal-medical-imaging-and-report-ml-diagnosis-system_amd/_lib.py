@@ -54,7 +54,7 @@ class PlanOp(C.Structure):
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
  OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PAIR_INPUT,
  OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL,
- OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK) = range(1, 25)
+ OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK, OP_BN_BWD_MASKED_DY) = range(1, 26)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -88,6 +88,8 @@ SIGNATURES = {
                              vp, vp, i32, vp, vp, vp, sz, vp]),
     "mmdx_bn_bwd": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp, vp,
                           vp, vp, f32, vp, sz, vp]),
+    "mmdx_bn_bwd_masked_dy": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp,
+                                    f32, vp, sz, vp]),
     "mmdx_bn_bwd_ex": (i32, [i32, i32, vp, vp, vp, i64, i32, vp, vp, vp, vp, i32, vp, i32, vp,
                              vp, vp, vp, f32, vp, vp, sz, vp]),
     "mmdx_bn_bwd_pool": (i32, [i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,

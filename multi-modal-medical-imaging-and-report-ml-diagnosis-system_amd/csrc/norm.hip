@@ -780,6 +780,24 @@ extern "C" int mmdx_bn_bwd_ex(int dtype, int train, const void* x, const void* y
                          d_residual, dgamma, dbeta, beta_acc, ws, ws_bytes, st, mk);
 }
 
+extern "C" int mmdx_bn_bwd_masked_dy(int dtype, int train, const void* x, const void* dy,
+                                     const uint8_t* dy_mask, long rows, int C,
+                                     const float* gamma, const float* bn_beta,
+                                     const float* save_mean, const float* save_rstd, void* dx,
+                                     float* dgamma, float* dbeta, float beta_acc, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_bwd_masked_dy: fp16 is the C5 path only");
+  MMDX_CHECK_ARG(rows > 0 && C > 0 && dy && dy_mask, "bn bwd masked dy: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16)
+    return bn_bwd_t<bf16>(train, x, nullptr, MaskedGrad<bf16>{(const bf16*)dy, dy_mask, C}, rows,
+                          C, gamma, bn_beta, save_mean, save_rstd, 0, nullptr, 0, dx, nullptr,
+                          dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+  return bn_bwd_t<float>(train, x, nullptr, MaskedGrad<float>{(const float*)dy, dy_mask, C},
+                         rows, C, gamma, bn_beta, save_mean, save_rstd, 0, nullptr, 0, dx,
+                         nullptr, dgamma, dbeta, beta_acc, ws, ws_bytes, st);
+}
+
 extern "C" int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
                            long rows, int C, const float* gamma, const float* bn_beta,
                            const float* save_mean, const float* save_rstd, int relu,

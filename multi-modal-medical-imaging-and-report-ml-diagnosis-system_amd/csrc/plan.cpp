@@ -102,6 +102,15 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                             (const float*)o.l[2], o.i[3], P(o, 7, ext), P(o, 8, ext),
                             (float*)P(o, 9, ext), (float*)P(o, 10, ext), o.f[0],
                             (const uint8_t*)o.l[3], P(o, 11, ext), (size_t)o.l[1], s);
+    case MMDX_OP_BN_BWD_MASKED_DY:
+      // i: train, C; l: rows, ws_bytes; f: beta_acc
+      // p: x, dy, dy_mask, gamma, beta, mean, rstd, dx, dgamma, dbeta, ws
+      return mmdx_bn_bwd_masked_dy(o.dtype, o.i[0], P(o, 0, ext), P(o, 1, ext),
+                                   (const uint8_t*)P(o, 2, ext), o.l[0], o.i[1],
+                                   (const float*)P(o, 3, ext), (const float*)P(o, 4, ext),
+                                   (const float*)P(o, 5, ext), (const float*)P(o, 6, ext),
+                                   P(o, 7, ext), (float*)P(o, 8, ext), (float*)P(o, 9, ext),
+                                   o.f[0], P(o, 10, ext), (size_t)o.l[1], s);
     case MMDX_OP_CONV_DGRAD_ACCMASK:
       // p: dy, w_crsk, dx, acc_src, acc_mask
       return mmdx_conv_dgrad_accmask(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),

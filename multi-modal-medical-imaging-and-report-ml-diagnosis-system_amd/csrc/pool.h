@@ -80,4 +80,24 @@ struct DenseGrad {
   __device__ __forceinline__ V row(long r, int c) const { return *(const V*)(dy + r * C + c); }
 };
 
+// dy with a 1-bit ReLU mask applied on the fly ([rows][C / VEC] bytes, mmdx_bn_fwd_ex): the
+// gradient that leaves a residual unit through its identity path, read by the downsample
+// BatchNorm's backward without being materialised (mmdx_bn_bwd_masked_dy)
+template <typename T>
+struct MaskedGrad {
+  typedef typename Vec16<T>::type V;
+  static constexpr int VEC = Vec16<T>::N;
+  const T* dy;
+  const uint8_t* mask;
+  int C;
+  __device__ __forceinline__ V row(long r, int c) const {
+    V v = *(const V*)(dy + r * C + c);
+    const unsigned b = mask[r * (C / VEC) + c / VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e)
+      if (!((b >> e) & 1u)) v[e] = from_f<T>(0.f);
+    return v;
+  }
+};
+
 }  // namespace mmdx

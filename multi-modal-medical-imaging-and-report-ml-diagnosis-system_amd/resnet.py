@@ -503,7 +503,7 @@ class _Plan:
                 return _Ext(2) if isinstance(x, _Ext) else x
 
             def unit_bwd(u, dout, want_dx, dx_acc=None, want_res=False, stats=None,
-                         feed=None, pool=None, no_dres=False, acc=None):
+                         feed=None, pool=None, no_dres=False, acc=None, dout_mask=None):
                 """BN(+res)(+ReLU) backward, wgrad (side stream), dgrad.  `stats`: this
                 unit's BN-backward partials, already made by the dgrad that produced `dout`;
                 `feed`: the unit whose dout this unit's dgrad produces (no residual) — its
@@ -524,7 +524,14 @@ class _Plan:
                 rmask = u.get("rmask") if want_res else None
                 out = u["out"] if want_res and rmask is None else None
                 sp, sb = stats if stats is not None else (None, 0)
-                if pool is not None:
+                if dout_mask is not None:
+                    # a downsample BN: its upstream gradient is the residual unit's dout with
+                    # that unit's ReLU bit mask applied on the fly (mmdx_bn_bwd_masked_dy)
+                    bw.add(L.OP_BN_BWD_MASKED_DY, dt, i=(int(train), K), l=(rows, wsn),
+                           f=(0.0,),
+                           p=(u["y"], dout, dout_mask, u["bn"].weight, u["bn"].bias, u["mean"],
+                              u["rstd"], dconv, g(u["bn"].weight), g(u["bn"].bias), _WS))
+                elif pool is not None:
                     # `dout` is the stem pool's OUTPUT gradient: the BN backward gathers
                     # dL/d(pool input) through the pool's argmax itself (mmdx_bn_bwd_pool)
                     am_, (pN, pH, pW, pC, pk, ps_, pp, pP, pQ) = pool
@@ -621,12 +628,16 @@ class _Plan:
                 # inside a block): it also makes unit i-1's BN-backward partials
                 # identity block (bf16, 1-bit ReLU mask kept): conv1's dgrad adds the masked
                 # block-output gradient itself, the residual unit writes no d_residual
-                acc_id = (ds_u is None and T == torch.bfloat16 and len(bu) > 1
-                          and bu[-1].get("rmask") is not None)
+                # (blocks with a downsample: its BN backward reads the same masked gradient)
+                mask_id = (T == torch.bfloat16 and len(bu) > 1
+                           and bu[-1].get("rmask") is not None)
+                acc_id = mask_id and ds_u is None
                 dh, dres, fed = unit_bwd(bu[-1], dx, True, want_res=True,
                                          feed=bu[-2] if len(bu) > 1 else None,
-                                         no_dres=acc_id)
+                                         no_dres=mask_id)
                 blk_dout = dx
+                ds_in = dict(dout_mask=bu[-1]["rmask"]) if mask_id else {}
+                ds_dout = blk_dout if mask_id else dres
                 for k in range(len(bu) - 2, -1, -1):
                     uu = bu[k]
                     if k == 0 and ds_u is not None and ds_u["d"].stride_h > 1:
@@ -635,7 +646,7 @@ class _Plan:
                         # its one output phase (beta 1; the phases no tap reaches are left
                         # alone) — instead of the downsample writing 3/4 zeros first and
                         # conv1 re-reading the whole tensor to accumulate onto it
-                        unit_bwd(ds_u, dres, False)
+                        unit_bwd(ds_u, ds_dout, False, **ds_in)
                         dh, _, _ = unit_bwd(uu, dh, True, stats=fed)
                         bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(1.0,),
                                  p=(ds_u["dconv"], ds_u["wc"], dh), d=ds_u["d"])
@@ -645,7 +656,7 @@ class _Plan:
                     elif k == 0:
                         # d(block input) = dgrad(conv1) + identity-path grad (beta = 1)
                         if ds_u is not None:
-                            dxi, _, _ = unit_bwd(ds_u, dres, True)
+                            dxi, _, _ = unit_bwd(ds_u, ds_dout, True, **ds_in)
                         else:
                             dxi = dres
                         dh, _, _ = unit_bwd(uu, dh, True, dx_acc=dxi, stats=fed)

@@ -838,3 +838,47 @@ def test_conv_dgrad_accmask(dev, cfg):
            src.data_ptr(), mask.data_ptr(), L.stream())
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_bwd_masked_dy(dev, dt):
+    """A downsample BN's backward reading its upstream gradient as dy + 1-bit ReLU mask
+    (mmdx_bn_bwd_masked_dy) equals mmdx_bn_bwd on the materialised masked dy, bit for bit."""
+    g = torch.Generator().manual_seed(9)
+    rows, C = 2500, 128
+    vec = 4 if dt == torch.float32 else 8
+    x = torch.randn(rows, C, generator=g).to(dev, dt)
+    dy = torch.randn(rows, C, generator=g).to(dev, dt)
+    pos = torch.rand(rows, C, generator=g) > 0.4
+    bits = (pos.view(rows, C // vec, vec).to(torch.int32)
+            << torch.arange(vec, dtype=torch.int32)).sum(-1)
+    mask = bits.to(torch.uint8).to(dev)
+    dym = torch.where(pos.to(dev), dy, torch.zeros_like(dy))
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.1).to(dev)
+    dc = L.dtype_code(dt)
+    ws_n = L.lib().mmdx_bn_workspace_size(rows, C)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    mean, rstd = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    y = torch.empty_like(x)
+    L.call("mmdx_bn_fwd", dc, 1, x.data_ptr(), rows, C, None, 0, 0, gam.data_ptr(),
+           bet.data_ptr(), None, None, 0.1, 1e-5, mean.data_ptr(), rstd.data_ptr(), None, 0,
+           y.data_ptr(), ws.data_ptr(), ws_n, L.stream())
+    outs = []
+    for masked in (False, True):
+        dx = torch.empty_like(x)
+        dgm, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        if masked:
+            L.call("mmdx_bn_bwd_masked_dy", dc, 1, x.data_ptr(), dy.data_ptr(), mask.data_ptr(),
+                   rows, C, gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                   dx.data_ptr(), dgm.data_ptr(), dbt.data_ptr(), 0.0, ws.data_ptr(), ws_n,
+                   L.stream())
+        else:
+            L.call("mmdx_bn_bwd", dc, 1, x.data_ptr(), None, dym.data_ptr(), rows, C,
+                   gam.data_ptr(), bet.data_ptr(), mean.data_ptr(), rstd.data_ptr(), 0, None, 0,
+                   dx.data_ptr(), None, dgm.data_ptr(), dbt.data_ptr(), 0.0, ws.data_ptr(), ws_n,
+                   L.stream())
+        outs.append((dx, dgm, dbt))
+    torch.cuda.synchronize()
+    for u, v, name in zip(outs[0], outs[1], ("dx", "dgamma", "dbeta")):
+        assert torch.equal(u, v), name
