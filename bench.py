@@ -271,7 +271,13 @@ class StepTimer:
         return _Ctx()
 
 
-def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd=None):
+def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd=None,
+              scaler=None):
+    """One train step.  `scaler` (mmdx.GradScaler, the fp16 C5 path): the loss
+    is scaled before the backward (TP:1056), the clip coefficient is taken on the unscaled
+    norm and folded with 1/scale into AdamW's gradient scale, an overflow skips the update
+    and backs the scale off (TP:1058-1061; the clip sees true gradients, the order
+    torch.amp documents — the reference's loop clips the scaled ones)."""
     import mmdx
     from mmdx import optim as MO
     from mmdx.schedule import TwoTowerForward, two_tower_backward
@@ -296,14 +302,19 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
         early = None
         if reducer is not None and text_early:
             early = lambda: reducer.launch(list(txt.parameters()) + list(fus.parameters()))
-        two_tower_backward(loss, z_img, z_txt, fus.parameters(),
-                           text_stream=side if side_bwd is None else side_bwd,
+        two_tower_backward(scaler.scale(loss) if scaler is not None else loss, z_img, z_txt,
+                           fus.parameters(), text_stream=side if side_bwd is None else side_bwd,
                            on_text_done=early)
         if reducer is not None:
             reducer.reduce()
-        _, scale = MO.grad_norm(params, 1.0)
-        opt.step(grad_scale=scale)
+        if scaler is not None:
+            step.norm = scaler.clip_and_step(opt, 1.0, unscale_first=True, params=params)
+            scaler.update()
+        else:
+            step.norm, scale = MO.grad_norm(params, 1.0)
+            opt.step(grad_scale=scale)
         return loss
+    step.norm = None
     return step
 
 
@@ -439,7 +450,9 @@ def main():
     early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "0")
     if reducer is not None and early_tail != "0":
         RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
-    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side)
+    # fp16 (C5): loss scaling with GradScaler semantics (TP:1025-1026, 1056-1061)
+    scaler = mmdx.GradScaler() if dtype == torch.float16 else None
+    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler)
     timer = StepTimer()
     if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders
         MF.GEMM_TIMER = timer
@@ -541,6 +554,7 @@ def main():
                    "parallelism": f"dp{world}" + ("-rccl-rehearsal" if dp and world == 1
                                                   else "")},
         "loss": round(float(loss.item()), 5),
+        "loss_scale": scaler.get_scale() if scaler is not None else None,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "host_ms_one_step_idle_device": round(host_one * 1e3, 3),
         "model_tflops": round(total_flops * samples / el / 1e12, 2),

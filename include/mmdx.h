@@ -529,6 +529,29 @@ int mmdx_grad_norm(int nchunks, const mmdx_adamw_tensor* table, float max_norm, 
 int mmdx_scale_grads(int nchunks, const mmdx_adamw_tensor* table, const float* scale,
                      void* stream);
 
+/* Mixed-precision loss scaling: torch.cuda.amp.GradScaler as the fusion loop drives it
+ * (TP:1025-1026 GradScaler(enabled=use_amp), TP:1056 scaler.scale(loss).backward(), TP:1058
+ * clip_grad_norm_, TP:1060-1061 scaler.step / scaler.update).
+ * mmdx_grad_norm_amp: as mmdx_grad_norm over gradients that hold loss_scale[0] * g;
+ * found_inf[0] = 1 if any gradient is inf/NaN; scale[0] = clip coefficient / loss_scale[0],
+ * the clip coefficient taken on the unscaled norm (unscale_first != 0: scaler.unscale_ before
+ * the clip) or on the scaled one (0: the reference's order, clip then scaler.step).
+ * mmdx_adamw_multi_amp: mmdx_adamw_multi that skips the whole step (no update, no step
+ * count) when found_inf[0] != 0 (scaler.step's skip).
+ * mmdx_amp_update_scale: scaler.update() (torch._amp_update_scale_): overflow -> scale *=
+ * backoff_factor, tracker = 0; else every growth_interval clean steps scale *= growth_factor.
+ * mmdx_mul_dev_scalar: out = x * s[0], fp32 (scaler.scale(loss) and its backward). */
+int mmdx_grad_norm_amp(int nchunks, const mmdx_adamw_tensor* table, float max_norm,
+                       const float* loss_scale, int unscale_first, float* norm, float* scale,
+                       float* found_inf, void* workspace, size_t ws_bytes, void* stream);
+int mmdx_adamw_multi_amp(int nchunks, const mmdx_adamw_tensor* table, float beta1, float beta2,
+                         float eps, float* step_dev, const float* grad_scale,
+                         const float* found_inf, void* stream);
+int mmdx_amp_update_scale(float* scale, int* growth_tracker, const float* found_inf,
+                          float growth_factor, float backoff_factor, int growth_interval,
+                          void* stream);
+int mmdx_mul_dev_scalar(const float* x, long n, const float* s, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

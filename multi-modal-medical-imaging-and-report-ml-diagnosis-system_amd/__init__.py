@@ -10,6 +10,7 @@ from .training_pipeline import (  # noqa: F401
     TextEncoderTransformer, get_compute_dtype, image_transfom_into_tensor,
     set_compute_dtype, tokenize_patient_details)
 from .optim import AdamW, clip_grad_norm_  # noqa: F401
+from .amp import GradScaler  # noqa: F401
 from .preprocess import preprocess_batch  # noqa: F401
 
 __version__ = "0.1.0"

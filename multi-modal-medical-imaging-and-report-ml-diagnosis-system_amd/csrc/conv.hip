@@ -2,6 +2,7 @@
 // Replaces every nn.Conv2d of the torchvision ResNet trunk that ImageEncoderCNN wraps
 // (training_pipeline.py:178-183, run through _backbone_forward_grad TP:285-289).
 #include <algorithm>
+#include <cstdlib>
 
 #include "igemm.h"
 #include "../../include/mmdx.h"
@@ -278,12 +279,35 @@ static bool is_pointwise(const ConvGeom& g) {
 // C4 step: 256 and 384 tie, 640 is 1.5 % slower
 constexpr long kNarrowBelow = 384;
 
+// 8-wave 256 x 128 tiles (one 512-thread block per CU, three 48 KB operand stages): for the
+// k-major conv GEMMs with N >= 128 and at least this many tiles (MMDX_CONV8_MIN; 0 = off)
+static long conv8_min_tiles() {
+  const char* e = getenv("MMDX_CONV8_MIN");  // read per launch: tests / A-B runs switch it
+  return e ? atol(e) : 160L;
+}
+
+template <class SA, class SB, class Epi>
+static bool try_conv8(const SA& sa, const SB& sb, const Epi& epi, int M, int N, int K,
+                      hipStream_t st) {
+  const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
+  const long lim = conv8_min_tiles();
+  if (lim <= 0 || N < 128 || tiles < lim || K < 128) return false;
+  hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaK<256, SA, 64, 8>, DmaK<128, SB, 64, 8>, Epi,
+                                       3, bf16, 512, 4, 2>),
+                     dim3((unsigned)tiles, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+  return true;
+}
+
 template <typename T, class SA, class Epi>
 static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int N, int K,
                          hipStream_t st, bool dma_ok) {
   DenseK<T> sb{(const T*)w, K, N, true};
   if constexpr (DmaOk<SA>::value) {
     if (dma_ok) {
+      if (try_conv8(sa, sb, epi, M, N, K, st)) {
+        MMDX_LAUNCH_CHECK();
+        return 0;
+      }
       // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
       const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
       if (N <= 64 || tiles128 < kNarrowBelow)
@@ -380,6 +404,10 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       if constexpr (sizeof(T) == 2) {
         if (dma_geom_ok(g, false, 32, M)) {
           const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+          if (try_conv8(sa, sb, epi, M, N, K, st)) {
+            MMDX_LAUNCH_CHECK();
+            continue;
+          }
           if (N <= 64 || tiles128 < kNarrowBelow)
             rc = launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
           else

@@ -830,9 +830,12 @@ __device__ __forceinline__ void bst_store8(const Epi& e, int m, int n, f32x4 lo,
 
 // Merge the per-thread column sums of the vec8 epilogue loop (threads with equal
 // threadIdx % C8 own the same 8 columns) and store the tile's partials.
-template <int BN, int NW>
+// SLABS > 1 (256-row tiles): the partial slots stay per 128 rows (what the consumer's
+// stat_blocks counts); the sums are additive, so the tile's sums go to its first slot and its
+// other slots inside the GEMM's M rows get zeros.
+template <int BN, int NW, int SLABS = 1>
 __device__ __forceinline__ void bn_stat_store(const BnStat& b, float* sg, float* sgx, float* red,
-                                              int tm, int tn, int N) {
+                                              int tm, int tn, int N, int M = 0) {
   constexpr int C8 = BN / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -857,7 +860,11 @@ __device__ __forceinline__ void bn_stat_store(const BnStat& b, float* sg, float*
       a += red[(w * BN + col) * 2];
       c += red[(w * BN + col) * 2 + 1];
     }
-    b.part[(long)(tn * BN + col) * b.tiles + b.tile0 + tm] = make_float2(a, c);
+    float2* dst = b.part + (long)(tn * BN + col) * b.tiles + b.tile0 + tm * SLABS;
+    dst[0] = make_float2(a, c);
+#pragma unroll
+    for (int s = 1; s < SLABS; ++s)
+      if ((tm * SLABS + s) * 128 < M) dst[s] = make_float2(0.f, 0.f);
   }
 }
 
@@ -1050,22 +1057,27 @@ struct EpiStore {
     }
     if constexpr (WTM == 128 && BM > 128) return;
     __syncthreads();
-    const int col = threadIdx.x;
-    if (col < BN && tn * BN + col < N) {
+    // the wave rows of each statistics slab (128 rows; the whole tile when BM <= 128) merge
+    constexpr int SLAB = BM > 128 ? 128 : BM, SLABS = BM / SLAB, WPS = WM / SLABS;
+    static_assert(WM % SLABS == 0, "wave rows per statistics slab");
+    const int col = threadIdx.x % BN, slab = threadIdx.x / BN;
+    if (slab < SLABS && tn * BN + col < N) {
       float nn = 0.f, mu = 0.f, mm = 0.f;
 #pragma unroll
-      for (int q = 0; q < WM; ++q) {
-        const float* o = red + (q * BN + col) * 3;
+      for (int qq = 0; qq < WPS; ++qq) {
+        const float* o = red + ((slab * WPS + qq) * BN + col) * 3;
         const float nb = FULL ? (float)WTM : o[0], mb = o[1], m2b = o[2];
         if (nb == 0.f) continue;
         if (nn == 0.f) { nn = nb; mu = mb; mm = m2b; continue; }
-        // full tiles: equal counts, f = nb / (q + 1) nb exactly
-        const float tot = nn + nb, d = mb - mu, f = FULL ? 1.f / (float)(q + 1) : nb / tot;
+        // full tiles: equal counts, f = nb / (qq + 1) nb exactly
+        const float tot = nn + nb, d = mb - mu, f = FULL ? 1.f / (float)(qq + 1) : nb / tot;
         mu += d * f;
         mm += m2b + d * d * nn * f;
         nn = tot;
       }
-      stats[(long)(tn * BN + col) * ((M + BM - 1) / BM) + tm] = make_float2(mu, mm);
+      if (nn > 0.f || SLABS == 1)
+        stats[(long)(tn * BN + col) * ((M + SLAB - 1) / SLAB) + tm * SLABS + slab] =
+            make_float2(mu, mm);
     }
   }
   __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
@@ -1415,11 +1427,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, char* lds, un
 // BK = 64: rows of 128 B (8 chunks), slot = chunk ^ (row & 7), an instruction fills 8 rows.
 // BK = 32: rows of 64 B (4 chunks), slot = chunk ^ ((row >> 1) & 3) (conflict-free for the
 // ds_read_b128 lane groups of a 16-row x 4-chunk fragment read), an instruction fills 16 rows.
-template <int ROWS, class Src, int BK_ = 64>
+template <int ROWS, class Src, int BK_ = 64, int NWV = NT / 64>
 struct DmaK {
   static constexpr int BK = BK_;
   static constexpr bool RMAJOR = false;
-  static constexpr int NW = NT / 64;
+  static constexpr int NW = NWV;                     // waves of the block
   static constexpr int CPR = BK / 8;                 // 16-B chunks per row
   static constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
   static constexpr int INSTR = ROWS / (RPI * NW);    // DMAs per wave per stage
@@ -1488,12 +1500,12 @@ struct DmaK {
 // [64 k][ROWS] bf16, one ROWS*2-byte line per k; a DMA instruction fills 1 KiB = KPI whole
 // k-lines.  Chunk slots are XOR-swizzled per k so the ds_read_b64_tr_b16 fragment reads (8
 // k-lines x 32 B per 32-lane group) hit every bank once.
-template <int ROWS, class Src, int BK_ = 64>
+template <int ROWS, class Src, int BK_ = 64, int NWV = NT / 64>
 struct DmaR {
   static constexpr int BK = BK_;
   static constexpr bool RMAJOR = true;
   static_assert(!Src::STEP || BK == 64, "lane stepping advances one 64-deep K tile");
-  static constexpr int NW = NT / 64;
+  static constexpr int NW = NWV;
   static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
   static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
   static constexpr int INSTR = BK / (KPI * NW); // DMAs per wave per stage
@@ -1557,11 +1569,16 @@ struct DmaR {
 // BK 32 x NS 4-5 keeps two blocks per CU with twice the bytes in flight of BK 64 x NS 2.
 // Epilogue: BatchNorm tile statistics straight from the accumulators (reg_stats), fp32
 // staging through LDS, then 8 consecutive columns per lane -> one 16-B bf16 store.
-template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16>
-__global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
-                                                          typename OB::SrcT sb, Epi epi, int M,
-                                                          int N, int K, int kper) {
-  constexpr int BK = OA::BK, WM = 2, WN = 2;
+// NTH = 512 (8 waves, one block per CU, 256 x 128 tiles, WM x WN = 4 x 2 waves of 64 x 64):
+// half the operand bytes per MFMA of two 128 x 128 blocks and twice the K tiles in flight
+// (NS = 3 stages of 48 KB) for the same LDS.
+template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16,
+          int NTH = NT, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
+                                                           typename OB::SrcT sb, Epi epi, int M,
+                                                           int N, int K, int kper) {
+  constexpr int BK = OA::BK;
+  static_assert(WM * WN * 64 == NTH && OA::NW * 64 == NTH && OB::NW * 64 == NTH, "waves");
   // fragments-first K loop (below): measured on the C4 conv shapes, 5-13 % faster for the
   // R-major (weight-gradient) operands and most 128-wide tiles, mixed on the 128x64 k-major
   // tiles (three blocks per CU there already cover the LDS latency)
@@ -1572,7 +1589,8 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int OP_BYTES = NS * STAGE;
   constexpr int LDC = BN + 4;
-  constexpr int EPI_BYTES = BM * LDC * 4 + 4 * BN * 3 * 4;  // staged tile + reduction scratch
+  constexpr int RED = WM * 3 > (NTH / 64) * 2 ? WM * 3 : (NTH / 64) * 2;  // floats per column
+  constexpr int EPI_BYTES = BM * LDC * 4 + RED * BN * 4;  // staged tile + reduction scratch
   constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
   // DMA instructions one wave issues per K tile (both operands)
   constexpr int PER_TILE = OA::INSTR + OB::INSTR;
@@ -1693,15 +1711,15 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   float* red = cst + BM * LDC;
   // fused consumer-BN backward statistics: the BN input y of this thread's output chunks is
   // loaded now, so its latency overlaps the accumulator staging below
-  constexpr int C8 = BN / 8, ITERS = BM * C8 / NT;
-  static_assert(NT % C8 == 0 && (BM * C8) % NT == 0, "vec8 epilogue geometry");
+  constexpr int C8 = BN / 8, ITERS = BM * C8 / NTH;
+  static_assert(NTH % C8 == 0 && (BM * C8) % NTH == 0, "vec8 epilogue geometry");
   const bool bst = Epi::BNSTAT && epi.bs.part != nullptr && epi.vec8_ok();
   bn_y8 yv[ITERS], ov[ITERS];
   if (bst) {
     const int n = tn * BN + (threadIdx.x % C8) * 8;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-      const int m = tm * BM + (threadIdx.x + it * NT) / C8;
+      const int m = tm * BM + (threadIdx.x + it * NTH) / C8;
       const bool in = m < M && n < N;
       yv[it] = in ? *(const bn_y8*)((const bf16*)epi.bs.y + epi.bn_off(m, n)) : bn_y8{};
       ov[it] = in && epi.bs.out ? *(const bn_y8*)((const bf16*)epi.bs.out + epi.bn_off(m, n))
@@ -1729,7 +1747,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     bn_coef8(epi.bs, tn * BN + col, N, bc);
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-      const int row = (threadIdx.x + it * NT) / C8;
+      const int row = (threadIdx.x + it * NTH) / C8;
       f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
       f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
       const int m = tm * BM + row, n = tn * BN + col;
@@ -1737,11 +1755,11 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
       bst_store8(epi, m, n, lo, hi);
       if (m < M && n < N) bn_acc8<bf16>(yv[it], ov[it], lo, hi, epi.bs, bc, sg, sgx);
     }
-    bn_stat_store<BN, NT / 64>(epi.bs, sg, sgx, red, tm, tn, N);
+    bn_stat_store<BN, NTH / 64, (BM > 128 ? BM / 128 : 1)>(epi.bs, sg, sgx, red, tm, tn, N, M);
   } else if (epi.vec8_ok()) {
     const int col = (threadIdx.x % C8) * 8;
 #pragma unroll 2
-    for (int c = threadIdx.x; c < BM * C8; c += NT) {
+    for (int c = threadIdx.x; c < BM * C8; c += NTH) {
       const int row = c / C8;
       const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
       const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
@@ -1749,7 +1767,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     }
   } else {
     constexpr int C4 = BN / 4;
-    for (int c = threadIdx.x; c < BM * C4; c += NT) {
+    for (int c = threadIdx.x; c < BM * C4; c += NTH) {
       const int row = c / C4, col = (c - row * C4) * 4;
       const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
       epi.apply4(tm * BM + row, tn * BN + col, v);

@@ -11,7 +11,10 @@
 
 namespace mmdx {
 
-__global__ void step_incr_kernel(float* step) { step[0] += 1.f; }
+__global__ void step_incr_kernel(float* step, const float* found_inf) {
+  if (found_inf && found_inf[0] != 0.f) return;  // GradScaler: an overflowed step is skipped
+  step[0] += 1.f;
+}
 
 __device__ __forceinline__ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -29,7 +32,9 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
 __global__ __launch_bounds__(256) void adamw_kernel(const mmdx_adamw_tensor* __restrict__ tab,
                                                     float beta1, float beta2, float eps,
                                                     const float* __restrict__ step,
-                                                    const float* __restrict__ gscale) {
+                                                    const float* __restrict__ gscale,
+                                                    const float* __restrict__ found_inf) {
+  if (found_inf && found_inf[0] != 0.f) return;
   const mmdx_adamw_tensor d = tab[blockIdx.x];
   const double s = (double)step[0];
   const double bc1 = 1.0 - pow((double)beta1, s);
@@ -94,32 +99,102 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const mmdx_adamw_tensor* __r
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
 
+// norm = sqrt(sum of partials); scale = clip coefficient (torch.nn.utils.clip_grad_norm_:
+// min(1, max_norm / (norm + 1e-6))).  AMP form (loss_scale != NULL, torch.amp.GradScaler):
+// the gradients hold loss_scale * g; found_inf = 1 when the sum is inf/NaN; with
+// unscale_first the clip sees the unscaled norm (scaler.unscale_ before the clip), otherwise
+// the scaled one (the reference's order, TP:1056-1060: clip, then scaler.step unscales);
+// scale additionally carries 1/loss_scale, so AdamW's grad_scale does the unscale.
 __global__ __launch_bounds__(256) void norm_finalize_kernel(const float* __restrict__ part, int n,
                                                             float max_norm, float* norm,
-                                                            float* scale) {
+                                                            float* scale,
+                                                            const float* __restrict__ loss_scale,
+                                                            int unscale_first, float* found_inf) {
   __shared__ float red[4];
   float acc = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
   acc = block_sum<256>(acc, red);
   if (threadIdx.x == 0) {
-    const float nrm = sqrtf(acc);
+    float nrm = sqrtf(acc);
+    const float inv = loss_scale ? 1.f / loss_scale[0] : 1.f;
+    if (loss_scale && unscale_first) nrm *= inv;
     norm[0] = nrm;
-    if (scale) scale[0] = max_norm > 0.f ? fminf(1.f, max_norm / (nrm + 1e-6f)) : 1.f;
+    float s = max_norm > 0.f ? fminf(1.f, max_norm / (nrm + 1e-6f)) : 1.f;
+    if (scale) scale[0] = s * inv;
+    if (found_inf) found_inf[0] = isfinite(acc) ? 0.f : 1.f;
   }
+}
+
+// torch._amp_update_scale_: overflow -> scale *= backoff, tracker = 0; otherwise tracker += 1
+// and every `interval` clean steps scale *= growth (kept only while finite).
+__global__ void amp_update_scale_kernel(float* scale, int* tracker, const float* found_inf,
+                                        float growth, float backoff, int interval) {
+  if (found_inf[0] != 0.f) {
+    scale[0] *= backoff;
+    tracker[0] = 0;
+  } else {
+    const int t = tracker[0] + 1;
+    if (t == interval) {
+      const float g = scale[0] * growth;
+      if (isfinite(g)) scale[0] = g;
+      tracker[0] = 0;
+    } else {
+      tracker[0] = t;
+    }
+  }
+}
+
+// out[i] = x[i] * s[0] (fp32; the loss scaling multiply and its backward)
+__global__ void mul_dev_scalar_kernel(const float* __restrict__ x, long n,
+                                      const float* __restrict__ s, float* __restrict__ out) {
+  const float v = s[0];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    out[i] = x[i] * v;
 }
 
 }  // namespace mmdx
 
 using namespace mmdx;
 
+extern "C" int mmdx_adamw_multi_amp(int nchunks, const mmdx_adamw_tensor* table, float beta1,
+                                    float beta2, float eps, float* step_dev,
+                                    const float* grad_scale, const float* found_inf,
+                                    void* stream) {
+  MMDX_CHECK_ARG(nchunks > 0 && table && step_dev, "adamw: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, st, step_dev, found_inf);
+  hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, st, table, beta1, beta2, eps,
+                     (const float*)step_dev, grad_scale, found_inf);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int mmdx_adamw_multi(int nchunks, const mmdx_adamw_tensor* table, float beta1,
                                 float beta2, float eps, float* step_dev,
                                 const float* grad_scale, void* stream) {
-  MMDX_CHECK_ARG(nchunks > 0 && table && step_dev, "adamw: bad args");
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, st, step_dev);
-  hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, st, table, beta1, beta2, eps,
-                     (const float*)step_dev, grad_scale);
+  return mmdx_adamw_multi_amp(nchunks, table, beta1, beta2, eps, step_dev, grad_scale, nullptr,
+                              stream);
+}
+
+extern "C" int mmdx_amp_update_scale(float* scale, int* growth_tracker, const float* found_inf,
+                                     float growth_factor, float backoff_factor,
+                                     int growth_interval, void* stream) {
+  MMDX_CHECK_ARG(scale && growth_tracker && found_inf && growth_interval > 0,
+                 "amp_update_scale: bad args");
+  hipLaunchKernelGGL(amp_update_scale_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, scale,
+                     growth_tracker, found_inf, growth_factor, backoff_factor, growth_interval);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_mul_dev_scalar(const float* x, long n, const float* s, float* out,
+                                   void* stream) {
+  MMDX_CHECK_ARG(x && s && out && n >= 0, "mul_dev_scalar: bad args");
+  if (n == 0) return 0;
+  const int blocks = (int)std::min<long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(mul_dev_scalar_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x,
+                     n, s, out);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -128,18 +203,26 @@ extern "C" size_t mmdx_grad_norm_workspace_size(int nchunks) {
   return (size_t)std::max(nchunks, 1) * sizeof(float);
 }
 
-extern "C" int mmdx_grad_norm(int nchunks, const mmdx_adamw_tensor* table, float max_norm,
-                              float* norm, float* scale, void* ws, size_t ws_bytes,
-                              void* stream) {
+extern "C" int mmdx_grad_norm_amp(int nchunks, const mmdx_adamw_tensor* table, float max_norm,
+                                  const float* loss_scale, int unscale_first, float* norm,
+                                  float* scale, float* found_inf, void* ws, size_t ws_bytes,
+                                  void* stream) {
   MMDX_CHECK_ARG(nchunks > 0 && table && norm, "grad_norm: bad args");
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_grad_norm_workspace_size(nchunks),
                  "grad_norm: workspace");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sumsq_kernel, dim3(nchunks), dim3(256), 0, st, table, (float*)ws);
   hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nchunks,
-                     max_norm, norm, scale);
+                     max_norm, norm, scale, loss_scale, unscale_first, found_inf);
   MMDX_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int mmdx_grad_norm(int nchunks, const mmdx_adamw_tensor* table, float max_norm,
+                              float* norm, float* scale, void* ws, size_t ws_bytes,
+                              void* stream) {
+  return mmdx_grad_norm_amp(nchunks, table, max_norm, nullptr, 0, norm, scale, nullptr, ws,
+                            ws_bytes, stream);
 }
 
 extern "C" int mmdx_scale_grads(int nchunks, const mmdx_adamw_tensor* table, const float* scale,

@@ -153,11 +153,14 @@ class AdamW(torch.optim.Optimizer):
         super().load_state_dict(state_dict)
         self._tables.clear()
         self._step_t = None
-        step = None
-        for st in self.state.values():
-            if "step" in st:
-                step = float(st["step"].item() if torch.is_tensor(st["step"]) else st["step"])
-                break
+        # one device step counter drives every parameter's bias correction: a state whose
+        # per-parameter steps differ (torch.optim.AdamW keeps one each) cannot be represented
+        steps = {float(st["step"].item() if torch.is_tensor(st["step"]) else st["step"])
+                 for st in self.state.values() if "step" in st}
+        if len(steps) > 1:
+            raise ValueError(f"mmdx AdamW keeps one step count for all parameters; the loaded "
+                             f"state has per-parameter steps {sorted(steps)}")
+        step = steps.pop() if steps else None
         if step is not None:
             dev = next((st["exp_avg"].device for st in self.state.values() if "exp_avg" in st),
                        None)
@@ -170,7 +173,11 @@ class AdamW(torch.optim.Optimizer):
                             st[k] = st[k].contiguous()
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: torch.Tensor | None = None):
+    def step(self, closure=None, grad_scale: torch.Tensor | None = None,
+             found_inf: torch.Tensor | None = None):
+        """torch.optim.AdamW.step.  grad_scale (device scalar) multiplies every gradient
+        (clip coefficient, and / or 1/loss_scale); found_inf (device scalar, GradScaler) skips
+        the whole update — step count included — when non-zero."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -191,11 +198,16 @@ class AdamW(torch.optim.Optimizer):
                     raise TypeError("fused AdamW expects dense fp32 params/grads")
                 st = self.state[p]
                 if not st:
+                    if self._step_t is not None:
+                        # torch would start this parameter's own step count at 1; the one
+                        # shared device counter cannot, so refuse rather than mis-correct
+                        raise ValueError(
+                            "mmdx AdamW: a parameter received its first gradient after the "
+                            "optimizer had already stepped; every parameter must get a "
+                            "gradient from the first step on (one shared step count)")
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p,
                                                         memory_format=torch.contiguous_format)
-                    if self._step_t is not None:
-                        st["step"] = self._step_t
                 g = p.grad
                 if not g.is_contiguous():
                     g = p.grad = g.contiguous()
@@ -215,8 +227,8 @@ class AdamW(torch.optim.Optimizer):
                 self.state[p]["step"] = self._step_t
         plan = _plan_for(self._tables, params, ms, vs, lrs, wds, dev)
         plan.upload(grads)
-        call("mmdx_adamw_multi", plan.n, ptr(plan.dev), float(b1), float(b2), float(eps),
-             ptr(self._step_t), ptr(grad_scale), stream())
+        call("mmdx_adamw_multi_amp", plan.n, ptr(plan.dev), float(b1), float(b2), float(eps),
+             ptr(self._step_t), ptr(grad_scale), ptr(found_inf), stream())
         return loss
 
 
@@ -224,8 +236,12 @@ _clip_cache: dict = {}
 
 
 @torch.no_grad()
-def grad_norm(parameters, max_norm: float = 0.0, apply: bool = False):
-    """Return (total_norm, clip_scale) as device scalars; optionally scale grads in place."""
+def grad_norm(parameters, max_norm: float = 0.0, apply: bool = False, loss_scale=None,
+              unscale_first: bool = False, found_inf=None):
+    """Return (total_norm, clip_scale) as device scalars; optionally scale grads in place.
+    With `loss_scale` (device scalar, GradScaler) the gradients hold loss_scale * g:
+    clip_scale also carries 1/loss_scale and `found_inf` (device scalar) is set to 1 when
+    any gradient is inf/NaN (mmdx_grad_norm_amp)."""
     if isinstance(parameters, torch.Tensor):
         parameters = [parameters]
     ps = [p for p in parameters if p.grad is not None]
@@ -239,8 +255,9 @@ def grad_norm(parameters, max_norm: float = 0.0, apply: bool = False):
     scale = torch.empty((), dtype=torch.float32, device=dev)
     ws_n = L.lib().mmdx_grad_norm_workspace_size(tab.n)
     ws = L.workspace(ws_n, dev)
-    call("mmdx_grad_norm", tab.n, ptr(tab.dev), float(max_norm), ptr(norm), ptr(scale),
-         ptr(ws), ws_n, stream())
+    call("mmdx_grad_norm_amp", tab.n, ptr(tab.dev), float(max_norm), ptr(loss_scale),
+         int(bool(unscale_first)), ptr(norm), ptr(scale), ptr(found_inf), ptr(ws), ws_n,
+         stream())
     if apply:
         call("mmdx_scale_grads", tab.n, ptr(tab.dev), ptr(scale), stream())
     return norm, scale

@@ -345,12 +345,19 @@ class T5Head:
         self.maxd = c.relative_attention_max_distance
         self.start = c.decoder_start_token_id if c.decoder_start_token_id is not None else 0
         self.pad = c.pad_token_id if c.pad_token_id is not None else 0
-        self.scale = c.d_model ** -0.5 if getattr(c, "tie_word_embeddings", True) else 1.0
+        # tied (t5-small): lm_head IS shared.weight, logits scaled by d_model^-0.5; untied
+        # (T5 v1.1 style): the separate lm_head.weight, no scale (modeling_t5.py)
+        self.tied = bool(getattr(c, "tie_word_embeddings", True))
+        self.scale = c.d_model ** -0.5 if self.tied else 1.0
         if c.feed_forward_proj != "relu" or c.d_kv != 64:
             raise NotImplementedError("mmdx T5 head: t5-small family (ReLU FFN, d_kv 64)")
 
     def _blocks(self):
         return self.m.decoder.block
+
+    def head_weight(self):
+        """The [V, D] output projection: the shared embedding when tied, else lm_head."""
+        return self.m.shared.weight if self.tied else self.m.lm_head.weight
 
     def hidden(self, dec_ids, enc, T):
         """Decoder hidden states before final_layer_norm: [B, L, D] in T."""
@@ -388,7 +395,7 @@ class T5Head:
         h = self.hidden(decoder_input_ids, enc, T)
         m = self.m
         lab = labels.long().contiguous() if labels is not None else None
-        loss, logits = _HeadFn.apply(h, m.shared.weight, m.decoder.final_layer_norm.weight, lab,
+        loss, logits = _HeadFn.apply(h, self.head_weight(), m.decoder.final_layer_norm.weight, lab,
                                      self.eps, self.p, m.training, self.scale)
         return (loss if labels is not None else None), logits
 
@@ -401,7 +408,7 @@ class T5Head:
         m = self.m
         last = h[:, -1, :].contiguous()
         hf, _ = _rms(last, m.decoder.final_layer_norm.weight, self.eps)
-        wc = F.cast(m.shared.weight, T)
+        wc = F.cast(self.head_weight(), T)
         V = wc.shape[0]
         logits = torch.empty((R, V), dtype=torch.float32, device=h.device)
         _mm(hf, wc, R, V, D, logits, alpha=self.scale)

@@ -25,6 +25,9 @@ from .optim import AdamW
 from .resnet import ResNetTrunk
 from .vit import VitTrunk
 
+HOPS_PROJECT_NAME = "medical_ml_project"   # TP:60-62 (names kept; the services are local)
+HOPS_FEATURE_GROUP_NAME = "cxr_features"
+VERSION = 1
 IMG_SIZE = 224  # TP:65
 TEXT_ENCODER_MODEl_NAME = "bert-base-uncased"  # TP:66 (name kept verbatim)
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
@@ -53,6 +56,52 @@ def get_compute_dtype() -> torch.dtype:
 def BCEWithLogitsLoss():
     """`torch.nn.BCEWithLogitsLoss()` (mean reduction) on the mmdx kernel (TP:843, 1015)."""
     return F.bce_with_logits
+
+
+# =====================================================================================
+# Feature store / S3 / registry surface (TP:72-103, 122-152, 650-804, 808-1127): the same
+# names over the local stand-ins of mmdx.registry (the cloud services are out of scope).
+# =====================================================================================
+from .registry import (get_image_from_s3, load_features_labels_from_feature_store,  # noqa: E402,F401
+                       parse_s3_url)
+
+
+def construct_input_label_pairs_for_image_encoder_dataset(df):  # TP:122-127
+    from .data import construct_input_label_pairs_for_image_encoder_dataset as f
+    return f(df)
+
+
+class CXR_ImageDataset(torch.utils.data.Dataset):
+    """TP:131-152: (image tensor, float32 label vector) pairs; image bytes via
+    get_image_from_s3(bucket, key) — the local S3 mirror."""
+
+    def __init__(self, img_s3_keys_input, bucket, labels=None, image_transform=None):
+        self.img_s3_keys_input = img_s3_keys_input
+        self.bucket = bucket
+        self.labels = labels
+        self.image_transform = image_transform
+
+    def __len__(self):
+        assert len(self.img_s3_keys_input) == len(self.labels)
+        return len(self.img_s3_keys_input)
+
+    def __getitem__(self, i):
+        import io
+        from PIL import Image
+        img = Image.open(io.BytesIO(get_image_from_s3(self.bucket, self.img_s3_keys_input[i])))
+        x = self.image_transform(img)
+        y = torch.tensor(self.labels[i], dtype=torch.float32)
+        return x, y
+
+
+def save_model_to_hopsworks_model_registry(*args, **kwargs):  # TP:650-804
+    from .training_driver import save_model_to_hopsworks_model_registry as f
+    return f(*args, **kwargs)
+
+
+def training_tests(*args, **kwargs):  # TP:808-1127
+    from .training_driver import training_tests as f
+    return f(*args, **kwargs)
 
 
 # =====================================================================================

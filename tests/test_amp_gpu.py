@@ -1,0 +1,128 @@
+"""GPU: mmdx.GradScaler against torch.amp.GradScaler driving torch.optim.AdamW, in the
+reference's order (TP:1056-1061: scale(loss).backward(), clip_grad_norm_(1.0) on the SCALED
+gradients, scaler.step, scaler.update) and in torch's documented order (unscale_ first).
+
+* A forced overflow (one inf gradient) skips the step — parameters, moments and the step
+  count untouched — and halves the scale; growth_interval clean steps double it.
+* Over a sequence of steps with an overflow in the middle, parameters match torch's to
+  rtol 1e-5 / atol 1e-7 (fp32 AdamW arithmetic, different summation orders in the norm).
+* The fused `clip_and_step` equals the unfused clip_grad_norm_ + scaler.step sequence.
+* scaler.scale(loss) and its backward multiply by the scale (mmdx_mul_dev_scalar).
+"""
+import pytest
+import torch
+
+import mmdx
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(64, 33), (33,), (1000,), (7, 5, 3)]
+    return [torch.randn(s, generator=g).to(dev) for s in shapes]
+
+
+def _grads(step, dev, inf_at=None):
+    g = torch.Generator().manual_seed(100 + step)
+    gs = [torch.randn(s, generator=g).to(dev) * 0.3 for s in [(64, 33), (33,), (1000,),
+                                                                (7, 5, 3)]]
+    if inf_at == step:
+        gs[2][17] = float("inf")
+    return gs
+
+
+def _run(dev, mine, order, n_steps=6, inf_at=3, interval=2):
+    ps = [torch.nn.Parameter(t.clone()) for t in _params(dev)]
+    groups = [{"params": ps[:2], "lr": 5e-4}, {"params": ps[2:], "lr": 2e-5}]
+    if mine:
+        opt = mmdx.AdamW(groups, weight_decay=1e-2)
+        sc = mmdx.GradScaler(init_scale=1024.0, growth_interval=interval)
+        clip = mmdx.clip_grad_norm_
+    else:
+        opt = torch.optim.AdamW(groups, weight_decay=1e-2)
+        sc = torch.amp.GradScaler("cuda", init_scale=1024.0, growth_interval=interval)
+        clip = torch.nn.utils.clip_grad_norm_
+    scales = []
+    for step in range(n_steps):
+        # scale a unit "loss" to create the scaler's state, then plant scaled gradients
+        s = sc.scale(torch.ones((), device=dev)).item()
+        for p, g in zip(ps, _grads(step, dev, inf_at)):
+            p.grad = (g * s).contiguous()
+        if order == "reference":
+            clip(ps, 1.0)
+            sc.step(opt)
+        elif order == "unscale_first":
+            sc.unscale_(opt)
+            clip(ps, 1.0)
+            sc.step(opt)
+        elif order == "fused":
+            sc.clip_and_step(opt, 1.0)
+        sc.update()
+        scales.append(sc.get_scale())
+    torch.cuda.synchronize()
+    return [p.detach().cpu() for p in ps], scales, opt
+
+
+@pytest.mark.parametrize("order", ["reference", "unscale_first"])
+def test_gradscaler_matches_torch(dev, order):
+    mine, s_mine, _ = _run(dev, True, order)
+    ref, s_ref, _ = _run(dev, False, order)
+    assert s_mine == s_ref, (s_mine, s_ref)
+    assert s_mine[3] == s_mine[2] / 2           # the overflow step backed off
+    for a, b in zip(mine, ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+
+
+def test_fused_clip_and_step_equals_reference_order(dev):
+    a, sa, _ = _run(dev, True, "reference")
+    b, sb, _ = _run(dev, True, "fused")
+    assert sa == sb
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-6, atol=1e-8)
+
+
+def test_overflow_skips_the_step(dev):
+    ps = [torch.nn.Parameter(t.clone()) for t in _params(dev)]
+    opt = mmdx.AdamW(ps, lr=1e-3)
+    sc = mmdx.GradScaler(init_scale=4096.0, growth_interval=2)
+    s = sc.scale(torch.ones((), device=dev)).item()
+    for p, g in zip(ps, _grads(0, dev)):
+        p.grad = g * s
+    sc.step(opt)
+    sc.update()
+    torch.cuda.synchronize()
+    after1 = [p.detach().clone() for p in ps]
+    st = opt.state[ps[0]]
+    m1 = st["exp_avg"].clone()
+    assert float(st["step"].item()) == 1.0
+    for p, g in zip(ps, _grads(1, dev, inf_at=1)):
+        p.grad = g * s
+    sc.step(opt)
+    sc.update()
+    torch.cuda.synchronize()
+    assert sc.get_scale() == 2048.0
+    assert float(sc.found_inf.item()) == 1.0
+    assert float(st["step"].item()) == 1.0     # no step counted
+    assert torch.equal(st["exp_avg"], m1)
+    for p, a in zip(ps, after1):
+        assert torch.equal(p.detach(), a)        # no update
+    for k in (2, 3):
+        for p, g in zip(ps, _grads(k, dev)):
+            p.grad = g * sc.get_scale()
+        sc.step(opt)
+        sc.update()
+    torch.cuda.synchronize()
+    assert sc.get_scale() == 4096.0             # grew back after growth_interval clean steps
+    assert float(st["step"].item()) == 3.0
+
+
+def test_scale_forward_backward(dev):
+    sc = mmdx.GradScaler(init_scale=256.0)
+    x = torch.tensor(0.75, device=dev, requires_grad=True)
+    y = sc.scale(x)
+    y.backward()
+    torch.cuda.synchronize()
+    assert y.item() == 192.0 and x.grad.item() == 256.0
+    off = mmdx.GradScaler(enabled=False)
+    assert off.scale(x) is x

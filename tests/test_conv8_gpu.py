@@ -1,0 +1,109 @@
+"""GPU: the 8-wave 256 x 128 conv kernel (igemm_dma_kernel<256, 128, ..., 512 threads>,
+three operand stages) against the 4-wave 128-row kernels, switched by MMDX_CONV8_MIN
+(0 = off, 1 = every eligible launch).
+
+Both kernels accumulate every output over the same K tiles in the same MFMA order, and the
+BatchNorm statistics of a 128-row slab merge the same two 64-row wave slices, so the forward
+output, its per-128-row (mean, M2) slabs, the stride-1 and phase-decomposed dgrads, the masked
+accumulation (accmask) and the eval-mode fused BN forward must be BIT-IDENTICAL.  The fused
+consumer-BN partial sums (dgrad_bnstat) are additive: a 256-row tile puts its sums in its
+first 128-row slot and zeros in the second, so the per-channel totals must agree to 1e-5
+(summation order only).  Ragged M (not a multiple of 256) and strided convs included.
+"""
+import pytest
+import torch
+
+from mmdx import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # N, C, H, W, K, k, s, p
+    (4, 128, 28, 28, 128, 3, 1, 1),
+    (3, 256, 14, 14, 512, 1, 1, 0),
+    (2, 128, 15, 15, 256, 3, 2, 1),
+    (2, 256, 14, 14, 1024, 1, 2, 0),
+    (8, 64, 28, 28, 128, 3, 1, 1),
+]
+
+
+def _run_all(dev, cfg, mode, monkeypatch):
+    monkeypatch.setenv("MMDX_CONV8_MIN", mode)
+    N, C, H, W, K, k, s, p = cfg
+    dt = torch.bfloat16
+    dc = 1
+    P, Q = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    d = L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q)
+    g = torch.Generator().manual_seed(sum(cfg))
+    w = (torch.randn(K, C, k, k, generator=g) * 0.05).to(dev)
+    wk = torch.empty(K, k, k, C, dtype=dt, device=dev)
+    wc = torch.empty(C, k, k, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", dc, d, C, w.data_ptr(), wk.data_ptr(), wc.data_ptr(),
+           L.stream())
+    x = torch.randn(N, H, W, C, generator=g).to(dev, dt)
+    dy = torch.randn(N, P, Q, K, generator=g).to(dev, dt)
+    out = {}
+    y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
+    part = torch.full((K, nst, 2), float("nan"), device=dev)
+    L.call("mmdx_conv_fwd", dc, d, x.data_ptr(), wk.data_ptr(), y.data_ptr(), part.data_ptr(),
+           L.stream())
+    out["y"], out["stats"] = y, part
+    gam = (torch.rand(K, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(K, generator=g) * 0.1).to(dev)
+    rm = (torch.randn(K, generator=g) * 0.1).to(dev)
+    rv = (torch.rand(K, generator=g) + 0.5).to(dev)
+    res = torch.randn(N, P, Q, K, generator=g).to(dev, dt)
+    ye = torch.empty_like(y)
+    L.call("mmdx_conv_fwd_bn_eval", dc, d, x.data_ptr(), wk.data_ptr(), ye.data_ptr(),
+           gam.data_ptr(), bet.data_ptr(), rm.data_ptr(), rv.data_ptr(), 1e-5, res.data_ptr(), 1,
+           L.stream())
+    out["eval"] = ye
+    dx0 = torch.randn(N, H, W, C, generator=g).to(dev, dt)
+    dx = dx0.clone()
+    L.call("mmdx_conv_dgrad", dc, d, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), 0.0,
+           L.stream())
+    out["dgrad"] = dx
+    if s == 1:
+        dxb = dx0.clone()
+        L.call("mmdx_conv_dgrad", dc, d, dy.data_ptr(), wc.data_ptr(), dxb.data_ptr(), 1.0,
+               L.stream())
+        out["dgrad_beta"] = dxb
+        pos = torch.rand(N, H, W, C, generator=g) > 0.5
+        bits = (pos.view(-1, C // 8, 8).to(torch.int32)
+                << torch.arange(8, dtype=torch.int32)).sum(-1)
+        mask = bits.to(torch.uint8).to(dev)
+        got = torch.empty_like(dx0)
+        L.call("mmdx_conv_dgrad_accmask", dc, d, dy.data_ptr(), wc.data_ptr(), got.data_ptr(),
+               dx0.data_ptr(), mask.data_ptr(), L.stream())
+        out["accmask"] = got
+    tiles = L.lib().mmdx_conv_dgrad_stat_blocks(dc, d)
+    if tiles > 0:
+        yb = torch.randn(N, H, W, C, generator=g).to(dev, dt)
+        gm = (torch.rand(C, generator=g) + 0.5).to(dev)
+        bt = (torch.randn(C, generator=g) * 0.1).to(dev)
+        mu = (torch.randn(C, generator=g) * 0.1).to(dev)
+        rs = (torch.rand(C, generator=g) + 0.5).to(dev)
+        sp = torch.full((C, tiles, 2), float("nan"), device=dev)
+        dxs = torch.empty_like(dx0)
+        L.call("mmdx_conv_dgrad_bnstat", dc, d, dy.data_ptr(), wc.data_ptr(), dxs.data_ptr(),
+               0.0, yb.data_ptr(), None, gm.data_ptr(), bt.data_ptr(), mu.data_ptr(),
+               rs.data_ptr(), 1, sp.data_ptr(), L.stream())
+        out["bnstat_dx"], out["bnstat_part"] = dxs, sp
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("cfg", SHAPES)
+def test_conv8_matches_4wave_kernel(dev, cfg, monkeypatch):
+    a = _run_all(dev, cfg, "0", monkeypatch)
+    b = _run_all(dev, cfg, "1", monkeypatch)
+    for key in a:
+        if key == "bnstat_part":
+            pa, pb = a[key], b[key]
+            assert torch.isfinite(pb).all(), "an unwritten partial slot"
+            ta, tb = pa.double().sum(1), pb.double().sum(1)
+            err = ((ta - tb).abs().max() / ta.abs().max().clamp(min=1e-12)).item()
+            assert err <= 1e-5, (key, err)
+            continue
+        assert torch.isfinite(b[key].float()).all(), key
+        assert torch.equal(a[key], b[key]), key

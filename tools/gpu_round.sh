@@ -17,9 +17,27 @@ step() {  # step <label> <timeout> <cmd...>
   [ $rc -le 1 ] || exit $rc
 }
 export TMPDIR=/tmp
-has tests && step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-has bench && step bench 600 python bench.py --steps "$steps" --warmup 5
+# PT overrides the test selection (e.g. PT="tests/test_amp_gpu.py -x"); TT the per-test limit
+has tests && step tests ${TS:-900} python -u -m pytest ${PT:-tests -m gpu -x} -v -s -rA \
+  --timeout ${TT:-120} --timeout-method thread
+has bench && step bench 600 python bench.py --steps "$steps" --warmup 5 ${BA:-}
+has c5 && step c5 600 python bench.py --config c5 --steps "$steps" --warmup 5 --no-cpu-baseline
+has c2 && step c2 600 python bench.py --config c2 --steps "$steps" --warmup 5 --no-cpu-baseline
+has c3 && step c3 600 python bench.py --config c3 --steps "$steps" --warmup 5 --no-cpu-baseline
 has convb && step convb 600 python tools/conv_bench.py --json "gpurun_out/${tag}_conv_shapes.json"
+# A/B of an env knob (AB_VAR, arms AB_A / AB_B): conv table per arm, then paired benches
+if has convab; then
+  for arm in "$AB_A" "$AB_B"; do
+    step "convab_$arm" 600 env "$AB_VAR=$arm" python tools/conv_bench.py --ops "${AB_OPS:-fwd,dgrad,wgrad}"
+  done
+fi
+if has benchab; then
+  for rep in 1 2; do
+    for arm in "$AB_A" "$AB_B"; do
+      step "benchab_${arm}_$rep" 300 env "$AB_VAR=$arm" python bench.py --steps 30 --warmup 5 --no-cpu-baseline ${BA:-}
+    done
+  done
+fi
 cd /tmp
 has prof && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$tag" \
   -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
