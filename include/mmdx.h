@@ -498,6 +498,23 @@ int mmdx_cross_entropy_bwd(int dtype, const float* logits, const int64_t* target
 int mmdx_log_softmax(const float* logits, long rows, long V, float* out, void* stream);
 /* dx = dy * (y > 0) (T5 DenseReluDense backward from the ReLU output) */
 int mmdx_relu_bwd(int dtype, const void* y, const void* dy, long n, void* dx, void* stream);
+/* One incremental decoder step of T5's causal self-attention over a KV cache (beam search of
+ * report_model.generate, IP:190-196 / TP:613-618): qkv [R][3*H*64] of position `pos`;
+ * caches [R][Lmax][H*64]; key j of row r is read from cache row slots[r*Lmax + j] (the beam's
+ * ancestry, so reordering beams moves no cache data); bias [H][Lmax][Lmax] fp32 relative-
+ * position bias (mmdx_t5_position_bias); out [R][H*64].  The step's K/V are appended at
+ * (row r, pos).  Lmax <= 512. */
+int mmdx_t5_decode_attn(int dtype, const void* qkv, int R, int H, int pos, int Lmax,
+                        void* k_cache, void* v_cache, const int* slots, const float* bias,
+                        void* out, void* stream);
+/* Beam-search candidate step (GenerationMixin._beam_search's topk, IP:190 num_beams): per
+ * batch row b, the k (<= 16) largest log_probs[b*nb + i][v] + run_scores[b*nb + i] over
+ * (i, v), ordered by value desc then flat index i*V + v asc; out_idx = that flat index.
+ * First writes -inf into log_probs at the n_ban (row, token) int pairs of ban_pairs
+ * (no_repeat_ngram_size) and, when eos_ban >= 0, at column eos_ban (min_new_tokens). */
+int mmdx_beam_topk(float* log_probs, int B, int nb, long V, const float* run_scores,
+                   const int* ban_pairs, int n_ban, int eos_ban, int k, float* out_val,
+                   long* out_idx, void* stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.AdamW (decoupled weight decay) over every tensor of every param group in

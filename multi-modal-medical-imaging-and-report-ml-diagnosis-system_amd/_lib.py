@@ -158,6 +158,8 @@ SIGNATURES = {
     "mmdx_cross_entropy_bwd": (i32, [i32, vp, vp, i64, i64, vp, vp, vp, vp, vp]),
     "mmdx_log_softmax": (i32, [vp, i64, i64, vp, vp]),
     "mmdx_relu_bwd": (i32, [i32, vp, vp, i64, vp, vp]),
+    "mmdx_t5_decode_attn": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "mmdx_beam_topk": (i32, [vp, i32, i32, i64, vp, vp, i32, i32, i32, vp, vp, vp]),
     "mmdx_adamw_multi": (i32, [i32, vp, f32, f32, f32, vp, vp, vp]),
     "mmdx_grad_norm_workspace_size": (sz, [i32]),
     "mmdx_grad_norm": (i32, [i32, vp, f32, vp, vp, vp, sz, vp]),

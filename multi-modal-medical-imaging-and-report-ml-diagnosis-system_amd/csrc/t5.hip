@@ -13,6 +13,7 @@
 // Row-wise kernels use one wave per row and 16-B vectors; the cross-attention over K <= 16
 // keys is a per-(row, head) CUDA-core kernel (its FLOPs are negligible next to the GEMMs).
 #include <algorithm>
+#include <climits>
 
 #include "common.h"
 #include "../../include/mmdx.h"
@@ -426,11 +427,181 @@ __global__ void relu_bwd_kernel(const T* __restrict__ y, const T* __restrict__ d
   GRID_STRIDE(i, n) dx[i] = to_f(y[i]) > 0.f ? dy[i] : from_f<T>(0.f);
 }
 
+// One incremental beam-search step of the decoder's causal self-attention with a KV cache
+// (generate, IP:190-196 / TP:613-618; transformers appends each step's K/V to a cache instead
+// of re-running the prefix).  Block (r, h), one wave: the query of position `pos` of row r
+// attends keys 0..pos of head h.  Beam search reorders rows without moving the cache: key j
+// of row r lives in cache row slots[r * Lmax + j]; this step's own K/V (qkv) are used
+// directly for j == pos and appended to the cache at (row r, pos) at the end (nothing reads
+// position pos of the cache in this launch).  Scores are unscaled (T5) plus the relative-
+// position bias[h][pos][j]; lanes own keys for the scores (<= DEC_MAXL / 64 per lane), then
+// dims for P.V.  fp32 math.
+constexpr int DEC_MAXL = 512;
+
+template <typename T>
+__global__ __launch_bounds__(64) void t5_decode_attn_kernel(
+    const T* __restrict__ qkv, int H, int pos, int Lmax, T* __restrict__ kc,
+    T* __restrict__ vc, const int* __restrict__ slots, const float* __restrict__ bias,
+    T* __restrict__ out) {
+  constexpr int NI = DEC_MAXL / 64;
+  const int r = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const long D = (long)H * 64;
+  const T* qrow = qkv + (long)r * 3 * D + h * 64;
+  const T* knew = qrow + D;
+  const T* vnew = qrow + 2 * D;
+  float q[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) q[d] = to_f(qrow[d]);
+  const float* brow = bias + ((long)h * Lmax + pos) * Lmax;
+  const int* srow = slots + (long)r * Lmax;
+  float sc[NI];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int j = lane + 64 * i;
+    sc[i] = -INFINITY;
+    if (j <= pos) {
+      const T* kr = j == pos ? knew : kc + ((long)srow[j] * Lmax + j) * D + h * 64;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) acc += q[d] * to_f(kr[d]);
+      sc[i] = acc + brow[j];
+      mx = fmaxf(mx, sc[i]);
+    }
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    sc[i] = lane + 64 * i <= pos ? __expf(sc[i] - mx) : 0.f;
+    sum += sc[i];
+  }
+  sum = wave_sum(sum);
+  const float inv = 1.f / sum;
+  float o = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int jn = min(64, pos + 1 - 64 * i);
+    for (int jj = 0; jj < jn; ++jj) {
+      const int j = 64 * i + jj;
+      const float pj = __shfl(sc[i], jj, 64);
+      const T* vr = j == pos ? vnew : vc + ((long)srow[j] * Lmax + j) * D + h * 64;
+      o += pj * to_f(vr[lane]);
+    }
+  }
+  out[(long)r * D + h * 64 + lane] = from_f<T>(o * inv);
+  kc[((long)r * Lmax + pos) * D + h * 64 + lane] = knew[lane];
+  vc[((long)r * Lmax + pos) * D + h * 64 + lane] = vnew[lane];
+}
+
+// Beam-search candidate selection (transformers' _beam_search: topk over the nb*V running
+// scores of a batch row): per batch row b (one block), the k largest of
+// lp[b*nb + i][v] + run_sc[b*nb + i] over (i, v), ordered by value descending then by flat
+// index i*V + v ascending (numpy's stable argsort order).  Before the scan the block writes
+// -inf into its rows of lp at the banned (row, token) pairs (no_repeat_ngram_size) and, when
+// eos >= 0, at the EOS column (min_new_tokens) — the logits processors of the step.
+// Each thread keeps a sorted top-KMAX of its strided slice in registers; k rounds of a block
+// arg-max over the threads' heads then pop the winners.
+constexpr int TOPK_MAX = 16;
+
+__device__ __forceinline__ bool beats(float va, long ia, float vb, long ib) {
+  return va > vb || (va == vb && ia < ib);
+}
+
+__global__ __launch_bounds__(256) void beam_topk_kernel(float* __restrict__ lp, int nb, long V,
+                                                        const float* __restrict__ run_sc,
+                                                        const int* __restrict__ ban, int nban,
+                                                        int eos, int k, float* __restrict__ oval,
+                                                        long* __restrict__ oidx) {
+  __shared__ float sv[256];
+  __shared__ long si[256];
+  __shared__ int swin;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long r0 = (long)b * nb;
+  for (int i = tid; i < nban; i += 256) {
+    const long r = ban[2 * i], t = ban[2 * i + 1];
+    if (r >= r0 && r < r0 + nb && t >= 0 && t < V) lp[r * V + t] = -INFINITY;
+  }
+  if (eos >= 0 && eos < V)
+    for (int i = tid; i < nb; i += 256) lp[(r0 + i) * V + eos] = -INFINITY;
+  __syncthreads();
+  float tv[TOPK_MAX];
+  long ti[TOPK_MAX];
+#pragma unroll
+  for (int j = 0; j < TOPK_MAX; ++j) { tv[j] = -INFINITY; ti[j] = LONG_MAX; }
+  const long n = (long)nb * V;
+  for (long e = tid; e < n; e += 256) {
+    const long i = e / V;
+    const float v = lp[r0 * V + e] + run_sc[r0 + i];
+    if (!beats(v, e, tv[TOPK_MAX - 1], ti[TOPK_MAX - 1])) continue;
+    // insertion into the sorted register list (compile-time indices only)
+    float cv = v;
+    long ci = e;
+#pragma unroll
+    for (int j = 0; j < TOPK_MAX; ++j) {
+      if (beats(cv, ci, tv[j], ti[j])) {
+        const float xv = tv[j];
+        const long xi = ti[j];
+        tv[j] = cv; ti[j] = ci;
+        cv = xv; ci = xi;
+      }
+    }
+  }
+  for (int q = 0; q < k; ++q) {
+    sv[tid] = tv[0];
+    si[tid] = ti[0];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w && beats(sv[tid + w], si[tid + w], sv[tid], si[tid])) {
+        sv[tid] = sv[tid + w];
+        si[tid] = si[tid + w];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      oval[(long)b * k + q] = sv[0];
+      oidx[(long)b * k + q] = si[0];
+    }
+    if (ti[0] == si[0]) {  // the winner pops its head (indices are unique)
+#pragma unroll
+      for (int j = 0; j < TOPK_MAX - 1; ++j) { tv[j] = tv[j + 1]; ti[j] = ti[j + 1]; }
+      tv[TOPK_MAX - 1] = -INFINITY;
+      ti[TOPK_MAX - 1] = LONG_MAX;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace mmdx
 
 using namespace mmdx;
 
 #define T5_DISPATCH(dtype, ...) MMDX_DISPATCH(dtype, __VA_ARGS__)
+
+extern "C" int mmdx_beam_topk(float* log_probs, int B, int nb, long V, const float* run_scores,
+                              const int* ban_pairs, int n_ban, int eos_ban, int k,
+                              float* out_val, long* out_idx, void* stream) {
+  MMDX_CHECK_ARG(log_probs && run_scores && out_val && out_idx && B > 0 && nb > 0 && V > 0 &&
+                     k > 0 && k <= TOPK_MAX && k <= (long)nb * V && (n_ban == 0 || ban_pairs),
+                 "beam topk: bad args (k=%d <= %d)", k, TOPK_MAX);
+  hipLaunchKernelGGL(beam_topk_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, log_probs, nb,
+                     V, run_scores, ban_pairs, n_ban, eos_ban, k, out_val, out_idx);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_t5_decode_attn(int dtype, const void* qkv, int R, int H, int pos, int Lmax,
+                                   void* k_cache, void* v_cache, const int* slots,
+                                   const float* bias, void* out, void* stream) {
+  MMDX_CHECK_ARG(qkv && k_cache && v_cache && slots && bias && out && R > 0 && H > 0 &&
+                     Lmax > 0 && Lmax <= DEC_MAXL && pos >= 0 && pos < Lmax,
+                 "t5 decode attention: bad args (pos=%d, Lmax=%d <= %d)", pos, Lmax, DEC_MAXL);
+  T5_DISPATCH(dtype, hipLaunchKernelGGL(t5_decode_attn_kernel<T>, dim3(R, H), dim3(64), 0,
+                                        (hipStream_t)stream, (const T*)qkv, H, pos, Lmax,
+                                        (T*)k_cache, (T*)v_cache, slots, bias, (T*)out));
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int mmdx_rmsnorm_fwd(int dtype, const void* x, long rows, int D, const float* w,
                                 float eps, void* y, float* save_rstd, void* stream) {

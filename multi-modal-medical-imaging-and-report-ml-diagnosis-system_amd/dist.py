@@ -129,7 +129,10 @@ class GradAllReducer:
             by_store.setdefault(_store_key(g), []).append(g)
         loose = []
         for key, gs in by_store.items():
-            flat = _whole_buffer(gs)
+            # a buffer that launch_region already started is the trunk's arena even when
+            # frozen parameters leave gaps in it (their slots are reduced too, unused): the
+            # rest must not also travel through the packed buckets
+            flat = _whole_buffer(gs, allow_gaps=key in self._regions)
             if flat is None:
                 loose += gs
                 continue
@@ -153,8 +156,15 @@ class GradAllReducer:
 
     def finish(self):
         inv = 1.0 / self.world
+        cur = None
         for bucket, flat, work, dest in self._pending:
             work.wait()
+            if flat.is_cuda:
+                # the buffer may have been allocated on another stream (launch() issued from
+                # the text stream): keep the allocator from reusing it before this stream's
+                # reads below have run
+                cur = cur or torch.cuda.current_stream(flat.device)
+                flat.record_stream(cur)
             averaged = self._op(flat) == dist.ReduceOp.AVG
             if flat.dtype != torch.float32:
                 flat = flat.float()
@@ -183,18 +193,19 @@ def _store_key(t):
     return (t.device.type, t.device.index, t.untyped_storage().data_ptr())
 
 
-def _whole_buffer(gs):
+def _whole_buffer(gs, allow_gaps=False):
     """The flat 1-D tensor over the storage `gs` share when they are >= 2 contiguous,
     same-dtype tensors whose sizes add up to the whole storage (views of one arena, disjoint
-    by construction), else None."""
-    if len(gs) < 2:
+    by construction), else None.  allow_gaps: a known arena (launch_region used it) whose
+    views cover only part of it (frozen parameters' slots get no gradient)."""
+    if len(gs) < 2 and not (allow_gaps and gs):
         return None
     g0 = gs[0]
     if any(g.dtype != g0.dtype or not g.is_contiguous() for g in gs):
         return None
     st = g0.untyped_storage()
     n = st.nbytes() // g0.element_size()
-    if sum(g.numel() for g in gs) != n:
+    if sum(g.numel() for g in gs) != n and not allow_gaps:
         return None
     return torch.empty(0, dtype=g0.dtype, device=g0.device).set_(st, 0, (n,), (1,))
 

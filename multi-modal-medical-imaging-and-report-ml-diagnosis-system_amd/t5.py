@@ -332,6 +332,142 @@ def shift_right(labels, start_id=0, pad_id=0):
     return out.masked_fill(out == -100, pad_id)
 
 
+class _DecodeState:
+    """KV-cached incremental decoder of one generate() call (what transformers' generate does
+    with its past_key_values): every decoder weight is cast / concatenated ONCE, the
+    cross-attention K/V of the condition tokens are computed once per block, the relative-
+    position bias is built once for the longest sequence, and each step runs the decoder on
+    ONE new token per running beam, appending its self-attention K/V to per-block caches
+    (mmdx_t5_decode_attn).  The beam's ancestry lives in a slot table (key j of row r is in
+    cache row slots[r, j]), so reordering beams moves no cache data.  The step ends on the
+    device with the logits processors and the candidate top-k (mmdx_beam_topk): only
+    2 * num_beams (score, index) pairs per batch row come back to the host."""
+
+    def __init__(self, head, enc_r, T, Lmax):
+        m = head.m
+        dev = enc_r.device
+        D, H = head.D, head.H
+        R, Kc = enc_r.shape[0], enc_r.shape[1]
+        self.head, self.T, self.dev, self.R, self.Lmax, self.D, self.H = head, T, dev, R, Lmax, D, H
+        self.V = head.head_weight().shape[0]
+        e2 = enc_r.to(T).contiguous().reshape(R * Kc, D)
+        self.Kc = Kc
+        self.blocks = []
+        for blk in head._blocks():
+            sa, ca, ff = blk.layer[0], blk.layer[1], blk.layer[2]
+            at, xt = sa.SelfAttention, ca.EncDecAttention
+            wkv2 = _cat_cast([xt.k.weight, xt.v.weight], T, dev)
+            kv = _mm(e2, wkv2, R * Kc, 2 * D, D, torch.empty((R * Kc, 2 * D), dtype=T, device=dev))
+            self.blocks.append(dict(
+                ln0=sa.layer_norm.weight.detach(), wqkv=_cat_cast([at.q.weight, at.k.weight,
+                                                                   at.v.weight], T, dev),
+                wo=F.cast(at.o.weight, T), ln1=ca.layer_norm.weight.detach(),
+                wq2=F.cast(xt.q.weight, T), kv=kv, wo2=F.cast(xt.o.weight, T),
+                ln2=ff.layer_norm.weight.detach(), wi=F.cast(ff.DenseReluDense.wi.weight, T),
+                wo3=F.cast(ff.DenseReluDense.wo.weight, T),
+                kc=torch.empty((R, Lmax, D), dtype=T, device=dev),
+                vc=torch.empty((R, Lmax, D), dtype=T, device=dev)))
+        self.I = self.blocks[0]["wi"].shape[0]
+        self.lnf = m.decoder.final_layer_norm.weight.detach()
+        self.w_head = F.cast(head.head_weight(), T)
+        self.table = m.shared.weight.detach()
+        rel = head._blocks()[0].layer[0].SelfAttention.relative_attention_bias.weight.detach()
+        self.bias = torch.empty((H, Lmax, Lmax), dtype=torch.float32, device=dev)
+        call("mmdx_t5_position_bias", ptr(rel), H, Lmax, head.nb, head.maxd, ptr(self.bias),
+             stream())
+        # per-step buffers
+        e = lambda *shape, dt=T: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+        self.h, self.n, self.att, self.x2 = e(R, D), e(R, D), e(R, D), e(R, D)
+        self.qkv, self.f = e(R, 3 * D), e(R, self.I)
+        self.logits = e(R, self.V, dt=torch.float32)
+        self.lp = e(R, self.V, dt=torch.float32)
+        # one host -> device upload per step: tokens (int64 [R]), run scores (fp32 [R]), the
+        # slot table (int32 [R, Lmax]) and the banned (row, token) pairs (int32, <= R*Lmax)
+        self.off_sc = 8 * R
+        self.off_slot = self.off_sc + 4 * R
+        self.off_ban = self.off_slot + 4 * R * Lmax
+        self.nbytes = self.off_ban + 8 * R * Lmax
+        self.stage_h = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
+        self.stage_d = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
+        self.out_v = e(1, dt=torch.float32)
+        self.out_i = e(1, dt=torch.int64)
+        self.host_v = self.host_i = None
+
+    def step(self, tokens, pos, slots, run_sc, bans, eos_ban, B, nb, k):
+        """Decoder step at position `pos` for every running beam; returns the top-k
+        (scores, flat indices i*V + v) per batch row as numpy arrays [B, k]."""
+        R, D, H, T, st = self.R, self.D, self.H, self.T, stream()
+        hb = self.stage_h.numpy()
+        hb[:self.off_sc].view(np.int64)[:] = tokens
+        hb[self.off_sc:self.off_slot].view(np.float32)[:] = run_sc
+        hb[self.off_slot:self.off_ban].view(np.int32)[:] = slots.reshape(-1)
+        nban = len(bans)
+        if nban:
+            hb[self.off_ban:self.off_ban + 8 * nban].view(np.int32)[:] = bans.reshape(-1)
+        nup = self.off_ban + 8 * nban
+        self.stage_d[:nup].copy_(self.stage_h[:nup], non_blocking=True)
+        toks = self.stage_d[:self.off_sc].view(torch.int64)
+        sc = self.stage_d[self.off_sc:self.off_slot].view(torch.float32)
+        sl = self.stage_d[self.off_slot:self.off_ban].view(torch.int32)
+        ban = self.stage_d[self.off_ban:].view(torch.int32)
+        hd = self.head
+        h, n, att, qkv = self.h, self.n, self.att, self.qkv
+        dc = L.dtype_code(T)
+        call("mmdx_embed_gather", dc, ptr(toks), R, D, ptr(self.table), ptr(h), st)
+        for b in self.blocks:
+            call("mmdx_rmsnorm_fwd", dc, ptr(h), R, D, ptr(b["ln0"]), float(hd.eps), ptr(n),
+                 None, st)
+            _mm(n, b["wqkv"], R, 3 * D, D, qkv)
+            call("mmdx_t5_decode_attn", dc, ptr(qkv), R, H, int(pos), self.Lmax, ptr(b["kc"]),
+                 ptr(b["vc"]), ptr(sl), ptr(self.bias), ptr(att), st)
+            _mm(att, b["wo"], R, D, D, h, beta=1.0)                    # h += attn out
+            call("mmdx_rmsnorm_fwd", dc, ptr(h), R, D, ptr(b["ln1"]), float(hd.eps), ptr(n),
+                 None, st)
+            _mm(n, b["wq2"], R, D, D, att)
+            call("mmdx_xattn_fwd", dc, ptr(att), D, ptr(b["kv"]), R, 1, self.Kc, H, 1.0, 0.0, 0,
+                 None, ptr(self.x2), None, st)
+            _mm(self.x2, b["wo2"], R, D, D, h, beta=1.0)             # h += cross-attn out
+            call("mmdx_rmsnorm_fwd", dc, ptr(h), R, D, ptr(b["ln2"]), float(hd.eps), ptr(n),
+                 None, st)
+            _mm(n, b["wi"], R, self.I, D, self.f, act=L.ACT_RELU)
+            _mm(self.f, b["wo3"], R, D, self.I, h, beta=1.0)          # h += FFN out
+        call("mmdx_rmsnorm_fwd", dc, ptr(h), R, D, ptr(self.lnf), float(hd.eps), ptr(n), None,
+             st)
+        _mm(n, self.w_head, R, self.V, D, self.logits, alpha=hd.scale)
+        call("mmdx_log_softmax", ptr(self.logits), R, self.V, ptr(self.lp), st)
+        if self.out_v.numel() != B * k:
+            self.out_v = torch.empty(B * k, dtype=torch.float32, device=self.dev)
+            self.out_i = torch.empty(B * k, dtype=torch.int64, device=self.dev)
+            self.host_v = torch.empty(B * k, dtype=torch.float32, pin_memory=True)
+            self.host_i = torch.empty(B * k, dtype=torch.int64, pin_memory=True)
+        call("mmdx_beam_topk", ptr(self.lp), B, nb, self.V, ptr(sc), ptr(ban), nban,
+             int(eos_ban), k, ptr(self.out_v), ptr(self.out_i), st)
+        self.host_v.copy_(self.out_v, non_blocking=True)
+        self.host_i.copy_(self.out_i, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return (self.host_v.numpy().reshape(B, k).copy(), self.host_i.numpy().reshape(B, k).copy())
+
+
+def _ngram_bans(hist, ngram):
+    """NoRepeatNGramLogitsProcessor for every row of hist [R, cur]: (row, token) pairs that
+    would complete an n-gram already in the row (vectorised; same pairs as the loop)."""
+    R, cur = hist.shape
+    if ngram <= 0 or cur + 1 < ngram:
+        return np.zeros((0, 2), dtype=np.int32)
+    w = ngram - 1
+    nwin = cur - ngram + 1
+    if nwin <= 0:
+        return np.zeros((0, 2), dtype=np.int32)
+    if w == 0:
+        rr = np.repeat(np.arange(R), cur)
+        return np.stack([rr, hist.reshape(-1)], 1).astype(np.int32)
+    prev = hist[:, cur - w:]
+    win = np.lib.stride_tricks.sliding_window_view(hist[:, :cur - 1], w, axis=1)[:, :nwin]
+    match = (win == prev[:, None, :]).all(axis=2)
+    rr, ss = np.nonzero(match)
+    return np.stack([rr, hist[rr, ss + w]], 1).astype(np.int32)
+
+
 class T5Head:
     """Runs `model` (a transformers T5ForConditionalGeneration) decoder-only on mmdx kernels."""
 
@@ -402,7 +538,9 @@ class T5Head:
     # -------------------------------------------------------------------------- generate
     @torch.no_grad()
     def _last_log_probs(self, seqs, enc, T):
-        """log_softmax of the last position's logits for each running sequence [R, V]."""
+        """log_softmax of the last position's logits for each running sequence [R, V], by
+        re-running the decoder over the whole prefix (no cache): the reference the
+        incremental decoder (_DecodeState) is tested against."""
         h = self.hidden(seqs, enc, T)
         R, Ls, D = h.shape
         m = self.m
@@ -440,6 +578,8 @@ class T5Head:
         max_len = prompt + max_new
         V = self.m.config.vocab_size
         k_keep = max(2, 1 + 1) * nb
+        if k_keep > 16:
+            raise NotImplementedError("mmdx beam search: num_beams <= 8")
         fill = pad or eos
         f32 = np.float32
         run_seq = np.full((B, nb, max_len), fill, dtype=np.int64)
@@ -454,28 +594,23 @@ class T5Head:
         unsat = np.ones((B, 1), dtype=bool)
         top_mask = np.zeros(k_keep, dtype=bool)
         top_mask[:nb] = True
-        enc_r = enc.repeat_interleave(nb, dim=0)
+        R = B * nb
+        dec = _DecodeState(self, enc.repeat_interleave(nb, dim=0), T, max_len)
+        slots = np.zeros((R, max_len), dtype=np.int32)  # cache row of key j for beam r
+        rows = np.arange(R, dtype=np.int32)
+        base = (np.arange(B) * nb)[:, None]
         cur = prompt
         while True:
-            flat = torch.from_numpy(run_seq[:, :, :cur].reshape(B * nb, cur)).to(dev)
-            lp = self._last_log_probs(flat, enc_r, T).cpu().numpy().astype(f32)
-            # logits processors
-            if cur - prompt < min_new:
-                lp[:, eos] = -np.inf
-            if ngram > 0 and cur + 1 >= ngram:
-                hist = run_seq[:, :, :cur].reshape(B * nb, cur)
-                for r in range(B * nb):
-                    row = hist[r]
-                    prev = tuple(row[cur - ngram + 1:cur])
-                    for s in range(cur - ngram + 1):
-                        if tuple(row[s:s + ngram - 1]) == prev:
-                            lp[r, row[s + ngram - 1]] = -np.inf
-            acc = lp.reshape(B, nb, V) + run_sc[:, :, None]
-            acc = acc.reshape(B, nb * V)
-            # top-k (descending; torch.topk order on ties is not pinned — ties are
-            # measure-zero on float scores)
-            idx = np.argsort(-acc, axis=1, kind="stable")[:, :k_keep]
-            tk_lp = np.take_along_axis(acc, idx, axis=1).astype(f32)
+            pos = cur - 1
+            slots[:, pos] = rows                         # this step's K/V: (row r, pos)
+            # logits processors (applied on the device): MinNewTokensLength bans EOS,
+            # NoRepeatNGram bans the tokens that would repeat an n-gram
+            bans = _ngram_bans(run_seq[:, :, :cur].reshape(R, cur), ngram)
+            eos_ban = eos if cur - prompt < min_new else -1
+            # top-k of the running scores + log-probs (descending; torch.topk order on ties
+            # is not pinned — ties are measure-zero on float scores)
+            tk_lp, idx = dec.step(run_seq[:, :, pos].reshape(R), pos, slots,
+                                  run_sc.reshape(R), bans, eos_ban, B, nb, k_keep)
             tk_beam = idx // V
             tk_tok = idx % V
             tk_seq = np.take_along_axis(run_seq, tk_beam[:, :, None], axis=1).copy()
@@ -485,6 +620,8 @@ class T5Head:
             # running beams for the next step
             tk_run = (tk_lp + hits.astype(f32) * f32(-1e9)).astype(f32)
             nxt = np.argsort(-tk_run, axis=1, kind="stable")[:, :nb]
+            parent = np.take_along_axis(tk_beam, nxt, axis=1) + base   # cache rows
+            slots = slots[parent.reshape(R)]
             run_seq = np.take_along_axis(tk_seq, nxt[:, :, None], axis=1)
             run_sc = np.take_along_axis(tk_run, nxt, axis=1)
             run_len = np.take_along_axis(tk_len, nxt, axis=1)

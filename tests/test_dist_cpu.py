@@ -53,6 +53,49 @@ def test_grad_allreduce_mean_gloo():
 SHAPES2 = ((40, 3), (7,), (16,), (5, 5))
 
 
+def _worker_frozen(rank, world, port, out):
+    """A partially frozen trunk: one arena slot has no gradient (requires_grad=False), the
+    early tail (trunk_hook) ran on the arena — the rest is reduced once, in place, and no
+    arena gradient also goes through a packed bucket (it would be reduced twice)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx.dist import GradAllReducer
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in SHAPES2]
+    params[1].requires_grad_(False)
+    g = torch.Generator().manual_seed(400 + rank)
+    flat = torch.randn(127, generator=g)
+    params[0].grad = flat[:120].view(40, 3).detach()
+    params[2].grad = torch.randn(16, generator=g)
+    params[3].grad = torch.randn(5, 5, generator=g)
+    red = GradAllReducer(params, world, bucket_bytes=64)
+    red.trunk_hook(flat, [(60, 120, None)])
+    red.launch()
+    assert all(b is None or id(params[0].grad) not in {id(t) for t in b}
+               for b, *_ in red._pending), "arena gradient in a packed bucket"
+    red.finish()
+    out[rank] = [params[0].grad.clone(), params[2].grad.clone(), params[3].grad.clone()]
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_frozen_trunk_slot_gloo():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_frozen, args=(world, port, out), nprocs=world, join=True)
+    exp = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(400 + r)
+        flat = torch.randn(127, generator=g)
+        exp.append([flat[:120].view(40, 3), torch.randn(16, generator=g),
+                    torch.randn(5, 5, generator=g)])
+    mean = [(a + b) / 2 for a, b in zip(*exp)]
+    for r in range(world):
+        for got, want in zip(out[r], mean):
+            assert torch.allclose(got, want, atol=1e-6)
+
+
 def _worker_flat(rank, world, port, out, region=0, detach=False):
     """Gradients that are views of one flat buffer (the trunk's gradient arena) are reduced
     in place; the others through buckets; a subset is launched early (overlap path).
