@@ -124,7 +124,7 @@ class _LSTMLayerFn(torch.autograd.Function):
         fw = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(T), B, Ls, H)
         fws = L.workspace(fw, dev)
         status = coop_status(dev) if fw else None
-        if status is not None:
+        if status is not None and not torch.cuda.is_current_stream_capturing():
             status.poll()  # an earlier launch that lost a peer fails this step loudly
         call("mmdx_lstm_fwd", L.dtype_code(T), ptr(xg), ptr(whh), B, Ls, H, ptr(hout), ptr(cs),
              ptr(gs), ptr(fws), fw, ptr(status.word) if status else None,

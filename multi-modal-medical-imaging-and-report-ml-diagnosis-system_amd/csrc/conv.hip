@@ -448,11 +448,30 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
 }
 
 struct WgradPlan { int bm, bn, splits, kper; };
+// 8-wave 256 x 128 weight-gradient tiles (one block per CU, three stages) for Kout >= 256
+// and C*R*S >= 128 (MMDX_WGRAD8=0: off); their splits target one block per CU
+static bool wgrad8_on() {
+  const char* e = getenv("MMDX_WGRAD8");
+  return !e || atoi(e) != 0;
+}
+
 static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   WgradPlan p;
   const int BK = dtype == BF16 ? KTile<bf16>::BK : KTile<float>::BK;
   const int M = d->K, N = d->R * d->S * d->C;
   const long K = (long)d->N * d->P * d->Q;
+  if (dtype == BF16 && M >= 256 && N >= 128 && wgrad8_on()) {
+    p.bm = 256;
+    p.bn = 128;
+    const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
+    const long ktiles = (K + BK - 1) / BK;
+    long s = (256L + tiles - 1) / tiles;
+    s = std::max(1L, std::min(s, ktiles / 16L));
+    const long kt_per = (ktiles + s - 1) / s;
+    p.kper = (int)(kt_per * BK);
+    p.splits = (int)((K + p.kper - 1) / p.kper);
+    return p;
+  }
   p.bm = M <= 64 ? 64 : 128;
   p.bn = N <= 64 ? 64 : 128;
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
@@ -474,6 +493,14 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
 template <typename T, class SB>
 static int wgrad_dma(const WgradPlan& p, const DenseR<T>& sa, const SB& sb, const EpiPartial& epi,
                      int M, int N, int K, hipStream_t st) {
+  if (p.bm == 256) {
+    const int nwg = ((M + 255) / 256) * ((N + 127) / 128);
+    hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaR<256, DenseR<T>, 64, 8>, DmaR<128, SB, 64, 8>,
+                                         EpiPartial, 3, bf16, 512, 4, 2>),
+                       dim3(nwg, 1, p.splits), dim3(512), 0, st, sa, sb, epi, M, N, K, p.kper);
+    MMDX_LAUNCH_CHECK();
+    return 0;
+  }
   if (p.bm == 128 && p.bn == 128)
     return launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, SB>>(sa, sb, epi, M, N, K,
                                                                         p.splits, p.kper, st);

@@ -1510,7 +1510,9 @@ struct DmaR {
   static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
   static constexpr int INSTR = BK / (KPI * NW); // DMAs per wave per stage
   static constexpr int BYTES = BK * ROWS * 2;
-  static_assert(ROWS == 64 || ROWS == 128, "R-major DMA tile rows");
+  // ROWS = 256: two LDS bank rows per k-line; the swizzle only permutes the low 4 chunk
+  // bits, so a fragment read's 16 chunk slots stay distinct mod 16 as for 128
+  static_assert(ROWS == 64 || ROWS == 128 || ROWS == 256, "R-major DMA tile rows");
   static_assert(BK == 64 || BK == 32, "K tile depth");
   typedef Src SrcT;
   __amdgpu_buffer_rsrc_t rsrc;
@@ -1518,7 +1520,7 @@ struct DmaR {
   typename Src::Lane ln[INSTR];  // per-lane pixel state of stepping sources (im2col^T)
   int kr[INSTR];
   __device__ static int sw(int k) {
-    return ROWS == 128 ? 2 * ((k & 3) | (((k >> 3) & 1) << 2))
+    return ROWS >= 128 ? 2 * ((k & 3) | (((k >> 3) & 1) << 2))
                        : 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
   }
   __device__ void init(const Src& s, int row0, int lane, int wid, int kbeg) {

@@ -88,3 +88,30 @@ def two_tower_backward(loss: torch.Tensor, z_img: torch.Tensor, z_txt: torch.Ten
         if on_text_done is not None:
             on_text_done()
     main.wait_stream(text_stream)
+
+
+class TowerEmbeddings(torch.nn.Module):
+    """`tower(...)["embeddings"]` as a module returning one tensor (what graph capture of a
+    tower's forward + backward needs): image towers take (images,), text towers
+    (input_ids, attention_mask)."""
+
+    def __init__(self, tower, text):
+        super().__init__()
+        self.tower = tower
+        self.text = text
+
+    def forward(self, *args):
+        if self.text:
+            return self.tower(input_ids=args[0], attention_mask=args[1])["embeddings"]
+        return self.tower(args[0])["embeddings"]
+
+
+def graph_tower(tower, sample_args, text, warmup=3):
+    """Capture one encoder tower's forward and backward as two HIP graphs
+    (torch.cuda.make_graphed_callables): a step then replays each with one host call instead
+    of issuing the tower's ~50 kernel launches per layer from Python.  The graphs read
+    `sample_args` in place (copy a new batch into them), replay on the caller's current
+    stream (the text tower keeps its side stream), and draw fresh dropout masks per replay
+    (the RNG counter advances on the device).  Returns the graphed callable."""
+    mod = TowerEmbeddings(tower, text)
+    return torch.cuda.make_graphed_callables(mod, tuple(sample_args), num_warmup_iters=warmup)
