@@ -77,3 +77,44 @@ def grad_report(mine: dict, ref: dict):
     """{name: (1 - cos, |norm ratio - 1|)} over the tensors both sides have."""
     return {n: (1.0 - cosine(mine[n], ref[n]), abs(norm_ratio(mine[n], ref[n]) - 1.0))
             for n in ref}
+
+
+def beam_score(t5, enc, seq, length_penalty=1.0, eos=1, pad=0):
+    """Length-normalised beam score of one generated sequence under transformers' T5 (the
+    reference's report head, fp64 teacher forcing): sum of log_softmax log-probs of the
+    generated tokens (the logits processors only mask tokens, they do not renormalise)
+    divided by (generated length) ** length_penalty, as GenerationMixin._beam_search scores a
+    finished hypothesis.  seq: 1-D ids starting with the decoder start token; trailing pads
+    after EOS (or after the end of a shorter hypothesis) are ignored."""
+    import copy
+    from transformers.modeling_outputs import BaseModelOutput
+    m = copy.deepcopy(t5).double().eval()
+    ids = [int(t) for t in seq]
+    n = len(ids)
+    if eos in ids[1:]:
+        n = ids.index(eos, 1) + 1
+    else:
+        while n > 1 and ids[n - 1] == pad:
+            n -= 1
+    x = torch.tensor([ids[:n]])
+    with torch.no_grad():
+        out = m(encoder_outputs=BaseModelOutput(last_hidden_state=enc.double()[None]),
+                decoder_input_ids=x[:, :-1])
+        lp = torch.log_softmax(out.logits[0], -1)
+    tot = sum(lp[i, ids[i + 1]].item() for i in range(n - 1))
+    return tot / float(n - 1) ** length_penalty
+
+
+def assert_beams_equivalent(t5, enc, got, want, length_penalty=1.0, rtol=1e-4):
+    """Beam-search outputs agree: identical ids, or — where duplicate beams tie to within an
+    ulp (a random-init T5 repeats tokens, so equal-score hypotheses are common and the
+    tie-break order follows the last bit of fp32 sums) — hypotheses with the same
+    length-normalised score under the reference model."""
+    for b in range(want.shape[0]):
+        g = [int(t) for t in got[b]]
+        w = [int(t) for t in want[b]]
+        if g == w[:len(g)] and all(t == 0 for t in w[len(g):]):
+            continue
+        sg = beam_score(t5, enc[b], g, length_penalty)
+        sw = beam_score(t5, enc[b], w, length_penalty)
+        assert abs(sg - sw) <= rtol * abs(sw), (b, sg, sw, g, w)

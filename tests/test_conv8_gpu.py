@@ -4,8 +4,9 @@ three operand stages) against the 4-wave 128-row kernels, switched by MMDX_CONV8
 
 Both kernels accumulate every output over the same K tiles in the same MFMA order, and the
 BatchNorm statistics of a 128-row slab merge the same two 64-row wave slices, so the forward
-output, its per-128-row (mean, M2) slabs, the stride-1 and phase-decomposed dgrads, the masked
-accumulation (accmask) and the eval-mode fused BN forward must be BIT-IDENTICAL.  The fused
+output, the stride-1 and phase-decomposed dgrads, the masked accumulation (accmask) and the
+eval-mode fused BN forward must be BIT-IDENTICAL; the per-128-row (mean, M2) slabs agree to
+rtol 2e-6 (a tile full in one kernel and ragged in the other merges on another code path).  The fused
 consumer-BN partial sums (dgrad_bnstat) are additive: a 256-row tile puts its sums in its
 first 128-row slot and zeros in the second, so the per-channel totals must agree to 1e-5
 (summation order only).  The weight gradients split K differently (one block per CU vs
@@ -109,6 +110,13 @@ def test_conv8_matches_4wave_kernel(dev, cfg, monkeypatch):
         if key == "wgrad":  # split boundaries differ (one block per CU vs two): fp32 order
             err = ((a[key] - b[key]).abs().max() / (a[key] - 0.25).abs().max()).item()
             assert err <= 1e-4, (key, err)
+            continue
+        if key == "stats":
+            # the same merges, but a tile that is full in one kernel and ragged in the other
+            # (M mod 256 != M mod 128) takes the general-count path there, where the
+            # compiler may contract a multiply-add differently: last-bit differences
+            assert torch.isfinite(b[key]).all(), "an unwritten statistics slab"
+            torch.testing.assert_close(b[key], a[key], rtol=2e-6, atol=1e-6, msg=key)
             continue
         if key == "bnstat_part":
             pa, pb = a[key], b[key]

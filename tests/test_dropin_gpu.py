@@ -14,8 +14,9 @@ drop-in, checked against the CPU oracle.
    - disease probabilities vs the oracle (oracle/ref_cpu.py on the same state dicts):
      max-abs <= 1e-5, the thresholded vector equal wherever |p - 0.5| > 1e-4;
    - report token ids identical to transformers' T5ForConditionalGeneration.generate on the
-     same weights and condition tokens (the T5 embedding scaled x4 in the bundle so
-     next-token margins exceed fp32 reordering noise, as in test_t5_gpu.py).
+     same weights and condition tokens, or of equal length-normalised score where duplicate
+     beams tie to within an ulp (the T5 embedding scaled x4 in the bundle so next-token
+     margins exceed fp32 reordering noise, as in test_t5_gpu.py).
 3. `load_model_from_hopsworks_model_registry` (IP:53-139) on the registry entry + inference.
 """
 import io
@@ -207,7 +208,8 @@ def test_views_bundle_rebuild_and_inference(trained):
                            max_new_tokens=180, min_new_tokens=150, num_beams=4,
                            no_repeat_ngram_size=3, length_penalty=1.1, early_stopping=True,
                            eos_token_id=1, pad_token_id=0)
-    assert out["report_ids"] == want[0].tolist()
+    from parity_util import assert_beams_equivalent
+    assert_beams_equivalent(t5, cond, torch.tensor([out["report_ids"]]), want, 1.1)
 
 
 def test_registry_load_and_inference(trained):
