@@ -41,6 +41,13 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
   }
 }
 
+// 8-wave 256 x 128 tiles (one block per CU, three 48 KB stages) for the unsplit 128 x 128
+// problems with at least this many 256-row tiles; 0 disables (read per launch for A/B runs)
+static long gemm8_min_tiles() {
+  const char* e = getenv("MMDX_GEMM8_MIN");
+  return e ? atol(e) : 160L;
+}
+
 template <typename T, int BM, int BN, bool AK, bool BKm, class Epi>
 static int launch_dense(const void* A, long lda, const void* B, long ldb, const Epi& epi,
                         int M, int N, int K, int splits, int kper, hipStream_t st) {
@@ -63,6 +70,21 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
     const bool oka = va && (AK ? K % 8 == 0 : M % 8 == 0) && abytes < (1L << 31);
     const bool okb = vb && (BKm ? K % 8 == 0 : N % 8 == 0) && bbytes < (1L << 31);
     if (oka && okb) {
+      if constexpr (BM == 128 && BN == 128) {
+        const long t8 = (long)((M + 255) / 256) * ((N + 127) / 128);
+        const long lim = gemm8_min_tiles();
+        if (splits == 1 && lim > 0 && t8 >= lim && K >= 128) {
+          typedef typename std::conditional<AK, DmaK<256, SA, 64, 8>, DmaR<256, SA, 64, 8>>::type
+              OA8;
+          typedef typename std::conditional<BKm, DmaK<128, SB, 64, 8>,
+                                            DmaR<128, SB, 64, 8>>::type OB8;
+          hipLaunchKernelGGL((igemm_dma_kernel<256, 128, OA8, OB8, Epi, 3, T, 512, 4, 2>),
+                             dim3((unsigned)t8, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K,
+                             kper);
+          MMDX_LAUNCH_CHECK();
+          return 0;
+        }
+      }
       typedef typename std::conditional<AK, DmaK<BM, SA>, DmaR<BM, SA>>::type OA;
       typedef typename std::conditional<BKm, DmaK<BN, SB>, DmaR<BN, SB>>::type OB;
       // three operand stages where the grid leaves one block per CU and K is long

@@ -557,21 +557,25 @@ class T5Head:
     @torch.no_grad()
     def generate(self, enc, num_beams=4, max_new_tokens=180, min_new_tokens=0,
                  no_repeat_ngram_size=0, length_penalty=1.0, early_stopping=True,
-                 eos_token_id=1, pad_token_id=0, T=torch.float32, **unused):
+                 eos_token_id=1, pad_token_id=0, T=torch.float32, _stepper=None, **unused):
         """Beam search as transformers' GenerationMixin._beam_search (vectorised form, the
         logits processors MinNewTokensLength + NoRepeatNGram, stopping on max length / EOS),
         restated on the host in float32 over decoder forwards on the GPU.  Returns the best
-        sequence per batch row, [B, 1 + generated] int64 (decoder start token first)."""
+        sequence per batch row, [B, 1 + generated] int64 (decoder start token first).
+
+        `_stepper` (tests only) replaces the device step: a callable (hist [R, cur] int64,
+        pos, slots, run_scores [R], bans, eos_ban) -> (top-k scores [B, k], flat indices
+        [B, k]) with k = 2 * num_beams; the host loop is then checked on its own."""
         was = self.m.training
         self.m.eval()
         try:
             return self._beam(enc, num_beams, max_new_tokens, min_new_tokens,
                               no_repeat_ngram_size, length_penalty, early_stopping,
-                              eos_token_id, pad_token_id, T)
+                              eos_token_id, pad_token_id, T, _stepper)
         finally:
             self.m.train(was)
 
-    def _beam(self, enc, nb, max_new, min_new, ngram, lp_pen, early, eos, pad, T):
+    def _beam(self, enc, nb, max_new, min_new, ngram, lp_pen, early, eos, pad, T, stepper):
         B = enc.shape[0]
         dev = enc.device
         prompt = 1
@@ -595,7 +599,11 @@ class T5Head:
         top_mask = np.zeros(k_keep, dtype=bool)
         top_mask[:nb] = True
         R = B * nb
-        dec = _DecodeState(self, enc.repeat_interleave(nb, dim=0), T, max_len)
+        if stepper is None:
+            dec = _DecodeState(self, enc.repeat_interleave(nb, dim=0), T, max_len)
+
+            def stepper(hist, pos, slots, sc, bans, eos_ban):
+                return dec.step(hist[:, pos], pos, slots, sc, bans, eos_ban, B, nb, k_keep)
         slots = np.zeros((R, max_len), dtype=np.int32)  # cache row of key j for beam r
         rows = np.arange(R, dtype=np.int32)
         base = (np.arange(B) * nb)[:, None]
@@ -605,12 +613,12 @@ class T5Head:
             slots[:, pos] = rows                         # this step's K/V: (row r, pos)
             # logits processors (applied on the device): MinNewTokensLength bans EOS,
             # NoRepeatNGram bans the tokens that would repeat an n-gram
-            bans = _ngram_bans(run_seq[:, :, :cur].reshape(R, cur), ngram)
+            hist = run_seq[:, :, :cur].reshape(R, cur)
+            bans = _ngram_bans(hist, ngram)
             eos_ban = eos if cur - prompt < min_new else -1
             # top-k of the running scores + log-probs (descending; torch.topk order on ties
             # is not pinned — ties are measure-zero on float scores)
-            tk_lp, idx = dec.step(run_seq[:, :, pos].reshape(R), pos, slots,
-                                  run_sc.reshape(R), bans, eos_ban, B, nb, k_keep)
+            tk_lp, idx = stepper(hist, pos, slots, run_sc.reshape(R), bans, eos_ban)
             tk_beam = idx // V
             tk_tok = idx % V
             tk_seq = np.take_along_axis(run_seq, tk_beam[:, :, None], axis=1).copy()

@@ -79,42 +79,85 @@ def grad_report(mine: dict, ref: dict):
             for n in ref}
 
 
-def beam_score(t5, enc, seq, length_penalty=1.0, eos=1, pad=0):
-    """Length-normalised beam score of one generated sequence under transformers' T5 (the
-    reference's report head, fp64 teacher forcing): sum of log_softmax log-probs of the
-    generated tokens (the logits processors only mask tokens, they do not renormalise)
-    divided by (generated length) ** length_penalty, as GenerationMixin._beam_search scores a
-    finished hypothesis.  seq: 1-D ids starting with the decoder start token; trailing pads
-    after EOS (or after the end of a shorter hypothesis) are ignored."""
-    import copy
+def hf_beam_stepper(t5, enc, nb, k):
+    """The reference's beam step as a stepper for T5Head.generate(_stepper=...): transformers'
+    T5 (the reference's report head, IP:190-196) re-run over every running prefix in fp32,
+    log_softmax of the last position, the MinNewTokens / NoRepeatNGram bans the host
+    loop hands over set to -inf, the running beam scores added, torch.topk over the
+    num_beams x vocab candidates of each batch row — GenerationMixin._beam_search's order of
+    operations.  enc: [B, Lc, D] condition tokens; the step runs where `t5` lives (a long
+    search re-runs every prefix: the GPU copy of transformers' model keeps that fast)."""
     from transformers.modeling_outputs import BaseModelOutput
-    m = copy.deepcopy(t5).double().eval()
-    ids = [int(t) for t in seq]
-    n = len(ids)
-    if eos in ids[1:]:
-        n = ids.index(eos, 1) + 1
-    else:
-        while n > 1 and ids[n - 1] == pad:
-            n -= 1
-    x = torch.tensor([ids[:n]])
-    with torch.no_grad():
-        out = m(encoder_outputs=BaseModelOutput(last_hidden_state=enc.double()[None]),
-                decoder_input_ids=x[:, :-1])
-        lp = torch.log_softmax(out.logits[0], -1)
-    tot = sum(lp[i, ids[i + 1]].item() for i in range(n - 1))
-    return tot / float(n - 1) ** length_penalty
+    B = enc.shape[0]
+    mdev = next(t5.parameters()).device
+    enc_r = enc.float().to(mdev).repeat_interleave(nb, dim=0)
+    V = t5.config.vocab_size
+
+    def step(hist, pos, slots, sc, bans, eos_ban):
+        with torch.no_grad():
+            out = t5(encoder_outputs=BaseModelOutput(last_hidden_state=enc_r),
+                     decoder_input_ids=torch.from_numpy(hist).to(mdev))
+            lp = torch.log_softmax(out.logits[:, -1].float(), -1)
+        if eos_ban >= 0:
+            lp[:, eos_ban] = -float("inf")
+        if len(bans):
+            b = torch.from_numpy(bans).long().to(mdev)
+            lp[b[:, 0], b[:, 1]] = -float("inf")
+        s = (lp + torch.from_numpy(sc).float().to(mdev)[:, None]).reshape(B, nb * V)
+        v, i = torch.topk(s, k + 1, dim=1)
+        step.last = v.cpu().numpy()  # k + 1 values: the gap below the k-th candidate
+        return v[:, :k].cpu().numpy().copy(), i[:, :k].cpu().numpy().copy()
+
+    step.vocab = V
+    return step
 
 
-def assert_beams_equivalent(t5, enc, got, want, length_penalty=1.0, rtol=1e-4):
-    """Beam-search outputs agree: identical ids, or — where duplicate beams tie to within an
-    ulp (a random-init T5 repeats tokens, so equal-score hypotheses are common and the
-    tie-break order follows the last bit of fp32 sums) — hypotheses with the same
-    length-normalised score under the reference model."""
-    for b in range(want.shape[0]):
-        g = [int(t) for t in got[b]]
-        w = [int(t) for t in want[b]]
-        if g == w[:len(g)] and all(t == 0 for t in w[len(g):]):
-            continue
-        sg = beam_score(t5, enc[b], g, length_penalty)
-        sw = beam_score(t5, enc[b], w, length_penalty)
-        assert abs(sg - sw) <= rtol * abs(sw), (b, sg, sw, g, w)
+class BeamStepCheck:
+    """Stepper that follows the reference's decisions (hf_beam_stepper) and checks the mmdx
+    device step (t5._DecodeState: KV-cached decoder, device logits processors, top-k) on the
+    same state at every step: the k top candidate scores agree to atol = tol * max(1, |lp|)
+    (lp: the candidate's log-prob, its score minus its parent beam's running score),
+    and the candidate index agrees wherever its score is separated from its neighbours (and
+    from the (k+1)-th score) by more than twice that tolerance.  `min_gap` records the smallest
+    separation seen: if it stays above the tolerance, the search has no near-tie and the
+    end-to-end mmdx output must equal the reference's bit for bit."""
+
+    def __init__(self, ref_step, dec, B, nb, k, tol=1e-4):
+        self.ref, self.dec = ref_step, dec
+        self.B, self.nb, self.k, self.tol = B, nb, k, tol
+        self.min_gap = float("inf")
+        self.ambiguous = 0   # candidates within 2 x tolerance of a neighbour (not compared)
+        self.max_err = 0.0   # largest |mmdx - reference| / max(1, |log-prob|)
+        self.steps = 0
+
+    def __call__(self, hist, pos, slots, sc, bans, eos_ban):
+        import numpy as np
+        rv, ri = self.ref(hist, pos, slots, sc, bans, eos_ban)
+        full = self.ref.last
+        mv, mi = self.dec.step(hist[:, pos], pos, slots, sc, bans, eos_ban, self.B, self.nb,
+                               self.k)
+        fin = np.isfinite(rv)
+        assert np.array_equal(fin, np.isfinite(mv)), (self.steps, rv, mv)
+        # the running score is added identically on both sides: the error scales with the
+        # candidate's own log-prob, not with the accumulated score
+        V = self.ref.vocab
+        par = np.take_along_axis(sc.reshape(self.B, self.nb), ri // V, axis=1)
+        lp = np.where(fin, rv - par, 0.0)
+        atol = self.tol * np.maximum(1.0, np.abs(lp))
+        diff = np.abs(np.where(fin, mv - rv, 0.0))
+        self.max_err = max(self.max_err, float((diff / atol).max()) * self.tol)
+        assert (diff <= atol).all(), (self.steps, float(diff.max()))
+        for b in range(self.B):
+            for j in range(self.k):
+                if not fin[b, j]:
+                    continue
+                up = full[b, j - 1] - full[b, j] if j > 0 else np.inf
+                dn = full[b, j] - full[b, j + 1]
+                gap = min(up, dn)
+                self.min_gap = min(self.min_gap, float(gap))
+                if gap > 2 * atol[b, j]:
+                    assert mi[b, j] == ri[b, j], (self.steps, b, j, mi[b], ri[b])
+                else:
+                    self.ambiguous += 1
+        self.steps += 1
+        return rv, ri

@@ -27,8 +27,11 @@ Dropout p = 0 on both sides (RNG streams cannot match).
   - logits max / rms error <= 1.25x autocast's (+1e-2 of |ref|), loss rel <= 1e-2;
   - per tensor, every conv / linear weight of the image trunk and `image.proj`:
     1 - cos <= 1.5x autocast's for that tensor + 2e-3, norm error <= 2x autocast's + 1e-2;
-  - BatchNorm gamma / beta (noise-dominated for both): norm error <= 2x autocast's + 2x the
-    autocast median over BN tensors + 1e-2;
+  - BatchNorm gamma / beta (noise-dominated for both): as distributions over the BN
+    tensors, the median 1 - cos and norm error <= 1.5x autocast's + 1e-2, the 90th
+    percentile and the maximum <= 2x autocast's + 1e-2;
+  - BERT key biases (exact gradient zero: the softmax cancels them): norm <= 2e-2 (fp32:
+    1e-4) x the same layer's query-bias gradient norm;
   - every other gradient (heads, text towers, ViT / BERT layers): 1 - cos <= max(2e-3,
     2x autocast's), norm error <= max(5e-3, 2x autocast's);
   - the update equals torch AdamW + clip on the step's own (unscaled) gradients (rtol 1e-5);
@@ -239,6 +242,21 @@ def _check_update(m, o32, cfg):
     assert not bad, bad[:10]
 
 
+def _zero_grad_names(names):
+    """BERT's key biases: q . (k + b) shifts every score of a query row by the same q . b,
+    which the softmax cancels, so their exact gradient is zero and both sides hold only
+    rounding noise (cosines between two noise draws mean nothing)."""
+    return [n for n in names if n.endswith("attention.self.key.bias")]
+
+
+def _check_zero_grads(mine, ref32, names, tol):
+    """A zero-gradient tensor must stay at the noise floor: its norm <= tol x the norm of
+    the same layer's query-bias gradient (a nonzero gradient of the same shape)."""
+    for n in names:
+        q = ref32[n.replace("key.bias", "query.bias")].norm().item()
+        assert mine[n].norm().item() <= tol * q, (n, mine[n].norm().item(), q)
+
+
 def _err(got, want):
     d = got - want
     return d.abs().max().item(), (d.norm() / want.norm()).item()
@@ -268,7 +286,9 @@ def test_benched_step_fp32_vs_oracle(dev, cfg):
     assert abs(m["loss"] - o["loss"]) <= 1e-5 * abs(o["loss"])
     assert abs(m["norm"] - o["norm"]) <= 1e-3 * o["norm"]
     assert set(m["grads"]) == set(o["grads"]), set(m["grads"]) ^ set(o["grads"])
-    rep = grad_report(m["grads"], o["grads"])
+    zero = _zero_grad_names(m["grads"])
+    _check_zero_grads(m["grads"], o["grads"], zero, 1e-4)
+    rep = {n: v for n, v in grad_report(m["grads"], o["grads"]).items() if n not in zero}
     worst = max(rep.items(), key=lambda kv: kv[1][0])
     print(f"  grads: median 1-cos {np.median([c for c, _ in rep.values()]):.2e}, worst {worst}")
     bad = [(n, c, r) for n, (c, r) in rep.items() if c > 1e-3 or r > 1.5e-2]
@@ -306,17 +326,25 @@ def test_benched_step_reduced_precision_vs_oracle(dev, cfg):
                                    "image.backbone.conv_proj"))] + ["image.proj.weight"]
     trunk = [n for n in trunk if n in mine] if cfg != "c5" else []
     bn = [n for n in mine if _is_bn(n)]
-    rest = [n for n in mine if n not in trunk and n not in bn]
-    bn_med = float(np.median([auto[n][1] for n in bn])) if bn else 0.0
+    zero = _zero_grad_names(mine)
+    _check_zero_grads(m["grads"], o32["grads"], zero, 2e-2)
+    rest = [n for n in mine if n not in trunk and n not in bn and n not in zero]
     bad = []
     for n in trunk:
         (c, r), (ca, ra) = mine[n], auto[n]
         if c > 1.5 * ca + 2e-3 or r > 2 * ra + 1e-2:
             bad.append(("trunk", n, c, ca, r, ra))
-    for n in bn:
-        (c, r), (ca, ra) = mine[n], auto[n]
-        if r > 2 * ra + 2 * bn_med + 1e-2:
-            bad.append(("bn", n, c, ca, r, ra))
+    if bn:
+        # BN gamma / beta: Σg and Σg·x̂ over N·H·W positions of a random-init train-mode
+        # trunk cancel to a small remainder, so in bf16 these gradients are mostly rounding
+        # noise for any implementation (autocast's own 1 - cos reaches ~1); two noise draws
+        # are compared as distributions over the BN tensors, not tensor by tensor
+        for q, k in ((50, 1.5), (90, 2.0), (100, 2.0)):
+            for j, what in ((0, "1-cos"), (1, "norm err")):
+                vm = float(np.percentile([mine[n][j] for n in bn], q))
+                va = float(np.percentile([auto[n][j] for n in bn], q))
+                if vm > k * va + 1e-2:
+                    bad.append(("bn", f"p{q} {what}", vm, va))
     for n in rest:
         (c, r), (ca, ra) = mine[n], auto[n]
         if c > max(2e-3, 2 * ca) or r > max(5e-3, 2 * ra):

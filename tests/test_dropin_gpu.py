@@ -19,6 +19,7 @@ drop-in, checked against the CPU oracle.
      margins exceed fp32 reordering noise, as in test_t5_gpu.py).
 3. `load_model_from_hopsworks_model_registry` (IP:53-139) on the registry entry + inference.
 """
+import copy
 import io
 import json
 import os
@@ -172,12 +173,6 @@ def test_views_bundle_rebuild_and_inference(trained):
     from mmdx.inference_pipeline import inference
     root, _ = trained
     blob = torch.load(root / "model" / "model_bundle.pt", map_location="cpu", weights_only=True)
-    blob["fusion_state"]["report_model.shared.weight"] = (
-        blob["fusion_state"]["report_model.shared.weight"] * 4.0)
-    for k in ("report_model.encoder.embed_tokens.weight",
-              "report_model.decoder.embed_tokens.weight", "report_model.lm_head.weight"):
-        if k in blob["fusion_state"]:
-            blob["fusion_state"][k] = blob["fusion_state"]["report_model.shared.weight"]
     bundle = _views_rebuild(blob)
     pil = Image.open(os.path.join(GOLD, "e1.jpg")).convert("RGB")
     with open(os.path.join(GOLD, "patient_details.json")) as f:
@@ -191,25 +186,41 @@ def test_views_bundle_rebuild_and_inference(trained):
           f"{len(out['report_ids']) - 1} tokens")
     assert out["model_version"] == 999 and out["report_generated"]
     ref_img, ref_txt, ref_fus, x, tok = _check_probs(out, blob, pil, text)
-    # the report: transformers' T5 on the same weights and condition tokens
+    # the report: transformers' T5 on the same weights and condition tokens.  The device
+    # step is checked along the reference's own 150-180-token search (BeamStepCheck; the
+    # reference step runs on transformers' GPU copy of the model, every prefix re-run), and
+    # the pipeline's ids must equal transformers' generate() when that search had no
+    # candidate within the tolerance of a neighbour.
     from transformers import T5Config, T5ForConditionalGeneration
+    from mmdx.t5 import T5Head, _DecodeState
+    from parity_util import BeamStepCheck, hf_beam_stepper
     cfg = bundle["fusion_model"].report_model.config.to_dict()
     t5 = T5ForConditionalGeneration(T5Config(**cfg))
     t5.load_state_dict({k[len("report_model."):]: v for k, v in blob["fusion_state"].items()
                         if k.startswith("report_model.")})
     t5.eval()
+    kw = dict(max_new_tokens=180, min_new_tokens=150, num_beams=4, no_repeat_ngram_size=3,
+              length_penalty=1.1, early_stopping=True, eos_token_id=1, pad_token_id=0)
     with torch.no_grad():
         z_img = ref_img(x)["embeddings"]
         z_txt = ref_txt(input_ids=tok["input_ids"],
                         attention_mask=tok["attention_mask"])["embeddings"]
         z_fuse = ref_fus(z_img, z_txt)["z_fuse"]
         cond = ref_fus.cond_proj(z_fuse).view(1, 4, 512)
-        want = t5.generate(encoder_outputs=BaseModelOutput(last_hidden_state=cond),
-                           max_new_tokens=180, min_new_tokens=150, num_beams=4,
-                           no_repeat_ngram_size=3, length_penalty=1.1, early_stopping=True,
-                           eos_token_id=1, pad_token_id=0)
-    from parity_util import assert_beams_equivalent
-    assert_beams_equivalent(t5, cond, torch.tensor([out["report_ids"]]), want, 1.1)
+        want = t5.generate(encoder_outputs=BaseModelOutput(last_hidden_state=cond), **kw)
+    t5g = copy.deepcopy(t5).to("cuda")
+    head = T5Head(bundle["fusion_model"].report_model)
+    condd = cond.to("cuda")
+    dec = _DecodeState(head, condd.repeat_interleave(4, dim=0), torch.float32, 181)
+    chk = BeamStepCheck(hf_beam_stepper(t5g, cond, 4, 8), dec, 1, 4, 8, tol=1e-5)
+    replay = head.generate(condd, _stepper=chk, **kw)
+    print(f"steps {chk.steps}, max err {chk.max_err:.2e}, min gap {chk.min_gap:.2e}, "
+          f"near-ties {chk.ambiguous}")
+    assert chk.steps >= 150
+    assert 151 <= len(out["report_ids"]) <= 181 and out["report_ids"][0] == 0
+    if chk.ambiguous == 0:
+        assert torch.equal(replay, want)
+        assert out["report_ids"] == want[0].tolist()
 
 
 def test_registry_load_and_inference(trained):

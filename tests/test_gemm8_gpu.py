@@ -1,0 +1,61 @@
+"""GPU: the 8-wave 256 x 128 dense GEMM tiles (MMDX_GEMM8_MIN, gemm_dense.hip) against the
+4-wave 128 x 128 kernel and a torch fp32 matmul, in the three operand layouts the Linear
+layers use: forward (A, B k-major), input gradient (B R-major), weight gradient (A and B
+R-major), fp16 and bf16, ragged M / N / K.
+
+Both tilings accumulate every output over the same K tiles in the same MFMA order, so the
+results must be BIT-IDENTICAL; the fp32 matmul check bounds the kernel error itself
+(rel 1e-2 of the output scale: 16-bit inputs, fp32 accumulation, 16-bit store).
+"""
+import pytest
+import torch
+
+from mmdx import functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # M, N, K  (>= 256 128x128 tiles, so the plan does not split K)
+    (2056, 2048, 776),
+    (4000, 1032, 200),
+    (2304, 2304, 768),
+]
+
+
+def _gemm(layout, a, b, M, N, K, out_dtype):
+    C = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    if layout == "fwd":  # C = A[M,K] . B[N,K]^T
+        F.gemm(a, K, 1, b, K, 1, M, N, K, C, N)
+    elif layout == "dgrad":  # C = A[M,K] . B[K,N]
+        F.gemm(a, K, 1, b, N, 0, M, N, K, C, N)
+    else:  # "wgrad": C = A[K,M]^T . B[K,N]
+        F.gemm(a, M, 0, b, N, 0, M, N, K, C, N)
+    return C
+
+
+def _operands(layout, M, N, K, dt, dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    ash = (K, M) if layout == "wgrad" else (M, K)
+    bsh = (N, K) if layout == "fwd" else (K, N)
+    a = torch.randn(*ash, generator=g).to(dt)
+    b = torch.randn(*bsh, generator=g).to(dt)
+    ad, bd = a.double(), b.double()
+    ref = ad @ bd.t() if layout == "fwd" else ad @ bd if layout == "dgrad" else ad.t() @ bd
+    return a.to(dev), b.to(dev), ref
+
+
+@pytest.mark.parametrize("layout", ["fwd", "dgrad", "wgrad"])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_gemm8_matches_4wave(dev, layout, dt, shape, monkeypatch):
+    M, N, K = shape
+    a, b, ref = _operands(layout, M, N, K, dt, dev, M + N + K)
+    for out_dtype in (dt, torch.float32):
+        monkeypatch.setenv("MMDX_GEMM8_MIN", "0")
+        c4 = _gemm(layout, a, b, M, N, K, out_dtype)
+        monkeypatch.setenv("MMDX_GEMM8_MIN", "1")
+        c8 = _gemm(layout, a, b, M, N, K, out_dtype)
+        torch.cuda.synchronize()
+        assert torch.isfinite(c8.float()).all()
+        assert torch.equal(c4, c8), (layout, dt, shape, out_dtype)
+        err = (c8.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= 1e-2, (layout, dt, shape, out_dtype, err)

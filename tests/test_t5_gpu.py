@@ -6,7 +6,7 @@ T5Config (t5-small geometry, 2 decoder layers for test time), fp32, dropout 0, t
 weights on both sides.  Tolerances (fp32): kernels rel <= 2e-5 (1e-4 for the 32128-way
 softmax paths); teacher-forced loss rel <= 1e-5, logits max-abs <= 1e-4 * max(1, |ref|),
 every parameter gradient and the condition-token gradient 1 - cos <= 1e-5 with the norm
-ratio within 1e-4; beam search: identical token ids.
+ratio within 1e-4; beam search: the device step along the reference's search (see the test).
 """
 import pytest
 import torch
@@ -180,30 +180,47 @@ def test_t5_teacher_forced_parity(dev):
     assert c <= 1e-5 and r <= 1e-4, (c, r)
 
 
-def test_t5_beam_generate_matches_transformers(dev):
+@pytest.mark.parametrize("eos_x", [1.0, 16.0])
+def test_t5_beam_generate_matches_transformers(dev, eos_x):
     """report_model.generate(encoder_outputs=cond, num_beams=4, no_repeat_ngram_size=3,
-    min_new_tokens, max_new_tokens, length_penalty=1.1, early_stopping=True) (IP:190-196):
-    identical token ids, or where duplicate beams tie to within an ulp, hypotheses of equal
-    length-normalised score under transformers' model (parity_util.assert_beams_equivalent).
-    The embedding is scaled x4 so next-token margins are well above fp32 reordering noise (a
-    random-init T5 is nearly uniform over 32128 tokens)."""
+    min_new_tokens, max_new_tokens, length_penalty=1.1, early_stopping=True) (IP:190-196).
+    (1) The device step (KV-cached decoder, device logits processors, top-k) is checked at
+    every step of the reference's own search (parity_util.BeamStepCheck: top-8 candidate
+    scores to 2e-5 of max(1, |score|), candidate ids wherever the score is separated from its
+    neighbours by more than twice that); the host loop driven by the reference step returns
+    transformers' ids exactly (its CPU test: test_beam_host_cpu.py).  (2) End to end, mmdx
+    generate() returns transformers' ids exactly when no candidate of that search was within
+    the tolerance of a neighbour (a near-tie may legitimately break either way in fp32).
+    eos_x scales the EOS embedding row (tied head) so hypotheses finish mid-search."""
     from transformers.modeling_outputs import BaseModelOutput
-    from mmdx.t5 import T5Head
-    ref = _t5(2, seed=4)
+    from mmdx.t5 import T5Head, _DecodeState
+    from parity_util import BeamStepCheck, hf_beam_stepper
+    ref = _t5(2, seed=4).eval()
     with torch.no_grad():
-        ref.shared.weight.mul_(4.0)
+        ref.shared.weight[1].mul_(eos_x)
     mine = _t5(2, seed=4)
     mine.load_state_dict(ref.state_dict())
     mine.to(dev).eval()
-    ref.eval()
     g = torch.Generator().manual_seed(21)
     enc = torch.randn(2, 4, 512, generator=g)
-    kw = dict(num_beams=4, max_new_tokens=14, min_new_tokens=6, no_repeat_ngram_size=3,
+    nb, max_new = 4, 14
+    kw = dict(num_beams=nb, max_new_tokens=max_new, min_new_tokens=3, no_repeat_ngram_size=3,
               length_penalty=1.1, early_stopping=True, eos_token_id=1, pad_token_id=0)
-    want = ref.generate(encoder_outputs=BaseModelOutput(last_hidden_state=enc), **kw)
-    got = T5Head(mine).generate(enc.to(dev), **kw)
-    from parity_util import assert_beams_equivalent
-    assert_beams_equivalent(ref, enc, got, want, kw["length_penalty"])
+    with torch.no_grad():
+        want = ref.generate(encoder_outputs=BaseModelOutput(last_hidden_state=enc), **kw)
+    head = T5Head(mine)
+    encd = enc.to(dev)
+    dec = _DecodeState(head, encd.repeat_interleave(nb, dim=0), torch.float32, 1 + max_new)
+    chk = BeamStepCheck(hf_beam_stepper(ref, enc, nb, 2 * nb), dec, 2, nb, 2 * nb, tol=2e-5)
+    replay = head.generate(encd, _stepper=chk, **kw)
+    print(f"steps {chk.steps}, max err {chk.max_err:.2e}, min gap {chk.min_gap:.2e}, "
+          f"near-ties {chk.ambiguous}")
+    assert chk.steps >= 4 and torch.equal(replay, want)
+    if eos_x != 1.0:
+        assert (want[:, 1:] == 1).any()
+    got = head.generate(encd, **kw)
+    if chk.ambiguous == 0:
+        assert torch.equal(got.cpu(), want), (got, want)
 
 
 def test_fusion_report_head_plumbing(dev):

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Dense bf16 GEMM throughput of the mmdx MFMA core (mmdx_gemm, both operands k-major),
-next to torch.matmul (hipBLASLt) on the same shapes — a calibration point for the conv core.
-    python tools/gemm_bench.py [--reps 20]
+"""Dense GEMM throughput of the mmdx MFMA core (mmdx_gemm) with the 4-wave 128 x 128 and the
+8-wave 256 x 128 tiles (MMDX_GEMM8_MIN 0 / 1), next to torch.matmul (hipBLASLt) on the same
+shapes: the C5 Linear layers (ViT-B/16 12608 tokens, BERT-base 8192 tokens; forward, input
+gradient, weight gradient) plus square calibration points.
+    python tools/gemm_bench.py [--reps 20] [--dtype f16|bf16]
 """
 import argparse
 import os
@@ -12,8 +14,9 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-SHAPES = [(4096, 4096, 4096), (8192, 8192, 8192), (25088, 256, 2304), (100352, 128, 1152),
-          (6272, 512, 4608), (401408, 64, 576), (25088, 1024, 256)]
+# (M tokens, out features, in features)
+LINEARS = [(12608, 2304, 768), (12608, 768, 768), (12608, 3072, 768), (12608, 768, 3072),
+           (8192, 2304, 768), (8192, 3072, 768), (8192, 768, 3072), (4096, 4096, 4096)]
 
 
 def timeit(fn, reps):
@@ -33,19 +36,40 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dtype", default="f16", choices=["f16", "bf16"])
     a = ap.parse_args()
-    import mmdx
+    import mmdx  # noqa: F401
     from mmdx import functional as F
+    dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     dev = torch.device("cuda", 0)
-    for M, N, K in SHAPES:
-        A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
-        B = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
-        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        ms = timeit(lambda: F.gemm(A, K, 1, B, K, 1, M, N, K, C, N), a.reps)
-        ms_t = timeit(lambda: torch.matmul(A, B.t()), a.reps)
-        fl = 2.0 * M * N * K
-        print(f"{M:7d}x{N:5d}x{K:5d}  mmdx {ms * 1e3:8.1f}us {fl / ms / 1e9:7.1f}TF   "
-              f"hipBLASLt {ms_t * 1e3:8.1f}us {fl / ms_t / 1e9:7.1f}TF", flush=True)
+    tot = {"4w": 0.0, "8w": 0.0, "blas": 0.0}
+    for T, O, I in LINEARS:
+        X = (torch.rand(T, I, device=dev) * 2 - 1).to(dt)
+        W = (torch.rand(O, I, device=dev) * 2 - 1).to(dt)
+        dY = (torch.rand(T, O, device=dev) * 2 - 1).to(dt)
+        cases = {  # name: (M, N, K, mmdx call, torch call)
+            "fwd": (T, O, I, lambda C: F.gemm(X, I, 1, W, I, 1, T, O, I, C, O),
+                    lambda: torch.matmul(X, W.t())),
+            "dgrad": (T, I, O, lambda C: F.gemm(dY, O, 1, W, I, 0, T, I, O, C, I),
+                      lambda: torch.matmul(dY, W)),
+            "wgrad": (O, I, T, lambda C: F.gemm(dY, O, 0, X, I, 0, O, I, T, C, I),
+                      lambda: torch.matmul(dY.t(), X)),
+        }
+        for name, (M, N, K, fn, tfn) in cases.items():
+            C = torch.empty(M, N, dtype=dt if name != "wgrad" else torch.float32, device=dev)
+            res = {}
+            for mode, lim in (("4w", "0"), ("8w", "1")):
+                os.environ["MMDX_GEMM8_MIN"] = lim
+                res[mode] = timeit(lambda: fn(C), a.reps)
+            res["blas"] = timeit(tfn, a.reps)
+            for k in tot:
+                tot[k] += res[k]
+            fl = 2.0 * M * N * K
+            print(f"{name:5s} {M:6d}x{N:5d}x{K:5d}  " + "  ".join(
+                f"{k} {v * 1e3:7.1f}us {fl / v / 1e9:6.1f}TF" for k, v in res.items()),
+                flush=True)
+    print("total ms: " + "  ".join(f"{k} {v:.3f}" for k, v in tot.items()), flush=True)
+    os.environ.pop("MMDX_GEMM8_MIN", None)
 
 
 if __name__ == "__main__":

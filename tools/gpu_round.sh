@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, headline bench, kernel-trace profile, two PMC passes.
 # usage (from the repo root, under gpurun): bash tools/gpu_round.sh <tag> <phases> [steps]
-#   phases: comma list of tests,bench,convb,prof,pmc
+#   phases: comma list of tests,abtest,bench,c5,c2,c3,gemmb,convb,convab,benchab,prof,pmc
 # Every GPU step has its own time limit; the script stops at the first step that faults,
 # aborts or times out (rc > 1), so nothing else touches the GPU after a failure.
 set -u
@@ -20,10 +20,18 @@ export TMPDIR=/tmp
 # PT overrides the test selection (e.g. PT="tests/test_amp_gpu.py -x"); TT the per-test limit
 has tests && step tests ${TS:-900} python -u -m pytest ${PT:-tests -m gpu -x} -v -s -rA \
   --timeout ${TT:-120} --timeout-method thread
+# the test selection PT2 once per arm of an env knob (AB_VAR = AB_A / AB_B)
+if has abtest; then
+  for arm in "$AB_A" "$AB_B"; do
+    step "abtest_$arm" ${TS:-900} env "$AB_VAR=$arm" python -u -m pytest $PT2 -v -s -rA \
+      --timeout ${TT:-120} --timeout-method thread
+  done
+fi
 has bench && step bench 600 python bench.py --steps "$steps" --warmup 5 ${BA:-}
 has c5 && step c5 600 python bench.py --config c5 --steps "$steps" --warmup 5 --no-cpu-baseline
 has c2 && step c2 600 python bench.py --config c2 --steps "$steps" --warmup 5 --no-cpu-baseline
 has c3 && step c3 600 python bench.py --config c3 --steps "$steps" --warmup 5 --no-cpu-baseline
+has gemmb && step gemmb 300 python tools/gemm_bench.py --dtype ${GD:-f16}
 has convb && step convb 600 python tools/conv_bench.py --json "gpurun_out/${tag}_conv_shapes.json"
 # A/B of an env knob (AB_VAR, arms AB_A / AB_B): conv table per arm, then paired benches
 if has convab; then
