@@ -438,7 +438,13 @@ def main():
     x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
     side = torch.cuda.Stream(device=dev, priority=-1)
     from mmdx.dist import GradAllReducer
-    reducer = GradAllReducer(params, world, rehearse=dp) if dp else None
+    # C5's packed buckets (ViT-B/16 + BERT-base: ~800 MB of per-tensor fp32 gradients) travel
+    # in bf16 by default — half the xGMI bytes, the mean taken in fp32 after the cast back
+    # (MMDX_DP_BUCKET_DTYPE=fp32 restores fp32); C2-C4 reduce in fp32
+    bdt = None
+    if vit and os.environ.get("MMDX_DP_BUCKET_DTYPE", "bf16") == "bf16":
+        bdt = torch.bfloat16
+    reducer = GradAllReducer(params, world, rehearse=dp, bucket_dtype=bdt) if dp else None
     # Opt-in: the trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward, each
     # from its own plan event (RCCL: a comm stream waits on the event, no host wait).  Off by
     # default: in the one-rank RCCL rehearsal it costs 0.43 ms/step (15.83 vs 15.40 ms) — the
@@ -570,6 +576,7 @@ def main():
                                                   else "")},
         "loss": round(float(loss.item()), 5),
         "loss_scale": scaler.get_scale() if scaler is not None else None,
+        "dp_bucket_dtype": ("bf16" if bdt is not None else "fp32") if dp else None,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "host_ms_one_step_idle_device": round(host_one * 1e3, 3),
         "model_tflops": round(total_flops * samples / el / 1e12, 2),

@@ -280,10 +280,14 @@ static bool is_pointwise(const ConvGeom& g) {
 constexpr long kNarrowBelow = 384;
 
 // 8-wave 256 x 128 tiles (one 512-thread block per CU, three 48 KB operand stages): for the
-// k-major conv GEMMs with N >= 128 and at least this many tiles (MMDX_CONV8_MIN; 0 = off)
+// k-major conv GEMMs with N >= 128 and at least this many tiles (MMDX_CONV8_MIN; 0 = off).
+// Off by default: at threshold 160 the isolated C4 forward convs took 2.51 vs 2.41 ms and the
+// dgrads 2.22 vs 2.11 ms, the train step 9001 / 8999 vs 9089 / 9059 samples/s (paired in one
+// call, profiles/r03_conv8_ab.txt) — one block per CU leaves no second block to cover a
+// block's barrier waits and epilogue
 static long conv8_min_tiles() {
   const char* e = getenv("MMDX_CONV8_MIN");  // read per launch: tests / A-B runs switch it
-  return e ? atol(e) : 160L;
+  return e ? atol(e) : 0L;
 }
 
 template <class SA, class SB, class Epi>

@@ -42,10 +42,20 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
 }
 
 // 8-wave 256 x 128 tiles (one block per CU, three 48 KB stages) for the unsplit 128 x 128
-// problems with at least this many 256-row tiles; 0 disables (read per launch for A/B runs)
+// problems with at least this many 256-row tiles (read per launch for A/B runs).  Off by
+// default: on every C5 Linear shape and at 4096^3 they ran 2-20 % slower than two 4-wave
+// 128 x 128 blocks per CU (tools/gemm_bench.py, profiles/r03_gemm8_ab.txt)
 static long gemm8_min_tiles() {
   const char* e = getenv("MMDX_GEMM8_MIN");
-  return e ? atol(e) : 160L;
+  return e ? atol(e) : 0L;
+}
+
+// 8-wave 256 x 256 tiles (waves 2 x 4 of 128 x 64, two 64 KB stages, one block per CU: a
+// quarter of the LDS-DMA and half the fragment reads per MFMA of the 64 x 64-per-wave tiles)
+// for unsplit problems with at least this many 256 x 256 tiles; 0 disables
+static long gemm256_min_tiles() {
+  const char* e = getenv("MMDX_GEMM256_MIN");
+  return e ? atol(e) : 0L;
 }
 
 template <typename T, int BM, int BN, bool AK, bool BKm, class Epi>
@@ -71,6 +81,19 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
     const bool okb = vb && (BKm ? K % 8 == 0 : N % 8 == 0) && bbytes < (1L << 31);
     if (oka && okb) {
       if constexpr (BM == 128 && BN == 128) {
+        const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+        const long lim256 = gemm256_min_tiles();
+        if (splits == 1 && lim256 > 0 && t256 >= lim256 && K >= 128) {
+          typedef typename std::conditional<AK, DmaK<256, SA, 64, 8>, DmaR<256, SA, 64, 8>>::type
+              OA8;
+          typedef typename std::conditional<BKm, DmaK<256, SB, 64, 8>,
+                                            DmaR<256, SB, 64, 8>>::type OB8;
+          hipLaunchKernelGGL((igemm_dma_kernel<256, 256, OA8, OB8, Epi, 2, T, 512, 2, 4>),
+                             dim3((unsigned)t256, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K,
+                             kper);
+          MMDX_LAUNCH_CHECK();
+          return 0;
+        }
         const long t8 = (long)((M + 255) / 256) * ((N + 127) / 128);
         const long lim = gemm8_min_tiles();
         if (splits == 1 && lim > 0 && t8 >= lim && K >= 128) {

@@ -1566,6 +1566,31 @@ struct DmaR {
   }
 };
 
+// Stores a staged fp32 tile cst [BM][LDC] (CW columns) at output (m0, n0): 8 consecutive
+// columns per lane -> one 16-B store where the epilogue allows it, else 4-column pieces.
+template <int BM, int CW, int LDC, int NTH, class Epi>
+__device__ __forceinline__ void epilogue_pass(const Epi& epi, const float* cst, int m0, int n0) {
+  if (epi.vec8_ok()) {
+    constexpr int C8 = CW / 8;
+    static_assert(NTH % C8 == 0, "vec8 epilogue geometry");
+    const int col = (threadIdx.x % C8) * 8;
+#pragma unroll 2
+    for (int c = threadIdx.x; c < BM * C8; c += NTH) {
+      const int row = c / C8;
+      const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
+      const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
+      epi.apply8_fast(m0 + row, n0 + col, lo, hi);
+    }
+  } else {
+    constexpr int C4 = CW / 4;
+    for (int c = threadIdx.x; c < BM * C4; c += NTH) {
+      const int row = c / C4, col = (c - row * C4) * 4;
+      const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
+      epi.apply4(m0 + row, n0 + col, v);
+    }
+  }
+}
+
 // NS operand stages (2..5) of BK = OA::BK (64 or 32): NS - 1 K tiles are in flight while one
 // is consumed (counted vmcnt).  NS = 3 at BK 64 where the grid leaves one block per CU anyway;
 // BK 32 x NS 4-5 keeps two blocks per CU with twice the bytes in flight of BK 64 x NS 2.
@@ -1584,14 +1609,21 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   // fragments-first K loop (below): measured on the C4 conv shapes, 5-13 % faster for the
   // R-major (weight-gradient) operands and most 128-wide tiles, mixed on the 128x64 k-major
   // tiles (three blocks per CU there already cover the LDS latency)
-  constexpr bool FRAG_FIRST = BN == 128 || OA::RMAJOR;
+  // (not at 128 x 64 per wave: the two K steps' fragments would not fit in 256 VGPRs)
+  constexpr bool FRAG_FIRST = BN == 128 || (OA::RMAJOR && BN < 256);
   static_assert(OB::BK == BK, "operand K tile depths differ");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int OP_BYTES = NS * STAGE;
-  constexpr int LDC = BN + 4;
   constexpr int RED = WM * 3 > (NTH / 64) * 2 ? WM * 3 : (NTH / 64) * 2;  // floats per column
+  // the fp32 tile is staged through LDS in NCH column passes: two for 256 x 256 tiles, whose
+  // full staging (266 KB) exceeds the CU's 160 KB
+  constexpr int NCH = BM * (BN + 4) * 4 + RED * BN * 4 > 160 * 1024 ? 2 : 1;
+  constexpr int CH = BN / NCH;  // staged columns per pass
+  static_assert(NCH == 1 || (WN % NCH == 0 && (BN / WN) * (WN / NCH) == CH),
+                "a staging pass holds whole wave columns");
+  constexpr int LDC = CH + 4;
   constexpr int EPI_BYTES = BM * LDC * 4 + RED * BN * 4;  // staged tile + reduction scratch
   constexpr int LDS_BYTES = OP_BYTES > EPI_BYTES ? OP_BYTES : EPI_BYTES;
   // DMA instructions one wave issues per K tile (both operands)
@@ -1711,70 +1743,81 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 
   float* cst = (float*)lds_raw;
   float* red = cst + BM * LDC;
-  // fused consumer-BN backward statistics: the BN input y of this thread's output chunks is
-  // loaded now, so its latency overlaps the accumulator staging below
-  constexpr int C8 = BN / 8, ITERS = BM * C8 / NTH;
-  static_assert(NTH % C8 == 0 && (BM * C8) % NTH == 0, "vec8 epilogue geometry");
-  const bool bst = Epi::BNSTAT && epi.bs.part != nullptr && epi.vec8_ok();
-  bn_y8 yv[ITERS], ov[ITERS];
-  if (bst) {
-    const int n = tn * BN + (threadIdx.x % C8) * 8;
+  if constexpr (NCH == 1) {
+    // fused consumer-BN backward statistics: the BN input y of this thread's output chunks
+    // is loaded now, so its latency overlaps the accumulator staging below
+    constexpr int C8 = BN / 8, ITERS = BM * C8 / NTH;
+    static_assert(NTH % C8 == 0 && (BM * C8) % NTH == 0, "vec8 epilogue geometry");
+    const bool bst = Epi::BNSTAT && epi.bs.part != nullptr && epi.vec8_ok();
+    bn_y8 yv[ITERS], ov[ITERS];
+    if (bst) {
+      const int n = tn * BN + (threadIdx.x % C8) * 8;
 #pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-      const int m = tm * BM + (threadIdx.x + it * NTH) / C8;
-      const bool in = m < M && n < N;
-      yv[it] = in ? *(const bn_y8*)((const bf16*)epi.bs.y + epi.bn_off(m, n)) : bn_y8{};
-      ov[it] = in && epi.bs.out ? *(const bn_y8*)((const bf16*)epi.bs.out + epi.bn_off(m, n))
-                                : bn_y8{};
+      for (int it = 0; it < ITERS; ++it) {
+        const int m = tm * BM + (threadIdx.x + it * NTH) / C8;
+        const bool in = m < M && n < N;
+        yv[it] = in ? *(const bn_y8*)((const bf16*)epi.bs.y + epi.bn_off(m, n)) : bn_y8{};
+        ov[it] = in && epi.bs.out ? *(const bn_y8*)((const bf16*)epi.bs.out + epi.bn_off(m, n))
+                                  : bn_y8{};
+      }
     }
-  }
-  if constexpr (Epi::REG_STATS)
-    epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
+    if constexpr (Epi::REG_STATS)
+      epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+    for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j)
+      for (int j = 0; j < RN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 + (lane & 15)] =
-            acc[i][j][r];
-  __syncthreads();
-  if constexpr (!Epi::REG_STATS) epi.template tile_stats<BM, BN, LDC>(cst, red, tm, tn);
-  if (bst) {  // vec8 stores + the statistics of every stored chunk (rows >= M excluded)
-    const int col = (threadIdx.x % C8) * 8;
-    BnCoef8 bc;
-    float sg[8], sgx[8];
+        for (int r = 0; r < 4; ++r)
+          cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 +
+              (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    if constexpr (!Epi::REG_STATS) epi.template tile_stats<BM, BN, LDC>(cst, red, tm, tn);
+    if (bst) {  // vec8 stores + the statistics of every stored chunk (rows >= M excluded)
+      const int col = (threadIdx.x % C8) * 8;
+      BnCoef8 bc;
+      float sg[8], sgx[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
-    bn_coef8(epi.bs, tn * BN + col, N, bc);
+      for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+      bn_coef8(epi.bs, tn * BN + col, N, bc);
 #pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-      const int row = (threadIdx.x + it * NTH) / C8;
-      f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
-      f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
-      const int m = tm * BM + row, n = tn * BN + col;
-      bst_accum8(epi, m, n, lo, hi);
-      bst_store8(epi, m, n, lo, hi);
-      if (m < M && n < N) bn_acc8<bf16>(yv[it], ov[it], lo, hi, epi.bs, bc, sg, sgx);
-    }
-    bn_stat_store<BN, NTH / 64, (BM > 128 ? BM / 128 : 1)>(epi.bs, sg, sgx, red, tm, tn, N, M);
-  } else if (epi.vec8_ok()) {
-    const int col = (threadIdx.x % C8) * 8;
-#pragma unroll 2
-    for (int c = threadIdx.x; c < BM * C8; c += NTH) {
-      const int row = c / C8;
-      const f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
-      const f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
-      epi.apply8_fast(tm * BM + row, tn * BN + col, lo, hi);
+      for (int it = 0; it < ITERS; ++it) {
+        const int row = (threadIdx.x + it * NTH) / C8;
+        f32x4 lo = *(const f32x4*)(cst + row * LDC + col);
+        f32x4 hi = *(const f32x4*)(cst + row * LDC + col + 4);
+        const int m = tm * BM + row, n = tn * BN + col;
+        bst_accum8(epi, m, n, lo, hi);
+        bst_store8(epi, m, n, lo, hi);
+        if (m < M && n < N) bn_acc8<bf16>(yv[it], ov[it], lo, hi, epi.bs, bc, sg, sgx);
+      }
+      bn_stat_store<BN, NTH / 64, (BM > 128 ? BM / 128 : 1)>(epi.bs, sg, sgx, red, tm, tn, N, M);
+      return;
     }
   } else {
-    constexpr int C4 = BN / 4;
-    for (int c = threadIdx.x; c < BM * C4; c += NTH) {
-      const int row = c / C4, col = (c - row * C4) * 4;
-      const f32x4 v = *(const f32x4*)(cst + row * LDC + col);
-      epi.apply4(tm * BM + row, tn * BN + col, v);
+    // column passes (256 x 256 tiles): the waves whose columns fall in pass h stage them; the
+    // epilogues used here take their statistics from the registers (REG_STATS) or keep none
+    // (EpiPartial, EpiPhase), and the fused consumer-BN path is not instantiated
+    if constexpr (Epi::REG_STATS)
+      epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) {
+      if (h > 0) __syncthreads();  // the previous pass's readers are done with cst
+      if ((wn * WTN) / CH == h) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN - h * CH +
+                  j * 16 + (lane & 15)] = acc[i][j][r];
+      }
+      __syncthreads();
+      epilogue_pass<BM, CH, LDC, NTH>(epi, cst, tm * BM, tn * BN + h * CH);
     }
+    return;
   }
+  epilogue_pass<BM, CH, LDC, NTH>(epi, cst, tm * BM, tn * BN);
 }
 
 // Loader bundles (give the kernel template one type per operand).

@@ -115,8 +115,9 @@ def hf_beam_stepper(t5, enc, nb, k):
 class BeamStepCheck:
     """Stepper that follows the reference's decisions (hf_beam_stepper) and checks the mmdx
     device step (t5._DecodeState: KV-cached decoder, device logits processors, top-k) on the
-    same state at every step: the k top candidate scores agree to atol = tol * max(1, |lp|)
-    (lp: the candidate's log-prob, its score minus its parent beam's running score),
+    same state at every step: the k top candidate scores agree to atol = tol * max(1, max |lp|)
+    over the batch row's candidates (lp: a candidate's log-prob, its score minus its parent
+    beam's running score; the rounding of a log-softmax scales with the row's logits),
     and the candidate index agrees wherever its score is separated from its neighbours (and
     from the (k+1)-th score) by more than twice that tolerance.  `min_gap` records the smallest
     separation seen: if it stays above the tolerance, the search has no near-tie and the
@@ -127,7 +128,7 @@ class BeamStepCheck:
         self.B, self.nb, self.k, self.tol = B, nb, k, tol
         self.min_gap = float("inf")
         self.ambiguous = 0   # candidates within 2 x tolerance of a neighbour (not compared)
-        self.max_err = 0.0   # largest |mmdx - reference| / max(1, |log-prob|)
+        self.max_err = 0.0   # largest |mmdx - reference| / the row's log-prob scale
         self.steps = 0
 
     def __call__(self, hist, pos, slots, sc, bans, eos_ban):
@@ -143,7 +144,8 @@ class BeamStepCheck:
         V = self.ref.vocab
         par = np.take_along_axis(sc.reshape(self.B, self.nb), ri // V, axis=1)
         lp = np.where(fin, rv - par, 0.0)
-        atol = self.tol * np.maximum(1.0, np.abs(lp))
+        scale = np.maximum(1.0, np.abs(lp).max(axis=1, keepdims=True))
+        atol = self.tol * np.broadcast_to(scale, lp.shape)
         diff = np.abs(np.where(fin, mv - rv, 0.0))
         self.max_err = max(self.max_err, float((diff / atol).max()) * self.tol)
         assert (diff <= atol).all(), (self.steps, float(diff.max()))

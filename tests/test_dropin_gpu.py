@@ -212,7 +212,7 @@ def test_views_bundle_rebuild_and_inference(trained):
     head = T5Head(bundle["fusion_model"].report_model)
     condd = cond.to("cuda")
     dec = _DecodeState(head, condd.repeat_interleave(4, dim=0), torch.float32, 181)
-    chk = BeamStepCheck(hf_beam_stepper(t5g, cond, 4, 8), dec, 1, 4, 8, tol=1e-5)
+    chk = BeamStepCheck(hf_beam_stepper(t5g, cond, 4, 8), dec, 1, 4, 8, tol=2e-5)
     replay = head.generate(condd, _stepper=chk, **kw)
     print(f"steps {chk.steps}, max err {chk.max_err:.2e}, min gap {chk.min_gap:.2e}, "
           f"near-ties {chk.ambiguous}")

@@ -1,7 +1,8 @@
-"""GPU: the 8-wave 256 x 128 dense GEMM tiles (MMDX_GEMM8_MIN, gemm_dense.hip) against the
-4-wave 128 x 128 kernel and a torch fp32 matmul, in the three operand layouts the Linear
-layers use: forward (A, B k-major), input gradient (B R-major), weight gradient (A and B
-R-major), fp16 and bf16, ragged M / N / K.
+"""GPU: the 8-wave dense GEMM tiles — 256 x 128 (MMDX_GEMM8_MIN) and 256 x 256 with 128 x 64
+per wave (MMDX_GEMM256_MIN), gemm_dense.hip — against the 4-wave 128 x 128 kernel and a torch
+fp32 matmul, in the three operand layouts the Linear layers use: forward (A, B k-major),
+input gradient (B R-major), weight gradient (A and B R-major), fp16 and bf16, ragged M / N /
+K.
 
 Both tilings accumulate every output over the same K tiles in the same MFMA order, so the
 results must be BIT-IDENTICAL; the fp32 matmul check bounds the kernel error itself
@@ -43,19 +44,23 @@ def _operands(layout, M, N, K, dt, dev, seed):
     return a.to(dev), b.to(dev), ref
 
 
+@pytest.mark.parametrize("knob", ["MMDX_GEMM8_MIN", "MMDX_GEMM256_MIN"])
 @pytest.mark.parametrize("layout", ["fwd", "dgrad", "wgrad"])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_gemm8_matches_4wave(dev, layout, dt, shape, monkeypatch):
+def test_gemm8_matches_4wave(dev, knob, layout, dt, shape, monkeypatch):
     M, N, K = shape
     a, b, ref = _operands(layout, M, N, K, dt, dev, M + N + K)
+    monkeypatch.setenv("MMDX_GEMM8_MIN", "0")
+    monkeypatch.setenv("MMDX_GEMM256_MIN", "0")
     for out_dtype in (dt, torch.float32):
-        monkeypatch.setenv("MMDX_GEMM8_MIN", "0")
+        monkeypatch.setenv(knob, "0")
         c4 = _gemm(layout, a, b, M, N, K, out_dtype)
-        monkeypatch.setenv("MMDX_GEMM8_MIN", "1")
+        monkeypatch.setenv(knob, "1")
         c8 = _gemm(layout, a, b, M, N, K, out_dtype)
         torch.cuda.synchronize()
         assert torch.isfinite(c8.float()).all()
+        monkeypatch.setenv(knob, "0")
         assert torch.equal(c4, c8), (layout, dt, shape, out_dtype)
         err = (c8.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
         assert err <= 1e-2, (layout, dt, shape, out_dtype, err)

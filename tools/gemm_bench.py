@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Dense GEMM throughput of the mmdx MFMA core (mmdx_gemm) with the 4-wave 128 x 128 and the
-8-wave 256 x 128 tiles (MMDX_GEMM8_MIN 0 / 1), next to torch.matmul (hipBLASLt) on the same
+"""Dense GEMM throughput of the mmdx MFMA core (mmdx_gemm) with the 4-wave 128 x 128, the
+8-wave 256 x 128 (MMDX_GEMM8_MIN) and the 8-wave 256 x 256 (MMDX_GEMM256_MIN, 128 x 64 per
+wave) tiles, next to torch.matmul (hipBLASLt) on the same
 shapes: the C5 Linear layers (ViT-B/16 12608 tokens, BERT-base 8192 tokens; forward, input
 gradient, weight gradient) plus square calibration points.
     python tools/gemm_bench.py [--reps 20] [--dtype f16|bf16]
@@ -42,7 +43,10 @@ def main():
     from mmdx import functional as F
     dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     dev = torch.device("cuda", 0)
-    tot = {"4w": 0.0, "8w": 0.0, "blas": 0.0}
+    tot = {"4w": 0.0, "8w": 0.0, "256": 0.0, "blas": 0.0}
+    arms = (("4w", {"MMDX_GEMM8_MIN": "0", "MMDX_GEMM256_MIN": "0"}),
+            ("8w", {"MMDX_GEMM8_MIN": "1", "MMDX_GEMM256_MIN": "0"}),
+            ("256", {"MMDX_GEMM8_MIN": "0", "MMDX_GEMM256_MIN": "1"}))
     for T, O, I in LINEARS:
         X = (torch.rand(T, I, device=dev) * 2 - 1).to(dt)
         W = (torch.rand(O, I, device=dev) * 2 - 1).to(dt)
@@ -58,8 +62,8 @@ def main():
         for name, (M, N, K, fn, tfn) in cases.items():
             C = torch.empty(M, N, dtype=dt if name != "wgrad" else torch.float32, device=dev)
             res = {}
-            for mode, lim in (("4w", "0"), ("8w", "1")):
-                os.environ["MMDX_GEMM8_MIN"] = lim
+            for mode, env in arms:
+                os.environ.update(env)
                 res[mode] = timeit(lambda: fn(C), a.reps)
             res["blas"] = timeit(tfn, a.reps)
             for k in tot:
@@ -70,6 +74,7 @@ def main():
                 flush=True)
     print("total ms: " + "  ".join(f"{k} {v:.3f}" for k, v in tot.items()), flush=True)
     os.environ.pop("MMDX_GEMM8_MIN", None)
+    os.environ.pop("MMDX_GEMM256_MIN", None)
 
 
 if __name__ == "__main__":
