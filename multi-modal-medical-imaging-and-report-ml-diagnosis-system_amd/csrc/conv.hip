@@ -454,9 +454,11 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
 struct WgradPlan { int bm, bn, splits, kper; };
 // 8-wave 256 x 128 weight-gradient tiles (one block per CU, three stages) for Kout >= 256
 // and C*R*S >= 128 (MMDX_WGRAD8=0: off); their splits target one block per CU
+// 8-wave 256 x 128 weight-gradient tiles (MMDX_WGRAD8=1; off by default: isolated C4 wgrads
+// 2.78 vs 2.51 ms, train step 8967 vs 9050 samples/s, profiles/r03_wgrad8_ab.txt)
 static bool wgrad8_on() {
   const char* e = getenv("MMDX_WGRAD8");
-  return !e || atoi(e) != 0;
+  return e && atoi(e) != 0;
 }
 
 static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
