@@ -196,7 +196,11 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
 
 // Backward A: per query block -> dS (T, global scratch [B,H,L,LP]) and dQ.
 template <typename T>
-__global__ void attn_bwd_q_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
+// (launch bounds: without them the compiler budgets registers for 1024-thread blocks, 128
+// VGPRs, and spilled 17 of the dP row tiles to scratch; the LDS footprint allows two blocks
+// per CU = two waves per SIMD anyway)
+__global__ __launch_bounds__(AttnCfg<T>::NW * 64, 2) void attn_bwd_q_kernel(
+    const T* __restrict__ qkv, const float* __restrict__ probs,
                                   const T* __restrict__ dout, int L, int H, float scale,
                                   float keep_scale, T* __restrict__ dS_g,
                                   T* __restrict__ dqkv) {

@@ -274,7 +274,13 @@ constexpr int COOP_DEBUG_DROP_PEER = 1;    // debug flag: workgroup 0 of directi
 
 typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
 
-// RT = 16-row tiles per wave (B <= 64 * RT): 8 waves = 2 unit groups x 4 row groups.
+// RT = 16-row tiles per wave (RT = 1: B <= 64; RT = 2: 128-row groups, grid z): 8 waves =
+// 2 unit groups x 4 row groups.  The workgroup's W_hh slice (128 gate columns x 256, 64 KB)
+// lives in LDS in fragment order (one contiguous 1 KiB per wave read): held in registers
+// (128 VGPRs per lane) the B = 128 kernel needed 275 registers and spilled 19 to scratch
+// inside the step loop, and a 256-row workgroup spilled 121.
+constexpr int COOP_WLDS_BYTES = 2 * 4 * (COOP_H / 32) * 64 * 16;  // [ug][g][ks][lane] x 16 B
+
 template <int RT>
 __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     const float* __restrict__ xg, const bf16* __restrict__ whh, int B, int L,
@@ -283,33 +289,44 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     int debug) {
   constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
   constexpr int NROWS = 64 * RT;
-  // [0, NROWS*COOP_LDH): h_{t-1} (MFMA A operand); then this workgroup's h_t slice [NROWS][32];
-  // then one int: the poller's verdict, broadcast to the workgroup
-  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * COOP_LDH + NROWS * COOP_UB + 8];
+  static_assert(RT == 1 || RT == 2, "row tiles per wave");
+  constexpr int WB = COOP_WLDS_BYTES / 2;  // bf16 elements of the W_hh image
+  // [0, WB): the W_hh fragments; then h_{t-1} [NROWS][COOP_LDH] (MFMA A operand); then
+  // this workgroup's h_t slice [NROWS][32]; then one int: the poller's verdict
+  __shared__ __attribute__((aligned(16))) bf16 sh_all[WB + NROWS * COOP_LDH + NROWS * COOP_UB + 8];
+  bf16* sh = sh_all + WB;
   bf16* sout = sh + NROWS * COOP_LDH;
   int* sgiveup = (int*)(sout + NROWS * COOP_UB);
   // the recurrence is the text tower's latency-critical chain and shares its CUs with the
   // image tower's conv blocks: its waves take issue priority over them
   __builtin_amdgcn_s_setprio(3);
   const int dir = blockIdx.y, blk = blockIdx.x;
+  // blockIdx.z: this group's NROWS batch rows (B > 128 runs as independent 128-row groups of
+  // COOP_NB workgroups: the recurrence of a row needs only its own row's hidden state)
+  const int rb0 = blockIdx.z * NROWS;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int ug = wid & 1, rg = wid >> 1;
   const int u0 = blk * COOP_UB + ug * 16;   // this wave's 16 units
   const int ucol = u0 + (lane & 15);        // this lane's unit (accumulator column)
   // W fragments: gate g, unit u0 + (lane & 15), k = ks*32 + 8*(lane >> 4) .. +7
   const bf16* W = whh + (long)dir * G4 * H;
-  bf16x8 wf[4][KS];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      wf[g][ks] = *(const bf16x8*)(W + (long)(g * H + ucol) * H + ks * 32 + 8 * (lane >> 4));
+  // fragment (g, ks) of unit group ug at sh_all[(((ug * 4 + g) * KS + ks) * 64 + lane) * 8]:
+  // gate g, unit blk * 32 + ug * 16 + (lane & 15), k = ks*32 + 8*(lane >> 4) .. +7; wave w
+  // copies unit group (w & 1)'s fragments g * KS + ks = w >> 1, + 4, ...
+  for (int f = wid >> 1; f < 4 * KS; f += 4) {
+    const int g = f / KS, ks = f - g * KS;
+    *(bf16x8*)(sh_all + ((((wid & 1) * 4 + g) * KS + ks) * 64 + lane) * 8) =
+        *(const bf16x8*)(W + (long)(g * H + blk * COOP_UB + (wid & 1) * 16 + (lane & 15)) * H +
+                         ks * 32 + 8 * (lane >> 4));
+  }
+  __syncthreads();
+  const bf16* wl = sh_all + ((ug * 4) * KS * 64 + lane) * 8;  // this wave's fragment base
   float creg[RT][4];
 #pragma unroll
   for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) creg[i][r] = 0.f;
-  unsigned* myctr = ctr + dir;
+  unsigned* myctr = ctr + dir * gridDim.z + blockIdx.z;
   bf16* hxd = hx + (long)dir * 2 * B * H;
   const __amdgpu_buffer_rsrc_t hrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)hxd, (short)0, 2 * B * H * 2, 0x00020000);
@@ -321,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
+        const int b = rb0 + (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
         const float* xp = xg + (((long)min(b, B - 1) * L + t) * 2 + dir) * G4 + ucol;
 #pragma unroll
         for (int g = 0; g < 4; ++g) xv[i][r][g] = xp[g * H];
@@ -369,14 +386,15 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     bf16* hdst = sh + hrow * COOP_LDH + (threadIdx.x & 31) * 8;
     if (s > 0) {
       const unsigned hsrc = (unsigned)(((s + 1) & 1) * B * H * 2 +  // the h_{t-1} buffer
-                                       (hrow * H + (threadIdx.x & 31) * 8) * 2);
+                                       ((rb0 + hrow) * H + (threadIdx.x & 31) * 8) * 2);
 #pragma unroll
       for (int i0 = 0; i0 < HCH; i0 += HB) {
         coop_v4u v[HB];
 #pragma unroll
         for (int i = 0; i < HB; ++i)
           v[i] = __builtin_amdgcn_raw_buffer_load_b128(
-              hrs, hrow + 16 * (i0 + i) < B ? hsrc + (i0 + i) * 16 * H * 2 : DMA_OOB, 0, COOP_SC1);
+              hrs, rb0 + hrow + 16 * (i0 + i) < B ? hsrc + (i0 + i) * 16 * H * 2 : DMA_OOB, 0,
+              COOP_SC1);
 #pragma unroll
         for (int i = 0; i < HB; ++i) *(coop_v4u*)(hdst + (i0 + i) * 16 * COOP_LDH) = v[i];
       }
@@ -386,45 +404,61 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     }
     __syncthreads();
     float hv[RT][4], cv[RT][4], gv[RT][4][4];
+    // every W fragment is read from LDS once per step, for all of the wave's row tiles
+    constexpr int IB = RT;
 #pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      const int rt16 = (rg + 4 * i) * 16;  // this row tile's first row
-      f32x4 acc[4];
+    for (int i0 = 0; i0 < RT; i0 += IB) {
+      f32x4 accs[IB][4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bf16* arow = sh + (rt16 + (lane & 15)) * COOP_LDH + 8 * (lane >> 4);
+      for (int ii = 0; ii < IB; ++ii)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) accs[ii][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 af = *(const bf16x8*)(arow + ks * 32);
+        bf16x8 w4[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[g][ks], acc[g], 0, 0, 0);
+        for (int g = 0; g < 4; ++g) w4[g] = *(const bf16x8*)(wl + (g * KS + ks) * 64 * 8);
+#pragma unroll
+        for (int ii = 0; ii < IB; ++ii) {
+          const bf16x8 af = *(const bf16x8*)(sh + ((rg + 4 * (i0 + ii)) * 16 + (lane & 15)) *
+                                                       COOP_LDH + 8 * (lane >> 4) + ks * 32);
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            accs[ii][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w4[g], accs[ii][g], 0, 0, 0);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gi = sigm(acc[0][r] + xv[i][r][0]);
-        const float gf = sigm(acc[1][r] + xv[i][r][1]);
-        const float gg = tanhf(acc[2][r] + xv[i][r][2]);
-        const float go = sigm(acc[3][r] + xv[i][r][3]);
-        const float c = gf * creg[i][r] + gi * gg;
-        creg[i][r] = c;
-        const bf16 h = from_f<bf16>(go * tanhf(c));
-        hv[i][r] = (float)h;
-        cv[i][r] = c;
-        gv[i][r][0] = gi; gv[i][r][1] = gf; gv[i][r][2] = gg; gv[i][r][3] = go;
-        const int row = rt16 + (lane >> 4) * 4 + r;
-        sout[row * COOP_UB + ug * 16 + (lane & 15)] = h;
+      for (int ii = 0; ii < IB; ++ii) {
+        const int i = i0 + ii;
+        const int rt16 = (rg + 4 * i) * 16;  // this row tile's first row
+        const f32x4* acc = accs[ii];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gi = sigm(acc[0][r] + xv[i][r][0]);
+          const float gf = sigm(acc[1][r] + xv[i][r][1]);
+          const float gg = tanhf(acc[2][r] + xv[i][r][2]);
+          const float go = sigm(acc[3][r] + xv[i][r][3]);
+          const float c = gf * creg[i][r] + gi * gg;
+          creg[i][r] = c;
+          const bf16 h = from_f<bf16>(go * tanhf(c));
+          hv[i][r] = (float)h;
+          cv[i][r] = c;
+          gv[i][r][0] = gi; gv[i][r][1] = gf; gv[i][r][2] = gg; gv[i][r][3] = go;
+          const int row = rt16 + (lane >> 4) * 4 + r;
+          sout[row * COOP_UB + ug * 16 + (lane & 15)] = h;
+        }
       }
     }
     __syncthreads();
     // publish h_t: 16-B sc1 stores of the [B][32] slice, drain, one agent atomic add
     if (s + 1 < L) {
       const int par_out = (s & 1) * B * H * 2;
-      for (int e = threadIdx.x; e < B * (COOP_UB / 8); e += 512) {
+      const int nrow = min(NROWS, B - rb0);
+      for (int e = threadIdx.x; e < nrow * (COOP_UB / 8); e += 512) {
         const int row = e / (COOP_UB / 8), c8 = e - row * (COOP_UB / 8);
         const coop_v4u v = *(const coop_v4u*)(sout + row * COOP_UB + c8 * 8);
         __builtin_amdgcn_raw_buffer_store_b128(
-            v, hrs, par_out + (row * H + blk * COOP_UB + c8 * 8) * 2, 0, COOP_SC1);
+            v, hrs, par_out + ((rb0 + row) * H + blk * COOP_UB + c8 * 8) * 2, 0, COOP_SC1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -436,7 +470,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
+        const int b = rb0 + (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
         if (b >= B) continue;
         hout[((long)b * L + t) * 2 * H + dir * H + ucol] = from_f<bf16>(hv[i][r]);
         const long sidx = ((long)dir * L + t) * B + b;
@@ -498,17 +532,17 @@ static bool coop_ok(int dtype, int B, int H) { return dtype == BF16 && H == COOP
 extern "C" size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H) {
   (void)L;
   if (!coop_ok(dtype, B, H)) return 0;
-  // h exchange [2 dir][2 parity][B][H] bf16 + 2 counters
+  // h exchange [2 dir][2 parity][B][H] bf16 + counters ([2 dir][row groups], 64 B zeroed)
   return (size_t)2 * 2 * B * H * 2 + 256;
 }
 
-// The cooperative forward needs its 2 x COOP_NB workgroups resident at once: one per CU
-// (~148 KB of LDS each) on distinct CUs.  Checked once per device and kernel variant: the
+// The cooperative forward needs its 2 x COOP_NB x groups workgroups resident at once: one per
+// CU (~140 KB of LDS each) on distinct CUs.  Checked once per device and kernel variant: the
 // device must have at least that many CUs and the kernel must fit one block per CU.  The
 // other streams' blocks cannot starve it: they always finish, and the spinning workgroups
-// hold at most 2 x COOP_NB of the 256 CUs.
+// hold at most 2 x COOP_NB x 2 = 32 of the 256 CUs.
 template <int RT>
-static bool coop_resident(hipStream_t st) {
+static bool coop_resident(hipStream_t st, int groups) {
   static std::atomic<int> ok[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
@@ -519,11 +553,11 @@ static bool coop_resident(hipStream_t st) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_fwd_coop_kernel<RT>, 512,
                                                      0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
-    v = (q && per_cu >= 1 && cus >= 2 * COOP_NB) ? 1 : -1;
+    v = (q && per_cu >= 1) ? cus : -1;
     ok[dev].store(v, std::memory_order_relaxed);
   }
   (void)st;
-  return v > 0;
+  return v > 0 && v >= 2 * COOP_NB * groups;
 }
 
 extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
@@ -540,10 +574,12 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
     unsigned* ctr = (unsigned*)((char*)ws + (size_t)2 * 2 * B * H * 2);
     const long spin_max = spin_limit > 0 ? spin_limit : COOP_SPIN_MAX;
     (void)hipMemsetAsync(ctr, 0, 64, st);
-    const dim3 grid(COOP_NB, 2);
+    // B > 128: independent groups of 128 rows (grid z), each with W_hh in LDS (RT = 2)
+    const int groups = B <= 128 ? 1 : (B + 127) / 128;
+    const dim3 grid(COOP_NB, 2, groups);
 #define COOP_LAUNCH(RT)                                                                      \
   do {                                                                                       \
-    MMDX_CHECK_ARG(coop_resident<RT>(st),                                                    \
+    MMDX_CHECK_ARG(coop_resident<RT>(st, groups),                                            \
                    "lstm fwd: the cooperative recurrence cannot be co-resident here");       \
     hipLaunchKernelGGL(lstm_fwd_coop_kernel<RT>, grid, dim3(512), 0, st, (const float*)xg,   \
                        (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr,   \
@@ -551,10 +587,8 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
   } while (0)
     if (B <= 64)
       COOP_LAUNCH(1);
-    else if (B <= 128)
-      COOP_LAUNCH(2);
     else
-      COOP_LAUNCH(4);
+      COOP_LAUNCH(2);
 #undef COOP_LAUNCH
     MMDX_LAUNCH_CHECK();
     return 0;

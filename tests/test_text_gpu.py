@@ -167,8 +167,9 @@ def test_text_encoder_transformer_bert(dev, dt):
 
 @pytest.mark.parametrize("B", [128, 200])
 def test_lstm_coop_forward_matches_partitioned(dev, B):
-    """The cooperative bf16 recurrence (W_hh in registers, h exchanged through a counter
-    barrier) reproduces the batch-partitioned kernel (same MFMA k order; fp32 contraction
+    """The cooperative bf16 recurrence (W_hh in LDS, h exchanged through a counter barrier;
+    B = 200 runs as two independent 128-row groups, the second ragged) reproduces the
+    batch-partitioned kernel (same MFMA k order; fp32 contraction
     order of the cell update may differ, so h may differ by one bf16 ulp): max abs
     difference <= 1e-2 on h (bf16, |h| < 1), c and gates."""
     H, Ls = 256, 24

@@ -23,7 +23,7 @@ has tests && step tests ${TS:-900} python -u -m pytest ${PT:-tests -m gpu -x} -v
 # the test selection PT2 once per arm of an env knob (AB_VAR = AB_A / AB_B)
 if has abtest; then
   for arm in "$AB_A" "$AB_B"; do
-    step "abtest_$arm" ${TS:-900} env "$AB_VAR=$arm" python -u -m pytest $PT2 -v -s -rA \
+    step "abtest_$(basename "$arm")" ${TS:-900} env "$AB_VAR=$arm" python -u -m pytest $PT2 -v -s -rA \
       --timeout ${TT:-120} --timeout-method thread
   done
 fi
@@ -36,13 +36,13 @@ has convb && step convb 600 python tools/conv_bench.py --json "gpurun_out/${tag}
 # A/B of an env knob (AB_VAR, arms AB_A / AB_B): conv table per arm, then paired benches
 if has convab; then
   for arm in "$AB_A" "$AB_B"; do
-    step "convab_$arm" 600 env "$AB_VAR=$arm" python tools/conv_bench.py --ops "${AB_OPS:-fwd,dgrad,wgrad}"
+    step "convab_$(basename "$arm")" 600 env "$AB_VAR=$arm" python tools/conv_bench.py --ops "${AB_OPS:-fwd,dgrad,wgrad}"
   done
 fi
 if has benchab; then
   for rep in 1 2; do
     for arm in "$AB_A" "$AB_B"; do
-      step "benchab_${arm}_$rep" 300 env "$AB_VAR=$arm" python bench.py --steps 30 --warmup 5 --no-cpu-baseline ${BA:-}
+      step "benchab_$(basename "$arm")_$rep" 300 env "$AB_VAR=$arm" python bench.py --steps 30 --warmup 5 --no-cpu-baseline ${BA:-}
     done
   done
 fi
