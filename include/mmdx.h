@@ -87,11 +87,19 @@ long mmdx_conv_pack_blocks(int K, int C, int RS);
 int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items, long total_blocks,
                          void* stream);
 /* stat_part (optional, fp32 pairs [K][mmdx_conv_fwd_stat_blocks(d)], channel-major): per-channel
- * (mean, M2) of each 128-row block of the output, computed from the fp32 accumulators in
- * the GEMM epilogue — the BatchNorm batch statistics without a separate pass over y. */
+ * (mean, M2) of each mmdx_conv_fwd_stat_rows(d)-row block of the output (128 rows; the direct
+ * pixel-pair stem kernel: one block of 2 output rows), computed from the fp32 accumulators in
+ * the GEMM epilogue — the BatchNorm batch statistics without a separate pass over y
+ * (replaces the BatchNorm2d reduction after backbone convs, TP:183 / torchvision). */
 int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d);
+int mmdx_conv_fwd_stat_rows(const mmdx_conv_desc* d);
 int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
                   void* y, float* stat_part, void* stream);
+/* The same with the statistics slab size the caller allocated stat_part for (stat_rows =
+ * mmdx_conv_fwd_stat_rows(d) when the buffer was sized; a plan built once keeps its layout
+ * whatever MMDX_STEM_DIRECT says later; a size the kernels cannot write is an error). */
+int mmdx_conv_fwd_rows(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
+                       void* y, float* stat_part, int stat_rows, void* stream);
 /* Eval-mode conv + BatchNorm2d (running statistics) (+residual) (+ReLU) in one launch:
  * y = act(conv(x, w) * s + t + residual), s = gamma / sqrt(running_var + eps),
  * t = beta - running_mean * s, applied in the conv epilogue on the fp32 accumulators.

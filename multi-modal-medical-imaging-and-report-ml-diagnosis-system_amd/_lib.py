@@ -68,7 +68,9 @@ SIGNATURES = {
     "mmdx_conv_pack_blocks": (i64, [i32, i32, i32]),
     "mmdx_conv_pack_multi": (i32, [i32, vp, i32, i64, vp]),
     "mmdx_conv_fwd_stat_blocks": (i32, [CD]),
+    "mmdx_conv_fwd_stat_rows": (i32, [CD]),
     "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
+    "mmdx_conv_fwd_rows": (i32, [i32, CD, vp, vp, vp, vp, i32, vp]),
     "mmdx_conv_fwd_bn_eval": (i32, [i32, CD, vp, vp, vp, vp, vp, vp, vp, f32, vp, i32, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
     "mmdx_conv_dgrad_stat_blocks": (i32, [i32, CD]),

@@ -339,11 +339,152 @@ static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K
   return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok);
 }
 
+// ---------------------------------------------------------------------------------------
+// Direct stem forward (bf16 pixel-pair stem: C = 8, S = 4 pair columns, stride (2, 1), no
+// padding, K = 64 output channels).  As an implicit GEMM its A operand is a 14x re-read of
+// the pair image (each input element feeds 7 filter rows x 4 pair columns at stride 2), so
+// the generic kernel moves 1.1 GB through L2 -> LDS for 0.26 GB of HBM traffic and runs at
+// 0.19 of the HBM roofline.  Here a block owns STEM_PB output rows of one image (all Q
+// columns, all 64 channels): the 2*(STEM_PB-1)+R input rows it reads are staged in LDS once,
+// and the A fragments are read straight from that image — k-step r of the MFMA loop is filter
+// row r, its 32 k = the 4 pair columns s x 8 channels, which sit contiguously at pair
+// q + s of input row 2p + r.  Same operand values, same k order, same MFMA sequence per output
+// as the implicit-GEMM kernel (bit-identical y); the BatchNorm partials are per block
+// (STEM_PB * Q rows: mmdx_conv_fwd_stat_rows).  Wave w owns output channels 16w..16w+15; its
+// 7 weight fragments stay in registers.
+// ---------------------------------------------------------------------------------------
+constexpr int STEM_PB = 2;   // output rows per block
+constexpr int STEM_LDY = 64 + 8;  // staged output row (bf16), padded
+
+static bool stem_direct_on() {
+  const char* e = getenv("MMDX_STEM_DIRECT");  // read per launch (A/B, tests)
+  return !e || atoi(e) != 0;
+}
+
+static bool stem_direct_geom(const ConvGeom& g) {
+  return g.C == 8 && g.S == 4 && (g.R == 7 || g.R == 8) && g.sh == 2 && g.sw == 1 && g.ph == 0 &&
+         g.pw == 0 && g.K == 64 && g.Q % 16 == 0 && g.Q <= 256 && g.P % STEM_PB == 0 &&
+         2 * (g.P - 1) + g.R <= g.H && g.Q + 3 <= g.W;
+}
+
+// NT: row tiles per block (STEM_PB * Q / 16) as a compile-time bound (14 for the 112-wide
+// ResNet stem; 32 covers Q <= 256) — the accumulators of unused tiles would hold registers
+template <int R, int NT>
+__global__ __launch_bounds__(256, 2) void stem_direct_fwd_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ w, bf16* __restrict__ y,
+    float2* __restrict__ part, int H, int W, int P, int Q) {
+  constexpr int IR = 2 * (STEM_PB - 1) + R;      // staged input rows
+  extern __shared__ __attribute__((aligned(16))) char stem_lds[];
+  bf16* xin = (bf16*)stem_lds;                   // [IR][W][8]
+  const int rows = STEM_PB * Q;                  // output rows (pixels) of this block
+  bf16* ys = xin + ((IR * W * 8 + 7) & ~7);      // [rows][STEM_LDY]
+  const int blocks_per_img = P / STEM_PB;
+  const int n = blockIdx.x / blocks_per_img, p0 = (blockIdx.x - n * blocks_per_img) * STEM_PB;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // the input rows 2*p0 .. 2*p0+IR-1 of image n are one contiguous span of IR*W*16 bytes
+  {
+    const bf16x8* src = (const bf16x8*)(x + ((long)n * H + 2 * p0) * W * 8);
+    bf16x8* dst = (bf16x8*)xin;
+    const int chunks = IR * W;
+    for (int i = threadIdx.x; i < chunks; i += 256) dst[i] = src[i];
+  }
+  // weight fragments: channel 16*wid + (lane & 15), k = r*32 + (lane >> 4)*8 .. +7
+  bf16x8 wf[R];
+  const bf16* wrow = w + (long)(16 * wid + (lane & 15)) * (R * 32) + (lane >> 4) * 8;
+#pragma unroll
+  for (int r = 0; r < R; ++r) wf[r] = *(const bf16x8*)(wrow + r * 32);
+  __syncthreads();
+  // output row tile mt: pixel row p0 + mt / (Q/16), columns (mt % (Q/16))*16 .. +15
+  constexpr int MAXT = NT;
+  const int nt = rows / 16, tq = Q / 16;
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (t < nt) {
+      const int pl = t / tq, q0 = (t - pl * tq) * 16;
+      const bf16* a0 = xin + ((2 * pl) * W + q0 + (lane & 15) + (lane >> 4)) * 8;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(a0 + r * W * 8), wf[r],
+                                                         acc[t], 0, 0, 0);
+    }
+  }
+  // BatchNorm partials of this block's rows for the wave's 16 channels: (mean, M2), exact
+  // two-pass over the accumulators, then merged over the four lane groups (equal counts)
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t)
+    if (t < nt) sum += (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float mean = sum / (float)rows;
+  float m2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t)
+    if (t < nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = acc[t][j] - mean;
+        m2 += d * d;
+      }
+  m2 += __shfl_xor(m2, 16, 64);
+  m2 += __shfl_xor(m2, 32, 64);
+  if (part && lane < 16)
+    part[(long)(16 * wid + lane) * gridDim.x + blockIdx.x] = make_float2(mean, m2);
+  // stage bf16 rows through LDS, then the block's output (rows contiguous pixels x 64
+  // channels) goes out as 16-B stores
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t)
+    if (t < nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ys[(t * 16 + (lane >> 4) * 4 + j) * STEM_LDY + 16 * wid + (lane & 15)] =
+            from_f<bf16>(acc[t][j]);
+  __syncthreads();
+  bf16x8* yo = (bf16x8*)(y + ((long)n * P + p0) * Q * 64);
+  for (int i = threadIdx.x; i < rows * 8; i += 256)
+    yo[i] = *(const bf16x8*)(ys + (i >> 3) * STEM_LDY + (i & 7) * 8);
+}
+
+static size_t stem_direct_lds(const ConvGeom& g) {
+  const int IR = 2 * (STEM_PB - 1) + g.R;
+  return (size_t)((IR * g.W * 8 + 7) & ~7) * 2 + (size_t)STEM_PB * g.Q * STEM_LDY * 2;
+}
+
+static int stem_direct_fwd(const ConvGeom& g, const void* x, const void* w, void* y,
+                           float* stats, hipStream_t st) {
+  const int blocks = g.N * (g.P / STEM_PB);
+  const size_t lds = stem_direct_lds(g);
+  MMDX_CHECK_ARG(lds <= 64 * 1024 && g.Q <= 256, "stem direct: tile does not fit");
+#define STEM_LAUNCH(RR, TT)                                                                   \
+  hipLaunchKernelGGL((stem_direct_fwd_kernel<RR, TT>), dim3(blocks), dim3(256), lds, st,       \
+                     (const bf16*)x, (const bf16*)w, (bf16*)y, (float2*)stats, g.H, g.W, g.P, g.Q)
+  const bool q112 = STEM_PB * g.Q / 16 == 14;
+  if (g.R == 7) {
+    if (q112) STEM_LAUNCH(7, 14); else STEM_LAUNCH(7, 32);
+  } else {
+    if (q112) STEM_LAUNCH(8, 14); else STEM_LAUNCH(8, 32);
+  }
+#undef STEM_LAUNCH
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+// stat_rows: the rows per statistics slab the caller sized `stats` for (128; 2*Q selects the
+// direct stem kernel, which writes one slab per block); without stats the env knob decides
 template <typename T>
 static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
-                      float* stats, hipStream_t st) {
+                      float* stats, int stat_rows, hipStream_t st) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
+  const bool direct = stem_direct_geom(g) && std::is_same<T, bf16>::value &&
+                      (stats ? stat_rows == STEM_PB * g.Q : stem_direct_on());
+  MMDX_CHECK_ARG(!stats || direct || stat_rows == 128,
+                 "conv fwd: statistics slabs of %d rows (128, or %d for the direct stem)",
+                 stat_rows, STEM_PB * g.Q);
+  if constexpr (std::is_same<T, bf16>::value)
+    if (direct) return stem_direct_fwd(g, x, w, y, stats, st);
   if (g.C % KTile<T>::BK == 0 && is_pointwise(g))  // x itself is the [M][C] A operand
     return conv_gemm<T>(PointFwdK<T>{{(const T*)x, g.C, M, true}}, w, y, M, N, K, 0.f, st,
                         stats, dma_geom_ok(g, false, 32, M));
@@ -480,6 +621,15 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   }
   p.bm = M <= 64 ? 64 : 128;
   p.bn = N <= 64 ? 64 : 128;
+  if (dtype == BF16 && stem_direct_geom(geom(d)) && d->R == 7) {
+    // the pixel-pair stem: K splits of whole 2-row pixel tiles (~256 splits), the layout the
+    // direct kernel needs; the implicit-GEMM kernel takes the same splits (same sums)
+    const long tile_px = (long)STEM_PB * d->Q, ptiles = K / tile_px;
+    const long tps = (ptiles + 255) / 256;
+    p.kper = (int)(tps * tile_px);
+    p.splits = (int)((ptiles + tps - 1) / tps);
+    return p;
+  }
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
   const long ktiles = (K + BK - 1) / BK;
   // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small).
@@ -494,6 +644,138 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   p.kper = (int)(kt_per * BK);
   p.splits = (int)((K + p.kper - 1) / p.kper);
   return p;
+}
+
+// ---------------------------------------------------------------------------------------
+// Direct stem weight gradient (the pixel-pair stem of stem_direct_fwd_kernel): dW'[k][kk] =
+// sum over pixels of dy[pixel][k] * x_pair[2p + r][q + s][c], kk = (r*4 + s)*8 + c.  As an
+// implicit GEMM its B operand is the same 14x re-read of the pair image; here a block owns one
+// K split of the plan (plan_wgrad: whole 2-row pixel tiles), stages each tile's dy rows
+// (224 pixels x 64 channels, k-lines padded to 144 B) and its input rows in LDS, and reads
+// both MFMA operands k-major with ds_read_b64_tr_b16 straight from them: the x operand's
+// k-line of pixel (p, q) at tap (r, s) is the 16-B pair chunk [2p + r][q + s] — consecutive
+// pixels are consecutive chunks, so no im2col exists anywhere.  The next tile's rows are
+// fetched into registers while the current one is multiplied.  Partials go to the plan's
+// split-K workspace in its [split][k][kk] layout and are reduced by wgrad_reduce as before.
+// Waves: 2 output-channel halves (2 m-tiles each) x 4 groups of tap columns (4, 4, 3, 3 of the
+// 14 n-tiles).
+// ---------------------------------------------------------------------------------------
+constexpr int STEM_LDD = 72;  // staged dy k-line (bf16): 64 channels + pad (conflict-free tr)
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* lo, const bf16* hi) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int R>
+__global__ __launch_bounds__(512, 1) void stem_direct_wgrad_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ ws, int H,
+    int W, int P, int Q, int tiles_per_split, int tiles_total) {
+  constexpr int IR = 2 * (STEM_PB - 1) + R;
+  constexpr int M = 64, N = R * 32;                 // k_out, kk
+  constexpr int NTT = N / 16;                        // n-tiles (14 for R = 7)
+  extern __shared__ __attribute__((aligned(16))) char stem_lds[];
+  const int rows = STEM_PB * Q;                      // pixels per tile
+  bf16* dys = (bf16*)stem_lds;                       // [rows][STEM_LDD]
+  bf16* xin = dys + rows * STEM_LDD;                 // [IR][W][8]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int mh = wid & 1, ng = wid >> 1;             // m-tiles 2mh, 2mh+1; n-tile group
+  static_assert(NTT >= 12 && NTT <= 16, "4 groups of 3-4 n-tiles");
+  // groups of 4, 4, then the rest split evenly (R = 7: 4, 4, 3, 3 of 14)
+  const int ntn = ng < 2 ? 4 : (ng == 2 ? (NTT - 8) / 2 : NTT - 8 - (NTT - 8) / 2);
+  const int nt0 = ng < 3 ? ng * 4 : 8 + (NTT - 8) / 2;
+  const int bpi = P / STEM_PB;
+  const int t0 = blockIdx.x * tiles_per_split;
+  const int nt = min(tiles_per_split, tiles_total - t0);  // the last split may be short
+  // per-thread 16-B chunks of one tile: dy rows*8 chunks, x IR*W chunks
+  constexpr int DYC = 4, XC = 3;                     // chunks per thread (rows <= 256, W <= 512)
+  bf16x8 rdy[DYC], rx[XC];
+  const int ndy = rows * 8, nx = IR * W;
+  auto fetch = [&](int t) {
+    const int n = t / bpi, p0 = (t - n * bpi) * STEM_PB;
+    const bf16x8* sdy = (const bf16x8*)(dy + ((long)n * P + p0) * Q * 64);
+    const bf16x8* sx = (const bf16x8*)(x + ((long)n * H + 2 * p0) * W * 8);
+#pragma unroll
+    for (int j = 0; j < DYC; ++j) {
+      const int i = threadIdx.x + j * 512;
+      if (i < ndy) rdy[j] = sdy[i];
+    }
+#pragma unroll
+    for (int j = 0; j < XC; ++j) {
+      const int i = threadIdx.x + j * 512;
+      if (i < nx) rx[j] = sx[i];
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < DYC; ++j) {
+      const int i = threadIdx.x + j * 512;
+      if (i < ndy) *(bf16x8*)(dys + (i >> 3) * STEM_LDD + (i & 7) * 8) = rdy[j];
+    }
+#pragma unroll
+    for (int j = 0; j < XC; ++j) {
+      const int i = threadIdx.x + j * 512;
+      if (i < nx) *(bf16x8*)(xin + i * 8) = rx[j];
+    }
+  };
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment lane roles (ds_read_b64_tr_b16): group g reads k-lines 8g + qq (and + 4),
+  // columns 4pp .. 4pp+3 of the 16-column tile
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  fetch(t0);
+  stage();
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) fetch(t0 + t + 1);  // in flight during the MFMAs
+    const int ksteps = rows / 32;
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const int k_lo = ks * 32 + 8 * g + qq, k_hi = k_lo + 4;   // this lane's two pixels
+      bf16x8 af[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int col = (2 * mh + a) * 16 + 4 * pp;
+        af[a] = tr_frag(dys + k_lo * STEM_LDD + col, dys + k_hi * STEM_LDD + col);
+      }
+      // x operand: pixel (pl, q) -> pair chunk [2 pl + r][q + s], channel 4 (pp & 1)
+      const int pl_lo = k_lo >= Q, q_lo = k_lo - pl_lo * Q;
+      const int pl_hi = k_hi >= Q, q_hi = k_hi - pl_hi * Q;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (b < ntn) {
+          const int tap = (nt0 + b) * 2 + (pp >> 1), r = tap >> 2, sx = tap & 3;
+          const int cofs = (pp & 1) * 4;
+          const bf16x8 bf =
+              tr_frag(xin + ((2 * pl_lo + r) * W + q_lo + sx) * 8 + cofs,
+                      xin + ((2 * pl_hi + r) * W + q_hi + sx) * 8 + cofs);
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf, acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with this tile's LDS rows
+    if (t + 1 < nt) {
+      stage();
+      __syncthreads();
+    }
+  }
+  // partial slab of this split: ws[z][k][kk]
+  float* o = ws + (long)blockIdx.x * M * N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < ntn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[((2 * mh + a) * 16 + (lane >> 4) * 4 + j) * N + (nt0 + b) * 16 + (lane & 15)] =
+              acc[a][b][j];
 }
 
 template <typename T, class SB>
@@ -536,6 +818,22 @@ static int conv_wgrad_t(const mmdx_conv_desc* d, int cm, const void* x, const vo
   const Im2colR<T> sb = make_im2colr<T>((const T*)x, g, N);  // one 64-pixel K tile per issue
   EpiPartial epi{(float*)ws, M, N};
   int rc;
+  if constexpr (sizeof(T) == 2) {
+    // the pixel-pair stem: whole 2-row pixel tiles per split -> the direct kernel
+    const int tile_px = STEM_PB * g.Q;
+    if (stem_direct_geom(g) && stem_direct_on() && g.R == 7 && p.kper % tile_px == 0 &&
+        K % tile_px == 0 && tile_px <= 256 && g.W * (2 * (STEM_PB - 1) + g.R) <= 3 * 512) {
+      const size_t lds = (size_t)tile_px * STEM_LDD * 2 +
+                         (size_t)(2 * (STEM_PB - 1) + g.R) * g.W * 16;
+      hipLaunchKernelGGL(stem_direct_wgrad_kernel<7>, dim3(p.splits), dim3(512), lds, st,
+                         (const bf16*)x, (const bf16*)dy, (float*)ws, g.H, g.W, g.P, g.Q,
+                         p.kper / tile_px, K / tile_px);
+      MMDX_LAUNCH_CHECK();
+      wgrad_reduce((const float*)ws, p.splits, g.K, g.C, cm, g.R * g.S, dw, beta, st);
+      MMDX_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if constexpr (sizeof(T) == 2) {
    if (dma_geom_ok(g, false, 1 << 30) && K < (1 << 23)) {
     // LDS-DMA wgrad: both operands R-major (M = Kout and N = R*S*C are multiples of 8).  A
@@ -611,18 +909,32 @@ extern "C" int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int 
   return 0;
 }
 
-extern "C" int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d) {
-  return (int)(((long)d->N * d->P * d->Q + 127) / 128);
+extern "C" int mmdx_conv_fwd_stat_rows(const mmdx_conv_desc* d) {
+  return stem_direct_geom(geom(d)) && stem_direct_on() ? STEM_PB * d->Q : 128;
 }
 
-extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,
-                             const void* w, void* y, float* stat_part, void* stream) {
+extern "C" int mmdx_conv_fwd_stat_blocks(const mmdx_conv_desc* d) {
+  const long rpb = mmdx_conv_fwd_stat_rows(d);
+  return (int)(((long)d->N * d->P * d->Q + rpb - 1) / rpb);
+}
+
+extern "C" int mmdx_conv_fwd_rows(int dtype, const mmdx_conv_desc* d, const void* x,
+                                  const void* w, void* y, float* stat_part, int stat_rows,
+                                  void* stream) {
   MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_fwd: fp16 is the C5 path only");
   int rc = check_desc(d, dtype == BF16 ? 8 : 4);
   if (rc) return rc;
   MMDX_CHECK_ARG((long)d->N * d->P * d->Q < (1L << 31), "conv fwd: too many pixels");
-  if (dtype == BF16) return conv_fwd_t<bf16>(d, x, w, y, stat_part, (hipStream_t)stream);
-  return conv_fwd_t<float>(d, x, w, y, stat_part, (hipStream_t)stream);
+  if (dtype == BF16)
+    return conv_fwd_t<bf16>(d, x, w, y, stat_part, stat_rows, (hipStream_t)stream);
+  return conv_fwd_t<float>(d, x, w, y, stat_part, stat_rows, (hipStream_t)stream);
+}
+
+extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,
+                             const void* w, void* y, float* stat_part, void* stream) {
+  MMDX_CHECK_ARG(d, "conv fwd: null descriptor");
+  return mmdx_conv_fwd_rows(dtype, d, x, w, y, stat_part,
+                            dtype == BF16 ? mmdx_conv_fwd_stat_rows(d) : 128, stream);
 }
 
 extern "C" int mmdx_conv_fwd_bn_eval(int dtype, const mmdx_conv_desc* d, const void* x,

@@ -41,7 +41,10 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_CONV_PACK:
       return mmdx_conv_pack_weight(o.dtype, &o.d, o.i[0], (const float*)P(o, 0, ext),
                                    P(o, 1, ext), P(o, 2, ext), s);
-    case MMDX_OP_CONV_FWD:
+    case MMDX_OP_CONV_FWD:  // i: rows per statistics slab (0: mmdx_conv_fwd's default)
+      if (o.i[0] > 0)
+        return mmdx_conv_fwd_rows(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
+                                  (float*)P(o, 3, ext), o.i[0], s);
       return mmdx_conv_fwd(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
                            (float*)P(o, 3, ext), s);
     case MMDX_OP_CONV_FWD_BNEVAL:

@@ -357,7 +357,9 @@ class _Plan:
                          mean=None, rstd=None, wc=wc, pair=pair is not None)
                 units.append(u)
                 return y, d, u
-            fw.timed("fwd", L.OP_CONV_FWD, stream=st, dtype=dt, p=(x, wk, y, part), d=d)
+            rpb = L.lib().mmdx_conv_fwd_stat_rows(d)  # rows per statistics slab (part)
+            fw.timed("fwd", L.OP_CONV_FWD, stream=st, dtype=dt, i=(rpb if train else 0,),
+                     p=(x, wk, y, part), d=d)
             out = None if stats_only else A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
             mean = A.new((K,), torch.float32, dev)
@@ -370,7 +372,7 @@ class _Plan:
             # (one byte per 16-B channel vector) instead of re-reading its output
             rmask = (A.new((rows, K // vec), torch.uint8, dev)
                      if keep and relu and res is not None and out is not None else None)
-            fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, 128, wsn),
+            fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, rpb, wsn),
                    f=(bn.momentum, bn.eps), stream=st,
                    p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
                       res, out, _WS2 if st else _WS, rmask))

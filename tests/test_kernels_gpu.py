@@ -669,7 +669,9 @@ def test_stem_pixel_pair_conv(dev, cfg, beta):
            L.stream())
     _close(y.permute(0, 3, 1, 2), yr.detach(), dt, f"stem fwd {cfg}")
     M = N * d.P * d.Q
-    cnt = torch.tensor([min(128, M - 128 * b) for b in range(nst)], dtype=torch.float64)
+    rpb = L.lib().mmdx_conv_fwd_stat_rows(d)  # 128, or a direct-stem block's rows
+    assert nst == (M + rpb - 1) // rpb
+    cnt = torch.tensor([min(rpb, M - rpb * b) for b in range(nst)], dtype=torch.float64)
     pm, p2 = part[..., 0].t().double().cpu(), part[..., 1].t().double().cpu()
     mean = (pm * cnt[:, None]).sum(0) / M
     m2 = (p2 + cnt[:, None] * (pm - mean) ** 2).sum(0)
@@ -686,6 +688,66 @@ def test_stem_pixel_pair_conv(dev, cfg, beta):
     dw = dw0.to(dev)
     L.call("mmdx_stem_pair_grad", dwp.data_ptr(), K, C, k, k, dw.data_ptr(), beta, L.stream())
     _close(dw, wr.grad + beta * dw0, dt, f"stem wgrad {cfg}")
+
+
+@pytest.mark.parametrize("cfg", [(2, 3, 32, 32, 64, 7, 2, 3), (3, 3, 64, 96, 64, 7, 2, 3),
+                                 (4, 3, 224, 224, 64, 7, 2, 3)])
+def test_stem_direct_matches_implicit_gemm(dev, cfg, monkeypatch):
+    """The direct stem forward and weight gradient (input rows staged in LDS once, operand
+    fragments read from them; MMDX_STEM_DIRECT) against the implicit-GEMM kernels on the same
+    pixel-pair operands: the
+    same MFMA sequence per output, so y is BIT-IDENTICAL; its BatchNorm partials are per
+    block of 2 output rows (mmdx_conv_fwd_stat_rows) and merge to the same per-channel mean
+    and variance (fp64 host merge, rel 1e-5)."""
+    dt = torch.bfloat16
+    N, C, H, W, K, k, s, p = cfg
+    g = torch.Generator().manual_seed(11 + sum(cfg))
+    x = torch.randn(N, C, H, W, generator=g).to(dev)
+    w = (torch.randn(K, C, k, k, generator=g) * 0.1).to(dev)
+    d = L.ConvDesc()
+    L.call("mmdx_stem_pair_desc", N, C, H, W, K, k, k, s, p, d)
+    xp = torch.empty(N, d.H, d.W, 8, dtype=dt, device=dev)
+    L.call("mmdx_stem_pair_input", x.data_ptr(), N, C, H, W, p, xp.data_ptr(), L.stream())
+    wp = torch.empty(K, d.R, d.S, 8, dtype=dt, device=dev)
+    L.call("mmdx_stem_pair_pack_weight", w.data_ptr(), K, C, k, k, wp.data_ptr(), L.stream())
+    M = N * d.P * d.Q
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MMDX_STEM_DIRECT", mode)
+        rpb = L.lib().mmdx_conv_fwd_stat_rows(d)
+        nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
+        assert rpb == (128 if mode == "0" else 2 * d.Q)
+        y = torch.empty(N, d.P, d.Q, K, dtype=dt, device=dev)
+        part = torch.full((K, nst, 2), float("nan"), device=dev)
+        L.call("mmdx_conv_fwd", 1, d, xp.data_ptr(), wp.data_ptr(), y.data_ptr(),
+               part.data_ptr(), L.stream())
+        torch.cuda.synchronize()
+        assert torch.isfinite(part).all()
+        cnt = torch.tensor([min(rpb, M - rpb * b) for b in range(nst)], dtype=torch.float64)
+        pm, p2 = part[..., 0].t().double().cpu(), part[..., 1].t().double().cpu()
+        mean = (pm * cnt[:, None]).sum(0) / M
+        var = (p2 + cnt[:, None] * (pm - mean) ** 2).sum(0) / M
+        res[mode] = (y, mean, var)
+    assert torch.equal(res["0"][0], res["1"][0])
+    for j in (1, 2):
+        a, b = res["0"][j], res["1"][j]
+        assert ((a - b).abs() / b.abs().clamp(min=1e-3)).max().item() <= 1e-5, j
+    # weight gradient: the direct kernel (whole 2-row pixel tiles per K split, operands read
+    # k-major from the staged dy / input rows) sums the same 32-pixel groups in the same order
+    # into the same split-K slabs: bit-identical
+    dy = torch.randn(N, d.P, d.Q, K, generator=g).to(dev, dt)
+    ws_n = L.lib().mmdx_conv_wgrad_workspace_size(1, d)
+    ws = torch.empty(max(1, ws_n), dtype=torch.uint8, device=dev)
+    dws = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MMDX_STEM_DIRECT", mode)
+        dwp = torch.full((K, 8, d.R, d.S), float("nan"), device=dev)
+        L.call("mmdx_conv_wgrad", 1, d, 8, xp.data_ptr(), dy.data_ptr(), dwp.data_ptr(), 0.0,
+               ws.data_ptr(), ws_n, L.stream())
+        torch.cuda.synchronize()
+        dws[mode] = dwp
+    assert torch.isfinite(dws["1"]).all()
+    assert torch.equal(dws["0"], dws["1"])
 
 
 def test_stem_pixel_pair_rejects_odd_width(dev):

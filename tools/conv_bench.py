@@ -79,31 +79,45 @@ def main():
         Cp = (C + 7) // 8 * 8
         P = (H + 2 * p - k) // s + 1
         Q = (W + 2 * p - k) // s + 1
-        d = L.ConvDesc(B, H, W, Cp, K, k, k, s, s, p, p, P, Q)
-        x = torch.randn(B, H, W, Cp, device=dev).to(dt)
         wm = torch.randn(K, C, k, k, device=dev) * 0.05
-        wk = torch.empty(K, k, k, Cp, dtype=dt, device=dev)
-        wc = torch.empty(Cp, k, k, K, dtype=dt, device=dev)
-        L.call("mmdx_conv_pack_weight", dc, d, C, L.ptr(wm), L.ptr(wk), L.ptr(wc), L.stream())
+        # the bf16 stem runs as the pixel-pair conv the train step uses (resnet.py,
+        # mmdx_stem_pair_*): [B][H+2p][(W+2p)/2][8] pairs, R x ceil(k/2) taps, stride (2, 1)
+        pair = info["tag"] == "stem" and s == 2 and C <= 4 and (W + 2 * p) % 2 == 0
+        if pair:
+            d = L.ConvDesc()
+            L.call("mmdx_stem_pair_desc", B, C, H, W, K, k, k, s, p, d)
+            x = torch.randn(B, d.H, d.W, 8, device=dev).to(dt)
+            wk = torch.empty(K, d.R, d.S, 8, dtype=dt, device=dev)
+            L.call("mmdx_stem_pair_pack_weight", L.ptr(wm), K, C, k, k, L.ptr(wk), L.stream())
+            wc = None
+            dw = torch.empty(K, 8, d.R, d.S, device=dev)
+        else:
+            d = L.ConvDesc(B, H, W, Cp, K, k, k, s, s, p, p, P, Q)
+            x = torch.randn(B, H, W, Cp, device=dev).to(dt)
+            wk = torch.empty(K, k, k, Cp, dtype=dt, device=dev)
+            wc = torch.empty(Cp, k, k, K, dtype=dt, device=dev)
+            L.call("mmdx_conv_pack_weight", dc, d, C, L.ptr(wm), L.ptr(wk), L.ptr(wc),
+                   L.stream())
+            dw = torch.empty_like(wm)
         y = torch.empty(B, P, Q, K, dtype=dt, device=dev)
         dy = torch.randn(B, P, Q, K, device=dev).to(dt)
         dx = torch.empty_like(x)
-        dw = torch.empty_like(wm)
+        cw = 8 if pair else C
         nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
-        part = torch.empty(nst, K, 2, device=dev)
+        part = torch.empty(K, nst, 2, device=dev)
         wsn = L.lib().mmdx_conv_wgrad_workspace_size(dc, d)
         ws = torch.empty(max(wsn, 16), dtype=torch.uint8, device=dev)
         ops = {
             "fwd": lambda: L.call("mmdx_conv_fwd", dc, d, L.ptr(x), L.ptr(wk), L.ptr(y),
                                   L.ptr(part), L.stream()),
-            "wgrad": lambda: L.call("mmdx_conv_wgrad", dc, d, C, L.ptr(x), L.ptr(dy), L.ptr(dw),
+            "wgrad": lambda: L.call("mmdx_conv_wgrad", dc, d, cw, L.ptr(x), L.ptr(dy), L.ptr(dw),
                                     0.0, L.ptr(ws), wsn, L.stream()),
         }
-        if info["dgrad"]:
+        if info["dgrad"] and not pair:
             ops["dgrad"] = lambda: L.call("mmdx_conv_dgrad", dc, d, L.ptr(dy), L.ptr(wc),
                                           L.ptr(dx), 0.0, L.stream())
         macs = B * P * Q * K * C * k * k
-        xb, yb, wb = B * H * W * Cp * 2, B * P * Q * K * 2, K * Cp * k * k * 2
+        xb, yb, wb = x.numel() * 2, B * P * Q * K * 2, wk.numel() * 2
         nbytes = {"fwd": xb + wb + yb, "dgrad": yb + wb + xb, "wgrad": xb + yb + 2 * wb}
         for name, fn in ops.items():
             if name not in a.ops.split(","):
