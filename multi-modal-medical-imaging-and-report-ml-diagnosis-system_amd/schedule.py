@@ -106,6 +106,21 @@ class TowerEmbeddings(torch.nn.Module):
         return self.tower(args[0])["embeddings"]
 
 
+class _UsedParams(torch.nn.Module):
+    """TowerEmbeddings whose registered parameters are only those the embeddings path uses
+    (make_graphed_callables differentiates w.r.t. every registered parameter and refuses
+    unused ones — a tower's warm-up `classifier` head is not on that path).  The tower itself
+    is held unregistered; the parameters are the tower's own Parameter objects."""
+
+    def __init__(self, inner, params):
+        super().__init__()
+        object.__setattr__(self, "inner", inner)
+        self.used = torch.nn.ParameterList(params)
+
+    def forward(self, *args):
+        return self.inner(*args)
+
+
 def graph_tower(tower, sample_args, text, warmup=3):
     """Capture one encoder tower's forward and backward as two HIP graphs
     (torch.cuda.make_graphed_callables): a step then replays each with one host call instead
@@ -114,4 +129,10 @@ def graph_tower(tower, sample_args, text, warmup=3):
     stream (the text tower keeps its side stream), and draw fresh dropout masks per replay
     (the RNG counter advances on the device).  Returns the graphed callable."""
     mod = TowerEmbeddings(tower, text)
-    return torch.cuda.make_graphed_callables(mod, tuple(sample_args), num_warmup_iters=warmup)
+    params = [p for p in tower.parameters() if p.requires_grad]
+    out = mod(*sample_args)  # one eager pass finds the parameters the embeddings depend on
+    grads = torch.autograd.grad(out.float().sum(), params, allow_unused=True)
+    used = [p for p, g in zip(params, grads) if g is not None]
+    del out, grads
+    return torch.cuda.make_graphed_callables(_UsedParams(mod, used), tuple(sample_args),
+                                             num_warmup_iters=warmup)

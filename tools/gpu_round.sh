@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, headline bench, kernel-trace profile, two PMC passes.
 # usage (from the repo root, under gpurun): bash tools/gpu_round.sh <tag> <phases> [steps]
-#   phases: comma list of tests,abtest,bench,c5,c2,c3,gemmb,convb,convab,benchab,prof,pmc
+#   phases: comma list of tests,abtest,bench,c5,c2,c3,gemmb,convb,convab,benchab,prof,pmc,pmcm
 # Every GPU step has its own time limit; the script stops at the first step that faults,
 # aborts or times out (rc > 1), so nothing else touches the GPU after a failure.
 set -u
@@ -53,7 +53,10 @@ has pmc && step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d 
   -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
 has pmc && step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmcw_$tag" \
   -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+has pmcm && step pmc_mfma 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+  -d "$R/gpurun_out/pmcm_$tag" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
 cd "$R"
+has pmcm && python tools/pmc_mfma.py "gpurun_out/pmcm_$tag" -o "gpurun_out/${tag}_mfma_util.json"
 has pmc && python tools/pmc_traffic.py "gpurun_out/pmcf_$tag" "gpurun_out/pmcw_$tag" --config c4 \
   --batch 128 -o "gpurun_out/${tag}_conv_traffic.json"
 exit 0
