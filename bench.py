@@ -272,7 +272,7 @@ class StepTimer:
 
 
 def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd=None,
-              scaler=None, image_fn=None, text_fn=None):
+              scaler=None):
     """One train step.  `scaler` (mmdx.GradScaler, the fp16 C5 path): the loss
     is scaled before the backward (TP:1056), the clip coefficient is taken on the unscaled
     norm and folded with 1/scale into AdamW's gradient scale, an overflow skips the update
@@ -291,8 +291,8 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
         # both towers issued at once: the image trunk (one native plan call) from this
         # thread onto the main stream, the text tower (Python-issued) from a worker thread
         # onto the side stream
-        z_img, z_txt = towers(image_fn or (lambda: img(x)["embeddings"]),
-                              text_fn or (lambda: txt(input_ids=ids, attention_mask=mask)
+        z_img, z_txt = towers(lambda: img(x)["embeddings"],
+                              (lambda: txt(input_ids=ids, attention_mask=mask)
                                           ["embeddings"]))
         main.wait_stream(side)
         logits = fus(z_img, z_txt)["disease_logits"]
@@ -459,21 +459,7 @@ def main():
         RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
     # fp16 (C5): loss scaling with GradScaler semantics (TP:1025-1026, 1056-1061)
     scaler = mmdx.GradScaler() if dtype == torch.float16 else None
-    # MMDX_GRAPH_TOWERS: the towers whose forward + backward replay as HIP graphs
-    # ("text", "image", "both"; the ResNet trunk is a native launch plan already)
-    graphed = os.environ.get("MMDX_GRAPH_TOWERS", "0")
-    image_fn = text_fn = None
-    if graphed in ("text", "both"):
-        from mmdx.schedule import graph_tower
-        with torch.cuda.stream(side):
-            gt = graph_tower(txt, (ids, mask), text=True)
-        text_fn = lambda: gt(ids, mask)  # noqa: E731
-    if graphed in ("image", "both"):
-        from mmdx.schedule import graph_tower
-        gi = graph_tower(img, (x,), text=False)
-        image_fn = lambda: gi(x)  # noqa: E731
-    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler,
-                     image_fn=image_fn, text_fn=text_fn)
+    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler)
     timer = StepTimer()
     if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders
         MF.GEMM_TIMER = timer
@@ -567,7 +553,7 @@ def main():
         "dtype": "fp16" if dtype == torch.float16 else "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
-        "launch": "eager" if graphed == "0" else f"hip-graph towers: {graphed}",
+        "launch": "eager",
         "stream_priority": "main+text",
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,

@@ -302,11 +302,31 @@ static bool try_conv8(const SA& sa, const SB& sb, const Epi& epi, int M, int N, 
   return true;
 }
 
+static bool fold_probe_on() {
+  const char* e = getenv("MMDX_FOLD_PROBE");  // timing probe only (tools/conv_bench.py)
+  return e && atoi(e) != 0;
+}
+
 template <typename T, class SA, class Epi>
 static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int N, int K,
                          hipStream_t st, bool dma_ok) {
   DenseK<T> sb{(const T*)w, K, N, true};
   if constexpr (DmaOk<SA>::value) {
+    if (dma_ok && fold_probe_on()) {
+      const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+      const int bn = (N <= 64 || tiles128 < kNarrowBelow) ? 64 : 128;
+      const int nwg = ((M + 127) / 128) * ((N + bn - 1) / bn);
+      if (bn == 64)
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, SA>, DmaK<64, DenseK<T>>, Epi, 2,
+                                             bf16, NT, 2, 2, 1>),
+                           dim3(nwg), dim3(NT), 0, st, sa, sb, epi, M, N, K, K);
+      else
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA>, DmaK<128, DenseK<T>>, Epi,
+                                             2, bf16, NT, 2, 2, 1>),
+                           dim3(nwg), dim3(NT), 0, st, sa, sb, epi, M, N, K, K);
+      MMDX_LAUNCH_CHECK();
+      return 0;
+    }
     if (dma_ok) {
       if (try_conv8(sa, sb, epi, M, N, K, st)) {
         MMDX_LAUNCH_CHECK();

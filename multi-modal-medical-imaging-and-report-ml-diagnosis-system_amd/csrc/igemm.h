@@ -1599,8 +1599,15 @@ __device__ __forceinline__ void epilogue_pass(const Epi& epi, const float* cst, 
 // NTH = 512 (8 waves, one block per CU, 256 x 128 tiles, WM x WN = 4 x 2 waves of 64 x 64):
 // half the operand bytes per MFMA of two 128 x 128 blocks and twice the K tiles in flight
 // (NS = 3 stages of 48 KB) for the same LDS.
+// FOLD (timing probe, tools/conv_bench.py --fold-probe): after its DMAs of a K tile land,
+// every lane re-reads the A chunks it issued, applies y*s[c]+t[c] and ReLU with per-channel
+// coefficients loaded for the tile's channels, and writes them back before the barrier —
+// the operand-side work a BatchNorm-apply folded into the consumer conv would add
+// (DESIGN.md §8).  The coefficients are probe constants: the results are not meaningful.
+__device__ float g_fold_probe_coef[2 * 2048];
+
 template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16,
-          int NTH = NT, int WM = 2, int WN = 2>
+          int NTH = NT, int WM = 2, int WN = 2, int FOLD = 0>
 __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                            typename OB::SrcT sb, Epi epi, int M,
                                                            int N, int K, int kper) {
@@ -1675,6 +1682,26 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (FOLD) {
+      static_assert(!OA::RMAJOR, "fold probe: k-major A operand");
+      char* st = lds_raw + (t % NS) * STAGE;
+      const int c0 = (kbeg + t * BK + oa.coff) & 2047;
+      float sc[8], sh[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = g_fold_probe_coef[c0 + e];
+        sh[e] = g_fold_probe_coef[2048 + ((c0 + e) & 2047)];
+      }
+#pragma unroll
+      for (int j = 0; j < OA::INSTR; ++j) {
+        bf16x8* pch = (bf16x8*)(st + (j * OA::NW + wid) * 1024 + lane * 16);
+        bf16x8 v = *pch;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = from_f<bf16>(fmaxf(to_f(v[e]) * sc[e] + sh[e], 0.f));
+        *pch = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     const char* as = lds_raw + (t % NS) * STAGE;
     const char* bs = as + OA::BYTES;

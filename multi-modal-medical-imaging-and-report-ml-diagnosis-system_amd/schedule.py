@@ -88,51 +88,3 @@ def two_tower_backward(loss: torch.Tensor, z_img: torch.Tensor, z_txt: torch.Ten
         if on_text_done is not None:
             on_text_done()
     main.wait_stream(text_stream)
-
-
-class TowerEmbeddings(torch.nn.Module):
-    """`tower(...)["embeddings"]` as a module returning one tensor (what graph capture of a
-    tower's forward + backward needs): image towers take (images,), text towers
-    (input_ids, attention_mask)."""
-
-    def __init__(self, tower, text):
-        super().__init__()
-        self.tower = tower
-        self.text = text
-
-    def forward(self, *args):
-        if self.text:
-            return self.tower(input_ids=args[0], attention_mask=args[1])["embeddings"]
-        return self.tower(args[0])["embeddings"]
-
-
-class _UsedParams(torch.nn.Module):
-    """TowerEmbeddings whose registered parameters are only those the embeddings path uses
-    (make_graphed_callables differentiates w.r.t. every registered parameter and refuses
-    unused ones — a tower's warm-up `classifier` head is not on that path).  The tower itself
-    is held unregistered; the parameters are the tower's own Parameter objects."""
-
-    def __init__(self, inner, params):
-        super().__init__()
-        object.__setattr__(self, "inner", inner)
-        self.used = torch.nn.ParameterList(params)
-
-    def forward(self, *args):
-        return self.inner(*args)
-
-
-def graph_tower(tower, sample_args, text, warmup=3):
-    """Capture one encoder tower's forward and backward as two HIP graphs
-    (torch.cuda.make_graphed_callables): a step then replays each with one host call instead
-    of issuing the tower's ~50 kernel launches per layer from Python.  The graphs read
-    `sample_args` in place (copy a new batch into them), replay on the caller's current
-    stream (the text tower keeps its side stream), and draw fresh dropout masks per replay
-    (the RNG counter advances on the device).  Returns the graphed callable."""
-    mod = TowerEmbeddings(tower, text)
-    params = [p for p in tower.parameters() if p.requires_grad]
-    out = mod(*sample_args)  # one eager pass finds the parameters the embeddings depend on
-    grads = torch.autograd.grad(out.float().sum(), params, allow_unused=True)
-    used = [p for p, g in zip(params, grads) if g is not None]
-    del out, grads
-    return torch.cuda.make_graphed_callables(_UsedParams(mod, used), tuple(sample_args),
-                                             num_warmup_iters=warmup)

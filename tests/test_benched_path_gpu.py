@@ -325,7 +325,13 @@ def test_benched_step_reduced_precision_vs_oracle(dev, cfg):
              and not n.startswith(("image.backbone.encoder", "image.backbone.class_token",
                                    "image.backbone.conv_proj"))] + ["image.proj.weight"]
     trunk = [n for n in trunk if n in mine] if cfg != "c5" else []
-    bn = [n for n in mine if _is_bn(n)]
+    # trunk weight gradients that bf16 autocast itself gets at 1 - cos > 0.05 (e.g. layer1's
+    # first conv, whose Σ over 128 x 56 x 56 positions of a random-init trunk cancels like the
+    # BN gradients below) are rounding noise too: their error against fp32 is a fresh noise
+    # draw whenever any upstream rounding moves, so they join the distribution check
+    noisy = [n for n in trunk if auto[n][0] > 0.05]
+    trunk = [n for n in trunk if n not in noisy]
+    bn = [n for n in mine if _is_bn(n)] + noisy
     zero = _zero_grad_names(mine)
     _check_zero_grads(m["grads"], o32["grads"], zero, 2e-2)
     rest = [n for n in mine if n not in trunk and n not in bn and n not in zero]

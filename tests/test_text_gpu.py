@@ -317,3 +317,4 @@ def test_bert_train_mode_with_default_dropout(dev):
     with torch.no_grad():
         ev = mine(input_ids=ids, attention_mask=mask)["embeddings"]
     assert not torch.allclose(ev.float(), out["embeddings"].detach().float())
+
