@@ -445,18 +445,25 @@ def main():
     if vit and os.environ.get("MMDX_DP_BUCKET_DTYPE", "bf16") == "bf16":
         bdt = torch.bfloat16
     reducer = GradAllReducer(params, world, rehearse=dp, bucket_dtype=bdt) if dp else None
-    # Opt-in: the trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward, each
-    # from its own plan event (RCCL: a comm stream waits on the event, no host wait).  Off by
-    # default: in the one-rank RCCL rehearsal it costs 0.43 ms/step (15.83 vs 15.40 ms) — the
-    # comm and RCCL streams' event waits share the process's 4 hardware queues with the text
-    # and weight-gradient streams and hold their work back — about what it could hide of the
-    # 94 MB trunk all-reduce at 8 GPUs.  The text tower's and fusion head's buckets still
-    # start as soon as their gradients are final (MMDX_DP_TEXT_EARLY, on: 0.08 ms here,
-    # ~66 MB of the collective hidden at N > 1).  gloo's CUDA path would stall the issuing
-    # host thread on the event (1.3 s/step in the one-GPU rehearsal).
-    early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "0")
-    if reducer is not None and early_tail != "0":
+    # The trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward.  The first
+    # version waited on a plan event from a comm stream: in the one-rank RCCL rehearsal it
+    # cost 0.43 ms/step (15.83 vs 15.40 ms) — the comm and RCCL streams' event waits share
+    # the process's 4 hardware queues with the text and weight-gradient streams.  The text
+    # tower's and fusion head's buckets start as soon as their gradients are final
+    # (MMDX_DP_TEXT_EARLY, on: 0.08 ms here, ~66 MB of the collective hidden at N > 1).
+    # gloo's CUDA path would stall the issuing host thread (1.3 s/step in the one-GPU
+    # rehearsal), so gloo keeps the after-backward reduce.
+    # Default (RCCL): the trunk backward plan is replayed in per-layer segments and the
+    # all-reduce of layers 4, 3, 2's gradient slices is issued between them from the
+    # weight-gradient stream itself (resnet.TRUNK_SEGMENT_HOOK): no comm stream, no event
+    # waits beyond RCCL's own, so the process stays within its 4 hardware queues (main, text,
+    # weight-gradient, RCCL).  MMDX_DP_EARLY_TAIL=event: the comm-stream variant above;
+    # 0: the whole arena after the backward.
+    early_tail = os.environ.get("MMDX_DP_EARLY_TAIL", "seg" if backend == "nccl" else "0")
+    if reducer is not None and early_tail == "event":
         RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
+    elif reducer is not None and early_tail not in ("0", ""):
+        RN.TRUNK_SEGMENT_HOOK = reducer.trunk_segment
     # fp16 (C5): loss scaling with GradScaler semantics (TP:1025-1026, 1056-1061)
     scaler = mmdx.GradScaler() if dtype == torch.float16 else None
     step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler)

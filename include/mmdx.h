@@ -553,6 +553,14 @@ int mmdx_grad_norm(int nchunks, const mmdx_adamw_tensor* table, float max_norm, 
 /* in-place g *= scale[0] over the .g fields (the mul_ of clip_grad_norm_) */
 int mmdx_scale_grads(int nchunks, const mmdx_adamw_tensor* table, const float* scale,
                      void* stream);
+/* Refresh the .g column of a device chunk table in stream order, without a host->device
+ * copy (the optimizer's gradient buffers move between steps): row r, whose tensor index is
+ * row_tensor[r] (a DEVICE int array built with the table), gets
+ * g = grads[row_tensor[r]] + off.  `grads` is a HOST array of n_tensors device pointers;
+ * they travel as kernel arguments (256 per launch).  A small hipMemcpyAsync from pinned
+ * memory made the issuing host thread wait for the stream on this runtime. */
+int mmdx_adamw_patch_grads(int nchunks, mmdx_adamw_tensor* table, const int* row_tensor,
+                           int n_tensors, const float* const* grads, void* stream);
 
 /* Mixed-precision loss scaling: torch.cuda.amp.GradScaler as the fusion loop drives it
  * (TP:1025-1026 GradScaler(enabled=use_amp), TP:1056 scaler.scale(loss).backward(), TP:1058

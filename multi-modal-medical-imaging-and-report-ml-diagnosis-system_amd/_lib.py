@@ -166,6 +166,7 @@ SIGNATURES = {
     "mmdx_grad_norm_workspace_size": (sz, [i32]),
     "mmdx_grad_norm": (i32, [i32, vp, f32, vp, vp, vp, sz, vp]),
     "mmdx_scale_grads": (i32, [i32, vp, vp, vp]),
+    "mmdx_adamw_patch_grads": (i32, [i32, vp, vp, i32, vp, vp]),
     "mmdx_grad_norm_amp": (i32, [i32, vp, f32, vp, i32, vp, vp, vp, vp, sz, vp]),
     "mmdx_adamw_multi_amp": (i32, [i32, vp, f32, f32, f32, vp, vp, vp, vp]),
     "mmdx_amp_update_scale": (i32, [vp, vp, vp, f32, f32, i32, vp]),

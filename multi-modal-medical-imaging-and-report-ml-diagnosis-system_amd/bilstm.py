@@ -129,8 +129,6 @@ class _LSTMLayerFn(torch.autograd.Function):
         call("mmdx_lstm_fwd", L.dtype_code(T), ptr(xg), ptr(whh), B, Ls, H, ptr(hout), ptr(cs),
              ptr(gs), ptr(fws), fw, ptr(status.word) if status else None,
              int(DEBUG["spin_limit"]), int(DEBUG["flags"]), stream())
-        if status is not None:
-            status.after_launch()
         ctx.save_for_backward(x, wih, whh, hout, cs, gs)
         ctx.H = H
         return hout
@@ -234,4 +232,9 @@ class BiLSTMEncoder(nn.Module):
                 getattr(m, "weight_ih" + sfx + "_reverse"),
                 getattr(m, "weight_hh" + sfx + "_reverse"),
                 getattr(m, "bias_ih" + sfx + "_reverse"), getattr(m, "bias_hh" + sfx + "_reverse"))
+        # the status word is sticky: one device->host copy after the last layer covers every
+        # cooperative launch of this forward
+        st = _STATUS.get((h.device.type, h.device.index))
+        if st is not None:
+            st.after_launch()
         return _Out(last_hidden_state=h)

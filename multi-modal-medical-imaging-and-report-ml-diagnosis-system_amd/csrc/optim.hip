@@ -153,6 +153,22 @@ __global__ void mul_dev_scalar_kernel(const float* __restrict__ x, long n,
     out[i] = x[i] * v;
 }
 
+// Per-step refresh of the table's gradient column from kernel arguments (no host->device
+// copy): row r of tensor t = row_tensor[r] in [t0, t0 + n) gets g = grads[t - t0] + off.
+constexpr int kPatchPtrs = 256;
+struct PatchArgs { const float* g[kPatchPtrs]; };
+
+__global__ __launch_bounds__(256) void patch_grads_kernel(mmdx_adamw_tensor* __restrict__ tab,
+                                                          const int* __restrict__ row_tensor,
+                                                          int nchunks, int t0, int n,
+                                                          PatchArgs a) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nchunks) return;
+  const int t = row_tensor[r] - t0;
+  if (t < 0 || t >= n) return;
+  tab[r].g = a.g[t] + tab[r].off;
+}
+
 }  // namespace mmdx
 
 using namespace mmdx;
@@ -230,6 +246,23 @@ extern "C" int mmdx_scale_grads(int nchunks, const mmdx_adamw_tensor* table, con
   MMDX_CHECK_ARG(nchunks > 0 && table && scale, "scale_grads: bad args");
   hipLaunchKernelGGL(scale_grads_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, table,
                      scale);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_adamw_patch_grads(int nchunks, mmdx_adamw_tensor* table,
+                                      const int* row_tensor, int n_tensors,
+                                      const float* const* grads, void* stream) {
+  MMDX_CHECK_ARG(nchunks > 0 && table && row_tensor && grads && n_tensors > 0,
+                 "adamw_patch_grads: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  for (int t0 = 0; t0 < n_tensors; t0 += kPatchPtrs) {
+    PatchArgs a{};
+    const int n = std::min(kPatchPtrs, n_tensors - t0);
+    for (int j = 0; j < n; ++j) a.g[j] = grads[t0 + j];
+    hipLaunchKernelGGL(patch_grads_kernel, dim3((nchunks + 255) / 256), dim3(256), 0, st, table,
+                       row_tensor, nchunks, t0, n, a);
+  }
   MMDX_LAUNCH_CHECK();
   return 0;
 }

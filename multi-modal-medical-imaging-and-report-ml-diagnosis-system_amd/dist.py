@@ -67,6 +67,20 @@ class GradAllReducer:
         for lo, hi, ev in regions:
             self.launch_region(grads, lo, hi, ev)
 
+    def trunk_segment(self, buf, lo: int, hi: int):
+        """resnet.TRUNK_SEGMENT_HOOK: all-reduce buf[lo:hi] in place, issued from the current
+        stream right after the last writer of the slice was enqueued on it.  With RCCL the
+        collective's stream waits on the current stream, so it starts when the slice is
+        final while the rest of the backward keeps running; no comm stream, no event, no
+        copy (nothing reads or writes the slice again before finish())."""
+        if not self.active or hi <= lo:
+            return
+        part = buf[lo:hi]
+        work = dist.all_reduce(part, op=self._op(part), group=self.group, async_op=True)
+        self._pending.append((None, part, work, None))
+        off = buf.storage_offset()
+        self._regions.setdefault(_store_key(buf), []).append((off + lo, off + hi))
+
     def launch_region(self, buf, lo: int, hi: int, event=None):
         """Start the all-reduce of the slice buf[lo:hi] of a flat gradient buffer once
         `event` (a torch.cuda.Event recorded after the slice is final) has fired; the rest of

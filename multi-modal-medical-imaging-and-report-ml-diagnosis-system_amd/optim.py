@@ -56,9 +56,13 @@ _CAPTURED: list = []  # staging buffers referenced by captured graphs: they must
 
 class _Plan:
     """Chunk table of one parameter set: every tensor split into <= CHUNK-element pieces,
-    one workgroup each.  Everything but the gradient pointers is built once; per step only
-    the gradient column is refreshed (numpy) and copied to the device through a small ring
-    of pinned staging buffers (skipped when the gradient buffers did not move)."""
+    one workgroup each.  The table lives on the device; everything but the gradient pointers
+    is fixed when it is built.  Per step only the gradient column changes (the gradient
+    buffers move between steps): mmdx_adamw_patch_grads rewrites it in stream order from
+    kernel arguments, skipped when no gradient moved.  (A per-step hipMemcpyAsync of the table
+    from pinned memory blocked the issuing thread until the stream reached it: 2.2 ms of host
+    time per C4 step in the r03h host profile, and an idle GPU queue behind it.)  A learning-
+    rate / weight-decay change re-uploads the whole table through pinned staging buffers."""
 
     RING = 3
 
@@ -76,31 +80,41 @@ class _Plan:
         self.tidx = np.asarray(tidx, dtype=np.int64)
         self.boff = np.asarray(boff, dtype=np.uint64)
         self.n = len(rows)
+        self.ntensors = len(params)
         self.nbytes = self.desc.nbytes
         self.dev = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+        self.row_tensor = torch.from_numpy(self.tidx.astype(np.int32)).to(device)
         self.ring = [torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
                      for _ in range(self.RING)]
         self.events = [None] * self.RING
         self.k = 0
         self.last = None
+        self.full = True   # the device table needs a whole upload (new, or lr/wd changed)
         self.hyper = (tuple(lrs), tuple(wds))
         _reserve_spare(self.nbytes)
 
     def set_hyper(self, lrs, wds):
         """A learning-rate / weight-decay change (scheduler, param_group edit) rewrites the
-        table's lr/wd columns in place; the next upload ships them."""
+        table's lr/wd columns in place; the next upload ships the whole table."""
         hyper = (tuple(lrs), tuple(wds))
         if hyper == self.hyper:
             return
         self.hyper = hyper
         self.desc["lr"] = np.asarray(lrs, dtype=np.float32)[self.tidx]
         self.desc["wd"] = np.asarray(wds, dtype=np.float32)[self.tidx]
-        self.last = None
+        self.full = True
 
     def upload(self, grads):
         gp = np.fromiter((g.data_ptr() for g in grads), dtype=np.uint64, count=len(grads))
         capturing = torch.cuda.is_current_stream_capturing()
-        if not capturing and self.last is not None and np.array_equal(gp, self.last):
+        if not self.full:
+            if not capturing and self.last is not None and np.array_equal(gp, self.last):
+                return
+            self.desc["g"] = gp[self.tidx] + self.boff
+            arr = (C.c_void_p * len(gp))(*gp.tolist())
+            call("mmdx_adamw_patch_grads", self.n, ptr(self.dev), ptr(self.row_tensor),
+                 self.ntensors, arr, stream())
+            self.last = None if capturing else gp
             return
         self.desc["g"] = gp[self.tidx] + self.boff
         if capturing:  # the graph keeps reading this buffer: never reuse it
@@ -119,6 +133,7 @@ class _Plan:
             ev.record()
             self.events[self.k] = ev
             self.k = (self.k + 1) % self.RING
+            self.full = False
 
 
 def _plan_for(cache: dict, params, ms, vs, lrs, wds, device):

@@ -242,20 +242,38 @@ class _OpList:
         self.add(L.OP_EVENT, i=(2 * k + 1,), stream=stream)
         self.conv_names.append(name)
 
+    def cut(self):
+        """Segment boundary at the current end of the list: run(between=...) returns to the
+        caller here (the data-parallel hook issues a layer's all-reduce from the host
+        between two segments, with nothing but the plan's own streams)."""
+        self.cuts = getattr(self, "cuts", []) + [len(self.ops)]
+
     def freeze(self):
         arr = (L.PlanOp * len(self.ops))(*self.ops)
         self.arr, self.n = arr, len(self.ops)
+        self.bounds = [0] + [c for c in getattr(self, "cuts", []) if 0 < c < self.n] + [self.n]
         self.ops = None
         return self
 
-    def run(self, ext, streams):
+    def run(self, ext, streams, between=None):
+        """Replay the list.  between(k): called after segment k (k = 0 .. cuts-1) is
+        enqueued and before segment k+1 is; None = one native call for the whole list."""
         exts = (ctypes.c_void_p * max(1, len(ext)))(*ext)
         sts = (ctypes.c_void_p * len(streams))(*streams)
         evs = None
         if CONV_TIMER.active and self.conv_names:
             evs = CONV_TIMER.take(self.conv_names)
             evs = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
-        call("mmdx_plan_run", self.arr, self.n, exts, evs, sts, len(streams))
+        if between is None or len(self.bounds) == 2:
+            call("mmdx_plan_run", self.arr, self.n, exts, evs, sts, len(streams))
+            return
+        sz = ctypes.sizeof(L.PlanOp)
+        base = ctypes.addressof(self.arr)
+        for k, (a, z) in enumerate(zip(self.bounds[:-1], self.bounds[1:])):
+            seg = ctypes.cast(base + a * sz, ctypes.POINTER(L.PlanOp))
+            call("mmdx_plan_run", seg, z - a, exts, evs, sts, len(streams))
+            if k < len(self.bounds) - 2:
+                between(k)
 
 
 class _Arena:
@@ -623,6 +641,7 @@ class _Plan:
                 if bi in done_at:
                     li = done_at[bi]
                     bw.add(L.OP_SIGNAL, p=(A.event(),), stream=1)
+                    bw.cut()  # TRUNK_SEGMENT_HOOK runs here (region k = segment k)
                     self.grad_regions.append((layer_lo[li], layer_hi[li], A.bufs[-1]))
                     if li == 3:
                         self.tail_event = A.bufs[-1]
@@ -695,8 +714,17 @@ class _Plan:
 # TRUNK_GRAD_HOOK(grads, regions): called right after the trunk backward is enqueued with the
 # flat fp32 gradient arena and [(lo, hi, event)] for layers 4, 3, 2 (backward order): after
 # `event` fires, grads[lo:hi] is final (data parallelism: start that slice's all-reduce
-# early, dist.GradAllReducer.launch_region).  None = no hook.
+# early from a comm stream waiting on the event, dist.GradAllReducer.launch_region).
+# None = no hook.
 TRUNK_GRAD_HOOK = None
+
+# TRUNK_SEGMENT_HOOK(grads, lo, hi): the backward plan is replayed in segments, one per layer
+# 4, 3, 2, and the hook is called between them with the weight-gradient stream current:
+# everything that writes grads[lo:hi] is already enqueued on that stream (its wgrads wait for
+# the layer's BN backward), so a collective issued from it (RCCL: its stream waits on the
+# current one) starts when the slice is final, with no stream or event of its own
+# (dist.GradAllReducer.trunk_segment).  Takes precedence over TRUNK_GRAD_HOOK.  None = off.
+TRUNK_SEGMENT_HOOK = None
 
 # Downsample branch of the forward on the side stream (False: in order on the main stream;
 # read when a plan is built — for A/B runs, tools/step_probe.py --ds-main).
@@ -780,9 +808,19 @@ class _TrunkFn(torch.autograd.Function):
         # weight gradients on a side stream (in order on the main stream measured 9.5 %
         # slower at C4: 7128 vs 7876 samples/s)
         side = _side_stream(ctx.trunk_ref, dev)
-        plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0], [stream(), side.cuda_stream])
+        seg_hook = TRUNK_SEGMENT_HOOK
+        between = None
+        if seg_hook is not None and plan.grad_regions:
+            regions = plan.grad_regions
+
+            def between(k):
+                lo, hi, _ev = regions[k]
+                with torch.cuda.stream(side):
+                    seg_hook(grads, lo, hi)
+        plan.bwd.run([dfeats.data_ptr(), grads.data_ptr(), x0], [stream(), side.cuda_stream],
+                     between=between)
         hook = TRUNK_GRAD_HOOK
-        if hook is not None and plan.grad_regions:
+        if between is None and hook is not None and plan.grad_regions:
             hook(grads, plan.grad_regions)
         plan.arena.owner = None
         ctx.plan = ctx.x = ctx.tok = ctx.trunk_ref = None

@@ -121,6 +121,9 @@ def _worker_flat(rank, world, port, out, region=0, detach=False):
         red.launch_region(flat, 100, flat.numel())
     elif region == 2:  # per-layer slices in backward order (resnet.TRUNK_GRAD_HOOK)
         red.trunk_hook(flat, [(100, 127, None), (60, 100, None), (30, 60, None)])
+    elif region == 3:  # in place from between the plan's segments (resnet.TRUNK_SEGMENT_HOOK)
+        for lo, hi in ((100, 127), (60, 100), (30, 60)):
+            red.trunk_segment(flat, lo, hi)
     red.launch([params[2]])
     red.launch()
     arena = {id(params[0].grad), id(params[1].grad)}
@@ -134,7 +137,8 @@ def _worker_flat(rank, world, port, out, region=0, detach=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("region,detach", [(0, False), (1, False), (2, False), (2, True)])
+@pytest.mark.parametrize("region,detach", [(0, False), (1, False), (2, False), (2, True),
+                                           (3, False), (3, True)])
 def test_grad_allreduce_flat_base_and_early_launch_gloo(region, detach):
     world = 2
     port = _free_port()

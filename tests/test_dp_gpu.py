@@ -59,14 +59,20 @@ def _worker(rank, world, port, out, early):
     img, txt, fus = _model()
     red = GradAllReducer([p for mod in (img, txt, fus) for p in mod.parameters()], world)
     tails = []
-    if early:  # layers 4, 3, 2 reduced from the plan's mid-backward events
+    if early == "event":  # layers 4, 3, 2 reduced from the plan's mid-backward events
         def hook(g, regions):
             tails.extend((lo, hi, g.numel()) for lo, hi, _ in regions)
             red.trunk_hook(g, regions)
         RN.TRUNK_GRAD_HOOK = hook
+    elif early == "seg":  # ... in place, issued between the backward plan's segments
+        def seg(g, lo, hi):
+            assert torch.cuda.current_stream() != torch.cuda.default_stream()
+            tails.append((lo, hi, g.numel()))
+            red.trunk_segment(g, lo, hi)
+        RN.TRUNK_SEGMENT_HOOK = seg
     named = _grads(img, txt, fus, x[a:b], ids[a:b], mask[a:b], y[a:b])
     red.reduce()
-    RN.TRUNK_GRAD_HOOK = None
+    RN.TRUNK_GRAD_HOOK = RN.TRUNK_SEGMENT_HOOK = None
     if early:  # three contiguous slices ending at the arena's end, in backward order
         assert len(tails) == 3, tails
         assert tails[0][1] == tails[0][2] and tails[1][1] == tails[0][0], tails
@@ -76,7 +82,7 @@ def _worker(rank, world, port, out, early):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("early", [False, True])
+@pytest.mark.parametrize("early", [False, "event", "seg"])
 def test_dp_two_ranks_match_full_batch(dev, early):
     from parity_util import cosine, norm_ratio, synth_batch
     x, ids, mask, y = synth_batch(4, 16, hw=64)
@@ -106,7 +112,7 @@ def test_dp_two_ranks_match_full_batch(dev, early):
 def _rccl_worker(port, out, early):
     """One-rank RCCL group: the nccl-backend path of GradAllReducer (AVG collectives, the
     arena found by storage and reduced in place, optional early trunk tail on a comm
-    stream, bucket unpack) must leave every gradient exactly as the local backward made it
+    stream or in place between the backward plan's segments, bucket unpack) must leave every gradient exactly as the local backward made it
     (the mean over one rank is the identity)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -126,10 +132,12 @@ def _rccl_worker(port, out, early):
         p.grad = None
     red = GradAllReducer(params, 1, rehearse=True)
     assert red._avg
-    if early:
+    if early == "event":
         RN.TRUNK_GRAD_HOOK = red.trunk_hook
+    elif early == "seg":
+        RN.TRUNK_SEGMENT_HOOK = red.trunk_segment
     _grads(img, txt, fus, x, ids, mask, y)
-    RN.TRUNK_GRAD_HOOK = None
+    RN.TRUNK_GRAD_HOOK = RN.TRUNK_SEGMENT_HOOK = None
     trunk_p = {id(p) for p in img.backbone.parameters()}
     trunk = {id(p.grad) for p in img.backbone.parameters() if p.grad is not None}
     red.launch()
@@ -153,7 +161,7 @@ def _rccl_worker(port, out, early):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("early", [False, True])
+@pytest.mark.parametrize("early", [False, "event", "seg"])
 def test_dp_rccl_one_rank_identity(dev, early):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()

@@ -464,6 +464,41 @@ def test_adamw_matches_torch(dev):
         assert torch.allclose(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6)
 
 
+def test_adamw_moving_grads_many_tensors(dev):
+    """The per-step gradient column refresh (mmdx_adamw_patch_grads, 256 pointers per
+    launch): 300 tensors whose gradient buffers move on some steps and stay on others, with
+    an lr change in between (whole-table re-upload) — every step equals torch.optim.AdamW."""
+    g = torch.Generator().manual_seed(11)
+    shapes = [(int(n),) for n in torch.randint(1, 3000, (300,), generator=g)] + [(70000,)]
+    ps = [torch.randn(s, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [torch.nn.Parameter(p.to(dev)) for p in ps]
+    o_ref = torch.optim.AdamW([{"params": ref[:150], "lr": 5e-4},
+                               {"params": ref[150:], "lr": 1e-3}], weight_decay=1e-2)
+    o_mine = mmdx.AdamW([{"params": mine[:150], "lr": 5e-4}, {"params": mine[150:], "lr": 1e-3}],
+                        weight_decay=1e-2)
+    for step in range(5):
+        grads = [torch.randn(s, generator=g) for s in shapes]
+        for p, gr in zip(ref, grads):
+            p.grad = gr.clone()
+        if step == 2:   # same device buffers as the previous step: no refresh needed
+            for p, gr in zip(mine, grads):
+                p.grad.copy_(gr)
+        else:
+            for p, gr in zip(mine, grads):
+                p.grad = gr.to(dev)
+        if step == 3:
+            for o in (o_ref, o_mine):
+                o.param_groups[1]["lr"] = 2e-4
+        norm_ref = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        norm = mmdx.clip_grad_norm_(mine, 1.0)
+        assert abs(float(norm) - float(norm_ref)) <= 1e-5 * float(norm_ref)
+        o_ref.step()
+        o_mine.step()
+        for a, b in zip(mine, ref):
+            assert torch.allclose(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6), step
+
+
 def test_adamw_state_roundtrip_and_lr_change(dev):
     """the fused AdamW must follow torch.optim.AdamW across (i) a
     state_dict() -> load_state_dict() into a NEW optimizer (new exp_avg / exp_avg_sq storage,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, headline bench, kernel-trace profile, two PMC passes.
 # usage (from the repo root, under gpurun): bash tools/gpu_round.sh <tag> <phases> [steps]
-#   phases: comma list of tests,abtest,bench,c5,c2,c3,gemmb,convb,convab,benchab,prof,pmc,pmcm
+#   phases: comma list of tests,abtest,bench,c5,c2,c3,host,rehab,gemmb,convb,convab,benchab,prof,pmc,pmcm
 # Every GPU step has its own time limit; the script stops at the first step that faults,
 # aborts or times out (rc > 1), so nothing else touches the GPU after a failure.
 set -u
@@ -31,6 +31,17 @@ has bench && step bench 600 python bench.py --steps "$steps" --warmup 5 ${BA:-}
 has c5 && step c5 600 python bench.py --config c5 --steps "$steps" --warmup 5 --no-cpu-baseline
 has c2 && step c2 600 python bench.py --config c2 --steps "$steps" --warmup 5 --no-cpu-baseline
 has c3 && step c3 600 python bench.py --config c3 --steps "$steps" --warmup 5 --no-cpu-baseline
+has host && step host 300 python tools/host_profile.py --config ${HC:-c4} --steps 5
+# the one-rank RCCL rehearsal of the data-parallel step, once per arm of AB_VAR
+if has rehab; then
+  for rep in 1 2; do
+    for arm in "$AB_A" "$AB_B"; do
+      step "rehab_$(basename "$arm")_$rep" 300 env "$AB_VAR=$arm" MMDX_DP_REHEARSE=1 \
+        python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port $((29500 + rep)) bench.py --steps 30 --warmup 5 --no-cpu-baseline
+    done
+  done
+fi
 has gemmb && step gemmb 300 python tools/gemm_bench.py --dtype ${GD:-f16}
 has convb && step convb 600 python tools/conv_bench.py --json "gpurun_out/${tag}_conv_shapes.json"
 # A/B of an env knob (AB_VAR, arms AB_A / AB_B): conv table per arm, then paired benches
