@@ -245,7 +245,8 @@ int mmdx_bn_bwd_pool(int dtype, int train, const void* x, const uint8_t* argmax,
  * (cross-stream order inside a plan: e.g. weight gradients on a side stream).
  * Argument packing per op: see csrc/plan.cpp (each op forwards to the entry point of the
  * same name above/below with its i/l/f/p fields in signature order).
- * Replaces: the per-layer Python dispatch of ImageEncoderCNN's trunk (TP:279-289). */
+ * Replaces: the per-layer Python dispatch of ImageEncoderCNN's trunk (TP:279-289) and of
+ * the BERT / ViT encoder layers (TP:360/470 AutoModel's BertLayer stack; vit_b_16). */
 enum {
   MMDX_OP_EVENT = 1, MMDX_OP_NCHW2NHWC, MMDX_OP_CONV_PACK, MMDX_OP_CONV_FWD, MMDX_OP_BN_FWD,
   MMDX_OP_MAXPOOL_FWD, MMDX_OP_AVGPOOL_FWD, MMDX_OP_CAST, MMDX_OP_AVGPOOL_BWD,
@@ -253,7 +254,11 @@ enum {
   MMDX_OP_SIGNAL, MMDX_OP_WAIT, MMDX_OP_CONV_DGRAD_BNSTAT, MMDX_OP_STEM_PAIR_INPUT,
   MMDX_OP_STEM_PAIR_PACK, MMDX_OP_STEM_PAIR_GRAD, MMDX_OP_CONV_PACK_MULTI,
   MMDX_OP_CONV_FWD_BNEVAL, MMDX_OP_MAXPOOL_BN_FWD, MMDX_OP_BN_BWD_POOL,
-  MMDX_OP_CONV_DGRAD_ACCMASK, MMDX_OP_BN_BWD_MASKED_DY
+  MMDX_OP_CONV_DGRAD_ACCMASK, MMDX_OP_BN_BWD_MASKED_DY,
+  /* transformer layer stacks (BERT / ViT encoders, one plan per stack and direction) */
+  MMDX_OP_GEMM, MMDX_OP_ATTN_FWD, MMDX_OP_ATTN_BWD, MMDX_OP_LN_FWD, MMDX_OP_LN_BWD,
+  MMDX_OP_GELU_BWD, MMDX_OP_BIAS_GRAD, MMDX_OP_ADD, MMDX_OP_DROPOUT_FWD, MMDX_OP_DROPOUT_BWD,
+  MMDX_OP_AXPBY
 };
 typedef struct {
   int op, dtype, stream;

@@ -54,7 +54,9 @@ class PlanOp(C.Structure):
  OP_AVGPOOL_FWD, OP_CAST, OP_AVGPOOL_BWD, OP_MAXPOOL_BWD, OP_BN_BWD, OP_CONV_WGRAD,
  OP_CONV_DGRAD, OP_SIGNAL, OP_WAIT, OP_CONV_DGRAD_BNSTAT, OP_STEM_PAIR_INPUT,
  OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL,
- OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK, OP_BN_BWD_MASKED_DY) = range(1, 26)
+ OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK, OP_BN_BWD_MASKED_DY,
+ OP_GEMM, OP_ATTN_FWD, OP_ATTN_BWD, OP_LN_FWD, OP_LN_BWD, OP_GELU_BWD, OP_BIAS_GRAD, OP_ADD,
+ OP_DROPOUT_FWD, OP_DROPOUT_BWD, OP_AXPBY) = range(1, 37)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.

@@ -360,6 +360,19 @@ class BertModel(nn.Module):
                               p_hidden=self.config.hidden_dropout_prob,
                               p_attn=self.config.attention_probs_dropout_prob,
                               training=self.training)
+        # the whole layer stack as one native launch plan per direction (xplan); the eager
+        # per-layer nodes when gradients are off or some encoder parameter is frozen
+        from . import xplan
+        params = [q for layer in self.encoder.layer for q in layer.params()]
+        keep = torch.is_grad_enabled()
+        pcfg = SimpleNamespace(heads=self.config.num_attention_heads,
+                               eps=self.config.layer_norm_eps,
+                               p=float(self.config.hidden_dropout_prob) if self.training else 0.0,
+                               pa=(float(self.config.attention_probs_dropout_prob)
+                                   if self.training and keep else 0.0))
+        out = xplan.run_stack("bert", h, mask, pcfg, self.encoder, params) if params else None
+        if out is not None:
+            return _Out(last_hidden_state=out)
         for layer in self.encoder.layer:
             h = _BertLayerFn.apply(h, mask, cfg, *layer.params())
         return _Out(last_hidden_state=h)

@@ -302,6 +302,33 @@ static bool try_conv8(const SA& sa, const SB& sb, const Epi& epi, int M, int N, 
   return true;
 }
 
+// BK = 32 K tiles with NS = 3..5 stages (MMDX_CONV_BK32 = NS; 0 = off): at 128 x 128 a
+// 64-deep stage is 32 KB and two blocks per CU leave room for two stages only (one tile in
+// flight while one is consumed); 16 KB stages keep two blocks per CU with NS - 1 tiles in
+// flight.  A/B knob for tools/conv_bench.py.
+static int conv_bk32_stages() {
+  const char* e = getenv("MMDX_CONV_BK32");
+  const int ns = e ? atoi(e) : 0;
+  return ns >= 3 && ns <= 5 ? ns : 0;
+}
+
+template <int BM, int BN, class SA, class SB, class Epi>
+static void launch_dma32(const SA& sa, const SB& sb, const Epi& epi, int M, int N, int K,
+                         int ns, hipStream_t st) {
+  typedef DmaK<BM, SA, 32> OA;
+  typedef DmaK<BN, SB, 32> OB;
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (ns == 3)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3>), dim3(nwg), dim3(NT), 0, st,
+                       sa, sb, epi, M, N, K, K);
+  else if (ns == 4)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 4>), dim3(nwg), dim3(NT), 0, st,
+                       sa, sb, epi, M, N, K, K);
+  else
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 5>), dim3(nwg), dim3(NT), 0, st,
+                       sa, sb, epi, M, N, K, K);
+}
+
 static bool fold_probe_on() {
   const char* e = getenv("MMDX_FOLD_PROBE");  // timing probe only (tools/conv_bench.py)
   return e && atoi(e) != 0;
@@ -334,6 +361,14 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
       }
       // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
       const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+      if (const int ns32 = conv_bk32_stages()) {
+        if (N <= 64 || tiles128 < kNarrowBelow)
+          launch_dma32<128, 64>(sa, sb, epi, M, N, K, ns32, st);
+        else
+          launch_dma32<128, 128>(sa, sb, epi, M, N, K, ns32, st);
+        MMDX_LAUNCH_CHECK();
+        return 0;
+      }
       if (N <= 64 || tiles128 < kNarrowBelow)
         return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
       return launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);

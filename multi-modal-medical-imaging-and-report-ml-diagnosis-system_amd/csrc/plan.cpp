@@ -148,6 +148,54 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
       // i: n_items; l: total_blocks; p: item table (device)
       return mmdx_conv_pack_multi(o.dtype, (const mmdx_pack_item*)P(o, 0, ext), o.i[0], o.l[0],
                                   s);
+    case MMDX_OP_GEMM:
+      // i: M, N, K, a_kmajor, b_kmajor, c_dtype, act; l: lda, ldb, ldc, ws_bytes;
+      // f: alpha, beta; p: A, B, C, bias, addend, preact, ws
+      return mmdx_gemm(o.dtype, o.i[0], o.i[1], o.i[2], P(o, 0, ext), o.l[0], o.i[3],
+                       P(o, 1, ext), o.l[1], o.i[4], P(o, 2, ext), o.l[2], o.i[5],
+                       (const float*)P(o, 3, ext), (const float*)P(o, 4, ext), o.i[6], o.f[0],
+                       o.f[1], P(o, 5, ext), P(o, 6, ext), (size_t)o.l[3], s);
+    case MMDX_OP_ATTN_FWD:
+      // i: B, L, H; f: scale, p_drop; l: seed; p: qkv, mask, counter, out, probs
+      return mmdx_attention_fwd(o.dtype, P(o, 0, ext), (const int64_t*)P(o, 1, ext), o.i[0],
+                                o.i[1], o.i[2], o.f[0], o.f[1], (uint64_t)o.l[0],
+                                (uint64_t*)P(o, 2, ext), P(o, 3, ext), (float*)P(o, 4, ext), s);
+    case MMDX_OP_ATTN_BWD:
+      // i: B, L, H; f: scale, p_drop; l: ws_bytes; p: qkv, probs, dout, mask, dqkv, ws
+      return mmdx_attention_bwd(o.dtype, P(o, 0, ext), (const float*)P(o, 1, ext), P(o, 2, ext),
+                                (const int64_t*)P(o, 3, ext), o.i[0], o.i[1], o.i[2], o.f[0],
+                                o.f[1], P(o, 4, ext), P(o, 5, ext), (size_t)o.l[0], s);
+    case MMDX_OP_LN_FWD:
+      // i: D; l: rows; f: eps; p: x, residual, gamma, beta, y, sum_out, mean, rstd
+      return mmdx_layernorm_fwd(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
+                                (const float*)P(o, 2, ext), (const float*)P(o, 3, ext), o.f[0],
+                                P(o, 4, ext), P(o, 5, ext), (float*)P(o, 6, ext),
+                                (float*)P(o, 7, ext), s);
+    case MMDX_OP_LN_BWD:
+      // i: D; l: rows, ws_bytes; f: beta_acc; p: xsum, dy, gamma, mean, rstd, dx, dgamma,
+      // dbeta, ws
+      return mmdx_layernorm_bwd(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
+                                (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
+                                (const float*)P(o, 4, ext), P(o, 5, ext), (float*)P(o, 6, ext),
+                                (float*)P(o, 7, ext), o.f[0], P(o, 8, ext), (size_t)o.l[1], s);
+    case MMDX_OP_GELU_BWD:  // l: n; p: pre, dy, dx
+      return mmdx_gelu_bwd(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], P(o, 2, ext), s);
+    case MMDX_OP_BIAS_GRAD:  // i: N; l: M, ws_bytes; f: beta_acc; p: dy, db, ws
+      return mmdx_bias_grad(o.dtype, P(o, 0, ext), o.l[0], o.i[0], (float*)P(o, 1, ext),
+                            o.f[0], P(o, 2, ext), (size_t)o.l[1], s);
+    case MMDX_OP_ADD:  // l: n; p: x, y, out
+      return mmdx_add(o.dtype, o.l[0], P(o, 0, ext), P(o, 1, ext), P(o, 2, ext), s);
+    case MMDX_OP_DROPOUT_FWD:
+      // f: p; l: n, seed, offset; p: x, counter, y, mask
+      return mmdx_dropout_fwd(o.dtype, P(o, 0, ext), o.l[0], o.f[0], (uint64_t)o.l[1],
+                              (uint64_t)o.l[2], (uint64_t*)P(o, 1, ext), P(o, 2, ext),
+                              (uint8_t*)P(o, 3, ext), s);
+    case MMDX_OP_DROPOUT_BWD:  // f: p; l: n; p: dy, mask, dx
+      return mmdx_dropout_bwd(o.dtype, P(o, 0, ext), (const uint8_t*)P(o, 1, ext), o.l[0],
+                              o.f[0], P(o, 2, ext), s);
+    case MMDX_OP_AXPBY:  // l: n; f: a, b; p: x, y, out
+      return mmdx_axpby(o.l[0], o.f[0], (const float*)P(o, 0, ext), o.f[1],
+                        (const float*)P(o, 1, ext), (float*)P(o, 2, ext), s);
     default:
       mmdx_set_error("plan: unknown op code %d", o.op);
       return -22;

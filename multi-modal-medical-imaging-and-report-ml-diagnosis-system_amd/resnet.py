@@ -255,14 +255,16 @@ class _OpList:
         self.ops = None
         return self
 
-    def run(self, ext, streams, between=None):
+    def run(self, ext, streams, between=None, timer=None):
         """Replay the list.  between(k): called after segment k (k = 0 .. cuts-1) is
-        enqueued and before segment k+1 is; None = one native call for the whole list."""
+        enqueued and before segment k+1 is; None = one native call for the whole list.
+        timer: the launch timer of the timed ops (default CONV_TIMER)."""
         exts = (ctypes.c_void_p * max(1, len(ext)))(*ext)
         sts = (ctypes.c_void_p * len(streams))(*streams)
         evs = None
-        if CONV_TIMER.active and self.conv_names:
-            evs = CONV_TIMER.take(self.conv_names)
+        timer = CONV_TIMER if timer is None else timer
+        if getattr(timer, "active", False) and self.conv_names:
+            evs = timer.take(self.conv_names)
             evs = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
         if between is None or len(self.bounds) == 2:
             call("mmdx_plan_run", self.arr, self.n, exts, evs, sts, len(streams))

@@ -278,6 +278,20 @@ class VitTrunk(nn.Module):
             raise ValueError("expected images [B,3,H,W]")
         h = _PatchTokensFn.apply(x.float(), self.conv_proj.weight, self.conv_proj.bias,
                                  self.class_token, self.encoder.pos_embedding, T)
+        from . import xplan
+        params = []
         for blk in self.encoder.layers:
-            h = blk(h)
+            at = blk.self_attention
+            params += [blk.ln_1.weight, blk.ln_1.bias, at.in_proj_weight, at.in_proj_bias,
+                       at.out_proj.weight, at.out_proj.bias, blk.ln_2.weight, blk.ln_2.bias,
+                       blk.mlp[0].weight, blk.mlp[0].bias, blk.mlp[3].weight, blk.mlp[3].bias]
+        # the 12 blocks as one native launch plan per direction (xplan); the eager per-block
+        # nodes when gradients are off or a block parameter is frozen
+        cfg = type("VitCfg", (), dict(heads=HEADS, eps=EPS))
+        out = xplan.run_stack("vit", h, None, cfg, self.encoder, params) if params else None
+        if out is not None:
+            h = out
+        else:
+            for blk in self.encoder.layers:
+                h = blk(h)
         return _ClassTokenLNFn.apply(h, self.encoder.ln.weight, self.encoder.ln.bias)

@@ -1,0 +1,450 @@
+"""Launch plans for the transformer encoder stacks (BERT-base text tower, ViT-B/16 image
+tower; BASELINE config C5).
+
+Each stack (all of its layers) is ONE autograd node, like the ResNet trunk (resnet._TrunkFn):
+its forward and its backward are recorded once per (shape, dtype, mode, parameter set) as
+op lists over a persistent buffer arena (include/mmdx.h launch plans, csrc/plan.cpp) and
+replayed by one native call per step.  The eager per-layer nodes (bert._BertLayerFn,
+vit._VitBlockFn) issue the same kernels in the same order from Python — ~35 ctypes calls and
+~30 allocations per layer and direction, 32 ms of host time per C5 step, most of the step;
+here the host cost per stack and direction is one call plus the launches themselves.
+
+Same arithmetic as the eager nodes (the plan-vs-eager tests require bit-identical outputs
+and gradients with dropout off).  Dropout draws from the per-device launch counter
+(_lib.rng_counter) under a seed fixed per plan op, so every replay draws fresh masks.
+Per-call buffers enter as external bases: the stack input and the attention mask (forward),
+the upstream gradient, the parameter-gradient arena and the mask (backward).  The parameter
+gradients are views of one flat fp32 buffer per backward (the data-parallel reducer finds it
+by storage and all-reduces it in place, like the trunk's arena).
+"""
+from __future__ import annotations
+
+import math
+import os
+import weakref
+
+import torch
+
+from . import _lib as L
+from . import functional as F
+from .resnet import _Arena, _Ext, _OpList, _Token
+
+_WS_TOKEN = 0x1   # placeholder operand for the plan's workspace (patched when sized)
+_F32 = torch.float32
+
+
+def enabled() -> bool:
+    """MMDX_STACK_PLANS=0 runs the eager per-layer nodes instead (A/B, debugging)."""
+    return os.environ.get("MMDX_STACK_PLANS", "1") != "0"
+
+
+class _Rec:
+    """Records C-ABI calls as plan ops; buffers come from the plan's arena."""
+
+    def __init__(self, arena, dev, T, ops):
+        self.arena, self.dev, self.T, self.ops = arena, dev, T, ops
+        self.dt = L.dtype_code(T)
+        self.ws_need = 0
+
+    def buf(self, shape, dtype=None):
+        return self.arena.new(shape, dtype or self.T, self.dev)
+
+    def _ws(self, n):
+        self.ws_need = max(self.ws_need, int(n))
+        return _WS_TOKEN if n > 0 else None
+
+    def cast(self, src, dst):
+        self.ops.add(L.OP_CAST, L.dtype_code(dst.dtype), i=(L.dtype_code(src.dtype),),
+                     l=(src.numel(),), p=(src, dst))
+
+    def copy(self, src, dst, n):
+        self.ops.add(L.OP_CAST, self.dt, i=(self.dt,), l=(n,), p=(src, dst))
+
+    def axpby(self, n, a, x, b, y, out):
+        self.ops.add(L.OP_AXPBY, i=(), l=(n,), f=(a, b), p=(x, y, out))
+
+    def gemm(self, A, lda, akm, B, ldb, bkm, M, N, K, C, ldc, c_dtype, bias=None, act=0,
+             preact=None, beta=0.0):
+        n = L.lib().mmdx_gemm_workspace_size(self.dt, M, N, K)
+        self.ops.timed(2 * M * N * K, L.OP_GEMM, dtype=self.dt,
+                       i=(M, N, K, int(akm), int(bkm), L.dtype_code(c_dtype), act),
+                       l=(lda, ldb, ldc, n), f=(1.0, beta),
+                       p=(A, B, C, bias, None, preact, self._ws(n)))
+
+    def attn_fwd(self, qkv, mask, B, Ls, H, scale, p_drop, seed, counter, out, probs):
+        self.ops.add(L.OP_ATTN_FWD, self.dt, i=(B, Ls, H), f=(scale, p_drop), l=(seed,),
+                     p=(qkv, mask, counter, out, probs))
+
+    def attn_bwd(self, qkv, probs, dout, mask, B, Ls, H, scale, p_drop, dqkv):
+        n = L.lib().mmdx_attention_workspace_size(self.dt, B, Ls, H)
+        self.ops.add(L.OP_ATTN_BWD, self.dt, i=(B, Ls, H), f=(scale, p_drop), l=(n,),
+                     p=(qkv, probs, dout, mask, dqkv, self._ws(n)))
+
+    def ln_fwd(self, x, res, g, b, eps, rows, D, y, xsum, mean, rstd):
+        self.ops.add(L.OP_LN_FWD, self.dt, i=(D,), l=(rows,), f=(eps,),
+                     p=(x, res, g, b, y, xsum, mean, rstd))
+
+    def ln_bwd(self, xsum, dy, g, mean, rstd, rows, D, dx, dg, db):
+        n = L.lib().mmdx_layernorm_workspace_size(rows, D)
+        self.ops.add(L.OP_LN_BWD, self.dt, i=(D,), l=(rows, n), f=(0.0,),
+                     p=(xsum, dy, g, mean, rstd, dx, dg, db, self._ws(n)))
+
+    def gelu_bwd(self, pre, dy, n, dx):
+        self.ops.add(L.OP_GELU_BWD, self.dt, l=(n,), p=(pre, dy, dx))
+
+    def colsum(self, dy, M, N, db):
+        n = L.lib().mmdx_bias_grad_workspace_size(M, N)
+        self.ops.add(L.OP_BIAS_GRAD, self.dt, i=(N,), l=(M, n), f=(0.0,),
+                     p=(dy, db, self._ws(n)))
+
+    def add(self, x, y, n, out):
+        self.ops.add(L.OP_ADD, self.dt, l=(n,), p=(x, y, out))
+
+    def dropout_fwd(self, x, n, p, seed, counter, y, mask):
+        self.ops.add(L.OP_DROPOUT_FWD, self.dt, f=(p,), l=(n, seed, 0), p=(x, counter, y, mask))
+
+    def dropout_bwd(self, dy, mask, n, p, dx):
+        self.ops.add(L.OP_DROPOUT_BWD, self.dt, f=(p,), l=(n,), p=(dy, mask, dx))
+
+
+class _GradLayout:
+    """Byte offsets of the parameter gradients in the flat fp32 gradient buffer."""
+
+    def __init__(self):
+        self.n = 0
+        self.items = []   # (param index, shape, element offset)
+
+    def take(self, shape, idx=None):
+        off = self.n
+        self.n += math.prod(shape)
+        if idx is not None:
+            self.items.append((idx, tuple(shape), off))
+        return off
+
+    @staticmethod
+    def ext(off):
+        return _Ext(1, 4 * off)
+
+
+class _StackPlan:
+    """Forward + backward op lists of one stack configuration over one arena."""
+
+    def __init__(self, dev, T):
+        self.arena = _Arena()
+        self.dev, self.T = dev, T
+        self.fwd = _OpList()
+        self.bwd = _OpList()
+        self.out = None
+        self.dx = None
+        self.grads = _GradLayout()
+
+    def finish(self, recs):
+        need = max(r.ws_need for r in recs)
+        ws = self.arena.new((max(1, need),), torch.uint8, self.dev)
+        for lst in (self.fwd, self.bwd):
+            for o in lst.ops:
+                for j in range(12):
+                    if o.ext[j] == -1 and o.p[j] == _WS_TOKEN:
+                        o.p[j] = ws.data_ptr()
+            lst.freeze()
+
+
+def _plans_for(owner, key, build):
+    cache = owner.__dict__.setdefault("_mmdx_stack_plans", {})
+    lst = cache.setdefault(key, [])
+    for pl in lst:
+        if not (pl.arena.owner is not None and pl.arena.owner() is not None):
+            return pl
+    pl = build()
+    lst.append(pl)
+    return pl
+
+
+def _seed(base):
+    """A dropout seed for a plan op, as the signed 64-bit value a plan field holds."""
+    v = L.dropout_seed(base)
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+# ------------------------------------------------------------------------ BERT encoder
+# per layer, in bert.BertLayer.params() order:
+# wq, bq, wk, bk, wv, bv, wo, bo, g1, b1, wi, bi, wo2, bo2, g2, b2
+_BERT_NP = 16
+
+
+def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
+    pl = _StackPlan(dev, T)
+    M = B * Ls
+    scale = 1.0 / math.sqrt(D // Hn)
+    counter = L.rng_counter(dev)
+    nl = len(params) // _BERT_NP
+    rf = _Rec(pl.arena, dev, T, pl.fwd)
+    x = _Ext(0)
+    mask = _Ext(1)
+    saves = []
+    for li in range(nl):
+        (wq, bq, wk, bk, wv, bv, wo, bo, g1, b1, wi, bi, wo2, bo2, g2,
+         b2) = params[li * _BERT_NP:(li + 1) * _BERT_NP]
+        wqkv = rf.buf((3 * D, D))
+        for j, w in enumerate((wq, wk, wv)):
+            rf.cast(w, wqkv[j * D:(j + 1) * D])
+        bqkv = rf.buf((3 * D,), _F32)
+        for j, bb in enumerate((bq, bk, bv)):
+            rf.axpby(D, 1.0, bb, 0.0, None, bqkv[j * D:(j + 1) * D])
+        qkv = rf.buf((M, 3 * D))
+        rf.gemm(x, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, T, bias=bqkv)
+        probs = rf.buf((B, Hn, Ls, Ls), _F32)
+        att = rf.buf((M, D))
+        rf.attn_fwd(qkv, mask, B, Ls, Hn, scale, pa, _seed(0xA770 + 7919 * li) if pa > 0 else 0,
+                    counter, att, probs)
+        woc = rf.buf((D, D))
+        rf.cast(wo, woc)
+        a = rf.buf((M, D))
+        rf.gemm(att, D, True, woc, D, True, M, D, D, a, D, T, bias=bo)
+        m1 = None
+        if p > 0:
+            ad, m1 = rf.buf((M, D)), rf.buf((M, D), torch.uint8)
+            rf.dropout_fwd(a, M * D, p, _seed(0xD401 + 7919 * li), counter, ad, m1)
+            a = ad
+        h1, xs1 = rf.buf((M, D)), rf.buf((M, D))
+        mu1, rs1 = rf.buf((M,), _F32), rf.buf((M,), _F32)
+        rf.ln_fwd(a, x, g1, b1, eps, M, D, h1, xs1, mu1, rs1)
+        wic = rf.buf((I, D))
+        rf.cast(wi, wic)
+        f, pre = rf.buf((M, I)), rf.buf((M, I))
+        rf.gemm(h1, D, True, wic, D, True, M, I, D, f, I, T, bias=bi, act=L.ACT_GELU,
+                preact=pre)
+        wo2c = rf.buf((D, I))
+        rf.cast(wo2, wo2c)
+        f2 = rf.buf((M, D))
+        rf.gemm(f, I, True, wo2c, I, True, M, D, I, f2, D, T, bias=bo2)
+        m2 = None
+        if p > 0:
+            fd, m2 = rf.buf((M, D)), rf.buf((M, D), torch.uint8)
+            rf.dropout_fwd(f2, M * D, p, _seed(0xD402 + 7919 * li), counter, fd, m2)
+            f2 = fd
+        h2, xs2 = rf.buf((M, D)), rf.buf((M, D))
+        mu2, rs2 = rf.buf((M,), _F32), rf.buf((M,), _F32)
+        rf.ln_fwd(f2, h1, g2, b2, eps, M, D, h2, xs2, mu2, rs2)
+        saves.append(dict(x=x, wqkv=wqkv, qkv=qkv, probs=probs, att=att, woc=woc, xs1=xs1,
+                          mu1=mu1, rs1=rs1, h1=h1, wic=wic, pre=pre, f=f, wo2c=wo2c, xs2=xs2,
+                          mu2=mu2, rs2=rs2, m1=m1, m2=m2))
+        x = h2
+    pl.out = x
+
+    # backward: ext 0 = upstream gradient [M, D] (compute dtype), 1 = gradient buffer,
+    # 2 = mask.  Shared temporaries across layers; Y carries d(layer output) downward.
+    rb = _Rec(pl.arena, dev, T, pl.bwd)
+    mask = _Ext(2)
+    X, Y = rb.buf((M, D)), rb.buf((M, D))
+    DX2 = rb.buf((M, D)) if p > 0 else None
+    DY1 = rb.buf((M, D)) if p > 0 else None
+    df, dpre = rb.buf((M, I)), rb.buf((M, I))
+    datt, dqkv = rb.buf((M, D)), rb.buf((M, 3 * D))
+    G = pl.grads
+    offs = []
+    for li in range(nl):  # gradient layout in forward order
+        base = li * _BERT_NP
+        o = {}
+        o["wqkv"] = G.take((3 * D, D))
+        for j in range(3):
+            G.items.append((base + 2 * j, (D, D), o["wqkv"] + j * D * D))
+        o["bqkv"] = G.take((3 * D,))
+        for j in range(3):
+            G.items.append((base + 2 * j + 1, (D,), o["bqkv"] + j * D))
+        for name, idx, shape in (("wo", 6, (D, D)), ("bo", 7, (D,)), ("g1", 8, (D,)),
+                                 ("b1", 9, (D,)), ("wi", 10, (I, D)), ("bi", 11, (I,)),
+                                 ("wo2", 12, (D, I)), ("bo2", 13, (D,)), ("g2", 14, (D,)),
+                                 ("b2", 15, (D,))):
+            o[name] = G.take(shape, base + idx)
+        offs.append(o)
+    gx = G.ext
+    dh = _Ext(0)
+    for li in range(nl - 1, -1, -1):
+        s, o = saves[li], offs[li]
+        g1 = params[li * _BERT_NP + 8]
+        g2 = params[li * _BERT_NP + 14]
+        rb.ln_bwd(s["xs2"], dh, g2, s["mu2"], s["rs2"], M, D, X, gx(o["g2"]), gx(o["b2"]))
+        dX2 = X
+        if p > 0:
+            rb.dropout_bwd(X, s["m2"], M * D, p, DX2)
+            dX2 = DX2
+        rb.gemm(dX2, D, True, s["wo2c"], I, False, M, I, D, df, I, T)
+        rb.gemm(dX2, D, False, s["f"], I, False, D, I, M, gx(o["wo2"]), I, _F32)
+        rb.colsum(dX2, M, D, gx(o["bo2"]))
+        rb.gelu_bwd(s["pre"], df, M * I, dpre)
+        rb.gemm(dpre, I, False, s["h1"], D, False, I, D, M, gx(o["wi"]), D, _F32)
+        rb.colsum(dpre, M, I, gx(o["bi"]))
+        rb.gemm(dpre, I, True, s["wic"], D, False, M, D, I, X, D, T, beta=1.0)
+        rb.ln_bwd(s["xs1"], X, g1, s["mu1"], s["rs1"], M, D, Y, gx(o["g1"]), gx(o["b1"]))
+        dY1 = Y
+        if p > 0:
+            rb.dropout_bwd(Y, s["m1"], M * D, p, DY1)
+            dY1 = DY1
+        rb.gemm(dY1, D, True, s["woc"], D, False, M, D, D, datt, D, T)
+        rb.gemm(dY1, D, False, s["att"], D, False, D, D, M, gx(o["wo"]), D, _F32)
+        rb.colsum(dY1, M, D, gx(o["bo"]))
+        rb.attn_bwd(s["qkv"], s["probs"], datt, mask, B, Ls, Hn, scale, pa, dqkv)
+        xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)  # the stack input
+        rb.gemm(dqkv, 3 * D, False, xin, D, False, 3 * D, D, M, gx(o["wqkv"]), D, _F32)
+        rb.colsum(dqkv, M, 3 * D, gx(o["bqkv"]))
+        rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, Y, D, T, beta=1.0)
+        dh = Y
+    pl.dx = Y
+    pl.finish((rf, rb))
+    return pl
+
+
+# ------------------------------------------------------------------------ ViT encoder
+# per block, in vit.EncoderBlock order:
+# g1, b1, w_in, b_in, w_out, b_out, g2, b2, w1, bb1, w2, bb2
+_VIT_NP = 12
+
+
+def _build_vit(params, N, S, D, heads, I, eps, T, dev):
+    pl = _StackPlan(dev, T)
+    M = N * S
+    scale = 1.0 / math.sqrt(D // heads)
+    nl = len(params) // _VIT_NP
+    rf = _Rec(pl.arena, dev, T, pl.fwd)
+    x = _Ext(0)
+    saves = []
+    for li in range(nl):
+        g1, b1, w_in, b_in, w_out, b_out, g2, b2, w1, bb1, w2, bb2 = \
+            params[li * _VIT_NP:(li + 1) * _VIT_NP]
+        u1, mu1, rs1 = rf.buf((M, D)), rf.buf((M,), _F32), rf.buf((M,), _F32)
+        rf.ln_fwd(x, None, g1, b1, eps, M, D, u1, None, mu1, rs1)
+        wqkv = rf.buf((3 * D, D))
+        rf.cast(w_in, wqkv)
+        qkv = rf.buf((M, 3 * D))
+        rf.gemm(u1, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, T, bias=b_in)
+        probs = rf.buf((N, heads, S, S), _F32)
+        att = rf.buf((M, D))
+        rf.attn_fwd(qkv, None, N, S, heads, scale, 0.0, 0, None, att, probs)
+        woc = rf.buf((D, D))
+        rf.cast(w_out, woc)
+        o_ = rf.buf((M, D))
+        rf.gemm(att, D, True, woc, D, True, M, D, D, o_, D, T, bias=b_out)
+        u2, a = rf.buf((M, D)), rf.buf((M, D))
+        mu2, rs2 = rf.buf((M,), _F32), rf.buf((M,), _F32)
+        rf.ln_fwd(o_, x, g2, b2, eps, M, D, u2, a, mu2, rs2)
+        w1c = rf.buf((I, D))
+        rf.cast(w1, w1c)
+        f, pre = rf.buf((M, I)), rf.buf((M, I))
+        rf.gemm(u2, D, True, w1c, D, True, M, I, D, f, I, T, bias=bb1, act=L.ACT_GELU,
+                preact=pre)
+        w2c = rf.buf((D, I))
+        rf.cast(w2, w2c)
+        out = rf.buf((M, D))
+        rf.copy(a, out, M * D)
+        rf.gemm(f, I, True, w2c, I, True, M, D, I, out, D, T, bias=bb2, beta=1.0)
+        saves.append(dict(x=x, u1=u1, mu1=mu1, rs1=rs1, wqkv=wqkv, qkv=qkv, probs=probs,
+                          att=att, woc=woc, a=a, u2=u2, mu2=mu2, rs2=rs2, w1c=w1c, pre=pre,
+                          f=f, w2c=w2c))
+        x = out
+    pl.out = x
+
+    # backward: ext 0 = upstream gradient, 1 = gradient buffer, 3 = the stack input
+    rb = _Rec(pl.arena, dev, T, pl.bwd)
+    df, dpre = rb.buf((M, I)), rb.buf((M, I))
+    du2, da_ln, DA = rb.buf((M, D)), rb.buf((M, D)), rb.buf((M, D))
+    datt, dqkv, du1, dx_ln = rb.buf((M, D)), rb.buf((M, 3 * D)), rb.buf((M, D)), rb.buf((M, D))
+    DX = rb.buf((M, D))
+    G = pl.grads
+    offs = []
+    for li in range(nl):
+        base = li * _VIT_NP
+        shapes = ((D,), (D,), (3 * D, D), (3 * D,), (D, D), (D,), (D,), (D,), (I, D), (I,),
+                  (D, I), (D,))
+        offs.append([G.take(sh, base + j) for j, sh in enumerate(shapes)])
+    gx = G.ext
+    dO = _Ext(0)
+    for li in range(nl - 1, -1, -1):
+        s, o = saves[li], offs[li]
+        g1 = params[li * _VIT_NP + 0]
+        g2 = params[li * _VIT_NP + 6]
+        rb.gemm(dO, D, True, s["w2c"], I, False, M, I, D, df, I, T)
+        rb.gemm(dO, D, False, s["f"], I, False, D, I, M, gx(o[10]), I, _F32)
+        rb.colsum(dO, M, D, gx(o[11]))
+        rb.gelu_bwd(s["pre"], df, M * I, dpre)
+        rb.gemm(dpre, I, False, s["u2"], D, False, I, D, M, gx(o[8]), D, _F32)
+        rb.colsum(dpre, M, I, gx(o[9]))
+        rb.gemm(dpre, I, True, s["w1c"], D, False, M, D, I, du2, D, T)
+        rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, da_ln, gx(o[6]), gx(o[7]))
+        rb.add(dO, da_ln, M * D, DA)
+        rb.gemm(DA, D, True, s["woc"], D, False, M, D, D, datt, D, T)
+        rb.gemm(DA, D, False, s["att"], D, False, D, D, M, gx(o[4]), D, _F32)
+        rb.colsum(DA, M, D, gx(o[5]))
+        rb.attn_bwd(s["qkv"], s["probs"], datt, None, N, S, heads, scale, 0.0, dqkv)
+        rb.gemm(dqkv, 3 * D, False, s["u1"], D, False, 3 * D, D, M, gx(o[2]), D, _F32)
+        rb.colsum(dqkv, M, 3 * D, gx(o[3]))
+        rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, du1, D, T)
+        xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)
+        rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, dx_ln, gx(o[0]), gx(o[1]))
+        rb.add(DA, dx_ln, M * D, DX)
+        dO = DX
+    pl.dx = DX
+    pl.finish((rf, rb))
+    return pl
+
+
+# ------------------------------------------------------------------------ autograd node
+class _StackFn(torch.autograd.Function):
+    """forward(h, mask, spec, *params) -> stack output; spec: ("bert", cfg) / ("vit", cfg)."""
+
+    @staticmethod
+    def forward(ctx, h, mask, spec, owner, *params):
+        kind, cfg = spec
+        T = h.dtype
+        dev = h.device
+        h = h.contiguous()
+        if kind == "bert":
+            B, Ls, D = h.shape
+            I = params[10].shape[0]
+            key = ("bert", B, Ls, D, T, cfg.p, cfg.pa, tuple(q.data_ptr() for q in params))
+            pl = _plans_for(owner, key, lambda: _build_bert(
+                params, B, Ls, D, cfg.heads, I, cfg.eps, cfg.p, cfg.pa, T, dev))
+            ext = [h.data_ptr(), mask.data_ptr()]
+        else:
+            N, S, D = h.shape
+            I = params[8].shape[0]
+            key = ("vit", N, S, D, T, tuple(q.data_ptr() for q in params))
+            pl = _plans_for(owner, key, lambda: _build_vit(
+                params, N, S, D, cfg.heads, I, cfg.eps, T, dev))
+            ext = [h.data_ptr(), 0]
+        strm = [torch.cuda.current_stream().cuda_stream]
+        pl.fwd.run(ext, strm, timer=F.GEMM_TIMER)
+        tok = _Token()
+        pl.arena.owner = weakref.ref(tok)
+        ctx.tok, ctx.plan, ctx.kind = tok, pl, kind
+        ctx.save_for_backward(h, mask if kind == "bert" else None)
+        ctx.nparams = len(params)
+        return pl.out.clone().view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        pl = ctx.plan
+        h, mask = ctx.saved_tensors
+        T = h.dtype
+        dout = F.cast(dout.contiguous(), T)
+        grads = torch.empty(pl.grads.n, dtype=_F32, device=h.device)
+        ext = [dout.data_ptr(), grads.data_ptr(),
+               mask.data_ptr() if mask is not None else 0, h.data_ptr()]
+        pl.bwd.run(ext, [torch.cuda.current_stream().cuda_stream], timer=F.GEMM_TIMER)
+        dx = pl.dx.clone().view(h.shape)
+        out = [None] * ctx.nparams
+        for idx, shape, off in pl.grads.items:
+            out[idx] = grads[off:off + math.prod(shape)].view(shape)
+        pl.arena.owner = None
+        ctx.plan = ctx.tok = None
+        return (dx, None, None, None, *out)
+
+
+def run_stack(kind, h, mask, cfg, owner, params):
+    """The stack through its plan, or None when the plan path does not apply (grad off or
+    a frozen parameter: the eager nodes handle those)."""
+    if not enabled() or not torch.is_grad_enabled():
+        return None
+    if not all(q.requires_grad for q in params):
+        return None
+    return _StackFn.apply(h, mask, (kind, cfg), owner, *params)

@@ -127,3 +127,18 @@ def test_conv8_matches_4wave_kernel(dev, cfg, monkeypatch):
             continue
         assert torch.isfinite(b[key].float()).all(), key
         assert torch.equal(a[key], b[key]), key
+
+
+@pytest.mark.parametrize("ns", ["3", "4", "5"])
+@pytest.mark.parametrize("cfg", SHAPES)
+def test_bk32_stages_match_bk64(dev, cfg, ns, monkeypatch):
+    """MMDX_CONV_BK32 = NS: the forward / stride-1 dgrad tiles with 32-deep K tiles in NS
+    stages run the same MFMA sequence per output (k-steps of 32 in the same order, same
+    128-row tiles): every output and statistics slab is bit-identical to the 64-deep kernel."""
+    monkeypatch.delenv("MMDX_CONV_BK32", raising=False)
+    a = _run_all(dev, cfg, "0", monkeypatch)
+    monkeypatch.setenv("MMDX_CONV_BK32", ns)
+    b = _run_all(dev, cfg, "0", monkeypatch)
+    for key in a:
+        assert torch.isfinite(b[key].float()).all(), key
+        assert torch.equal(a[key], b[key]), key
