@@ -438,8 +438,9 @@ def main():
     x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
     side = torch.cuda.Stream(device=dev, priority=-1)
     from mmdx.dist import GradAllReducer
-    # C5's packed buckets (ViT-B/16 + BERT-base: ~800 MB of per-tensor fp32 gradients) travel
-    # in bf16 by default — half the xGMI bytes, the mean taken in fp32 after the cast back
+    # C5's packed buckets (the ViT-B/16 and BERT-base gradients outside the two encoder
+    # stacks, whose flat gradient buffers reduce in place in fp32) travel in bf16 by default —
+    # half the xGMI bytes, the mean taken in fp32 after the cast back
     # (MMDX_DP_BUCKET_DTYPE=fp32 restores fp32); C2-C4 reduce in fp32
     bdt = None
     if vit and os.environ.get("MMDX_DP_BUCKET_DTYPE", "bf16") == "bf16":

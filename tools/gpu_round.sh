@@ -59,7 +59,7 @@ if has benchab; then
 fi
 cd /tmp
 has prof && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$tag" \
-  -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
+  -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ${PA:-}
 has pmc && step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmcf_$tag" \
   -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
 has pmc && step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmcw_$tag" \
