@@ -701,17 +701,28 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
   }
 }
 
-__global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int D,
-                                       float* dgamma, float* dbeta, float beta_acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float a = 0.f, b = 0.f;
-  for (int k = 0; k < nblk; ++k) {
-    a += part[((long)k * 2 + 0) * D + c];
-    b += part[((long)k * 2 + 1) * D + c];
+// dgamma / dbeta from the per-block partials [nblk][2][D]: 32 columns x 8 lanes per block,
+// the lanes stride the blocks (the first version had one thread per column over all nblk
+// partials — 3 blocks at D = 768: 82 us per call, 4.5 ms per C5 step)
+__global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __restrict__ part,
+                                                              int nblk, int D, float* dgamma,
+                                                              float* dbeta, float beta_acc) {
+  __shared__ float red[8][32];
+  const int cc = threadIdx.x & 31, lane = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cc, which = blockIdx.y;  // 0: dgamma, 1: dbeta
+  float acc = 0.f;
+  if (c < D) {
+#pragma unroll 4
+    for (int k = lane; k < nblk; k += 8) acc += part[((long)k * 2 + which) * D + c];
   }
-  if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + a : a;
-  if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + b : b;
+  red[lane][cc] = acc;
+  __syncthreads();
+  if (lane != 0 || c >= D) return;
+  float s = 0.f;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) s += red[l][cc];
+  float* out = which ? dbeta : dgamma;
+  if (out) out[c] = beta_acc != 0.f ? beta_acc * out[c] + s : s;
 }
 
 }  // namespace mmdx
@@ -870,7 +881,7 @@ extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, l
   MMDX_DISPATCH(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nblk), dim3(256), shm, st,
                                           (const T*)xsum, (const T*)dy, rows, D, gamma,
                                           save_mean, save_rstd, (T*)dx, (float*)ws));
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 31) / 32, 2), dim3(256), 0, st,
                      (const float*)ws, (int)nblk, D, dgamma, dbeta, beta_acc);
   MMDX_LAUNCH_CHECK();
   return 0;

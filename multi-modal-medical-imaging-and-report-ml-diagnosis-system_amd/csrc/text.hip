@@ -76,10 +76,54 @@ __global__ void embed_pos_bwd_kernel(const T* __restrict__ ds, int B, int L, int
     dpos[i] += acc;
   }
 }
-// token-type grads: dtype[t,d] = sum over rows with tt==t (deterministic, per column)
+// token-type grads: dtype[t,d] += sum over rows with tt==t (deterministic).  A block owns 8
+// column vectors (128 B of a row) x 32 row lanes striding all rows, then an LDS tree over the
+// lanes.  (The first version ran one thread per column over every row: 3 blocks, 2.4 ms per
+// C5 step.)
 template <typename T>
-__global__ void embed_type_bwd_kernel(const int64_t* __restrict__ tt, long rows, int D,
-                                      const T* __restrict__ ds, float* __restrict__ dtab) {
+__global__ __launch_bounds__(256) void embed_type_bwd_kernel(const int64_t* __restrict__ tt,
+                                                             long rows, int D,
+                                                             const T* __restrict__ ds,
+                                                             float* __restrict__ dtab) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  __shared__ float red[32][8 * VEC][2];
+  const int cv = threadIdx.x & 7, lane = threadIdx.x >> 3;
+  const int j = blockIdx.x * 8 + cv;
+  const bool ok = j < D / VEC;
+  float a0[VEC], a1[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) a0[e] = a1[e] = 0.f;
+  if (ok) {
+#pragma unroll 4
+    for (long r = lane; r < rows; r += 32) {
+      const V v = ((const V*)(ds + r * D))[j];
+      const bool one = tt && tt[r] == 1;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float g = to_f(v[e]);
+        a0[e] += one ? 0.f : g;
+        a1[e] += one ? g : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    red[lane][cv * VEC + e][0] = a0[e];
+    red[lane][cv * VEC + e][1] = a1[e];
+  }
+  __syncthreads();
+  if (threadIdx.x >= 8 * VEC * 2) return;
+  const int c = threadIdx.x >> 1, t = threadIdx.x & 1;  // one (column, type) per thread
+  if (blockIdx.x * 8 * VEC + c >= D) return;
+  float s = 0.f;
+  for (int l = 0; l < 32; ++l) s += red[l][c][t];
+  dtab[(long)t * D + blockIdx.x * 8 * VEC + c] += s;
+}
+// D not a multiple of the vector width: one column per thread
+template <typename T>
+__global__ void embed_type_bwd_scalar_kernel(const int64_t* __restrict__ tt, long rows, int D,
+                                             const T* __restrict__ ds, float* __restrict__ dtab) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= D) return;
   float a0 = 0.f, a1 = 0.f;
@@ -217,9 +261,15 @@ extern "C" int mmdx_embed_bwd(int dtype, const int64_t* ids, const int64_t* tt, 
     if (dpos)
       hipLaunchKernelGGL(embed_pos_bwd_kernel<T>, dim3(grid_for((long)L * D)), dim3(256), 0, st,
                          (const T*)dsum, B, L, D, dpos);
-    if (dtype_tab)
-      hipLaunchKernelGGL(embed_type_bwd_kernel<T>, dim3((D + 255) / 256), dim3(256), 0, st, tt,
-                         rows, D, (const T*)dsum, dtype_tab);
+    if (dtype_tab) {
+      constexpr int VEC = Vec16<T>::N;
+      if (D % VEC == 0 && ((uintptr_t)dsum & 15) == 0)
+        hipLaunchKernelGGL(embed_type_bwd_kernel<T>, dim3((D / VEC + 7) / 8), dim3(256), 0, st,
+                           tt, rows, D, (const T*)dsum, dtype_tab);
+      else
+        hipLaunchKernelGGL(embed_type_bwd_scalar_kernel<T>, dim3((D + 255) / 256), dim3(256), 0,
+                           st, tt, rows, D, (const T*)dsum, dtype_tab);
+    }
   });
   MMDX_LAUNCH_CHECK();
   return 0;
