@@ -58,6 +58,15 @@ static long gemm256_min_tiles() {
   return e ? atol(e) : 0L;
 }
 
+// The 256 x 256 tiles with 32-deep K tiles in NS = 3 / 4 stages (MMDX_GEMM256_NS; 0 = the
+// 64-deep two-stage kernel): 32 KB stages, NS - 1 tiles in flight behind a counted vmcnt
+// instead of a vmcnt(0) drain per K tile (A/B knob)
+static int gemm256_stages() {
+  const char* e = getenv("MMDX_GEMM256_NS");
+  const int ns = e ? atoi(e) : 0;
+  return ns == 3 || ns == 4 ? ns : 0;
+}
+
 template <typename T, int BM, int BN, bool AK, bool BKm, class Epi>
 static int launch_dense(const void* A, long lda, const void* B, long ldb, const Epi& epi,
                         int M, int N, int K, int splits, int kper, hipStream_t st) {
@@ -84,6 +93,22 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
         const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
         const long lim256 = gemm256_min_tiles();
         if (splits == 1 && lim256 > 0 && t256 >= lim256 && K >= 128) {
+          if (const int ns = gemm256_stages()) {
+            typedef typename std::conditional<AK, DmaK<256, SA, 32, 8>,
+                                              DmaR<256, SA, 32, 8>>::type OA32;
+            typedef typename std::conditional<BKm, DmaK<256, SB, 32, 8>,
+                                              DmaR<256, SB, 32, 8>>::type OB32;
+            if (ns == 3)
+              hipLaunchKernelGGL((igemm_dma_kernel<256, 256, OA32, OB32, Epi, 3, T, 512, 2, 4>),
+                                 dim3((unsigned)t256, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N,
+                                 K, kper);
+            else
+              hipLaunchKernelGGL((igemm_dma_kernel<256, 256, OA32, OB32, Epi, 4, T, 512, 2, 4>),
+                                 dim3((unsigned)t256, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N,
+                                 K, kper);
+            MMDX_LAUNCH_CHECK();
+            return 0;
+          }
           typedef typename std::conditional<AK, DmaK<256, SA, 64, 8>, DmaR<256, SA, 64, 8>>::type
               OA8;
           typedef typename std::conditional<BKm, DmaK<256, SB, 64, 8>,

@@ -180,9 +180,11 @@ struct DenseR {
   // LDS-DMA lane state: element offset k*ld of this lane's k-line, stepped one 64-deep K tile
   // per issue (an add instead of a multiply per DMA; the operand is < 2 GiB)
   static constexpr bool STEP = true;
+  static constexpr bool STEP_ANY = true;  // any K-tile depth (lane_step_by)
   struct Lane { int koff; };
   __device__ Lane lane_at(int k) const { return Lane{k * (int)ld}; }
   __device__ void lane_step(Lane& l) const { l.koff += (int)ld << 6; }
+  __device__ void lane_step_by(Lane& l, int bk) const { l.koff += (int)ld * bk; }
   template <bool CHECK_K>
   __device__ int roff_at(RowState rs, const Lane& l, int k, int klim) const {
     const int o = (l.koff + rs) * (int)sizeof(T);  // < 0 for an out-of-range row
@@ -1504,7 +1506,12 @@ template <int ROWS, class Src, int BK_ = 64, int NWV = NT / 64>
 struct DmaR {
   static constexpr int BK = BK_;
   static constexpr bool RMAJOR = true;
-  static_assert(!Src::STEP || BK == 64, "lane stepping advances one 64-deep K tile");
+  template <class S, class = void> struct AnyStep { static constexpr bool value = false; };
+  template <class S> struct AnyStep<S, decltype((void)S::STEP_ANY)> {
+    static constexpr bool value = S::STEP_ANY;
+  };
+  static_assert(!Src::STEP || BK == 64 || AnyStep<Src>::value,
+                "lane stepping advances one 64-deep K tile");
   static constexpr int NW = NWV;
   static constexpr int CPR = ROWS / 8;          // 16-B chunks per k-line
   static constexpr int KPI = 64 / CPR;          // k-lines per DMA instruction
@@ -1546,7 +1553,10 @@ struct DmaR {
     for (int j = 0; j < INSTR; ++j) {
       const int o = s.template roff_at<CHECK_K>(rs[j], ln[j], k0 + kr[j], klim);
       dma16(rsrc, stage + (j * NW + wid) * 1024, o >= 0 ? (unsigned)o : DMA_OOB);
-      if constexpr (Src::STEP) s.lane_step(ln[j]);
+      if constexpr (Src::STEP) {
+        if constexpr (BK == 64) s.lane_step(ln[j]);
+        else s.lane_step_by(ln[j], BK);
+      }
     }
   }
   // lane 4q+p of 16-lane group g reads k-line ks+8g+q (and +4), columns r16+4p..+3, and gets

@@ -43,10 +43,14 @@ def main():
     from mmdx import functional as F
     dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     dev = torch.device("cuda", 0)
-    tot = {"4w": 0.0, "8w": 0.0, "256": 0.0, "blas": 0.0}
-    arms = (("4w", {"MMDX_GEMM8_MIN": "0", "MMDX_GEMM256_MIN": "0"}),
-            ("8w", {"MMDX_GEMM8_MIN": "1", "MMDX_GEMM256_MIN": "0"}),
-            ("256", {"MMDX_GEMM8_MIN": "0", "MMDX_GEMM256_MIN": "1"}))
+    tot = {"4w": 0.0, "8w": 0.0, "256": 0.0, "256s3": 0.0, "256s4": 0.0, "blas": 0.0}
+    off = {"MMDX_GEMM8_MIN": "0", "MMDX_GEMM256_MIN": "0", "MMDX_GEMM256_NS": "0"}
+    arms = (("4w", dict(off)),
+            ("8w", dict(off, MMDX_GEMM8_MIN="1")),
+            ("256", dict(off, MMDX_GEMM256_MIN="1")),
+            # 256 x 256 with 32-deep K tiles, 3 / 4 stages behind a counted vmcnt
+            ("256s3", dict(off, MMDX_GEMM256_MIN="1", MMDX_GEMM256_NS="3")),
+            ("256s4", dict(off, MMDX_GEMM256_MIN="1", MMDX_GEMM256_NS="4")))
     for T, O, I in LINEARS:
         X = (torch.rand(T, I, device=dev) * 2 - 1).to(dt)
         W = (torch.rand(O, I, device=dev) * 2 - 1).to(dt)
@@ -62,9 +66,18 @@ def main():
         for name, (M, N, K, fn, tfn) in cases.items():
             C = torch.empty(M, N, dtype=dt if name != "wgrad" else torch.float32, device=dev)
             res = {}
+            ref = None
             for mode, env in arms:
                 os.environ.update(env)
                 res[mode] = timeit(lambda: fn(C), a.reps)
+                fn(C)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = C.clone()
+                elif not torch.equal(C, ref):  # every tile variant keeps the K order
+                    err = ((C.float() - ref.float()).abs().max() /
+                           ref.float().abs().max()).item()
+                    print(f"  {mode}: output differs from 4w (max rel {err:.2e})", flush=True)
             res["blas"] = timeit(tfn, a.reps)
             for k in tot:
                 tot[k] += res[k]
@@ -73,8 +86,8 @@ def main():
                 f"{k} {v * 1e3:7.1f}us {fl / v / 1e9:6.1f}TF" for k, v in res.items()),
                 flush=True)
     print("total ms: " + "  ".join(f"{k} {v:.3f}" for k, v in tot.items()), flush=True)
-    os.environ.pop("MMDX_GEMM8_MIN", None)
-    os.environ.pop("MMDX_GEMM256_MIN", None)
+    for k in off:
+        os.environ.pop(k, None)
 
 
 if __name__ == "__main__":
