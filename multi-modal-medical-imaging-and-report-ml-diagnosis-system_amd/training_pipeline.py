@@ -287,12 +287,40 @@ class _HashWordTokenizer:
                 "attention_mask": mask}
 
 
+class _WordPieceTokenizer:
+    """bert-base-uncased's tokenizer (what AutoTokenizer builds at TP:323: BertTokenizerFast,
+    lower-casing, BERT basic tokenisation, greedy longest-match WordPiece, [CLS] ... [SEP],
+    truncation, [PAD] padding) from a local vocab.txt, on the `tokenizers` library that
+    BertTokenizerFast wraps.  (transformers 5.x's BertTokenizerFast(vocab_file=...) no longer
+    reads the file: it returned [UNK] for every word.)"""
+
+    def __init__(self, vocab):
+        from tokenizers import BertWordPieceTokenizer
+        self.tok = BertWordPieceTokenizer(vocab, lowercase=True)
+        self.pad_id = self.tok.token_to_id("[PAD]")
+
+    def __call__(self, text_list, padding="max_length", truncation=True, return_tensors="pt",
+                 max_length=96):
+        if truncation:
+            self.tok.enable_truncation(max_length)
+        else:
+            self.tok.no_truncation()
+        if padding == "max_length":
+            self.tok.enable_padding(length=max_length, pad_id=self.pad_id, pad_token="[PAD]")
+        else:
+            self.tok.enable_padding(pad_id=self.pad_id, pad_token="[PAD]")
+        enc = self.tok.encode_batch(list(text_list))
+        return {"input_ids": torch.tensor([e.ids for e in enc], dtype=torch.long),
+                "token_type_ids": torch.tensor([e.type_ids for e in enc], dtype=torch.long),
+                "attention_mask": torch.tensor([e.attention_mask for e in enc],
+                                               dtype=torch.long)}
+
+
 def _tokenizer():
     if _TOKENIZER[0] is None:
         vocab = os.environ.get("MMDX_BERT_VOCAB")
         if vocab:
-            from transformers import BertTokenizerFast
-            _TOKENIZER[0] = BertTokenizerFast(vocab_file=vocab, do_lower_case=True)
+            _TOKENIZER[0] = _WordPieceTokenizer(vocab)
         else:
             _TOKENIZER[0] = _HashWordTokenizer()
     return _TOKENIZER[0]
