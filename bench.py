@@ -437,6 +437,8 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     x, ids, mask, y = synth(cfg, B, dev, 1234 + rank)
     side = torch.cuda.Stream(device=dev, priority=-1)
+    if os.environ.get("MMDX_TEXT_STREAM", "side") == "main":  # A/B: towers in series
+        side = torch.cuda.current_stream()
     from mmdx.dist import GradAllReducer
     # C5's packed buckets (the ViT-B/16 and BERT-base gradients outside the two encoder
     # stacks, whose flat gradient buffers reduce in place in fp32) travel in bf16 by default —
