@@ -34,7 +34,7 @@ extern "C" {
 #endif
 
 enum { MMDX_F32 = 0, MMDX_BF16 = 1 };
-enum { MMDX_ACT_NONE = 0, MMDX_ACT_RELU = 1, MMDX_ACT_GELU = 2 };
+enum { MMDX_ACT_NONE = 0, MMDX_ACT_RELU = 1, MMDX_ACT_GELU = 2, MMDX_ACT_GELU_BWD = 3 };
 
 int mmdx_version(void);
 const char* mmdx_last_error(void);
@@ -45,6 +45,9 @@ const char* mmdx_last_error(void);
  * A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m];  same for B with (n,k).
  * c_dtype may differ from dtype (bf16 compute -> fp32 weight-gradient output).
  * preact (optional, c_dtype, ld = ldc) receives alpha*acc + bias before the activation.
+ * act = MMDX_ACT_GELU_BWD: preact is an INPUT (the forward's pre-activation, read, not
+ * written) and C = alpha*acc * gelu'(preact) (+ beta*C): the GELU backward fused into the
+ * GEMM that produces the post-activation gradient (BERT / ViT FFN, fusion MLP).
  * Replaces: nn.Linear fwd/bwd in ImageEncoderCNN.proj/classifier (TP:189,194),
  * TextEncoderTransformer.proj/classifier (TP:365,367), BERT dense layers (TP:360 ->
  * transformers BertModel), fusion_mlp[0] + GELU (TP:534-536), disease_head (TP:542). */

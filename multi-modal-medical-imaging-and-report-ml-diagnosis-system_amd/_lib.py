@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMDX_LIB_PATH") or os.path.join(_HERE, "lib", "libmmdx_hip.so")
 
 F32, BF16, F16 = 0, 1, 2
-ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD = 0, 1, 2, 3
 
 vp, i32, i64, f32, sz, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_size_t, C.c_uint64
 

@@ -161,12 +161,13 @@ class _BertLayerFn(torch.autograd.Function):
         X, dg2, db2 = _ln_bwd(xs2, dh2, g2, mu2, rs2)
         dX2 = _dropout_bwd(X, ctx.m2, ctx.p) if ctx.m2 is not None else X
         # FFN down: f2 = f Wo2^T + bo2
-        df = torch.empty((M, I), dtype=T, device=dev)
-        F.gemm(dX2, D, True, wo2c, I, False, M, I, D, df, I, compute_dtype=T)
+        # dpre = (dX2 Wo2) * gelu'(pre): the GELU backward in the GEMM epilogue
+        dpre = torch.empty((M, I), dtype=T, device=dev)
+        F.gemm(dX2, D, True, wo2c, I, False, M, I, D, dpre, I, act=L.ACT_GELU_BWD, preact=pre,
+               compute_dtype=T)
         dWo2 = torch.empty((D, I), dtype=torch.float32, device=dev)
         F.gemm(dX2, D, False, f, I, False, D, I, M, dWo2, I, compute_dtype=T)
         dbo2 = F._bias_grad(dX2, M, D, torch.empty(D, dtype=torch.float32, device=dev))
-        dpre = F._gelu_bwd(pre, df)
         dWi = torch.empty((I, D), dtype=torch.float32, device=dev)
         F.gemm(dpre, I, False, h1, D, False, I, D, M, dWi, D, compute_dtype=T)
         dbi = F._bias_grad(dpre, M, I, torch.empty(I, dtype=torch.float32, device=dev))

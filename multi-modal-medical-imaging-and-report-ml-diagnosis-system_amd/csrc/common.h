@@ -20,7 +20,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
 enum Dtype { F32 = 0, BF16 = 1, F16 = 2 };
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };
 
 constexpr int WAVE = 64;
 

@@ -938,10 +938,11 @@ struct EpiStore {
   __device__ __forceinline__ void apply(int m, int n, float v) const {
     if (m >= M || n >= N) return;
     v = alpha * v;
-    if (bias) v += bias[n];
     const long off = (long)m * ldc + n;
+    if (act == ACT_GELU_BWD) v *= gelu_erf_grad(to_f(preact[off]));  // preact is an input
+    if (bias) v += bias[n];
     if (addend) v += addend[off];
-    if (preact) preact[off] = from_f<OutT>(v);
+    if (preact && act != ACT_GELU_BWD) preact[off] = from_f<OutT>(v);
     if (act == ACT_RELU) v = fmaxf(v, 0.f);
     else if (act == ACT_GELU) v = gelu_erf(v);
     if (beta != 0.f) v += beta * to_f(C[off]);
@@ -950,8 +951,9 @@ struct EpiStore {
   }
   // Block-uniform: every 8-column chunk can take one 16-B (bf16) / 2x16-B (fp32) store.
   __device__ __forceinline__ bool vec8_ok() const {
-    return !bias && !addend && !preact && act == ACT_NONE && ldc % 8 == 0 &&
-           ((uintptr_t)C & 15) == 0;
+    return !bias && !addend && ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
+           ((!preact && act == ACT_NONE) ||
+            (act == ACT_GELU_BWD && !acc_src && ((uintptr_t)preact & 15) == 0));
   }
   // 8 consecutive columns n..n+7 of row m (vec8_ok() checked by the caller)
   __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
@@ -964,6 +966,19 @@ struct EpiStore {
     const long off = (long)m * ldc + n;
     typedef __attribute__((ext_vector_type(8))) OutT O8;
     O8 o;
+    if (act == ACT_GELU_BWD) {  // C = alpha*acc * gelu'(pre) (+ beta*C)
+      const O8 pr = *(const O8*)(preact + off);
+      O8 c{};
+      if (beta != 0.f) c = *(const O8*)(C + off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = alpha * (j < 4 ? lo[j] : hi[j - 4]) * gelu_erf_grad(to_f(pr[j]));
+        if (beta != 0.f) v += beta * to_f(c[j]);
+        o[j] = from_f<OutT>(v);
+      }
+      *(O8*)(C + off) = o;
+      return;
+    }
     if (acc_src) {  // 8 columns = one mask byte (bf16) or two (fp32)
       const O8 c = *(const O8*)(acc_src + off);
       constexpr int VM = 16 / (int)sizeof(OutT);

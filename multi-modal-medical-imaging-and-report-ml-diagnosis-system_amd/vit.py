@@ -166,12 +166,13 @@ class _VitBlockFn(torch.autograd.Function):
         dev = x.device
         M = N * S
         dO = F.cast(dout.contiguous().reshape(M, D), T)
-        df = torch.empty((M, I), dtype=T, device=dev)
-        F.gemm(dO, D, True, w2c, I, False, M, I, D, df, I, compute_dtype=T)
+        # dpre = (dO W2) * gelu'(pre): the GELU backward in the GEMM epilogue
+        dpre = torch.empty((M, I), dtype=T, device=dev)
+        F.gemm(dO, D, True, w2c, I, False, M, I, D, dpre, I, act=L.ACT_GELU_BWD, preact=pre,
+               compute_dtype=T)
         dW2 = torch.empty((D, I), dtype=torch.float32, device=dev)
         F.gemm(dO, D, False, f, I, False, D, I, M, dW2, I, compute_dtype=T)
         dbb2 = _colsum(dO, M, D)
-        dpre = F._gelu_bwd(pre, df)
         dW1 = torch.empty((I, D), dtype=torch.float32, device=dev)
         F.gemm(dpre, I, False, u2, D, False, I, D, M, dW1, D, compute_dtype=T)
         dbb1 = _colsum(dpre, M, I)

@@ -239,7 +239,7 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
     X, Y = rb.buf((M, D)), rb.buf((M, D))
     DX2 = rb.buf((M, D)) if p > 0 else None
     DY1 = rb.buf((M, D)) if p > 0 else None
-    df, dpre = rb.buf((M, I)), rb.buf((M, I))
+    dpre = rb.buf((M, I))
     datt, dqkv = rb.buf((M, D)), rb.buf((M, 3 * D))
     G = pl.grads
     offs = []
@@ -269,10 +269,10 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         if p > 0:
             rb.dropout_bwd(X, s["m2"], M * D, p, DX2)
             dX2 = DX2
-        rb.gemm(dX2, D, True, s["wo2c"], I, False, M, I, D, df, I, T)
+        rb.gemm(dX2, D, True, s["wo2c"], I, False, M, I, D, dpre, I, T, act=L.ACT_GELU_BWD,
+                preact=s["pre"])
         rb.gemm(dX2, D, False, s["f"], I, False, D, I, M, gx(o["wo2"]), I, _F32)
         rb.colsum(dX2, M, D, gx(o["bo2"]))
-        rb.gelu_bwd(s["pre"], df, M * I, dpre)
         rb.gemm(dpre, I, False, s["h1"], D, False, I, D, M, gx(o["wi"]), D, _F32)
         rb.colsum(dpre, M, I, gx(o["bi"]))
         rb.gemm(dpre, I, True, s["wic"], D, False, M, D, I, X, D, T, beta=1.0)
@@ -346,7 +346,7 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
 
     # backward: ext 0 = upstream gradient, 1 = gradient buffer, 3 = the stack input
     rb = _Rec(pl.arena, dev, T, pl.bwd)
-    df, dpre = rb.buf((M, I)), rb.buf((M, I))
+    dpre = rb.buf((M, I))
     du2, da_ln, DA = rb.buf((M, D)), rb.buf((M, D)), rb.buf((M, D))
     datt, dqkv, du1, dx_ln = rb.buf((M, D)), rb.buf((M, 3 * D)), rb.buf((M, D)), rb.buf((M, D))
     DX = rb.buf((M, D))
@@ -363,10 +363,10 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         s, o = saves[li], offs[li]
         g1 = params[li * _VIT_NP + 0]
         g2 = params[li * _VIT_NP + 6]
-        rb.gemm(dO, D, True, s["w2c"], I, False, M, I, D, df, I, T)
+        rb.gemm(dO, D, True, s["w2c"], I, False, M, I, D, dpre, I, T, act=L.ACT_GELU_BWD,
+                preact=s["pre"])
         rb.gemm(dO, D, False, s["f"], I, False, D, I, M, gx(o[10]), I, _F32)
         rb.colsum(dO, M, D, gx(o[11]))
-        rb.gelu_bwd(s["pre"], df, M * I, dpre)
         rb.gemm(dpre, I, False, s["u2"], D, False, I, D, M, gx(o[8]), D, _F32)
         rb.colsum(dpre, M, I, gx(o[9]))
         rb.gemm(dpre, I, True, s["w1c"], D, False, M, D, I, du2, D, T)

@@ -3,6 +3,7 @@
 Tolerances: fp32 path (exact-f32 MFMA, different summation order) rel 1e-5 of the output
 scale; bf16 path rel 2e-2 (bf16 inputs, fp32 accumulation).
 """
+import math
 import pytest
 import torch
 import torch.nn.functional as tF
@@ -61,6 +62,43 @@ def test_gemm_gelu_preact_beta(dev, dt):
            compute_dtype=dt)
     _close(pre, pre_ref, dt, "preact")
     _close(C, tF.gelu(pre_ref) + 0.5 * C0, dt, "gelu+beta")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("MNK,beta", [((96, 256, 128), 0.0), ((200, 3072, 768), 0.0),
+                                      ((37, 130, 64), 0.5), ((4096, 64, 2048), 0.0)])
+def test_gemm_gelu_bwd_epilogue(dev, dt, MNK, beta):
+    """act = MMDX_ACT_GELU_BWD: C = (A B^T) * gelu'(pre) (+ beta C), pre read from `preact`
+    (the FFN backward's fused GELU gradient); vector and scalar epilogues (N % 8 != 0),
+    split-K (K = 2048 on a small grid) through the reduce kernel."""
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M + N)
+    A, B = torch.randn(M, K, generator=g) / 8, torch.randn(N, K, generator=g) / 8
+    P = torch.randn(M, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    Ad, Bd, Pd = A.to(dev, dt), B.to(dev, dt), P.to(dev, dt)
+    A, B, P = Ad.float().cpu(), Bd.float().cpu(), Pd.float().cpu()
+    x = P.double()
+    grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * math.pi) ** 0.5
+    ref = (A.double() @ B.double().T) * grad + beta * C0.to(dt).double()
+    C = C0.to(dev, dt)
+    L.call("mmdx_gemm", L.dtype_code(dt), M, N, K, Ad.data_ptr(), K, 1, Bd.data_ptr(), K, 1,
+           C.data_ptr(), N, L.dtype_code(dt), None, None, L.ACT_GELU_BWD, 1.0, beta,
+           Pd.data_ptr(), *_ws(dt, M, N, K, dev), L.stream())
+    torch.cuda.synchronize()
+    err = ((C.double().cpu() - ref).abs().max() / ref.abs().max()).item()
+    assert err <= (2e-5 if dt == torch.float32 else 1e-2), err
+    assert torch.equal(Pd.float().cpu(), P), "the pre-activation input was written"
+
+
+def _ws(dt, M, N, K, dev):
+    n = L.lib().mmdx_gemm_workspace_size(L.dtype_code(dt), M, N, K)
+    w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _WS_KEEP.append(w)
+    return w.data_ptr(), n
+
+
+_WS_KEEP = []
 
 
 CONVS = [  # N, C, H, W, K, k, s, p
