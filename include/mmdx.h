@@ -78,7 +78,8 @@ int mmdx_conv_pack_weight(int dtype, const mmdx_conv_desc* d, int c_master,
  * first_block; item i owns blocks [first_block_i, first_block_{i+1}) (the last runs to
  * total_blocks), mmdx_conv_pack_blocks(K, C, R*S) of them.  Same packing as
  * mmdx_conv_pack_weight for unpadded weights: c_master must equal C (channel-padded weights
- * use mmdx_conv_pack_weight). */
+ * use mmdx_conv_pack_weight).  Items with RS = 1 and no crsk are plain [K][C] casts: the
+ * transformer encoder stacks cast every layer's weights with one such launch (bf16 / fp16). */
 typedef struct {
   const float* w;      /* fp32 KCRS master */
   void* krsc;          /* packed [K][R][S][C] or NULL */

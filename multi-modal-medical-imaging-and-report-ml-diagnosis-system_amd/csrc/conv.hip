@@ -950,11 +950,13 @@ extern "C" long mmdx_conv_pack_blocks(int K, int C, int RS) {
 
 extern "C" int mmdx_conv_pack_multi(int dtype, const mmdx_pack_item* items, int n_items,
                                     long total_blocks, void* stream) {
-  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_pack_multi: fp16 is the C5 path only");
   MMDX_CHECK_ARG(items && n_items > 0 && total_blocks > 0 && total_blocks < (1L << 31),
                  "conv pack multi: bad item table");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == BF16)
+  if (dtype == F16)  // the C5 encoder stacks' weight casts (RS = 1 items: plain [K][C] copies)
+    hipLaunchKernelGGL(pack_multi_kernel<f16>, dim3((unsigned)total_blocks), dim3(256), 0, st,
+                       items, n_items);
+  else if (dtype == BF16)
     hipLaunchKernelGGL(pack_multi_kernel<bf16>, dim3((unsigned)total_blocks), dim3(256), 0, st,
                        items, n_items);
   else

@@ -57,6 +57,27 @@ class _Rec:
         self.ops.add(L.OP_CAST, L.dtype_code(dst.dtype), i=(L.dtype_code(src.dtype),),
                      l=(src.numel(),), p=(src, dst))
 
+    def cast_weight(self, w, dst):
+        """fp32 [K][C] master -> compute-dtype copy; every one of the stack's is cast by ONE
+        multi-tensor launch at the head of the forward (flush_weight_casts)."""
+        self.packs = getattr(self, "packs", []) + [(w, dst)]
+
+    def flush_weight_casts(self):
+        packs = getattr(self, "packs", [])
+        if not packs:
+            return
+        items = (L.PackItem * len(packs))()
+        nb = 0
+        for j, (w, dst) in enumerate(packs):
+            K, Cc = w.shape[0], w.numel() // w.shape[0]
+            items[j] = L.PackItem(w.data_ptr(), dst.data_ptr(), None, K, Cc, Cc, 1, nb)
+            nb += L.lib().mmdx_conv_pack_blocks(K, Cc, 1)
+        raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
+        tbl = self.buf((raw.numel(),), torch.uint8)
+        tbl.copy_(raw)
+        self.ops.add(L.OP_CONV_PACK_MULTI, self.dt, i=(len(packs),), l=(nb,), p=(tbl,))
+        self.ops.ops.insert(0, self.ops.ops.pop())
+
     def copy(self, src, dst, n):
         self.ops.add(L.OP_CAST, self.dt, i=(self.dt,), l=(n,), p=(src, dst))
 
@@ -187,7 +208,7 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
          b2) = params[li * _BERT_NP:(li + 1) * _BERT_NP]
         wqkv = rf.buf((3 * D, D))
         for j, w in enumerate((wq, wk, wv)):
-            rf.cast(w, wqkv[j * D:(j + 1) * D])
+            rf.cast_weight(w, wqkv[j * D:(j + 1) * D])
         bqkv = rf.buf((3 * D,), _F32)
         for j, bb in enumerate((bq, bk, bv)):
             rf.axpby(D, 1.0, bb, 0.0, None, bqkv[j * D:(j + 1) * D])
@@ -198,7 +219,7 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         rf.attn_fwd(qkv, mask, B, Ls, Hn, scale, pa, _seed(0xA770 + 7919 * li) if pa > 0 else 0,
                     counter, att, probs)
         woc = rf.buf((D, D))
-        rf.cast(wo, woc)
+        rf.cast_weight(wo, woc)
         a = rf.buf((M, D))
         rf.gemm(att, D, True, woc, D, True, M, D, D, a, D, T, bias=bo)
         m1 = None
@@ -210,12 +231,12 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         mu1, rs1 = rf.buf((M,), _F32), rf.buf((M,), _F32)
         rf.ln_fwd(a, x, g1, b1, eps, M, D, h1, xs1, mu1, rs1)
         wic = rf.buf((I, D))
-        rf.cast(wi, wic)
+        rf.cast_weight(wi, wic)
         f, pre = rf.buf((M, I)), rf.buf((M, I))
         rf.gemm(h1, D, True, wic, D, True, M, I, D, f, I, T, bias=bi, act=L.ACT_GELU,
                 preact=pre)
         wo2c = rf.buf((D, I))
-        rf.cast(wo2, wo2c)
+        rf.cast_weight(wo2, wo2c)
         f2 = rf.buf((M, D))
         rf.gemm(f, I, True, wo2c, I, True, M, D, I, f2, D, T, bias=bo2)
         m2 = None
@@ -231,6 +252,7 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
                           mu2=mu2, rs2=rs2, m1=m1, m2=m2))
         x = h2
     pl.out = x
+    rf.flush_weight_casts()
 
     # backward: ext 0 = upstream gradient [M, D] (compute dtype), 1 = gradient buffer,
     # 2 = mask.  Shared temporaries across layers; Y carries d(layer output) downward.
@@ -315,26 +337,26 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         u1, mu1, rs1 = rf.buf((M, D)), rf.buf((M,), _F32), rf.buf((M,), _F32)
         rf.ln_fwd(x, None, g1, b1, eps, M, D, u1, None, mu1, rs1)
         wqkv = rf.buf((3 * D, D))
-        rf.cast(w_in, wqkv)
+        rf.cast_weight(w_in, wqkv)
         qkv = rf.buf((M, 3 * D))
         rf.gemm(u1, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, T, bias=b_in)
         probs = rf.buf((N, heads, S, S), _F32)
         att = rf.buf((M, D))
         rf.attn_fwd(qkv, None, N, S, heads, scale, 0.0, 0, None, att, probs)
         woc = rf.buf((D, D))
-        rf.cast(w_out, woc)
+        rf.cast_weight(w_out, woc)
         o_ = rf.buf((M, D))
         rf.gemm(att, D, True, woc, D, True, M, D, D, o_, D, T, bias=b_out)
         u2, a = rf.buf((M, D)), rf.buf((M, D))
         mu2, rs2 = rf.buf((M,), _F32), rf.buf((M,), _F32)
         rf.ln_fwd(o_, x, g2, b2, eps, M, D, u2, a, mu2, rs2)
         w1c = rf.buf((I, D))
-        rf.cast(w1, w1c)
+        rf.cast_weight(w1, w1c)
         f, pre = rf.buf((M, I)), rf.buf((M, I))
         rf.gemm(u2, D, True, w1c, D, True, M, I, D, f, I, T, bias=bb1, act=L.ACT_GELU,
                 preact=pre)
         w2c = rf.buf((D, I))
-        rf.cast(w2, w2c)
+        rf.cast_weight(w2, w2c)
         out = rf.buf((M, D))
         rf.copy(a, out, M * D)
         rf.gemm(f, I, True, w2c, I, True, M, D, I, out, D, T, bias=bb2, beta=1.0)
@@ -343,6 +365,7 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
                           f=f, w2c=w2c))
         x = out
     pl.out = x
+    rf.flush_weight_casts()
 
     # backward: ext 0 = upstream gradient, 1 = gradient buffer, 3 = the stack input
     rb = _Rec(pl.arena, dev, T, pl.bwd)
