@@ -1,0 +1,74 @@
+"""Structure of the transformer-stack launch plans (mmdx.xplan), recorded on the host with
+CPU tensors standing in for device memory (nothing is launched): the parameter-gradient
+layout tiles one flat buffer exactly (what the data-parallel reducer relies on), every
+weight is cast by the single multi-tensor launch at the head of the forward, the workspace
+placeholder is patched everywhere, and the op mix per layer is the eager node's.  The
+plans' arithmetic is checked on the GPU against the eager nodes (test_stack_plans_gpu.py).
+"""
+import math
+
+import pytest
+import torch
+
+from mmdx import _lib as L
+from mmdx import bert as MB
+from mmdx import xplan
+from mmdx.vit import VitTrunk
+
+CPU = torch.device("cpu")
+
+
+def _ops(lst):
+    return [lst.arr[i] for i in range(lst.n)]
+
+
+def _check_layout(pl, params):
+    items = sorted(pl.grads.items, key=lambda t: t[2])
+    assert sorted(i for i, _, _ in items) == list(range(len(params)))
+    off = 0
+    for idx, shape, o in items:
+        assert o == off, "gaps or overlaps in the gradient buffer"
+        assert tuple(params[idx].shape) == shape
+        off += math.prod(shape)
+    assert off == pl.grads.n == sum(q.numel() for q in params)
+
+
+def _check_ops(pl, n_weights, n_layers, gemm_fwd, gemm_bwd):
+    fwd, bwd = _ops(pl.fwd), _ops(pl.bwd)
+    assert fwd[0].op == L.OP_CONV_PACK_MULTI and fwd[0].i[0] == n_weights
+    assert not any(o.op == L.OP_CAST and o.dtype != o.i[0] for o in fwd[1:]), \
+        "a weight cast outside the multi-tensor launch"
+    for o in fwd + bwd:
+        for j in range(12):
+            assert not (o.ext[j] == -1 and o.p[j] == 1), "unpatched workspace placeholder"
+    assert sum(o.op == L.OP_GEMM for o in fwd) == gemm_fwd * n_layers
+    assert sum(o.op == L.OP_GEMM for o in bwd) == gemm_bwd * n_layers
+    assert not any(o.op == L.OP_GELU_BWD for o in bwd), "GELU backward not fused"
+    assert sum(o.op == L.OP_EVENT for o in fwd) == 2 * len(pl.fwd.conv_names)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_bert_stack_plan_structure(p):
+    m = MB.BertModel.from_name("bert-base-uncased@2")
+    params = [q for lay in m.encoder.layer for q in lay.params()]
+    pl = xplan._build_bert(params, 2, 16, 768, 12, 3072, 1e-12, p, p, torch.bfloat16, CPU)
+    _check_layout(pl, params)
+    # per layer: 3 (q, k, v) + out + FFN up + FFN down weights cast; GEMMs fwd 4, bwd 8
+    _check_ops(pl, 6 * 2, 2, 4, 8)
+    drop = sum(o.op == L.OP_DROPOUT_FWD for o in _ops(pl.fwd))
+    assert drop == (4 if p > 0 else 0)
+    seeds = [o.l[1] for o in _ops(pl.fwd) if o.op == L.OP_DROPOUT_FWD]
+    assert len(set(seeds)) == len(seeds), "two dropout ops share a seed"
+
+
+def test_vit_stack_plan_structure():
+    m = VitTrunk(layers=2)
+    params = []
+    for blk in m.encoder.layers:
+        at = blk.self_attention
+        params += [blk.ln_1.weight, blk.ln_1.bias, at.in_proj_weight, at.in_proj_bias,
+                   at.out_proj.weight, at.out_proj.bias, blk.ln_2.weight, blk.ln_2.bias,
+                   blk.mlp[0].weight, blk.mlp[0].bias, blk.mlp[3].weight, blk.mlp[3].bias]
+    pl = xplan._build_vit(params, 2, 197, 768, 12, 3072, 1e-6, torch.float16, CPU)
+    _check_layout(pl, params)
+    _check_ops(pl, 4 * 2, 2, 4, 8)
