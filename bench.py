@@ -316,6 +316,7 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
             opt.step(grad_scale=scale)
         return loss
     step.norm = None
+    step.towers = towers   # (tools/host_profile.py profiles the text thread through it)
     return step
 
 

@@ -4,6 +4,7 @@ Python enqueue time per step goes.   python tools/host_profile.py [--config c4] 
 import argparse
 import cProfile
 import os
+import time
 import pstats
 import sys
 
@@ -31,14 +32,24 @@ def main():
         step()
     torch.cuda.synchronize()
     pr = cProfile.Profile()
+    pt = cProfile.Profile()   # the text tower's worker thread (TwoTowerForward)
+    pool = step.towers._pool
+    pool.submit(pt.enable).result()
     pr.enable()
+    t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    host = (time.perf_counter() - t0) / a.steps
     pr.disable()
+    pool.submit(pt.disable).result()
     torch.cuda.synchronize()
+    print(f"host time per step (main thread, wall, device busy): {host * 1e3:.2f} ms")
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(35)
     st.sort_stats("cumulative").print_stats(25)
+    print("=== text tower thread ===")
+    st2 = pstats.Stats(pt)
+    st2.sort_stats("cumulative").print_stats(25)
 
 
 if __name__ == "__main__":
