@@ -745,10 +745,25 @@ def _side_stream(trunk, dev):
     return st
 
 
+# recorded configurations kept per module; older keys (another batch shape, re-allocated
+# parameters) whose arenas are all idle are dropped, so their buffers can be freed
+MAX_PLAN_KEYS = 4
+
+
 def _plans_for(trunk, key, build):
     """A free arena for `key` (recording a new one if every recorded arena is held)."""
     cache = trunk.__dict__.setdefault("_mmdx_plans", {})
-    lst = cache.setdefault(key, [])
+    return plan_cache_get(cache, key, build)
+
+
+def plan_cache_get(cache, key, build):
+    """Shared by the trunk and the encoder-stack plans: an idle plan recorded for `key`, or a
+    new one; least recently used keys beyond MAX_PLAN_KEYS are evicted when idle."""
+    lst = cache.pop(key, [])
+    cache[key] = lst   # most recently used last
+    for old in [k for k in cache if k != key][:max(0, len(cache) - MAX_PLAN_KEYS)]:
+        if not any(pl.arena.busy() for pl in cache[old]):
+            del cache[old]
     for pl in lst:
         if not pl.arena.busy():
             return pl

@@ -27,7 +27,7 @@ import torch
 
 from . import _lib as L
 from . import functional as F
-from .resnet import _Arena, _Ext, _OpList, _Token
+from .resnet import _Arena, _Ext, _OpList, _Token, plan_cache_get
 
 _WS_TOKEN = 0x1   # placeholder operand for the plan's workspace (patched when sized)
 _F32 = torch.float32
@@ -172,13 +172,7 @@ class _StackPlan:
 
 def _plans_for(owner, key, build):
     cache = owner.__dict__.setdefault("_mmdx_stack_plans", {})
-    lst = cache.setdefault(key, [])
-    for pl in lst:
-        if not (pl.arena.owner is not None and pl.arena.owner() is not None):
-            return pl
-    pl = build()
-    lst.append(pl)
-    return pl
+    return plan_cache_get(cache, key, build)
 
 
 def _seed(base):

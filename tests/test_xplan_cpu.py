@@ -72,3 +72,35 @@ def test_vit_stack_plan_structure():
     pl = xplan._build_vit(params, 2, 197, 768, 12, 3072, 1e-6, torch.float16, CPU)
     _check_layout(pl, params)
     _check_ops(pl, 4 * 2, 2, 4, 8)
+
+
+def test_plan_cache_evicts_idle_stale_keys(monkeypatch):
+    """Plans recorded for keys no longer used (other batch shapes, re-allocated parameters)
+    are dropped once more than MAX_PLAN_KEYS keys exist and their arenas are idle; a busy
+    arena (its backward still pending) is never dropped."""
+    from mmdx import resnet as RN
+
+    class _A:
+        def __init__(self):
+            self.b = False
+
+        def busy(self):
+            return self.b
+
+    class _P:
+        def __init__(self):
+            self.arena = _A()
+
+    monkeypatch.setattr(RN, "MAX_PLAN_KEYS", 2)
+    cache = {}
+    p0 = RN.plan_cache_get(cache, "k0", _P)
+    p0.arena.b = True                       # k0's backward pending
+    RN.plan_cache_get(cache, "k1", _P)
+    RN.plan_cache_get(cache, "k2", _P)
+    RN.plan_cache_get(cache, "k3", _P)
+    assert "k0" in cache                    # busy: kept
+    p0.arena.b = False
+    RN.plan_cache_get(cache, "k4", _P)
+    assert len(cache) <= 3 and "k0" not in cache and "k4" in cache
+    again = RN.plan_cache_get(cache, "k4", _P)
+    assert again is cache["k4"][0]          # an idle plan of the key is reused
