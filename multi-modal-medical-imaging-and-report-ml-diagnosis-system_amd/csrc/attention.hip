@@ -13,6 +13,7 @@
 // and no mask tensor: dV = P'^T dO, dP = keep * (dO V^T) / (1 - p),
 // dS = P o (dP - rowsum(P o dP)).
 #include <algorithm>
+#include <type_traits>
 
 #include "igemm.h"
 #include "../../include/mmdx.h"
@@ -39,34 +40,90 @@ __device__ __forceinline__ float rowgroup_sum(float v) {
   return v;
 }
 
-template <typename T>
-__device__ __forceinline__ void load_rows(T* dst, int ld, const T* src, long src_ld, int rows,
-                                          int rows_valid, int nthreads) {
-  // rows x 64 elements (16-B vectors), zero beyond rows_valid
-  typedef typename Vec16<T>::type V;
-  constexpr int VEC = Vec16<T>::N;
-  constexpr int VPR = HD / VEC;
-  for (int i = threadIdx.x; i < rows * VPR; i += nthreads) {
-    const int r = i / VPR, c = (i - r * VPR) * VEC;
-    V v{};
-    if (r < rows_valid) v = *(const V*)(src + r * src_ld + c);
-    *(V*)(dst + r * ld + c) = v;
+// Global -> LDS staging of rows x 64-element head slices (16-B vectors, zero beyond
+// rows_valid).  Every thread issues all U loads of a round before its first LDS store, so a
+// round costs one memory latency; the former load-store-per-vector loop serialised 7-16 of
+// them per block and made the attention kernels latency bound (isolated ViT fwd 128 us).
+template <typename T, bool TR>
+__device__ __forceinline__ void put_row_vec(T* dst, int ld, int r, int c,
+                                            const typename Vec16<T>::type& v) {
+  if (TR) {  // dst[c][r] = src[r][c]
+#pragma unroll
+    for (int j = 0; j < Vec16<T>::N; ++j) dst[(c + j) * ld + r] = v[j];
+  } else {
+    *(typename Vec16<T>::type*)(dst + r * ld + c) = v;
   }
 }
-template <typename T>
-__device__ __forceinline__ void load_rows_T(T* dst, int ld, const T* src, long src_ld, int rows,
-                                            int rows_valid, int nthreads) {
-  // dst[c][r] = src[r][c] for rows x 64
+// Two tiles of identical row geometry (K and V, or V and K, of one head): U vectors of each
+// in flight per thread per round.  TA / TB: whether tile a / b is stored transposed.
+template <typename T, int U, bool TA, bool TB>
+__device__ __forceinline__ void stage_pair(T* da, int lda, const T* sa, T* db, int ldb,
+                                           const T* sb, long src_ld, int rows, int rows_valid,
+                                           int nthreads) {
   typedef typename Vec16<T>::type V;
-  constexpr int VEC = Vec16<T>::N;
-  constexpr int VPR = HD / VEC;
-  for (int i = threadIdx.x; i < rows * VPR; i += nthreads) {
-    const int r = i / VPR, c = (i - r * VPR) * VEC;
-    V v{};
-    if (r < rows_valid) v = *(const V*)(src + r * src_ld + c);
+  constexpr int VEC = Vec16<T>::N, VPR = HD / VEC;
+  const int total = rows * VPR;
+  for (int i0 = threadIdx.x; i0 < total; i0 += U * nthreads) {
+    V va[U], vb[U];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) dst[(c + j) * ld + r] = v[j];
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nthreads, r = i / VPR, c = (i - r * VPR) * VEC;
+      va[u] = V{};
+      vb[u] = V{};
+      if (i < total && r < rows_valid) {
+        va[u] = *(const V*)(sa + r * src_ld + c);
+        vb[u] = *(const V*)(sb + r * src_ld + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nthreads, r = i / VPR, c = (i - r * VPR) * VEC;
+      if (i < total) {
+        put_row_vec<T, TA>(da, lda, r, c, va[u]);
+        put_row_vec<T, TB>(db, ldb, r, c, vb[u]);
+      }
+    }
   }
+}
+template <typename T, int U, bool TR>
+__device__ __forceinline__ void stage_rows(T* dst, int ld, const T* src, long src_ld, int rows,
+                                           int rows_valid, int nthreads) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N, VPR = HD / VEC;
+  const int total = rows * VPR;
+  for (int i0 = threadIdx.x; i0 < total; i0 += U * nthreads) {
+    V v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nthreads, r = i / VPR, c = (i - r * VPR) * VEC;
+      v[u] = V{};
+      if (i < total && r < rows_valid) v[u] = *(const V*)(src + r * src_ld + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nthreads, r = i / VPR, c = (i - r * VPR) * VEC;
+      if (i < total) put_row_vec<T, TR>(dst, ld, r, c, v[u]);
+    }
+  }
+}
+
+// XCD-aware block order for a 1-D grid of nb blocks per (batch, head): the 8 XCDs take linear
+// block ids round-robin and each has its own L2, so the nb blocks of one head, which all read
+// that head's K and V (or Q, dO, P), get ids congruent mod 8 and share one XCD's L2 instead
+// of fetching the head once per XCD.
+__device__ __forceinline__ void attn_block(int nb, int H, int& blk, int& h, int& b) {
+  const int n = blockIdx.x, bh = gridDim.x / nb;
+  int hl;
+  if ((bh & 7) == 0) {
+    const int k = n >> 3;
+    blk = k % nb;
+    hl = (k / nb) * 8 + (n & 7);
+  } else {
+    blk = n % nb;
+    hl = n / nb;
+  }
+  h = hl % H;
+  b = hl / H;
 }
 
 __device__ __forceinline__ uint32_t attn_hash64(uint64_t x) {
@@ -76,12 +133,13 @@ __device__ __forceinline__ uint32_t attn_hash64(uint64_t x) {
   return (uint32_t)x;
 }
 
+// (launch bounds: the LDS footprint allows two blocks per CU; the default 1024-thread budget
+// of 128 VGPRs spilled the staged K / V vectors)
 template <typename T>
-__global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask,
-                                const float* __restrict__ bias, int causal, int L, int H,
-                                float scale, float p_drop, uint64_t seed,
-                                const uint64_t* __restrict__ ctr, T* __restrict__ out,
-                                float* __restrict__ probs) {
+__global__ __launch_bounds__(AttnCfg<T>::NW * 64, 2) void attn_fwd_kernel(
+    const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bias,
+    int causal, int L, int H, float scale, float p_drop, uint64_t seed,
+    const uint64_t* __restrict__ ctr, T* __restrict__ out, float* __restrict__ probs) {
   typedef MfmaOp<T> Op;
   constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
   constexpr int LDQ = HD + PAD;
@@ -97,9 +155,9 @@ __global__ void attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __rest
   const int nth = NW * 64;
   const long row_ld = 3L * H * HD;
   const T* base = qkv + (long)b * L * row_ld + h * HD;
-  load_rows<T>(Qs, LDQ, base + (long)q0 * row_ld, row_ld, QB, min(QB, L - q0), nth);
-  load_rows<T>(Ks, LDQ, base + (long)H * HD, row_ld, LP, L, nth);
-  load_rows_T<T>(Vt, LDV, base + 2L * H * HD, row_ld, LP, L, nth);
+  stage_pair<T, 4, false, true>(Ks, LDQ, base + (long)H * HD, Vt, LDV, base + 2L * H * HD,
+                                row_ld, LP, L, nth);
+  stage_rows<T, 4, false>(Qs, LDQ, base + (long)q0 * row_ld, row_ld, QB, min(QB, L - q0), nth);
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nkt = LP / 16;
@@ -219,10 +277,10 @@ __global__ __launch_bounds__(AttnCfg<T>::NW * 64, 2) void attn_bwd_q_kernel(
   const int nth = NW * 64;
   const long row_ld = 3L * H * HD;
   const T* base = qkv + (long)b * L * row_ld + h * HD;
-  load_rows<T>(dOs, LDQ, dout + ((long)b * L + q0) * H * HD + h * HD, (long)H * HD, QB,
-               min(QB, L - q0), nth);
-  load_rows<T>(Vs, LDQ, base + 2L * H * HD, row_ld, LP, L, nth);
-  load_rows_T<T>(Kt, LDV, base + (long)H * HD, row_ld, LP, L, nth);
+  stage_pair<T, 8, false, true>(Vs, LDQ, base + 2L * H * HD, Kt, LDV, base + (long)H * HD,
+                                row_ld, LP, L, nth);
+  stage_rows<T, 4, false>(dOs, LDQ, dout + ((long)b * L + q0) * H * HD + h * HD, (long)H * HD,
+                          QB, min(QB, L - q0), nth);
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nkt = LP / 16;
@@ -300,7 +358,7 @@ __global__ __launch_bounds__(AttnCfg<T>::NW * 64, 2) void attn_bwd_q_kernel(
 // 32-query chunks through LDS.
 constexpr int QC = 32;
 template <typename T>
-__global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
+__global__ __launch_bounds__(AttnCfg<T>::NW * 64, 2) void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __restrict__ probs,
                                    const T* __restrict__ dout, const T* __restrict__ dS_g, int L,
                                    int H, float scale, float keep_scale, T* __restrict__ dqkv) {
   typedef MfmaOp<T> Op;
@@ -310,8 +368,9 @@ __global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __res
   __shared__ __attribute__((aligned(16))) T dSt[KB * LDC];   // [key][q]
   __shared__ __attribute__((aligned(16))) T dOt[HD * LDC];   // [d][q]
   __shared__ __attribute__((aligned(16))) T Qt[HD * LDC];    // [d][q]
-  const int k0 = blockIdx.x * KB, h = blockIdx.y, b = blockIdx.z;
-  const int nth = NW * 64;
+  int kb, h, b;
+  attn_block((L + KB - 1) / KB, H, kb, h, b);
+  const int k0 = kb * KB;
   const int LP = (L + 31) & ~31;  // multiple of the bf16 MFMA K (32)
   const long row_ld = 3L * H * HD;
   const T* qbase = qkv + (long)b * L * row_ld + h * HD;
@@ -321,19 +380,61 @@ __global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __res
   f32x4 dv[HD / 16], dk[HD / 16];
 #pragma unroll
   for (int j = 0; j < HD / 16; ++j) dv[j] = dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int qc = 0; qc < L; qc += QC) {
-    for (int i = threadIdx.x; i < KB * QC; i += nth) {
-      const int kk = i / QC, qq = i - kk * QC;
-      const int key = k0 + kk, q = qc + qq;
+  // Chunk staging: thread (kk, qg) owns key k0+kk and the 8 queries qg*8.. of a chunk, so
+  // the P / dS reads are key-contiguous across lanes (coalesced rows of [q][key]) and land in
+  // LDS as one [key][q] vector store each; the dO / Q slices of the chunk are NV vectors per
+  // thread.  The next chunk's loads are issued into registers before this chunk's MFMAs.
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N, VPR = HD / VEC, NTH = NW * 64;
+  constexpr int QG = 8, NV = QC * VPR / NTH;
+  static_assert(KB * QC == NTH * QG && NV * NTH == QC * VPR, "chunk staging shape");
+  const int kk = threadIdx.x % KB, qg = threadIdx.x / KB;
+  float pr[QG];
+  T dsr[QG];
+  V dov[NV], qv[NV];
+  auto fetch = [&](int qc) {
+    const int key = k0 + kk;
+#pragma unroll
+    for (int u = 0; u < QG; ++u) {
+      const int q = qc + qg * QG + u;
       const bool ok = key < L && q < L;
-      const float v = ok ? pb[(long)q * L + key] : 0.f;
-      Pt[kk * LDC + qq] = from_f<T>(__builtin_signbitf(v) ? 0.f : v * keep_scale);  // P'
-      dSt[kk * LDC + qq] = ok ? dsb[(long)q * LP + key] : from_f<T>(0.f);
+      pr[u] = ok ? pb[(long)q * L + key] : 0.f;
+      dsr[u] = ok ? dsb[(long)q * LP + key] : from_f<T>(0.f);
     }
-    load_rows_T<T>(dOt, LDC, dout + ((long)b * L + qc) * H * HD + h * HD, (long)H * HD, QC,
-                   min(QC, L - qc), nth);
-    load_rows_T<T>(Qt, LDC, qbase + (long)qc * row_ld, row_ld, QC, min(QC, L - qc), nth);
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      const int i = threadIdx.x + n * NTH, r = i / VPR, c = (i - r * VPR) * VEC;
+      const int q = qc + r;
+      dov[n] = V{};
+      qv[n] = V{};
+      if (q < L) {
+        dov[n] = *(const V*)(dout + ((long)b * L + q) * H * HD + h * HD + c);
+        qv[n] = *(const V*)(qbase + (long)q * row_ld + c);
+      }
+    }
+  };
+  fetch(0);
+  for (int qc = 0; qc < L; qc += QC) {
+#pragma unroll
+    for (int w = 0; w < QG / VEC; ++w) {
+      V pv, sv;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float v = pr[w * VEC + j];
+        pv[j] = from_f<T>(__builtin_signbitf(v) ? 0.f : v * keep_scale);  // P'
+        sv[j] = dsr[w * VEC + j];
+      }
+      *(V*)(Pt + kk * LDC + qg * QG + w * VEC) = pv;
+      *(V*)(dSt + kk * LDC + qg * QG + w * VEC) = sv;
+    }
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      const int i = threadIdx.x + n * NTH, r = i / VPR, c = (i - r * VPR) * VEC;
+      put_row_vec<T, true>(dOt, LDC, r, c, dov[n]);
+      put_row_vec<T, true>(Qt, LDC, r, c, qv[n]);
+    }
     __syncthreads();
+    if (qc + QC < L) fetch(qc + QC);
     const T* ap = Pt + (wid * 16 + (lane & 15)) * LDC + (lane >> 4) * Op::FRAG;
     const T* as = dSt + (wid * 16 + (lane & 15)) * LDC + (lane >> 4) * Op::FRAG;
 #pragma unroll
@@ -361,6 +462,310 @@ __global__ void attn_bwd_kv_kernel(const T* __restrict__ qkv, const float* __res
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// 16-bit (bf16 / f16) kernels with swapped products.  S^T = K Q^T (and dP^T = V dO^T) puts
+// one query on each lane's column: lane (ql = lane & 15, g = lane >> 4) of wave w holds,
+// for every 16-key tile j, the four keys j*16 + g*4 + r (r = 0..3) of query q0 + w*16 + ql.
+// Consequences:
+//  * the row softmax (and the dP row dot) is a per-lane sum plus two cross-group shuffles;
+//  * a lane's 4 consecutive keys are one 16-B probability store / load;
+//  * the 8 keys of tiles (2t, 2t+1) at offsets g*4 .. g*4+3 are, in that order, the k
+//    elements of the MFMA B operand P^T (dS^T) of the next product O^T = V^T P^T
+//    (dQ^T = K^T dS^T): no LDS round trip for P / dS.  The A operand V^T (K^T) takes the
+//    same permuted key order from a row-major LDS image with two ds_read_b64_tr_b16;
+//  * Q and dO, the B operands of the first product, come straight from HBM into registers.
+// ---------------------------------------------------------------------------------------
+constexpr int LDR = HD + 8;    // 144-B rows: ds_read_b128 operand rows
+constexpr int LDT = HD + 16;   // 160-B rows: 8 consecutive rows of a 32-B column block fall
+                               // on distinct banks -> conflict-free transposed reads
+constexpr int LDP = 20;        // fp32 [16][16] probability tile transpose, padded: conflict-free
+                               // 16-B writes and 4-B column reads
+typedef short s16x4v __attribute__((__vector_size__(4 * sizeof(short))));
+typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
+
+// Rows row0 .. row0+3 of 16 columns col0.. of a row-major [rows][LDT] 16-bit LDS tile,
+// delivered column-major: lane i of each 16-lane group gets column col0 + i, row e in
+// element e.  Every lane of the wave must execute it (EXEC all ones).
+template <typename T>
+__device__ __forceinline__ s16x4v tr_read4(const T* tile, int row0, int col0) {
+  const int l = threadIdx.x & 15;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4v*)(tile + (row0 + (l >> 2)) * LDT + col0 + 4 * (l & 3)));
+}
+template <typename T>
+__device__ __forceinline__ typename MfmaOp<T>::frag_t join_frag(s16x4v lo, s16x4v hi) {
+  union { s16x4v h[2]; typename MfmaOp<T>::frag_t f; } u;
+  u.h[0] = lo;
+  u.h[1] = hi;
+  return u.f;
+}
+// 4 consecutive 16-bit elements as one 8-B store
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, float a, float b, float c, float d) {
+  union { T e[4]; uint2 u; } pk;
+  pk.e[0] = from_f<T>(a); pk.e[1] = from_f<T>(b); pk.e[2] = from_f<T>(c); pk.e[3] = from_f<T>(d);
+  *(uint2*)dst = pk.u;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void attn_fwd16_kernel(
+    const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bias,
+    int causal, int L, int H, float scale, float p_drop, uint64_t seed,
+    const uint64_t* __restrict__ ctr, T* __restrict__ out, float* __restrict__ probs) {
+  typedef MfmaOp<T> Op;
+  typedef typename Op::frag_t F;
+  static_assert(Op::FRAG == 8 && Op::KS == 32, "16-bit MFMA 16x16x32 operands");
+  constexpr int QB = 64;
+  const int LP = (L + 31) & ~31;
+  const int nkt = LP / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Ks = (T*)smem_raw;               // [LP][LDR]  A operand rows of S^T
+  T* Vs = Ks + LP * LDR;              // [LP][LDT]  transposed reads for V^T
+  float* madd = (float*)(Vs + LP * LDT);   // [LP] additive key mask
+  int qb, h, b;
+  attn_block((L + QB - 1) / QB, H, qb, h, b);
+  const int q0 = qb * QB;
+  const long row_ld = 3L * H * HD;
+  const T* base = qkv + (long)b * L * row_ld + h * HD;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ql = lane & 15, g = lane >> 4;
+  const int q = q0 + wid * 16 + ql;
+  F qf[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    qf[k] = F{};
+    if (q < L) qf[k] = *(const F*)(base + (long)q * row_ld + k * 32 + g * 8);
+  }
+  stage_pair<T, 4, false, false>(Ks, LDR, base + (long)H * HD, Vs, LDT, base + 2L * H * HD,
+                                 row_ld, LP, L, 256);
+  for (int k = threadIdx.x; k < LP; k += 256)
+    madd[k] = k < L ? (mask && mask[(long)b * L + k] == 0 ? MASK_NEG : 0.f) : -INFINITY;
+  __syncthreads();
+  // s[j][r] = S[q][j*16 + g*4 + r]
+  f32x4 s[MAXKT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (j >= nkt) continue;
+    const T* a = Ks + (j * 16 + ql) * LDR + g * 8;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) s[j] = Op::mma(Op::ld(a + k * 32), qf[k], s[j]);
+    const f32x4 ma = *(const f32x4*)(madd + j * 16 + g * 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = j * 16 + g * 4 + r;
+      float v = s[j][r] * scale + ma[r];
+      // additive score bias [H][L][L] (T5 relative position bias) and causal mask
+      if (bias && key < L && q < L) v += bias[((long)h * L + q) * L + key];
+      if (causal && key > q && key < L) v = MASK_NEG;
+      s[j][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[j][r] = __expf(s[j][r] - mx);
+      sum += s[j][r];
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  float* pbase = probs ? probs + (((long)b * H + h) * L) * L : nullptr;
+  const bool vec_p = (L & 3) == 0;
+  // L % 4 != 0: the lane's 4 keys are not a 16-B aligned run of a row; the wave transposes
+  // each 16 x 16 tile through its LDS scratch so a store covers 64 contiguous bytes of 4 rows
+  float* pscr = madd + LP + wid * 16 * LDP;
+  const bool drop = p_drop > 0.f;
+  const float keep_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
+  const uint64_t rbase = drop ? seed * 0x9E3779B97F4A7C15ULL + (ctr ? ctr[0] << 32 : 0ull) +
+                                    (((uint64_t)b * H + h) * L) * (uint64_t)L
+                              : 0ull;
+  F pf[MAXKT / 2];
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+    f32x4 pv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = j * 16 + g * 4 + r;
+      const float p = s[j][r] * inv;
+      bool keep = true;
+      if (drop) {
+        const float u = (attn_hash64(rbase + (uint64_t)q * L + key) >> 8) * (1.f / 16777216.f);
+        keep = u >= p_drop;
+      }
+      pf[j >> 1][(j & 1) * 4 + r] = from_f<T>(keep ? p * keep_scale : 0.f);
+      pv[r] = keep ? p : -p;
+    }
+    if (pbase) {
+      const int k0 = j * 16 + g * 4;
+      if (vec_p) {
+        if (q < L && k0 < L) *(f32x4*)(pbase + (long)q * L + k0) = pv;
+      } else {
+        *(f32x4*)(pscr + ql * LDP + g * 4) = pv;   // [q][key] of the tile
+        const int key = j * 16 + ql;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // in-order LDS within the wave: no barrier
+          const int qr = q0 + wid * 16 + g * 4 + r;
+          const float v = pscr[(g * 4 + r) * LDP + ql];
+          if (qr < L && key < L) pbase[(long)qr * L + key] = v;
+        }
+      }
+    }
+  }
+  // O^T[d][q] = sum_key V^T[d][key] P'^T[key][q]
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < MAXKT / 2; ++t) {
+    if (2 * t >= nkt) continue;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const F vf = join_frag<T>(tr_read4(Vs, 2 * t * 16 + g * 4, dt * 16),
+                                tr_read4(Vs, (2 * t + 1) * 16 + g * 4, dt * 16));
+      o[dt] = Op::mma(vf, pf[t], o[dt]);
+    }
+  }
+  if (q < L) {
+    T* orow = out + ((long)b * L + q) * H * HD + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+      store4<T>(orow + dt * 16 + g * 4, o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+  }
+}
+
+// Backward A (16-bit): dP^T = V dO^T, dS = P o (dP - rowsum(P o dP)) -> dS_g [B,H,L,LP],
+// dQ^T = scale K^T dS^T.
+template <typename T>
+__global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
+    const T* __restrict__ qkv, const float* __restrict__ probs, const T* __restrict__ dout,
+    int L, int H, float scale, float keep_scale, T* __restrict__ dS_g, T* __restrict__ dqkv) {
+  typedef MfmaOp<T> Op;
+  typedef typename Op::frag_t F;
+  constexpr int QB = 64;
+  const int LP = (L + 31) & ~31;
+  const int nkt = LP / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Vs = (T*)smem_raw;               // [LP][LDR]  A operand rows of dP^T
+  T* Ks = Vs + LP * LDR;              // [LP][LDT]  transposed reads for K^T
+  int qb, h, b;
+  attn_block((L + QB - 1) / QB, H, qb, h, b);
+  const int q0 = qb * QB;
+  const long row_ld = 3L * H * HD;
+  const T* base = qkv + (long)b * L * row_ld + h * HD;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ql = lane & 15, g = lane >> 4;
+  const int q = q0 + wid * 16 + ql;
+  F of[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    of[k] = F{};
+    if (q < L) of[k] = *(const F*)(dout + ((long)b * L + q) * H * HD + h * HD + k * 32 + g * 8);
+  }
+  stage_pair<T, 4, false, false>(Vs, LDR, base + 2L * H * HD, Ks, LDT, base + (long)H * HD,
+                                 row_ld, LP, L, 256);
+  __syncthreads();
+  // saved probabilities P[q][j*16 + g*4 + r] -> pv[j][r]: one 16-B load per tile when
+  // L % 4 == 0; otherwise 4 loads of 64 contiguous bytes of 4 rows each, transposed through
+  // the wave's LDS scratch (in-order LDS within the wave: no barrier)
+  const float* pbase = probs + (((long)b * H + h) * L) * L;
+  f32x4 s[MAXKT], pv[MAXKT];
+  if ((L & 3) == 0) {
+#pragma unroll
+    for (int j = 0; j < MAXKT; ++j) {
+      pv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j < nkt && q < L && j * 16 + g * 4 < L)
+        pv[j] = *(const f32x4*)(pbase + (long)q * L + j * 16 + g * 4);
+    }
+  } else {
+    float* pscr = (float*)(Ks + LP * LDT) + LP + wid * 16 * LDP;
+#pragma unroll
+    for (int j = 0; j < MAXKT; ++j) {
+      pv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j >= nkt) continue;
+      const int key = j * 16 + ql;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qr = q0 + wid * 16 + g * 4 + r;
+        if (qr < L && key < L) pv[j][r] = pbase[(long)qr * L + key];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXKT; ++j) {
+      if (j >= nkt) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pscr[(g * 4 + r) * LDP + ql] = pv[j][r];
+      pv[j] = *(const f32x4*)(pscr + ql * LDP + g * 4);
+    }
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (j >= nkt) continue;
+    const f32x4 pr = pv[j];
+    const T* a = Vs + (j * 16 + ql) * LDR + g * 8;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) s[j] = Op::mma(Op::ld(a + k * 32), of[k], s[j]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // dP = keep * dP' / (1 - p); dropped elements are saved with the sign bit set
+      s[j][r] = __builtin_signbitf(pr[r]) ? 0.f : s[j][r] * keep_scale;
+      pv[j][r] = fabsf(pr[r]);
+      dot += pv[j][r] * s[j][r];
+    }
+  }
+  dot += __shfl_xor(dot, 16, 64);
+  dot += __shfl_xor(dot, 32, 64);
+  T* dsrow = dS_g + ((((long)b * H + h) * L) + q) * LP;
+  F df[MAXKT / 2];
+#pragma unroll
+  for (int j = 0; j < MAXKT; ++j) {
+    if (j >= nkt) continue;
+    float ds[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const T dst = from_f<T>(pv[j][r] * (s[j][r] - dot));
+      df[j >> 1][(j & 1) * 4 + r] = dst;
+      ds[r] = (float)dst;
+    }
+    if (q < L) store4<T>(dsrow + j * 16 + g * 4, ds[0], ds[1], ds[2], ds[3]);
+  }
+  // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < MAXKT / 2; ++t) {
+    if (2 * t >= nkt) continue;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const F kf = join_frag<T>(tr_read4(Ks, 2 * t * 16 + g * 4, dt * 16),
+                                tr_read4(Ks, (2 * t + 1) * 16 + g * 4, dt * 16));
+      o[dt] = Op::mma(kf, df[t], o[dt]);
+    }
+  }
+  if (q < L) {
+    T* drow = dqkv + ((long)b * L + q) * 3 * H * HD + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+      store4<T>(drow + dt * 16 + g * 4, o[dt][0] * scale, o[dt][1] * scale, o[dt][2] * scale,
+                o[dt][3] * scale);
+  }
+}
+
+static size_t smem16(int L) {
+  const size_t LP = (L + 31) & ~31;
+  return LP * (LDR + LDT) * 2 + (LP + 4 * 16 * LDP) * sizeof(float);
+}
+
 template <typename T>
 static size_t fwd_smem(int L) {
   constexpr int NW = AttnCfg<T>::NW, QB = NW * 16, PAD = Vec16<T>::N;
@@ -386,14 +791,23 @@ extern "C" int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* 
                  "attention: dropout needs the saved probabilities (training)");
   hipStream_t st = (hipStream_t)stream;
   MMDX_DISPATCH(dtype, {
-    constexpr int QB = AttnCfg<T>::NW * 16;
-    const size_t sm = fwd_smem<T>(L);
-    MMDX_CHECK_ARG(sm <= 160 * 1024, "attention: L=%d needs %zu B LDS", L, sm);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3((L + QB - 1) / QB, H, B),
-                       dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, mask, bias, causal, L,
-                       H, scale, p_drop, seed, (const uint64_t*)counter, (T*)out, probs);
+    if constexpr (std::is_same<T, float>::value) {
+      constexpr int QB = AttnCfg<T>::NW * 16;
+      const size_t sm = fwd_smem<T>(L);
+      MMDX_CHECK_ARG(sm <= 160 * 1024, "attention: L=%d needs %zu B LDS", L, sm);
+      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3((L + QB - 1) / QB, H, B),
+                         dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, mask, bias, causal,
+                         L, H, scale, p_drop, seed, (const uint64_t*)counter, (T*)out, probs);
+    } else {
+      const size_t sm = smem16(L);
+      (void)hipFuncSetAttribute((const void*)attn_fwd16_kernel<T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      hipLaunchKernelGGL(attn_fwd16_kernel<T>, dim3((L + 63) / 64 * H * B), dim3(256), sm, st,
+                         (const T*)qkv, mask, bias, causal, L, H, scale, p_drop, seed,
+                         (const uint64_t*)counter, (T*)out, probs);
+    }
   });
   if (p_drop > 0.f && counter)
     hipLaunchKernelGGL(attn_counter_incr_kernel, dim3(1), dim3(1), 0, st, counter);
@@ -424,22 +838,28 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_attention_workspace_size(dtype, B, L, H),
                  "attention bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-#define ATTN_BWD(T)                                                                            \
-  {                                                                                            \
-    constexpr int QB = AttnCfg<T>::NW * 16;                                                    \
-    const size_t sm = fwd_smem<T>(L);                                                          \
-    MMDX_CHECK_ARG(sm <= 160 * 1024, "attention bwd: L=%d needs %zu B LDS", L, sm);           \
-    (void)hipFuncSetAttribute((const void*)attn_bwd_q_kernel<T>,                                     \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);                  \
-    hipLaunchKernelGGL(attn_bwd_q_kernel<T>, dim3((L + QB - 1) / QB, H, B),                    \
-                       dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, probs,                \
-                       (const T*)dout, L, H, scale, keep_scale, (T*)ws, (T*)dqkv);             \
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((L + QB - 1) / QB, H, B),                   \
-                       dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs, (const T*)dout, \
-                       (const T*)ws, L, H, scale, keep_scale, (T*)dqkv);                       \
-  }
-  if (dtype == BF16) ATTN_BWD(bf16) else if (dtype == F16) ATTN_BWD(f16) else ATTN_BWD(float)
-#undef ATTN_BWD
+  MMDX_DISPATCH(dtype, {
+    constexpr int QB = AttnCfg<T>::NW * 16;
+    if constexpr (std::is_same<T, float>::value) {
+      const size_t sm = fwd_smem<T>(L);
+      MMDX_CHECK_ARG(sm <= 160 * 1024, "attention bwd: L=%d needs %zu B LDS", L, sm);
+      (void)hipFuncSetAttribute((const void*)attn_bwd_q_kernel<T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      hipLaunchKernelGGL(attn_bwd_q_kernel<T>, dim3((L + QB - 1) / QB, H, B),
+                         dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, probs,
+                         (const T*)dout, L, H, scale, keep_scale, (T*)ws, (T*)dqkv);
+    } else {
+      const size_t sm = smem16(L);
+      (void)hipFuncSetAttribute((const void*)attn_bwd_q16_kernel<T>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      hipLaunchKernelGGL(attn_bwd_q16_kernel<T>, dim3((L + 63) / 64 * H * B), dim3(256), sm, st,
+                         (const T*)qkv, probs, (const T*)dout, L, H, scale, keep_scale,
+                         (T*)ws, (T*)dqkv);
+    }
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((L + QB - 1) / QB * H * B),
+                       dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs, (const T*)dout,
+                       (const T*)ws, L, H, scale, keep_scale, (T*)dqkv);
+  });
   MMDX_LAUNCH_CHECK();
   return 0;
 }

@@ -57,11 +57,15 @@ def main():
             L.call("mmdx_attention_bwd", L.dtype_code(dt), qkv.data_ptr(), probs.data_ptr(),
                    dout.data_ptr(), mp, B, Ls, H, scale, 0.0, dqkv.data_ptr(), ws.data_ptr(), n,
                    L.stream())
-        tf, tb = timeit(fwd, a.reps), timeit(bwd, a.reps)
+        def fwd_np():  # inference form: probabilities not saved
+            L.call("mmdx_attention_fwd", L.dtype_code(dt), qkv.data_ptr(), mp, B, Ls, H, scale,
+                   0.0, 0, None, out.data_ptr(), None, L.stream())
+        tf, tb, tn = timeit(fwd, a.reps), timeit(bwd, a.reps), timeit(fwd_np, a.reps)
         fl = 4.0 * B * H * Ls * Ls * 64
         pbytes = B * H * Ls * Ls * 4
         print(f"{name:5s} B{B} L{Ls} H{H}: fwd {tf:7.1f} us ({fl / tf / 1e6:6.1f} TF, P "
-              f"{pbytes / tf / 1e3:6.1f} GB/s)  bwd {tb:7.1f} us ({2 * fl / tb / 1e6:6.1f} TF)",
+              f"{pbytes / tf / 1e3:6.1f} GB/s)  bwd {tb:7.1f} us ({2 * fl / tb / 1e6:6.1f} TF)  "
+              f"fwd w/o P {tn:7.1f} us",
               flush=True)
 
 
