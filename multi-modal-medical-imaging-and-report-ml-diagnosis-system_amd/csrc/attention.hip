@@ -1,11 +1,15 @@
 // Multi-head self-attention core for BERT-base / ViT-B (head dim 64, L <= 256).
 //
-// Forward: one workgroup per (query block, head, batch); K, V^T of the head and the Q block
-// live in LDS; S = Q K^T on MFMA, row softmax in registers (16-lane shuffles on the 16x16
-// C layout), P -> LDS, O = P V on MFMA.  Probabilities are saved (fp32) for the backward.
+// Forward: one workgroup per (query block, head, batch); K and V of the head live in LDS.
+// bf16 / f16 (the training dtypes) use swapped products (attn_fwd16_kernel, 8 waves = 128
+// queries): S^T = K Q^T leaves each query on one lane column, the row softmax is a per-lane
+// sum plus two shuffles, and P^T feeds O^T = V^T P^T straight from registers (V^T through
+// transposed LDS reads).  fp32: S = Q K^T, 16-lane softmax, P -> LDS, O = P V.
+// Probabilities are saved (fp32) for the backward.
 // Backward: kernel A per query block: dP = dO V^T, dS = P o (dP - rowsum(P o dP)),
-// dQ = scale dS K; kernel B per key block, streaming query chunks: dV = P^T dO,
-// dK = scale dS^T Q.  Additive key mask as BertSelfAttention (large negative on pads).
+// dQ = scale dS K (16-bit: swapped as the forward); kernel B per key block, streaming query
+// chunks: dV = P^T dO, dK = scale dS^T Q.  Blocks of one head share an XCD (attn_block).
+// Additive key mask as BertSelfAttention (large negative on pads).
 // Attention-probability dropout (BertSelfAttention's dropout on attention_probs, train
 // mode): P' = P * keep / (1 - p) feeds O = P' V; keep comes from a counter-based hash of
 // (seed, device launch counter, b, h, q, key).  The saved probabilities carry the keep bit
@@ -13,6 +17,7 @@
 // and no mask tensor: dV = P'^T dO, dP = keep * (dO V^T) / (1 - p),
 // dS = P o (dP - rowsum(P o dP)).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "igemm.h"
@@ -507,15 +512,15 @@ __device__ __forceinline__ void store4(T* dst, float a, float b, float c, float 
   *(uint2*)dst = pk.u;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256, 2) void attn_fwd16_kernel(
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd16_kernel(
     const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bias,
     int causal, int L, int H, float scale, float p_drop, uint64_t seed,
     const uint64_t* __restrict__ ctr, T* __restrict__ out, float* __restrict__ probs) {
   typedef MfmaOp<T> Op;
   typedef typename Op::frag_t F;
   static_assert(Op::FRAG == 8 && Op::KS == 32, "16-bit MFMA 16x16x32 operands");
-  constexpr int QB = 64;
+  constexpr int QB = NW * 16;
   const int LP = (L + 31) & ~31;
   const int nkt = LP / 16;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -529,6 +534,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_kernel(
   const T* base = qkv + (long)b * L * row_ld + h * HD;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ql = lane & 15, g = lane >> 4;
   const int q = q0 + wid * 16 + ql;
+  const bool idle = q0 + wid * 16 >= L;   // a wave of padding queries: stage, then leave
   F qf[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -536,10 +542,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_kernel(
     if (q < L) qf[k] = *(const F*)(base + (long)q * row_ld + k * 32 + g * 8);
   }
   stage_pair<T, 4, false, false>(Ks, LDR, base + (long)H * HD, Vs, LDT, base + 2L * H * HD,
-                                 row_ld, LP, L, 256);
-  for (int k = threadIdx.x; k < LP; k += 256)
+                                 row_ld, LP, L, NW * 64);
+  for (int k = threadIdx.x; k < LP; k += NW * 64)
     madd[k] = k < L ? (mask && mask[(long)b * L + k] == 0 ? MASK_NEG : 0.f) : -INFINITY;
-  __syncthreads();
+  __syncthreads();   // the only barrier: idle waves may leave after it
+  if (idle) return;
   // s[j][r] = S[q][j*16 + g*4 + r]
   f32x4 s[MAXKT];
   float mx = -INFINITY;
@@ -643,14 +650,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_kernel(
 }
 
 // Backward A (16-bit): dP^T = V dO^T, dS = P o (dP - rowsum(P o dP)) -> dS_g [B,H,L,LP],
-// dQ^T = scale K^T dS^T.
-template <typename T>
-__global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
+// dQ^T = scale K^T dS^T.  Two passes over the key tiles: the first only accumulates the row
+// dot, the second recomputes each dP tile pair (28 extra MFMAs per wave), forms dS and feeds
+// it straight into the dQ product, so no dP / dS tile array stays live (<= 128 VGPRs: two
+// 8-wave blocks per CU).
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_q16_kernel(
     const T* __restrict__ qkv, const float* __restrict__ probs, const T* __restrict__ dout,
     int L, int H, float scale, float keep_scale, T* __restrict__ dS_g, T* __restrict__ dqkv) {
   typedef MfmaOp<T> Op;
   typedef typename Op::frag_t F;
-  constexpr int QB = 64;
+  constexpr int QB = NW * 16;
   const int LP = (L + 31) & ~31;
   const int nkt = LP / 16;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -663,6 +673,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
   const T* base = qkv + (long)b * L * row_ld + h * HD;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ql = lane & 15, g = lane >> 4;
   const int q = q0 + wid * 16 + ql;
+  const bool idle = q0 + wid * 16 >= L;   // a wave of padding queries: stage, then leave
   F of[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -670,13 +681,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
     if (q < L) of[k] = *(const F*)(dout + ((long)b * L + q) * H * HD + h * HD + k * 32 + g * 8);
   }
   stage_pair<T, 4, false, false>(Vs, LDR, base + 2L * H * HD, Ks, LDT, base + (long)H * HD,
-                                 row_ld, LP, L, 256);
-  __syncthreads();
+                                 row_ld, LP, L, NW * 64);
+  __syncthreads();   // the only barrier: idle waves may leave after it
+  if (idle) return;
   // saved probabilities P[q][j*16 + g*4 + r] -> pv[j][r]: one 16-B load per tile when
   // L % 4 == 0; otherwise 4 loads of 64 contiguous bytes of 4 rows each, transposed through
   // the wave's LDS scratch (in-order LDS within the wave: no barrier)
   const float* pbase = probs + (((long)b * H + h) * L) * L;
-  f32x4 s[MAXKT], pv[MAXKT];
+  f32x4 pv[MAXKT];
   if ((L & 3) == 0) {
 #pragma unroll
     for (int j = 0; j < MAXKT; ++j) {
@@ -705,39 +717,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
       pv[j] = *(const f32x4*)(pscr + ql * LDP + g * 4);
     }
   }
+  // dP'[q][j*16 + g*4 + r] -> dP = keep * dP' / (1 - p); dropped elements are saved with the
+  // sign bit set
+  auto dp_tile = [&](int j) {
+    f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+    const T* a = Vs + (j * 16 + ql) * LDR + g * 8;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) t = Op::mma(Op::ld(a + k * 32), of[k], t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t[r] = __builtin_signbitf(pv[j][r]) ? 0.f : t[r] * keep_scale;
+    return t;
+  };
   float dot = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXKT; ++j) {
-    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (j >= nkt) continue;
-    const f32x4 pr = pv[j];
-    const T* a = Vs + (j * 16 + ql) * LDR + g * 8;
+    const f32x4 t = dp_tile(j);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) s[j] = Op::mma(Op::ld(a + k * 32), of[k], s[j]);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      // dP = keep * dP' / (1 - p); dropped elements are saved with the sign bit set
-      s[j][r] = __builtin_signbitf(pr[r]) ? 0.f : s[j][r] * keep_scale;
-      pv[j][r] = fabsf(pr[r]);
-      dot += pv[j][r] * s[j][r];
-    }
+    for (int r = 0; r < 4; ++r) dot += fabsf(pv[j][r]) * t[r];
   }
   dot += __shfl_xor(dot, 16, 64);
   dot += __shfl_xor(dot, 32, 64);
   T* dsrow = dS_g + ((((long)b * H + h) * L) + q) * LP;
-  F df[MAXKT / 2];
-#pragma unroll
-  for (int j = 0; j < MAXKT; ++j) {
-    if (j >= nkt) continue;
-    float ds[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const T dst = from_f<T>(pv[j][r] * (s[j][r] - dot));
-      df[j >> 1][(j & 1) * 4 + r] = dst;
-      ds[r] = (float)dst;
-    }
-    if (q < L) store4<T>(dsrow + j * 16 + g * 4, ds[0], ds[1], ds[2], ds[3]);
-  }
   // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
   f32x4 o[HD / 16];
 #pragma unroll
@@ -745,11 +746,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
 #pragma unroll
   for (int t = 0; t < MAXKT / 2; ++t) {
     if (2 * t >= nkt) continue;
+    F df;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int j = 2 * t + h2;
+      const f32x4 tp = dp_tile(j);
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const T dst = from_f<T>(fabsf(pv[j][r]) * (tp[r] - dot));
+        df[h2 * 4 + r] = dst;
+        ds[r] = (float)dst;
+      }
+      if (q < L) store4<T>(dsrow + j * 16 + g * 4, ds[0], ds[1], ds[2], ds[3]);
+    }
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) {
       const F kf = join_frag<T>(tr_read4(Ks, 2 * t * 16 + g * 4, dt * 16),
                                 tr_read4(Ks, (2 * t + 1) * 16 + g * 4, dt * 16));
-      o[dt] = Op::mma(kf, df[t], o[dt]);
+      o[dt] = Op::mma(kf, df, o[dt]);
     }
   }
   if (q < L) {
@@ -761,9 +776,95 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q16_kernel(
   }
 }
 
-static size_t smem16(int L) {
+// Backward B (16-bit), swapped products, per key block of 16*NW keys, one key
+// per lane column: dV^T[d][key] = sum_q dO^T[d][q] P'[q][key] and
+// dK^T[d][key] = scale * sum_q Q^T[d][q] dS[q][key].  The head's Q and dO rows are staged
+// whole in LDS (one barrier) and read as the A operands through transposed reads; the
+// B operands P' and dS come straight from HBM into registers, 8 queries per lane per step
+// (each load instruction covers 64 contiguous bytes of 4 rows).
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_kv16_kernel(
+    const T* __restrict__ qkv, const float* __restrict__ probs, const T* __restrict__ dout,
+    const T* __restrict__ dS_g, int L, int H, float scale, float keep_scale,
+    T* __restrict__ dqkv) {
+  typedef MfmaOp<T> Op;
+  typedef typename Op::frag_t F;
+  constexpr int KB = NW * 16;
+  const int LP = (L + 31) & ~31;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Qs = (T*)smem_raw;               // [LP][LDT]
+  T* Os = Qs + LP * LDT;              // [LP][LDT]  dO
+  int kb, h, b;
+  attn_block((L + KB - 1) / KB, H, kb, h, b);
+  const int k0 = kb * KB;
+  const long row_ld = 3L * H * HD;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, kl = lane & 15, g = lane >> 4;
+  const int key = k0 + wid * 16 + kl;
+  const bool idle = k0 + wid * 16 >= L;   // a wave of padding keys: stage, then leave
+  stage_rows<T, 4, false>(Qs, LDT, qkv + (long)b * L * row_ld + h * HD, row_ld, LP, L, NW * 64);
+  stage_rows<T, 4, false>(Os, LDT, dout + (long)b * L * H * HD + h * HD, (long)H * HD, LP, L,
+                          NW * 64);
+  __syncthreads();   // the only barrier
+  if (idle) return;
+  const float* pb = probs + (((long)b * H + h) * L) * L;
+  const T* dsb = dS_g + (((long)b * H + h) * L) * LP;
+  const bool kok = key < L;
+  f32x4 dv[HD / 16], dk[HD / 16];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int qs = 0; qs < LP; qs += 32) {
+    F pf, sf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = qs + g * 8 + e;
+      const bool ok = kok && q < L;
+      const float v = ok ? pb[(long)q * L + key] : 0.f;
+      pf[e] = from_f<T>(__builtin_signbitf(v) ? 0.f : v * keep_scale);  // P'
+      sf[e] = ok ? dsb[(long)q * LP + key] : from_f<T>(0.f);
+    }
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const F of = join_frag<T>(tr_read4(Os, qs + g * 8, dt * 16),
+                                tr_read4(Os, qs + g * 8 + 4, dt * 16));
+      dv[dt] = Op::mma(of, pf, dv[dt]);
+      const F qf = join_frag<T>(tr_read4(Qs, qs + g * 8, dt * 16),
+                                tr_read4(Qs, qs + g * 8 + 4, dt * 16));
+      dk[dt] = Op::mma(qf, sf, dk[dt]);
+    }
+  }
+  if (kok) {
+    T* row = dqkv + ((long)b * L + key) * 3 * H * HD + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      store4<T>(row + (long)H * HD + dt * 16 + g * 4, dk[dt][0] * scale, dk[dt][1] * scale,
+                dk[dt][2] * scale, dk[dt][3] * scale);
+      store4<T>(row + 2L * H * HD + dt * 16 + g * 4, dv[dt][0], dv[dt][1], dv[dt][2],
+                dv[dt][3]);
+    }
+  }
+}
+
+static size_t smem16(int L, int nw) {
   const size_t LP = (L + 31) & ~31;
-  return LP * (LDR + LDT) * 2 + (LP + 4 * 16 * LDP) * sizeof(float);
+  return LP * (LDR + LDT) * 2 + (LP + (size_t)nw * 16 * LDP) * sizeof(float);
+}
+
+// queries per forward block: 128 (8 waves) halves the K/V staging per query and doubles the
+// resident waves per CU (the LDS, not the registers, bounds residency); MMDX_ATTN_FWD_NW=4
+// selects 64
+static int fwd16_nw() {
+  static const int nw = [] {
+    const char* e = getenv("MMDX_ATTN_FWD_NW");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return nw;
+}
+static int bwd16_nw() {   // the same for the dQ kernel; MMDX_ATTN_BWD_NW=4 selects 64
+  static const int nw = [] {
+    const char* e = getenv("MMDX_ATTN_BWD_NW");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return nw;
 }
 
 template <typename T>
@@ -801,12 +902,17 @@ extern "C" int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* 
                          dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, mask, bias, causal,
                          L, H, scale, p_drop, seed, (const uint64_t*)counter, (T*)out, probs);
     } else {
-      const size_t sm = smem16(L);
-      (void)hipFuncSetAttribute((const void*)attn_fwd16_kernel<T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-      hipLaunchKernelGGL(attn_fwd16_kernel<T>, dim3((L + 63) / 64 * H * B), dim3(256), sm, st,
-                         (const T*)qkv, mask, bias, causal, L, H, scale, p_drop, seed,
-                         (const uint64_t*)counter, (T*)out, probs);
+      auto launch = [&](auto kern, int nw) {
+        const size_t sm = smem16(L, nw);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        const int qb = nw * 16;
+        hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
+                           (const T*)qkv, mask, bias, causal, L, H, scale, p_drop, seed,
+                           (const uint64_t*)counter, (T*)out, probs);
+      };
+      if (fwd16_nw() == 8) launch(attn_fwd16_kernel<T, 8>, 8);
+      else launch(attn_fwd16_kernel<T, 4>, 4);
     }
   });
   if (p_drop > 0.f && counter)
@@ -849,16 +955,31 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
                          dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, probs,
                          (const T*)dout, L, H, scale, keep_scale, (T*)ws, (T*)dqkv);
     } else {
-      const size_t sm = smem16(L);
-      (void)hipFuncSetAttribute((const void*)attn_bwd_q16_kernel<T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-      hipLaunchKernelGGL(attn_bwd_q16_kernel<T>, dim3((L + 63) / 64 * H * B), dim3(256), sm, st,
-                         (const T*)qkv, probs, (const T*)dout, L, H, scale, keep_scale,
-                         (T*)ws, (T*)dqkv);
+      auto launch = [&](auto kern, int nw) {
+        const size_t sm = smem16(L, nw);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sm);
+        const int qb = nw * 16;
+        hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
+                           (const T*)qkv, probs, (const T*)dout, L, H, scale, keep_scale,
+                           (T*)ws, (T*)dqkv);
+      };
+      if (bwd16_nw() == 8) launch(attn_bwd_q16_kernel<T, 8>, 8);
+      else launch(attn_bwd_q16_kernel<T, 4>, 4);
     }
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((L + QB - 1) / QB * H * B),
-                       dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs, (const T*)dout,
-                       (const T*)ws, L, H, scale, keep_scale, (T*)dqkv);
+    if constexpr (std::is_same<T, float>::value) {
+      hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((L + QB - 1) / QB * H * B),
+                         dim3(AttnCfg<T>::NW * 64), 0, st, (const T*)qkv, probs,
+                         (const T*)dout, (const T*)ws, L, H, scale, keep_scale, (T*)dqkv);
+    } else {
+      const size_t sm = (size_t)((L + 31) & ~31) * LDT * 2 * sizeof(T);
+      auto kv16 = attn_bwd_kv16_kernel<T, 8>;
+      (void)hipFuncSetAttribute((const void*)kv16, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sm);
+      hipLaunchKernelGGL(kv16, dim3((L + 127) / 128 * H * B), dim3(512),
+                         sm, st, (const T*)qkv, probs, (const T*)dout, (const T*)ws, L, H,
+                         scale, keep_scale, (T*)dqkv);
+    }
   });
   MMDX_LAUNCH_CHECK();
   return 0;
