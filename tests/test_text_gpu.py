@@ -25,9 +25,14 @@ def _ref_attention(q, k, v, mask, scale):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,Ls,H", [(2, 128, 12), (3, 37, 2), (2, 197, 4), (1, 256, 1)])
+@pytest.mark.parametrize("B,Ls,H", [(2, 128, 12), (3, 37, 2), (2, 197, 4), (1, 256, 1),
+                                    (1, 1, 3), (2, 16, 8), (4, 129, 6)])
 @pytest.mark.parametrize("masked", [True, False])
 def test_attention(dev, dt, B, Ls, H, masked):
+    """Forward, saved probabilities and backward against torch fp32.  The shapes cover the
+    16-bit kernels' cases: L % 4 != 0 (probability tiles transposed through LDS), a second
+    128-query block holding one query (L 129), single-key rows (L 1), and B*H not a multiple
+    of 8 (plain block order instead of the XCD-grouped one)."""
     g = torch.Generator().manual_seed(B * Ls + H)
     qkv = torch.randn(B, Ls, 3, H, 64, generator=g)
     if dt != torch.float32:
@@ -52,6 +57,12 @@ def test_attention(dev, dt, B, Ls, H, masked):
            B, Ls, H, scale, 0.0, 0, None, out.data_ptr(), probs.data_ptr(), L.stream())
     tol = 1e-4 if dt == torch.float32 else 3e-2
     assert rel_err(out, o) <= tol
+    with torch.no_grad():
+        q, k = qkv[:, :, 0], qkv[:, :, 1]
+        sc = torch.einsum("blhd,bmhd->bhlm", q, k) * scale
+        if mask is not None:
+            sc = sc + (1.0 - mask[:, None, None, :].float()) * -1e30
+        assert rel_err(probs, sc.softmax(-1)) <= 1e-4
     dqkv = torch.empty_like(qd)
     n = L.lib().mmdx_attention_workspace_size(dc, B, Ls, H)
     ws = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -231,19 +242,20 @@ def test_lstm_coop_lost_peer_raises(dev):
     assert int(st.word[0]) == 0
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_attention_prob_dropout(dev, dt):
+@pytest.mark.parametrize("dt,Ls", [(torch.float32, 128), (torch.bfloat16, 128),
+                                   (torch.float16, 97)])
+def test_attention_prob_dropout(dev, dt, Ls):
     """Attention-probability dropout (BertSelfAttention's, train mode).  The kept set is read
     back from the saved probabilities' sign bit; forward and backward must equal an explicit
     reference that applies exactly that mask: O = (P*keep/(1-p)) V, autograd for the
     gradients.  The drop rate must be p (binomial 6-sigma band) and a second launch (device
     counter advanced) must draw a different mask."""
-    B, Ls, H, pd = 2, 128, 4, 0.1
+    B, H, pd = 2, 4, 0.1
     g = torch.Generator().manual_seed(7)
     qkv = torch.randn(B, Ls, 3, H, 64, generator=g)
-    if dt == torch.bfloat16:
-        qkv = qkv.bfloat16().float()
-    lens = torch.tensor([128, 70])
+    if dt != torch.float32:
+        qkv = qkv.to(dt).float()
+    lens = torch.tensor([Ls, 70])
     mask = (torch.arange(Ls)[None] < lens[:, None]).long()
     scale = 0.125
     dc = L.dtype_code(dt)
@@ -272,8 +284,8 @@ def test_attention_prob_dropout(dev, dt):
     pdrop = p * keep.float() / (1 - pd)
     o = torch.einsum("bhlm,bmhd->blhd", pdrop, v)
     do = torch.randn(o.shape, generator=g)
-    if dt == torch.bfloat16:
-        do = do.bfloat16().float()
+    if dt != torch.float32:
+        do = do.to(dt).float()
     o.backward(do)
     tol = 1e-4 if dt == torch.float32 else 3e-2
     assert rel_err(out, o) <= tol
