@@ -6,6 +6,7 @@
 // reproducible, no E[x^2]-E[x]^2 cancellation across the 10^5..10^6 rows of a layer).
 // All elementwise passes move 16 B per lane (8 bf16 / 4 fp32).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "pool.h"
@@ -619,39 +620,75 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
   }
 }
 
-constexpr int LN_BWD_ROWS = 32;  // rows per block (8 per wave)
+// rows per block = 4 waves x rpw rows; each wave loads its next row while reducing the
+// current one (isolated bwd at 12608 x 768 fp16 was 25.9 us, 2.3 TB/s, with 8 rows per wave
+// and no prefetch).  The workspace is sized for the smallest rpw (the most partials).
+constexpr int LN_RPW_MIN = 4;
+constexpr int LN_BWD_ROWS = 4 * LN_RPW_MIN;   // rows per block at LN_RPW_MIN
+static int ln_bwd_rpw() {   // MMDX_LN_BWD_RPW = 4 | 8 (default 8)
+  static const int r = [] {
+    const char* e = getenv("MMDX_LN_BWD_RPW");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return r;
+}
 
 // dx per row; per-block partial dgamma/dbeta -> part[blk][2][D]
-template <typename T>
+// MV: 16-B vectors per lane (ceil(D / VEC / 64)), a template argument so the register arrays
+// are sized for D (MV everywhere held 194 VGPRs at D = 768: two waves per SIMD)
+template <typename T, int MV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
                                                      const T* __restrict__ dy, long rows, int D,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ smean,
                                                      const float* __restrict__ srstd,
                                                      T* __restrict__ dx,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, int rpw) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2][D]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nv = D / VEC;
-  float pg[LN_MAXV][VEC], pb[LN_MAXV][VEC];
+  float pg[MV][VEC], pb[MV][VEC];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i)
+  for (int i = 0; i < MV; ++i)
 #pragma unroll
     for (int j = 0; j < VEC; ++j) pg[i][j] = pb[i][j] = 0.f;
-  for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
-    const long row = blockIdx.x * (long)LN_BWD_ROWS + w * (LN_BWD_ROWS / 4) + rr;
-    if (row >= rows) break;
-    const float mean = smean[row], rstd = srstd[row];
-    float xh[LN_MAXV][VEC], g[LN_MAXV][VEC];
-    float s1 = 0.f, s2 = 0.f;
+  const long row0 = (blockIdx.x * 4L + w) * rpw;
+  V an[MV], dn[MV];
+  float mean_n = 0.f, rstd_n = 0.f;
+  auto fetch = [&](long row) {
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
+    for (int i = 0; i < MV; ++i) {
       const int vi = lane + i * 64;
       if (vi < nv) {
-        const V a = *(const V*)(xs + row * D + vi * VEC);
-        const V d = *(const V*)(dy + row * D + vi * VEC);
+        an[i] = *(const V*)(xs + row * D + vi * VEC);
+        dn[i] = *(const V*)(dy + row * D + vi * VEC);
+      }
+    }
+    mean_n = smean[row];
+    rstd_n = srstd[row];
+  };
+  if (row0 < rows) fetch(row0);
+  for (int rr = 0; rr < rpw; ++rr) {
+    const long row = row0 + rr;
+    if (row >= rows) break;
+    const float mean = mean_n, rstd = rstd_n;
+    V av[MV], dv[MV];
+#pragma unroll
+    for (int i = 0; i < MV; ++i) {
+      av[i] = an[i];
+      dv[i] = dn[i];
+    }
+    if (rr + 1 < rpw && row + 1 < rows) fetch(row + 1);
+    float xh[MV][VEC], g[MV][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nv) {
+        const V a = av[i];
+        const V d = dv[i];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const int c = vi * VEC + j;
@@ -668,7 +705,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
     s1 = wave_sum(s1) / D;
     s2 = wave_sum(s2) / D;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
+    for (int i = 0; i < MV; ++i) {
       const int vi = lane + i * 64;
       if (vi < nv) {
         V o;
@@ -679,7 +716,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
     }
   }
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < MV; ++i) {
     const int vi = lane + i * 64;
     if (vi < nv)
 #pragma unroll
@@ -701,26 +738,28 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
   }
 }
 
-// dgamma / dbeta from the per-block partials [nblk][2][D]: 32 columns x 8 lanes per block,
-// the lanes stride the blocks (the first version had one thread per column over all nblk
-// partials — 3 blocks at D = 768: 82 us per call, 4.5 ms per C5 step)
-__global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __restrict__ part,
-                                                              int nblk, int D, float* dgamma,
-                                                              float* dbeta, float beta_acc) {
-  __shared__ float red[8][32];
+// dgamma / dbeta from the per-block partials [nblk][2][D]: 32 columns x 32 lanes per block,
+// the lanes stride the blocks with 8 loads in flight each (the first version had one thread
+// per column over all nblk partials — 3 blocks at D = 768: 82 us per call, 4.5 ms per C5
+// step; 8 lanes with 4 loads in flight still left ~12 us at 394 partials)
+constexpr int LN_FIN_LANES = 32;
+__global__ __launch_bounds__(1024) void ln_bwd_finalize_kernel(const float* __restrict__ part,
+                                                               int nblk, int D, float* dgamma,
+                                                               float* dbeta, float beta_acc) {
+  __shared__ float red[LN_FIN_LANES][33];
   const int cc = threadIdx.x & 31, lane = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cc, which = blockIdx.y;  // 0: dgamma, 1: dbeta
   float acc = 0.f;
   if (c < D) {
-#pragma unroll 4
-    for (int k = lane; k < nblk; k += 8) acc += part[((long)k * 2 + which) * D + c];
+#pragma unroll 8
+    for (int k = lane; k < nblk; k += LN_FIN_LANES) acc += part[((long)k * 2 + which) * D + c];
   }
   red[lane][cc] = acc;
   __syncthreads();
   if (lane != 0 || c >= D) return;
   float s = 0.f;
 #pragma unroll
-  for (int l = 0; l < 8; ++l) s += red[l][cc];
+  for (int l = 0; l < LN_FIN_LANES; ++l) s += red[l][cc];
   float* out = which ? dbeta : dgamma;
   if (out) out[c] = beta_acc != 0.f ? beta_acc * out[c] + s : s;
 }
@@ -873,15 +912,25 @@ extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, l
                                   float beta_acc, void* ws, size_t ws_bytes, void* stream) {
   const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC, "layernorm bwd: D=%d", D);
-  const long nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  const int rpw = ln_bwd_rpw();
+  const long nblk = (rows + 4 * rpw - 1) / (4 * rpw);
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_layernorm_workspace_size(rows, D),
                  "layernorm bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = 8 * (size_t)D * sizeof(float);
-  MMDX_DISPATCH(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nblk), dim3(256), shm, st,
-                                          (const T*)xsum, (const T*)dy, rows, D, gamma,
-                                          save_mean, save_rstd, (T*)dx, (float*)ws));
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 31) / 32, 2), dim3(256), 0, st,
+  const int mv = (D / VEC + 63) / 64;
+  MMDX_DISPATCH(dtype, {
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), shm, st, (const T*)xsum, (const T*)dy,
+                         rows, D, gamma, save_mean, save_rstd, (T*)dx, (float*)ws, rpw);
+    };
+    if (mv == 1) launch(ln_bwd_kernel<T, 1>);
+    else if (mv == 2) launch(ln_bwd_kernel<T, 2>);
+    else if (mv == 3) launch(ln_bwd_kernel<T, 3>);
+    else launch(ln_bwd_kernel<T, 4>);
+  });
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 31) / 32, 2), dim3(32 * LN_FIN_LANES), 0,
+                     st,
                      (const float*)ws, (int)nblk, D, dgamma, dbeta, beta_acc);
   MMDX_LAUNCH_CHECK();
   return 0;
