@@ -41,6 +41,33 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
   }
 }
 
+// The same for N % 4 == 0 and M * N < 2^31: 4 consecutive columns per thread (16-B partial
+// loads, 4 splits' loads in flight, 32-bit index math — the scalar kernel's 64-bit divisions
+// and one-load-at-a-time split loop made it ~12 us per C5 weight gradient); the sum over the
+// splits keeps the order z = 0, 1, ..., so the result is the scalar kernel's bit for bit.
+template <typename OutT>
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ ws,
+                                                             int splits, int M, int N,
+                                                             EpiStore<OutT> epi) {
+  const int total4 = M * N / 4, n4 = N / 4;
+  const f32x4* w = (const f32x4*)ws;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {
+      const f32x4 a = w[(long)z * total4 + i], b = w[(long)(z + 1) * total4 + i];
+      const f32x4 c = w[(long)(z + 2) * total4 + i], d = w[(long)(z + 3) * total4 + i];
+      v += a;
+      v += b;
+      v += c;
+      v += d;
+    }
+    for (; z < splits; ++z) v += w[(long)z * total4 + i];
+    const int m = i / n4;
+    epi.apply4(m, (i - m * n4) * 4, v);
+  }
+}
+
 // 8-wave 256 x 128 tiles (one block per CU, three 48 KB stages) for the unsplit 128 x 128
 // problems with at least this many 256-row tiles (read per launch for A/B runs).  Off by
 // default: on every C5 Linear shape and at 4096^3 they ran 2-20 % slower than two 4-wave
@@ -191,9 +218,19 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
   int rc = dispatch_major<T>(p, A, lda, ak, B, ldb, bk, part, M, N, K, st);
   if (rc) return rc;
   const long total = (long)M * N;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(splitk_reduce_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
-                     (const float*)ws, p.splits, M, N, epi);
+  static const bool vec_reduce = [] {   // MMDX_SPLITK_VEC=0: the scalar reduce (A/B knob)
+    const char* e = getenv("MMDX_SPLITK_VEC");
+    return !(e && atoi(e) == 0);
+  }();
+  if (vec_reduce && N % 4 == 0 && total < (1L << 31) && ((uintptr_t)ws & 15) == 0) {
+    const int blocks = (int)std::min<long>((total / 4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(splitk_reduce4_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
+                       (const float*)ws, p.splits, M, N, epi);
+  } else {
+    const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
+                       (const float*)ws, p.splits, M, N, epi);
+  }
   MMDX_LAUNCH_CHECK();
   return 0;
 }
