@@ -85,6 +85,19 @@ static long gemm256_min_tiles() {
   return e ? atol(e) : 0L;
 }
 
+// The same threshold for the forward orientation only (both operands k-major: x W^T), where
+// the isolated C5 table has the 256 x 256 tiles 3-8 % ahead on the ViT-B shapes while the
+// backward orientations and the BERT-base shapes lose (profiles/r03n_gemm_bench_f16.txt).
+// Default 400 tiles: the ViT-B QKV and FFN-up GEMMs at 64 images (450 / 600 tiles); C5
+// 2227 / 2234 vs 2204 / 2193 samples/s (profiles/r03u_c5_ab_gemm256fwd.txt); 0 disables
+static long gemm256_fwd_min_tiles() {
+  static const long v = [] {
+    const char* e = getenv("MMDX_GEMM256_FWD_MIN");
+    return e ? atol(e) : 400L;
+  }();
+  return v;
+}
+
 // The 256 x 256 tiles with 32-deep K tiles in NS = 3 / 4 stages (MMDX_GEMM256_NS; 0 = the
 // 64-deep two-stage kernel): 32 KB stages, NS - 1 tiles in flight behind a counted vmcnt
 // instead of a vmcnt(0) drain per K tile (A/B knob)
@@ -118,7 +131,8 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
     if (oka && okb) {
       if constexpr (BM == 128 && BN == 128) {
         const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-        const long lim256 = gemm256_min_tiles();
+        long lim256 = gemm256_min_tiles();
+        if (AK && BKm && lim256 == 0) lim256 = gemm256_fwd_min_tiles();
         if (splits == 1 && lim256 > 0 && t256 >= lim256 && K >= 128) {
           if (const int ns = gemm256_stages()) {
             typedef typename std::conditional<AK, DmaK<256, SA, 32, 8>,

@@ -64,3 +64,26 @@ def test_gemm8_matches_4wave(dev, knob, layout, dt, shape, monkeypatch):
         assert torch.equal(c4, c8), (layout, dt, shape, out_dtype)
         err = (c8.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
         assert err <= 1e-2, (layout, dt, shape, out_dtype, err)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_gemm256_forward_epilogue(dev, dt, monkeypatch):
+    """The 256 x 256 tiles under the Linear forward's fused epilogue (bias + GELU + the saved
+    pre-activation, the FFN-up GEMM; MMDX_GEMM256_FWD_MIN selects these tiles for the large
+    ViT-B forward GEMMs by default) are bit-identical to the 4-wave kernel."""
+    from mmdx import _lib as L
+    M, N, K = 3152, 3072, 768
+    a, b, ref = _operands("fwd", M, N, K, dt, dev, 11)
+    bias = torch.randn(N, device=dev)
+    outs = []
+    for knob in ("0", "1"):
+        monkeypatch.setenv("MMDX_GEMM256_MIN", knob)
+        C = torch.empty(M, N, dtype=dt, device=dev)
+        pre = torch.empty(M, N, dtype=dt, device=dev)
+        F.gemm(a, K, 1, b, K, 1, M, N, K, C, N, bias=bias, act=L.ACT_GELU, preact=pre)
+        outs.append((C, pre))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    pre_ref = ref + bias.double().cpu()
+    err = (outs[1][1].double().cpu() - pre_ref).abs().max().item() / pre_ref.abs().max().item()
+    assert err <= 1e-2
