@@ -7,8 +7,9 @@
 // transposed LDS reads).  fp32: S = Q K^T, 16-lane softmax, P -> LDS, O = P V.
 // Probabilities are saved (fp32) for the backward.
 // Backward: kernel A per query block: dP = dO V^T, dS = P o (dP - rowsum(P o dP)),
-// dQ = scale dS K (16-bit: swapped as the forward); kernel B per key block, streaming query
-// chunks: dV = P^T dO, dK = scale dS^T Q.  Blocks of one head share an XCD (attn_block).
+// dQ = scale dS K; kernel B per key block: dV = P^T dO, dK = scale dS^T Q (fp32: streaming
+// query chunks through LDS; 16-bit: swapped as the forward, the head's Q and dO staged whole,
+// P' and dS read straight into registers).  Blocks of one head share an XCD (attn_block).
 // Additive key mask as BertSelfAttention (large negative on pads).
 // Attention-probability dropout (BertSelfAttention's dropout on attention_probs, train
 // mode): P' = P * keep / (1 - p) feeds O = P' V; keep comes from a counter-based hash of
