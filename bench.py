@@ -74,44 +74,6 @@ def conv_flops_per_sample(trunk, hw=224):
     return 2 * fwd, 2 * dgrad, 2 * fwd
 
 
-def conv_bytes_per_step(trunk, B, hw=224, elt=2):
-    """Algorithmic HBM bytes of one step's conv launches (each tensor touched once):
-    fwd x + w + y; dgrad dy + w + dx (+dx read when accumulating a residual branch, ignored);
-    wgrad x + dy + dw (fp32).  Returns (total bytes, number of conv launches)."""
-    tot = 0
-    n = 0
-    H = W = hw
-
-    def one(c, H, W, dgrad):
-        k, s, p = c.kernel_size, c.stride, c.padding
-        P = (H + 2 * p - k) // s + 1
-        Q = (W + 2 * p - k) // s + 1
-        x = B * H * W * c.in_channels * elt
-        y = B * P * Q * c.out_channels * elt
-        w = c.out_channels * c.in_channels * k * k
-        b = (x + w * elt + y) + (x + w * 4 + y)  # fwd, wgrad
-        if dgrad:
-            b += y + w * elt + x
-        return b, (3 if dgrad else 2), P, Q
-
-    b, m, H, W = one(trunk[0], H, W, False)
-    tot += b
-    n += m
-    H, W = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
-    for layer in list(trunk)[4:8]:
-        for blk in layer:
-            Hb, Wb = H, W
-            for c, _, _ in blk.units():
-                b, m, H, W = one(c, H, W, True)
-                tot += b
-                n += m
-            if blk.downsample is not None:
-                b, m, _, _ = one(blk.downsample[0], Hb, Wb, True)
-                tot += b
-                n += m
-    return tot, n
-
-
 def load_traffic(cfg_name, batch):
     """HBM bytes per conv launch from the committed PMC pass (tools/pmc_traffic.py), or None."""
     import glob
@@ -281,6 +243,7 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
     import mmdx
     from mmdx import optim as MO
     from mmdx.schedule import TwoTowerForward, two_tower_backward
+    from mmdx.trace import rng
     towers = TwoTowerForward(text_stream=side)
     text_early = os.environ.get("MMDX_DP_TEXT_EARLY", "1") != "0"
 
@@ -295,8 +258,9 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
                               (lambda: txt(input_ids=ids, attention_mask=mask)
                                           ["embeddings"]))
         main.wait_stream(side)
-        logits = fus(z_img, z_txt)["disease_logits"]
-        loss = mmdx.BCEWithLogitsLoss()(logits, y)
+        with rng("mmdx/fusion_fwd"):
+            logits = fus(z_img, z_txt)["disease_logits"]
+            loss = mmdx.BCEWithLogitsLoss()(logits, y)
         # = loss.backward(), with the text tower's backward queued before the image trunk's;
         # N > 1: the text tower's and fusion head's gradients start their RCCL all-reduce
         # (from the text stream) while the image trunk is still in its backward
@@ -308,12 +272,13 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
                            on_text_done=early)
         if reducer is not None:
             reducer.reduce()
-        if scaler is not None:
-            step.norm = scaler.clip_and_step(opt, 1.0, unscale_first=True, params=params)
-            scaler.update()
-        else:
-            step.norm, scale = MO.grad_norm(params, 1.0)
-            opt.step(grad_scale=scale)
+        with rng("mmdx/optimizer"):
+            if scaler is not None:
+                step.norm = scaler.clip_and_step(opt, 1.0, unscale_first=True, params=params)
+                scaler.update()
+            else:
+                step.norm, scale = MO.grad_norm(params, 1.0)
+                opt.step(grad_scale=scale)
         return loss
     step.norm = None
     step.towers = towers   # (tools/host_profile.py profiles the text thread through it)
@@ -541,14 +506,22 @@ def main():
     samples = B * world * args.steps
     value = samples / el
     ms_step = el / args.steps * 1e3
+    # every timed launch carries its algorithmic cost (resnet.LaunchCost: kind, FLOPs, bytes)
+    fam_flops = sum(tag[1] for tag, _, _ in timer.pairs)
+    fam_bytes = sum(tag[2] for tag, _, _ in timer.pairs)
+    # combined per-launch roofline: each launch's own roof max(FLOPs / MFMA peak, bytes / HBM
+    # peak), summed over the family, against the family's summed launch durations
+    roof_ms = sum(max(tag[1] / (PEAK_BF16_TFLOPS * 1e9), tag[2] / (PEAK_HBM_GBS * 1e6))
+                  for tag, _, _ in timer.pairs)
+    flop_ms = fam_flops / (PEAK_BF16_TFLOPS * 1e9)
+    byte_ms = fam_bytes / (PEAK_HBM_GBS * 1e6)
+    conv_tf = fam_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    conv_gbs = fam_bytes / (conv_ms * 1e-3) / 1e9 if conv_ms > 0 else 0.0
     if vit:
-        gemm_flops = sum(f for f, _, _ in timer.pairs)   # all timed steps
-        conv_tf = gemm_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-        conv_flops = gemm_flops / max(1, conv_steps) / B
-        alg_bytes, alg_launches = 0, max(1, n_conv // max(1, conv_steps))
-    else:
-        conv_tf = conv_flops * B * conv_steps / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-        alg_bytes, alg_launches = conv_bytes_per_step(img.backbone, B)
+        conv_flops = fam_flops / max(1, conv_steps) / B
+    alg_bytes = fam_bytes / max(1, conv_steps)
+    alg_launches = max(1, n_conv // max(1, conv_steps))
+    hbm_bound = byte_ms > flop_ms
     traffic = load_traffic(args.config, B)
     result = {
         "metric": "multimodal samples/sec (train fwd+bwd) at 1/2/4/8 MI355X; MFMA util %",
@@ -580,27 +553,41 @@ def main():
         "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
                                           (PEAK_BF16_TFLOPS * world), 2),
         "mfma_util_pmc": load_mfma_util(args.config),
+        "amp": ({"loss_scaling": "mmdx.GradScaler (init 2^16, growth 2 per 2000 clean steps, "
+                                 "backoff 0.5, device-side inf check, overflow skips AdamW)",
+                 "clip_order": "unscale -> clip_grad_norm_(1.0) -> AdamW (torch.amp's "
+                               "documented order); the reference TP:1056-1058 clips the "
+                               "SCALED gradients before scaler.step unscales them"}
+                if scaler is not None else None),
         "roofline": {
             "kernel": ("igemm_dma_kernel (dense GEMMs of the ViT-B/16 and BERT-base encoders, "
                        "fwd + both backward GEMMs)") if vit else
                       "igemm_dma_kernel (implicit-GEMM conv fwd/dgrad/wgrad, all ResNet convs)",
-            "bound": "mfma",
-            "achieved": round(conv_tf, 2),
-            "peak": PEAK_BF16_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(conv_tf / PEAK_BF16_TFLOPS, 4),
+            # the family's bound: the larger of its summed FLOP time and byte time at peak
+            "bound": "hbm" if hbm_bound else "mfma",
+            "achieved": round(conv_gbs if hbm_bound else conv_tf, 2),
+            "peak": PEAK_HBM_GBS if hbm_bound else PEAK_BF16_TFLOPS,
+            "unit": "GB/s" if hbm_bound else "TFLOP/s",
+            "frac": round((conv_gbs / PEAK_HBM_GBS) if hbm_bound
+                          else (conv_tf / PEAK_BF16_TFLOPS), 4),
             "traffic": traffic[0] if traffic else None,
             "traffic_unit": "HBM bytes per conv launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)",
             "traffic_source": traffic[1] if traffic else None,
-            "algorithmic_bytes_per_launch": (round(alg_bytes / alg_launches) if not vit
-                                             else None),
+            "algorithmic_bytes_per_launch": round(alg_bytes / alg_launches),
+            "mfma_achieved_tflops": round(conv_tf, 2),
+            "mfma_frac": round(conv_tf / PEAK_BF16_TFLOPS, 4),
+            "hbm_achieved_gbs": round(conv_gbs, 1),
+            "hbm_frac": round(conv_gbs / PEAK_HBM_GBS, 4),
+            "combined_roof_ms_per_step": round(roof_ms / conv_steps, 3),
+            "combined_frac": round(roof_ms / conv_ms, 4) if conv_ms > 0 else None,
+            "combined_frac_note": "sum over launches of max(FLOPs/2.5 PF, bytes/8 TB/s) "
+                                  "divided by the summed launch durations",
             "family_ms_per_step": round(conv_ms / conv_steps, 3),
             "busy_ms_per_step": round(busy_ms / conv_steps, 3),
-            "busy_achieved": (round(conv_tf * conv_ms / busy_ms, 2) if busy_ms > 0 else None),
-            "busy_frac": (round(conv_tf * conv_ms / busy_ms / PEAK_BF16_TFLOPS, 4)
-                          if busy_ms > 0 else None),
+            "busy_combined_frac": (round(roof_ms / busy_ms, 4) if busy_ms > 0 else None),
             "family_launches_per_step": n_conv // max(1, conv_steps),
             "family_gflop_per_sample": round(conv_flops / 1e9, 3),
+            "family_alg_gb_per_step": round(alg_bytes / 1e9, 3),
             "timed_steps_with_events": conv_steps,
         },
     }

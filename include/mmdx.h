@@ -13,7 +13,9 @@
  * the reference's class/function surface and binds these symbols with ctypes.
  *
  * Conventions
- *   dtype:      0 = fp32 (parity path, exact-f32 MFMA), 1 = bf16 (throughput path)
+ *   dtype:      0 = fp32 (parity path, exact-f32 MFMA), 1 = bf16 (throughput path),
+ *               2 = fp16 (C5's "fp16 MFMA": dense GEMM, attention, LayerNorm, text / ViT
+ *               kernels; the ResNet and BiLSTM entry points reject it)
  *   images:     NHWC, channels innermost; conv weights packed [Cout][R][S][Cin] ("KRSC")
  *               for fwd and [Cin][R][S][Cout] ("CRSK") for dgrad; fp32 master weights
  *               and gradients stay in PyTorch's [Cout][Cin][R][S] ("KCRS") layout.
@@ -33,7 +35,7 @@
 extern "C" {
 #endif
 
-enum { MMDX_F32 = 0, MMDX_BF16 = 1 };
+enum { MMDX_F32 = 0, MMDX_BF16 = 1, MMDX_F16 = 2 };
 enum { MMDX_ACT_NONE = 0, MMDX_ACT_RELU = 1, MMDX_ACT_GELU = 2, MMDX_ACT_GELU_BWD = 3 };
 
 int mmdx_version(void);

@@ -18,6 +18,8 @@ import os
 import torch
 import torch.distributed as dist
 
+from .trace import rng
+
 BUCKET_BYTES = 64 << 20
 
 
@@ -76,7 +78,8 @@ class GradAllReducer:
         if not self.active or hi <= lo:
             return
         part = buf[lo:hi]
-        work = dist.all_reduce(part, op=self._op(part), group=self.group, async_op=True)
+        with rng("mmdx/allreduce/trunk_segment"):
+            work = dist.all_reduce(part, op=self._op(part), group=self.group, async_op=True)
         self._pending.append((None, part, work, None))
         off = buf.storage_offset()
         self._regions.setdefault(_store_key(buf), []).append((off + lo, off + hi))
@@ -127,6 +130,10 @@ class GradAllReducer:
         """Start the all-reduce of these parameters' gradients (default: all remaining)."""
         if not self.active:
             return
+        with rng("mmdx/allreduce/launch"):
+            self._launch(params)
+
+    def _launch(self, params):
         ps = self.params if params is None else [p for p in params if p.requires_grad]
         grads = []
         for p in ps:
@@ -169,6 +176,10 @@ class GradAllReducer:
         return dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
 
     def finish(self):
+        with rng("mmdx/allreduce/finish"):
+            self._finish()
+
+    def _finish(self):
         inv = 1.0 / self.world
         cur = None
         for bucket, flat, work, dest in self._pending:

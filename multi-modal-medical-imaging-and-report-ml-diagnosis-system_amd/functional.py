@@ -33,6 +33,18 @@ class _NoTimer:
 GEMM_TIMER = _NoTimer()
 
 
+def gemm_cost(M, N, K, dt, c_dt, beta=0.0, act=L.ACT_NONE, preact=None):
+    """LaunchCost of one GEMM: 2MNK FLOPs; A, B read once, C written (read too when
+    beta != 0), the pre-activation written (GELU) or read (GELU backward)."""
+    from .resnet import LaunchCost
+    e = 4 if dt == L.F32 else 2
+    ce = 4 if c_dt == L.F32 else 2
+    b = (M * K + N * K) * e + M * N * ce * (2 if beta else 1)
+    if preact is not None:
+        b += M * N * ce
+    return LaunchCost("gemm", 2 * M * N * K, b)
+
+
 # ----------------------------------------------------------------------------- primitives
 def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, Cout, ldc, *, bias=None, addend=None,
          act=L.ACT_NONE, alpha=1.0, beta=0.0, preact=None, compute_dtype=None):
@@ -40,7 +52,7 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, Cout, ldc, *, bias=None, a
     dt = L.dtype_code(compute_dtype if compute_dtype is not None else A.dtype)
     ws_n = L.lib().mmdx_gemm_workspace_size(dt, M, N, K)
     ws = L.workspace(ws_n, Cout.device)
-    with GEMM_TIMER(2 * M * N * K):
+    with GEMM_TIMER(gemm_cost(M, N, K, dt, L.dtype_code(Cout.dtype), beta, act, preact)):
         call("mmdx_gemm", dt, M, N, K, ptr(A), lda, int(a_kmajor), ptr(B), ldb, int(b_kmajor),
              ptr(Cout), ldc, L.dtype_code(Cout.dtype), ptr(bias), ptr(addend), act,
              float(alpha), float(beta), ptr(preact), ptr(ws), ws_n, stream())

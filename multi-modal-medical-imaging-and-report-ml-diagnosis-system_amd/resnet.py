@@ -42,6 +42,34 @@ class _NoTimer:
 CONV_TIMER = _NoTimer()
 
 
+class LaunchCost(tuple):
+    """Tag of a timed launch: (kind, algorithmic FLOPs, algorithmic HBM bytes — every tensor
+    it must read or write touched once).  bench.py prices each launch against its own roof,
+    max(FLOPs / MFMA peak, bytes / HBM bandwidth)."""
+    __slots__ = ()
+
+    def __new__(cls, kind, flops, nbytes):
+        return tuple.__new__(cls, (kind, int(flops), int(nbytes)))
+
+    kind = property(lambda s: s[0])
+    flops = property(lambda s: s[1])
+    nbytes = property(lambda s: s[2])
+
+
+def conv_cost(kind, conv, N, H, W, P, Q, elt, extra_read=0):
+    """LaunchCost of one conv launch over an N x H x W input (true channels, unpadded):
+    fwd x + w + y; dgrad dy + w + dx (+ extra_read: a tensor the epilogue adds); wgrad
+    x + dy + dw (fp32)."""
+    k = conv.kernel_size
+    macs = N * P * Q * conv.out_channels * conv.in_channels * k * k
+    x = N * H * W * conv.in_channels * elt
+    y = N * P * Q * conv.out_channels * elt
+    w = conv.out_channels * conv.in_channels * k * k
+    b = {"fwd": x + w * elt + y, "dgrad": y + w * elt + x + extra_read,
+         "wgrad": x + y + w * 4}[kind]
+    return LaunchCost(kind, 2 * macs, b)
+
+
 # ----------------------------------------------------------------------------- modules
 class Conv2d(nn.Module):
     def __init__(self, cin, cout, k, stride=1, padding=0):
@@ -349,6 +377,9 @@ class _Plan:
             the post-activation tensor is never written (u["out"] is None)."""
             d = pair if pair is not None else _desc(N, H, W, C, conv)
             K, k = conv.out_channels, conv.kernel_size
+            pq = (d.P, d.Q)
+            cost = lambda kind, extra=0: conv_cost(kind, conv, N, H, W, pq[0], pq[1],  # noqa
+                                                   T.itemsize, extra)
             y = A.new((N, d.P, d.Q, K), T, dev)
             nstat = L.lib().mmdx_conv_fwd_stat_blocks(d) if train else 0
             part = A.new((K, nstat, 2), torch.float32, dev) if train else None
@@ -369,16 +400,16 @@ class _Plan:
                 # materialised and no bn_apply pass runs
                 if join is not None:
                     fw.add(L.OP_WAIT, p=(join,), stream=st)
-                fw.timed("fwd", L.OP_CONV_FWD_BNEVAL, stream=st, dtype=dt, i=(int(relu),),
+                fw.timed(cost("fwd"), L.OP_CONV_FWD_BNEVAL, stream=st, dtype=dt, i=(int(relu),),
                          f=(bn.eps,),
                          p=(x, wk, y, bn.weight, bn.bias, bn.running_mean, bn.running_var, res),
                          d=d)
                 u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=None, out=y,
-                         mean=None, rstd=None, wc=wc, pair=pair is not None)
+                         mean=None, rstd=None, wc=wc, pair=pair is not None, res=res)
                 units.append(u)
                 return y, d, u
             rpb = L.lib().mmdx_conv_fwd_stat_rows(d)  # rows per statistics slab (part)
-            fw.timed("fwd", L.OP_CONV_FWD, stream=st, dtype=dt, i=(rpb if train else 0,),
+            fw.timed(cost("fwd"), L.OP_CONV_FWD, stream=st, dtype=dt, i=(rpb if train else 0,),
                      p=(x, wk, y, part), d=d)
             out = None if stats_only else A.new((N, d.P, d.Q, K), T, dev)
             rows = N * d.P * d.Q
@@ -397,7 +428,7 @@ class _Plan:
                    p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean, rstd,
                       res, out, _WS2 if st else _WS, rmask))
             u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
-                     rstd=rstd, wc=wc, pair=pair is not None, rmask=rmask)
+                     rstd=rstd, wc=wc, pair=pair is not None, rmask=rmask, res=res, cost=cost)
             units.append(u)
             return out, d, u
 
@@ -535,6 +566,12 @@ class _Plan:
                 rows = d.N * d.P * d.Q
                 dconv = A.new(tuple(u["y"].shape), T, dev)
                 u["dconv"] = dconv
+                # kept for the per-launch parity test (tests/test_trunk_launches_gpu.py):
+                # the BN backward's upstream gradient and where its ReLU mask comes from
+                u["dout"], u["dout_mask"] = dout, dout_mask
+                u["bwd_kind"] = ("masked" if dout_mask is not None else
+                                 "pool" if pool is not None else
+                                 "res" if want_res else "relu" if u["relu"] else "plain")
                 # no_dres: the identity path's gradient is added by conv1's dgrad epilogue
                 # from (dout, ReLU bit mask) instead (mmdx_conv_dgrad_accmask)
                 dres = (A.new(tuple(u["y"].shape), T, dev) if want_res and not no_dres
@@ -577,13 +614,15 @@ class _Plan:
                 cv = u["conv"]
                 if u["pair"]:  # pair-conv gradient [K][8][R][S2], mapped to the master layout
                     dwp = A.new((d.K, d.C, d.R, d.S), torch.float32, dev)
-                    bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(d.C,), l=(wsn,),
+                    bw.timed(u["cost"]("wgrad"), L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(d.C,),
+                             l=(wsn,),
                              f=(0.0,), p=(xref(u["x"]), dconv, dwp, _WS2), d=d)
                     bw.add(L.OP_STEM_PAIR_GRAD, stream=1,
                            i=(d.K, cv.in_channels, cv.kernel_size, cv.kernel_size), f=(0.0,),
                            p=(dwp, g(cv.weight)))
                 else:
-                    bw.timed("wgrad", L.OP_CONV_WGRAD, stream=1, dtype=dt, i=(u["cm"],),
+                    bw.timed(u["cost"]("wgrad"), L.OP_CONV_WGRAD, stream=1, dtype=dt,
+                             i=(u["cm"],),
                              l=(wsn,), f=(0.0,), p=(xref(u["x"]), dconv, g(cv.weight), _WS2),
                              d=d)
                 dx, fed = None, None
@@ -599,21 +638,27 @@ class _Plan:
                     tiles = (L.lib().mmdx_conv_dgrad_stat_blocks(dt, d)
                              if feed is not None and beta == 0.0 and feed["relu"] else 0)
                     if acc is not None:  # dx = dgrad + (ReLU bit ? acc_src : 0)
-                        bw.timed("dgrad", L.OP_CONV_DGRAD_ACCMASK, dtype=dt,
+                        xb = d.N * d.H * d.W * d.C * T.itemsize
+                        bw.timed(u["cost"]("dgrad", xb + xb // 16), L.OP_CONV_DGRAD_ACCMASK,
+                                 dtype=dt,
                                  p=(dconv, u["wc"], dx, acc[0], acc[1]), d=d)
                     elif tiles > 0:
                         fed = (A.new((d.C, tiles, 2), torch.float32, dev), tiles)
                         fb = feed["bn"]
-                        bw.timed("dgrad", L.OP_CONV_DGRAD_BNSTAT, dtype=dt, i=(1,), f=(0.0,),
+                        bw.timed(u["cost"]("dgrad", d.N * d.H * d.W * d.C * T.itemsize),
+                                 L.OP_CONV_DGRAD_BNSTAT, dtype=dt, i=(1,), f=(0.0,),
                                  p=(dconv, u["wc"], dx, feed["y"], fb.weight, fb.bias,
                                     feed["mean"], feed["rstd"], fed[0], None), d=d)
                     else:
-                        bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(beta,),
-                                 p=(dconv, u["wc"], dx), d=d)
+                        xb = d.N * d.H * d.W * d.C * T.itemsize if beta else 0
+                        bw.timed(u["cost"]("dgrad", xb), L.OP_CONV_DGRAD, dtype=dt,
+                                 f=(beta,), p=(dconv, u["wc"], dx), d=d)
+                u["dx"] = dx
                 return dx, dres, fed
 
             N_, H_, W_, C_ = self.out_geom
             dx = A.new((N_, H_, W_, C_), T, dev)
+            self.dtop = dx
             bw.add(L.OP_AVGPOOL_BWD, dt, i=(N_, H_ * W_, C_), p=(_Ext(0), dx))
             # Per-layer gradient regions for data parallelism.  engine_params is in forward
             # order, so layer k's gradients are one contiguous slice of the arena and layers
@@ -671,8 +716,10 @@ class _Plan:
                         # conv1 re-reading the whole tensor to accumulate onto it
                         unit_bwd(ds_u, ds_dout, False, **ds_in)
                         dh, _, _ = unit_bwd(uu, dh, True, stats=fed)
-                        bw.timed("dgrad", L.OP_CONV_DGRAD, dtype=dt, f=(1.0,),
-                                 p=(ds_u["dconv"], ds_u["wc"], dh), d=ds_u["d"])
+                        dd_ = ds_u["d"]
+                        bw.timed(ds_u["cost"]("dgrad", dd_.N * dd_.H * dd_.W * dd_.C
+                                              * T.itemsize), L.OP_CONV_DGRAD, dtype=dt,
+                                 f=(1.0,), p=(ds_u["dconv"], ds_u["wc"], dh), d=dd_)
                     elif k == 0 and acc_id:
                         dh, _, _ = unit_bwd(uu, dh, True, stats=fed,
                                             acc=(blk_dout, bu[-1]["rmask"]))
@@ -708,6 +755,9 @@ class _Plan:
                 for j in range(12):
                     if o.ext[j] == -1 and o.p[j] in (_WS_TOKEN, _WS2_TOKEN):
                         o.p[j] = ws[0 if o.p[j] == _WS_TOKEN else 1].data_ptr()
+        # the recorded units, blocks and stem pool buffers (read by the per-launch parity test)
+        self.units, self.blocks = units, blocks
+        self.stem_pool = dict(u=stem_u, argmax=am, pooled=pooled, geom=stem_geom, fused=pool_bn)
         self.fwd = fw.freeze()
         if self.bwd is not None:
             self.bwd.freeze()

@@ -15,6 +15,8 @@ import threading
 
 import torch
 
+from .trace import rng
+
 
 class TwoTowerForward:
     """Issue the two encoder towers' forwards (TP:1000-1007 `image_encoder.encode` /
@@ -34,7 +36,7 @@ class TwoTowerForward:
         self._lock = threading.Lock()
 
     def _text(self, fn, device, grad):
-        with torch.set_grad_enabled(grad):
+        with torch.set_grad_enabled(grad), rng("mmdx/text_fwd"):
             if self.text_stream is None:
                 return fn()
             torch.cuda.set_device(device)
@@ -46,7 +48,8 @@ class TwoTowerForward:
             dev = torch.cuda.current_device() if self.text_stream is not None else None
             fut = self._pool.submit(self._text, text_fn, dev, torch.is_grad_enabled())
             try:
-                z_img = image_fn()
+                with rng("mmdx/image_fwd"):
+                    z_img = image_fn()
             finally:
                 z_txt = fut.result()
             return z_img, z_txt
@@ -73,18 +76,23 @@ def two_tower_backward(loss: torch.Tensor, z_img: torch.Tensor, z_txt: torch.Ten
     the image trunk is still in its backward)."""
     head = [p for p in head_params if p.requires_grad]
     inputs = [t for t in (z_img, z_txt) if t.requires_grad] + head
-    loss.backward(inputs=inputs, retain_graph=True)
+    with rng("mmdx/head_bwd"):
+        loss.backward(inputs=inputs, retain_graph=True)
     if text_stream is None or not torch.cuda.is_available():
-        _tower(z_img)
-        _tower(z_txt)
+        with rng("mmdx/image_bwd"):
+            _tower(z_img)
+        with rng("mmdx/text_bwd"):
+            _tower(z_txt)
         if on_text_done is not None:
             on_text_done()
         return
     main = torch.cuda.current_stream()
     text_stream.wait_stream(main)  # dL/dz_txt was produced on the current stream
-    _tower(z_img)
+    with rng("mmdx/image_bwd"):
+        _tower(z_img)
     with torch.cuda.stream(text_stream):
-        _tower(z_txt)
+        with rng("mmdx/text_bwd"):
+            _tower(z_txt)
         if on_text_done is not None:
             on_text_done()
     main.wait_stream(text_stream)

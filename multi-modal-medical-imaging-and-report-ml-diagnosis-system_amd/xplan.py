@@ -87,7 +87,8 @@ class _Rec:
     def gemm(self, A, lda, akm, B, ldb, bkm, M, N, K, C, ldc, c_dtype, bias=None, act=0,
              preact=None, beta=0.0):
         n = L.lib().mmdx_gemm_workspace_size(self.dt, M, N, K)
-        self.ops.timed(2 * M * N * K, L.OP_GEMM, dtype=self.dt,
+        self.ops.timed(F.gemm_cost(M, N, K, self.dt, L.dtype_code(c_dtype), beta, act, preact),
+                       L.OP_GEMM, dtype=self.dt,
                        i=(M, N, K, int(akm), int(bkm), L.dtype_code(c_dtype), act),
                        l=(lda, ldb, ldc, n), f=(1.0, beta),
                        p=(A, B, C, bias, None, preact, self._ws(n)))

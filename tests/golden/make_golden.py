@@ -72,17 +72,18 @@ def bert_case():
     return dict(ids=ids, mask=mask, embeddings=out["embeddings"], logits=out["logits"])
 
 
-def c1_case():
-    """BASELINE config 1: backend/sample_images/e1.jpg through image_transfom_into_tensor
-    (TP:112-119) + a 64-token synthetic report, single forward, R50 + BERT-base."""
+def c1_case(name="e1.jpg", seed=14):
+    """BASELINE config 1: a reference sample image (backend/sample_images/e1.jpg, e2.jpg)
+    through image_transfom_into_tensor (TP:112-119) + a 64-token synthetic report, single
+    forward, R50 + BERT-base."""
     from PIL import Image
     from oracle.ref_cpu import reference_transform
-    img = Image.open(os.path.join(HERE, "e1.jpg")).convert("RGB")
+    img = Image.open(os.path.join(HERE, name)).convert("RGB")
     x = reference_transform(img)[None]
     torch.manual_seed(0)
     model = R.RefMultimodal("resnet50", "bert-base-uncased", dropout=0.0)
     model.eval()
-    g = torch.Generator().manual_seed(14)
+    g = torch.Generator().manual_seed(seed)
     ids = torch.randint(1000, 30522, (1, 64), generator=g)
     ids[0, 0], ids[0, -1] = 101, 102
     mask = torch.ones(1, 64, dtype=torch.long)
@@ -92,9 +93,13 @@ def c1_case():
 
 
 def main():
+    import sys
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    cases = {"fusion": fusion_case(), "resnet18": resnet_case("resnet18"),
-             "resnet50": resnet_case("resnet50"), "bert2": bert_case(), "c1": c1_case()}
+    cases = {"fusion": fusion_case, "resnet18": lambda: resnet_case("resnet18"),
+             "resnet50": lambda: resnet_case("resnet50"), "bert2": bert_case, "c1": c1_case,
+             "c1_e2": lambda: c1_case("e2.jpg", 15)}
+    only = sys.argv[1:]   # e.g. `python make_golden.py c1_e2`: regenerate only those cases
+    cases = {k: f() for k, f in cases.items() if not only or k in only}
     for name, d in cases.items():
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **{k: v.numpy() for k, v in d.items()})

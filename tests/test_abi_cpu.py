@@ -54,3 +54,20 @@ def test_plan_op_layout_matches_c(lib):
     import ctypes
     import mmdx._lib as L
     assert lib.mmdx_plan_op_size() == ctypes.sizeof(L.PlanOp)
+
+
+def _header_enum(prefix):
+    src = open(os.path.join(ROOT, "include", "mmdx.h")).read()
+    return {k: int(v) for k, v in re.findall(rf"\b({prefix}[A-Z0-9_]+)\s*=\s*(\d+)", src)}
+
+
+def test_dtype_and_activation_codes_match_header():
+    """The dtype codes the host passes (fp16 = 2 for C5) and the activation codes are the
+    ones include/mmdx.h defines."""
+    import mmdx._lib as L
+    dt = _header_enum("MMDX_F")
+    dt.update(_header_enum("MMDX_BF"))
+    assert dt == {"MMDX_F32": L.F32, "MMDX_BF16": L.BF16, "MMDX_F16": L.F16}
+    act = _header_enum("MMDX_ACT_")
+    assert act["MMDX_ACT_NONE"] == 0 and act["MMDX_ACT_GELU"] == L.ACT_GELU
+    assert act["MMDX_ACT_GELU_BWD"] == L.ACT_GELU_BWD

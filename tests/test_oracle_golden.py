@@ -36,10 +36,12 @@ def test_oracle_matches_golden(case):
         _cmp(got[k], want[k])
 
 
-def test_c1_golden_logits():
+@pytest.mark.parametrize("case,image,seed", [("c1", "e1.jpg", 14), ("c1_e2", "e2.jpg", 15)])
+def test_c1_golden_logits(case, image, seed):
+    """C1 on both of the reference's sample images (backend/sample_images/e1.jpg, e2.jpg)."""
     torch.set_num_threads(4)
-    got = G.c1_case()
-    want = _load("c1")
+    got = G.c1_case(image, seed)
+    want = _load(case)
     _cmp(got["x"], want["x"], 1e-6)
     _cmp(got["logits"], want["logits"])
     assert want["logits"].shape == (1, 13)

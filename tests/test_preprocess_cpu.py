@@ -57,7 +57,9 @@ def _emulate(arrays):
 
 
 def images():
-    ims = [Image.open(os.path.join(HERE, "golden", "e1.jpg")).convert("RGB")]
+    # the reference's two sample images (backend/sample_images/e1.jpg, e2.jpg)
+    ims = [Image.open(os.path.join(HERE, "golden", f)).convert("RGB")
+           for f in ("e1.jpg", "e2.jpg")]
     g = np.random.default_rng(0)
     for (w, h, mode) in ((512, 384, "RGB"), (300, 700, "L"), (256, 333, "RGB"),
                          (240, 231, "RGB"), (1023, 517, "L"), (256, 256, "RGB")):
