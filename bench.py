@@ -406,12 +406,12 @@ def main():
     if os.environ.get("MMDX_TEXT_STREAM", "side") == "main":  # A/B: towers in series
         side = torch.cuda.current_stream()
     from mmdx.dist import GradAllReducer
-    # C5's packed buckets (the ViT-B/16 and BERT-base gradients outside the two encoder
-    # stacks, whose flat gradient buffers reduce in place in fp32) travel in bf16 by default —
-    # half the xGMI bytes, the mean taken in fp32 after the cast back
-    # (MMDX_DP_BUCKET_DTYPE=fp32 restores fp32); C2-C4 reduce in fp32
+    # Every gradient reduces in fp32 (the mean of 8 bf16 sums would drop ~3 bits against
+    # the fp32 DDP mean).  MMDX_DP_BUCKET_DTYPE=bf16 sends C5's packed buckets (the ViT-B/16 and
+    # BERT-base gradients outside the two encoder stacks: embeddings, patch projection,
+    # heads) in bf16, half their xGMI bytes, the mean taken in fp32 after the cast back.
     bdt = None
-    if vit and os.environ.get("MMDX_DP_BUCKET_DTYPE", "bf16") == "bf16":
+    if vit and os.environ.get("MMDX_DP_BUCKET_DTYPE", "fp32") == "bf16":
         bdt = torch.bfloat16
     reducer = GradAllReducer(params, world, rehearse=dp, bucket_dtype=bdt) if dp else None
     # The trunk's layer 4, 3, 2 gradients start their all-reduce mid-backward.  The first
@@ -433,6 +433,13 @@ def main():
         RN.TRUNK_GRAD_HOOK = reducer.trunk_hook
     elif reducer is not None and early_tail not in ("0", ""):
         RN.TRUNK_SEGMENT_HOOK = reducer.trunk_segment
+        # C5: the ViT-B/16 and BERT-base encoder stacks' backward plans are cut every
+        # xplan.SEG_LAYERS layers and each finished group's gradient slice is all-reduced in
+        # place from there, beside the remaining layers' backward (the same hook: issued
+        # with the backward's stream current; every rank issues the collectives in the same
+        # order — image stack, then text stack — from the thread running the backward)
+        from mmdx import xplan as XP
+        XP.STACK_SEGMENT_HOOK = reducer.trunk_segment
     # fp16 (C5): loss scaling with GradScaler semantics (TP:1025-1026, 1056-1061)
     scaler = mmdx.GradScaler() if dtype == torch.float16 else None
     step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler)

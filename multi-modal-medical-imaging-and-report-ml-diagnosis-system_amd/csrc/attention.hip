@@ -23,6 +23,24 @@
 
 #include "igemm.h"
 #include "../../include/mmdx.h"
+#include <mutex>
+#include <set>
+#include <utility>
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize -> the full 160 KB of LDS) once per kernel
+// and device, so no attribute call is issued again on the launch path: a launch sequence
+// captured into a hipGraph then holds nothing but kernel nodes (the first call of each kernel
+// runs eagerly, e.g. torch.cuda.make_graphed_callables' warm-up iterations).
+static void mmdx_lds_max_once(const void* kern) {
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  if (done.insert({dev, kern}).second)
+    (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 
 namespace mmdx {
 
@@ -897,16 +915,14 @@ extern "C" int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* 
       constexpr int QB = AttnCfg<T>::NW * 16;
       const size_t sm = fwd_smem<T>(L);
       MMDX_CHECK_ARG(sm <= 160 * 1024, "attention: L=%d needs %zu B LDS", L, sm);
-      (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      mmdx_lds_max_once((const void*)attn_fwd_kernel<T>);
       hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3((L + QB - 1) / QB, H, B),
                          dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, mask, bias, causal,
                          L, H, scale, p_drop, seed, (const uint64_t*)counter, (T*)out, probs);
     } else {
       auto launch = [&](auto kern, int nw) {
         const size_t sm = smem16(L, nw);
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
+        mmdx_lds_max_once((const void*)kern);
         const int qb = nw * 16;
         hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
                            (const T*)qkv, mask, bias, causal, L, H, scale, p_drop, seed,
@@ -950,16 +966,14 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
     if constexpr (std::is_same<T, float>::value) {
       const size_t sm = fwd_smem<T>(L);
       MMDX_CHECK_ARG(sm <= 160 * 1024, "attention bwd: L=%d needs %zu B LDS", L, sm);
-      (void)hipFuncSetAttribute((const void*)attn_bwd_q_kernel<T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      mmdx_lds_max_once((const void*)attn_bwd_q_kernel<T>);
       hipLaunchKernelGGL(attn_bwd_q_kernel<T>, dim3((L + QB - 1) / QB, H, B),
                          dim3(AttnCfg<T>::NW * 64), sm, st, (const T*)qkv, probs,
                          (const T*)dout, L, H, scale, keep_scale, (T*)ws, (T*)dqkv);
     } else {
       auto launch = [&](auto kern, int nw) {
         const size_t sm = smem16(L, nw);
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sm);
+        mmdx_lds_max_once((const void*)kern);
         const int qb = nw * 16;
         hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
                            (const T*)qkv, probs, (const T*)dout, L, H, scale, keep_scale,
@@ -975,8 +989,7 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
     } else {
       const size_t sm = (size_t)((L + 31) & ~31) * LDT * 2 * sizeof(T);
       auto kv16 = attn_bwd_kv16_kernel<T, 8>;
-      (void)hipFuncSetAttribute((const void*)kv16, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sm);
+      mmdx_lds_max_once((const void*)kv16);
       hipLaunchKernelGGL(kv16, dim3((L + 127) / 128 * H * B), dim3(512),
                          sm, st, (const T*)qkv, probs, (const T*)dout, (const T*)ws, L, H,
                          scale, keep_scale, (T*)dqkv);

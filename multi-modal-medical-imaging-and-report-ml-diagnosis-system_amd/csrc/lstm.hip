@@ -281,6 +281,13 @@ typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
 // inside the step loop, and a 256-row workgroup spilled 121.
 constexpr int COOP_WLDS_BYTES = 2 * 4 * (COOP_H / 32) * 64 * 16;  // [ug][g][ks][lane] x 16 B
 
+// Zeroes the cooperative recurrence's step counters ahead of its launch.  A kernel rather than
+// hipMemsetAsync: the launch sequence captured into a hipGraph is then kernel nodes only,
+// ordered on the stream like any other launch.
+__global__ void lstm_coop_ctr_zero_kernel(unsigned* __restrict__ ctr) {
+  if (threadIdx.x < 16) ctr[threadIdx.x] = 0u;
+}
+
 template <int RT>
 __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     const float* __restrict__ xg, const bf16* __restrict__ whh, int B, int L,
@@ -573,7 +580,7 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
     bf16* hx = (bf16*)ws;
     unsigned* ctr = (unsigned*)((char*)ws + (size_t)2 * 2 * B * H * 2);
     const long spin_max = spin_limit > 0 ? spin_limit : COOP_SPIN_MAX;
-    (void)hipMemsetAsync(ctr, 0, 64, st);
+    hipLaunchKernelGGL(lstm_coop_ctr_zero_kernel, dim3(1), dim3(64), 0, st, ctr);
     // B > 128: independent groups of 128 rows (grid z), each with W_hh in LDS (RT = 2)
     const int groups = B <= 128 ? 1 : (B + 127) / 128;
     const dim3 grid(COOP_NB, 2, groups);

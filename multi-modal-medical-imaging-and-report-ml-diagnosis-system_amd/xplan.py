@@ -159,6 +159,19 @@ class _StackPlan:
         self.out = None
         self.dx = None
         self.grads = _GradLayout()
+        # [(lo, hi)] element ranges of the gradient buffer that are final at each backward
+        # segment boundary (groups of SEG_LAYERS layers, last layer first)
+        self.grad_regions = []
+
+    def cut_after_layers(self, li, nl, start):
+        """Segment boundary after layer li's backward (layers run nl-1 .. 0): every
+        SEG_LAYERS layers, the gradients of layers li .. li+SEG_LAYERS-1 are final.
+        start(j) = first gradient element of layer j (start(nl) = the buffer's end)."""
+        seg = SEG_LAYERS
+        if seg <= 0 or li == 0 or (nl - li) % seg:
+            return
+        self.bwd.cut()
+        self.grad_regions.append((start(li), start(min(nl, li + seg))))
 
     def finish(self, recs):
         need = max(r.ws_need for r in recs)
@@ -169,6 +182,16 @@ class _StackPlan:
                     if o.ext[j] == -1 and o.p[j] == _WS_TOKEN:
                         o.p[j] = ws.data_ptr()
             lst.freeze()
+
+
+# Layers per backward segment of a stack plan.  Between segments the backward returns to the
+# host, which calls STACK_SEGMENT_HOOK(grads, lo, hi) with the stream the backward runs on
+# current: grads[lo:hi] (those layers' parameter gradients) is final once that stream reaches
+# this point, so the data-parallel reducer issues its in-place all-reduce right there
+# (dist.GradAllReducer.trunk_segment; RCCL's stream waits on the current one) and it runs
+# beside the remaining layers' backward.  None = one native call for the whole backward.
+SEG_LAYERS = int(os.environ.get("MMDX_DP_STACK_SEG_LAYERS", "3"))
+STACK_SEGMENT_HOOK = None
 
 
 def _plans_for(owner, key, build):
@@ -307,6 +330,7 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         rb.colsum(dqkv, M, 3 * D, gx(o["bqkv"]))
         rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, Y, D, T, beta=1.0)
         dh = Y
+        pl.cut_after_layers(li, nl, lambda j: offs[j]["wqkv"] if j < nl else G.n)
     pl.dx = Y
     pl.finish((rf, rb))
     return pl
@@ -401,6 +425,7 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, dx_ln, gx(o[0]), gx(o[1]))
         rb.add(DA, dx_ln, M * D, DX)
         dO = DX
+        pl.cut_after_layers(li, nl, lambda j: offs[j][0] if j < nl else G.n)
     pl.dx = DX
     pl.finish((rf, rb))
     return pl
@@ -448,7 +473,14 @@ class _StackFn(torch.autograd.Function):
         grads = torch.empty(pl.grads.n, dtype=_F32, device=h.device)
         ext = [dout.data_ptr(), grads.data_ptr(),
                mask.data_ptr() if mask is not None else 0, h.data_ptr()]
-        pl.bwd.run(ext, [torch.cuda.current_stream().cuda_stream], timer=F.GEMM_TIMER)
+        hook = STACK_SEGMENT_HOOK
+        between = None
+        if hook is not None and pl.grad_regions:
+            def between(k):
+                lo, hi = pl.grad_regions[k]
+                hook(grads, lo, hi)
+        pl.bwd.run(ext, [torch.cuda.current_stream().cuda_stream], timer=F.GEMM_TIMER,
+                   between=between)
         dx = pl.dx.clone().view(h.shape)
         out = [None] * ctx.nparams
         for idx, shape, off in pl.grads.items:

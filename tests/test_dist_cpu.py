@@ -1,4 +1,5 @@
 """CPU: the DP gradient all-reduce (mmdx.dist.GradAllReducer) over gloo, world_size 2."""
+import math
 import os
 import socket
 
@@ -216,3 +217,56 @@ def test_whole_buffer_detection():
     assert _whole_buffer([a]) is None                          # a lone tensor: bucketed
     c = torch.zeros(12, dtype=torch.float64)
     assert _whole_buffer([c[:4], c[4:].float()]) is None       # not one storage / dtype
+
+
+def _worker_stack(rank, world, port, out, sizes, regions):
+    """A transformer stack's flat gradient buffer (xplan): the backward's segment hook
+    (xplan.STACK_SEGMENT_HOOK -> GradAllReducer.trunk_segment) reduces each finished group of
+    layers in place mid-backward, then launch() reduces the rest (layer 0's group) and the
+    other gradients."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx.dist import GradAllReducer
+    g = torch.Generator().manual_seed(500 + rank)
+    flat = torch.randn(sum(sizes), generator=g)
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes] + \
+        [torch.nn.Parameter(torch.zeros(9))]
+    o = 0
+    for p, n in zip(params, sizes):
+        p.grad = flat[o:o + n].detach()
+        o += n
+    params[-1].grad = torch.randn(9, generator=g)
+    red = GradAllReducer(params, world, bucket_bytes=64)
+    for lo, hi in regions:
+        red.trunk_segment(flat, lo, hi)
+    red.launch()
+    stack = {id(p.grad) for p in params[:-1]}
+    assert all(b is None or not stack & {id(t) for t in b} for b, *_ in red._pending)
+    red.finish()
+    out[rank] = [p.grad.clone() for p in params]
+    dist.destroy_process_group()
+
+
+def test_stack_segment_allreduce_gloo(monkeypatch):
+    from mmdx import xplan
+    from test_xplan_cpu import _small_vit_params
+    monkeypatch.setattr(xplan, "SEG_LAYERS", 2)
+    params = _small_vit_params(6)
+    pl = xplan._build_vit(params, 2, 17, 64, 1, 128, 1e-6, torch.float16, torch.device("cpu"))
+    assert len(pl.grad_regions) == 2
+    sizes = [math.prod(sh) for _, sh, _ in sorted(pl.grads.items, key=lambda t: t[2])]
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_stack, args=(world, port, out, sizes, list(pl.grad_regions)),
+             nprocs=world, join=True)
+    exp = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(500 + r)
+        flat = torch.randn(sum(sizes), generator=g)
+        exp.append(list(flat.split(sizes)) + [torch.randn(9, generator=g)])
+    for r in range(world):
+        for got, a, b in zip(out[r], exp[0], exp[1]):
+            assert torch.allclose(got, (a + b) / 2, atol=1e-6)

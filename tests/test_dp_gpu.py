@@ -24,10 +24,13 @@ def _port():
     return p
 
 
-def _model():
+def _model(kind="resnet"):
     sys.path.insert(0, HERE)
     from parity_util import build_pair
-    _, img, txt, fus = build_pair("resnet18", "embed-mean")
+    if kind == "stack":   # C5's towers: the ViT-B/16 and BERT encoder stacks (launch plans)
+        _, img, txt, fus = build_pair("vit_b_16", "bert-base-uncased", bert_layers=4)
+    else:
+        _, img, txt, fus = build_pair("resnet18", "embed-mean")
     return img, txt, fus
 
 
@@ -121,10 +124,12 @@ def _rccl_worker(port, out, early):
     dist.init_process_group("nccl", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     from mmdx import resnet as RN
+    from mmdx import xplan as XP
     from mmdx.dist import GradAllReducer
     from parity_util import synth_batch
-    x, ids, mask, y = synth_batch(4, 16, hw=64)
-    img, txt, fus = _model()
+    kind = "stack" if early == "stack" else "resnet"
+    x, ids, mask, y = synth_batch(2, 16, hw=224) if kind == "stack" else synth_batch(4, 16, hw=64)
+    img, txt, fus = _model(kind)
     params = [p for mod in (img, txt, fus) for p in mod.parameters()]
     _grads(img, txt, fus, x, ids, mask, y)
     ref = {id(p): p.grad.detach().clone() for p in params if p.grad is not None}
@@ -136,10 +141,17 @@ def _rccl_worker(port, out, early):
         RN.TRUNK_GRAD_HOOK = red.trunk_hook
     elif early == "seg":
         RN.TRUNK_SEGMENT_HOOK = red.trunk_segment
+    elif early == "stack":   # the encoder stacks' backward segments (xplan.STACK_SEGMENT_HOOK)
+        XP.STACK_SEGMENT_HOOK = red.trunk_segment
     _grads(img, txt, fus, x, ids, mask, y)
-    RN.TRUNK_GRAD_HOOK = RN.TRUNK_SEGMENT_HOOK = None
-    trunk_p = {id(p) for p in img.backbone.parameters()}
-    trunk = {id(p.grad) for p in img.backbone.parameters() if p.grad is not None}
+    RN.TRUNK_GRAD_HOOK = RN.TRUNK_SEGMENT_HOOK = XP.STACK_SEGMENT_HOOK = None
+    if kind == "stack":
+        out["segments"] = len(red._pending)   # 3 ViT groups + 1 BERT group, issued mid-backward
+        trunk_p = {id(p) for p in list(img.backbone.encoder.layers.parameters())
+                   + list(txt.encoder.encoder.layer.parameters())}
+    else:
+        trunk_p = {id(p) for p in img.backbone.parameters()}
+    trunk = {id(p.grad) for p in params if id(p) in trunk_p and p.grad is not None}
     red.launch()
     packed = sum(1 for b, *_ in red._pending if b is not None for t in b if id(t) in trunk)
     red.finish()
@@ -161,7 +173,7 @@ def _rccl_worker(port, out, early):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("early", [False, "event", "seg"])
+@pytest.mark.parametrize("early", [False, "event", "seg", "stack"])
 def test_dp_rccl_one_rank_identity(dev, early):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
@@ -173,3 +185,5 @@ def test_dp_rccl_one_rank_identity(dev, early):
     assert out["n"] > 50
     assert out["packed"] == 0, "trunk arena gradients went through a packed bucket"
     assert out["bad"] == [], out["bad"]
+    if early == "stack":
+        assert out["segments"] == 4, out["segments"]

@@ -104,3 +104,39 @@ def test_plan_cache_evicts_idle_stale_keys(monkeypatch):
     assert len(cache) <= 3 and "k0" not in cache and "k4" in cache
     again = RN.plan_cache_get(cache, "k4", _P)
     assert again is cache["k4"][0]          # an idle plan of the key is reused
+
+
+def _small_vit_params(nl, D=64, I=128):
+    g = torch.Generator().manual_seed(0)
+    shapes = ((D,), (D,), (3 * D, D), (3 * D,), (D, D), (D,), (D,), (D,), (I, D), (I,),
+              (D, I), (D,))
+    return [torch.randn(sh, generator=g) for _ in range(nl) for sh in shapes]
+
+
+@pytest.mark.parametrize("seg", [3, 1, 0])
+def test_stack_backward_segments(monkeypatch, seg):
+    """The stack backward is cut every SEG_LAYERS layers; each cut's gradient region is the
+    contiguous slice of those layers' parameter gradients (the data-parallel reducer issues
+    its in-place all-reduce there, xplan.STACK_SEGMENT_HOOK).  The regions cover the layers
+    above layer 0's group exactly once, last layer first."""
+    monkeypatch.setattr(xplan, "SEG_LAYERS", seg)
+    nl = 12
+    params = _small_vit_params(nl)
+    pl = xplan._build_vit(params, 2, 17, 64, 1, 128, 1e-6, torch.float16, CPU)
+    per_layer = sum(q.numel() for q in params[:12])
+    if seg == 0:
+        assert pl.grad_regions == [] and len(pl.bwd.bounds) == 2
+        return
+    want = []
+    top = nl
+    while top - seg > 0:
+        want.append(((top - seg) * per_layer, top * per_layer))
+        top -= seg
+    assert pl.grad_regions == want
+    assert len(pl.bwd.bounds) == len(want) + 2
+    # bert: same rule over its layout
+    m = MB.BertModel.from_name("bert-base-uncased@2")
+    bp = [q for lay in m.encoder.layer for q in lay.params()]
+    bpl = xplan._build_bert(bp, 2, 16, 768, 12, 3072, 1e-12, 0.0, 0.0, torch.bfloat16, CPU)
+    n1 = sum(q.numel() for q in bp[:16])
+    assert bpl.grad_regions == ([(n1, 2 * n1)] if seg == 1 else [])
