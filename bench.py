@@ -509,6 +509,23 @@ def main():
                 hi = max(hi, b)
         busy_ms += hi - lo
     conv_flops, total_flops = model_flops_per_sample(cfg, img, txt)
+    table = os.environ.get("MMDX_BENCH_LAUNCH_TABLE")
+    if table and rank == 0 and timer.pairs:
+        # per-launch in-step durations (launch order of one step, averaged over the timed
+        # steps with events) against each launch's own roof max(FLOPs/peak, bytes/BW)
+        per = len(timer.pairs) // conv_steps
+        with open(table, "w") as fh:
+            fh.write("idx kind gflop mb us roof_us frac bound shape\n")
+            for i in range(per):
+                tag = timer.pairs[i][0]
+                us = sum(timer.pairs[i + k * per][1].elapsed_time(timer.pairs[i + k * per][2])
+                         for k in range(conv_steps)) / conv_steps * 1e3
+                fr = tag[1] / (PEAK_BF16_TFLOPS * 1e6)
+                br = tag[2] / (PEAK_HBM_GBS * 1e3)
+                roof = max(fr, br)
+                fh.write(f"{i} {tag[0]} {tag[1] / 1e9:.3f} {tag[2] / 1e6:.2f} {us:.1f} "
+                         f"{roof:.1f} {roof / us if us > 0 else 0:.3f} "
+                         f"{'mfma' if fr > br else 'hbm'} {tag[3].replace(' ', '_')}\n")
 
     samples = B * world * args.steps
     value = samples / el

@@ -42,7 +42,7 @@ def gemm_cost(M, N, K, dt, c_dt, beta=0.0, act=L.ACT_NONE, preact=None):
     b = (M * K + N * K) * e + M * N * ce * (2 if beta else 1)
     if preact is not None:
         b += M * N * ce
-    return LaunchCost("gemm", 2 * M * N * K, b)
+    return LaunchCost("gemm", 2 * M * N * K, b, f"{M}x{N}x{K}")
 
 
 # ----------------------------------------------------------------------------- primitives

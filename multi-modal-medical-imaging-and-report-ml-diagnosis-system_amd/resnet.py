@@ -48,8 +48,8 @@ class LaunchCost(tuple):
     max(FLOPs / MFMA peak, bytes / HBM bandwidth)."""
     __slots__ = ()
 
-    def __new__(cls, kind, flops, nbytes):
-        return tuple.__new__(cls, (kind, int(flops), int(nbytes)))
+    def __new__(cls, kind, flops, nbytes, label=""):
+        return tuple.__new__(cls, (kind, int(flops), int(nbytes), label))
 
     kind = property(lambda s: s[0])
     flops = property(lambda s: s[1])
@@ -67,7 +67,9 @@ def conv_cost(kind, conv, N, H, W, P, Q, elt, extra_read=0):
     w = conv.out_channels * conv.in_channels * k * k
     b = {"fwd": x + w * elt + y, "dgrad": y + w * elt + x + extra_read,
          "wgrad": x + y + w * 4}[kind]
-    return LaunchCost(kind, 2 * macs, b)
+    return LaunchCost(kind, 2 * macs, b,
+                      f"C{conv.in_channels}->K{conv.out_channels} {k}x{k}/{conv.stride} "
+                      f"in{N}x{H}x{W}")
 
 
 # ----------------------------------------------------------------------------- modules

@@ -180,6 +180,10 @@ def test_capture_text_tower_fwd_bwd(dev, name, dt):
     want = out.detach().clone()
     wgrads = {n: p.grad.clone() for n, p in tower.named_parameters() if p.grad is not None}
     tower.zero_grad(set_to_none=True)
+    # the eager graph must be gone before capture: a live `out` keeps its AccumulateGrad
+    # nodes bound to the eager stream, and the captured backward would then synchronise with
+    # that stream (torch warns; hipStreamEndCapture crashed on it)
+    del out
     gt = torch.cuda.make_graphed_callables(tower, (ids, mask))
     tower.zero_grad(set_to_none=True)
     out = gt(ids, mask)
