@@ -233,8 +233,25 @@ class StepTimer:
         return _Ctx()
 
 
+def graph_text_tower(txt, ids, mask):
+    """The text tower's forward and backward as two hipGraphs (torch.cuda.make_graphed_callables
+    over the mmdx launch sequence; tests/test_graph_capture_gpu.py checks replay == eager bit
+    for bit): one replay call each per step instead of the tower's Python-issued launches.
+    Returns text_fn() -> z_txt for make_step."""
+    class _Tower(torch.nn.Module):
+        def __init__(self, t):
+            super().__init__()
+            self.t = t
+
+        def forward(self, i, m):
+            return self.t(input_ids=i, attention_mask=m)["embeddings"]
+
+    g = torch.cuda.make_graphed_callables(_Tower(txt), (ids, mask), allow_unused_input=True)
+    return lambda: g(ids, mask)
+
+
 def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd=None,
-              scaler=None):
+              scaler=None, text_fn=None):
     """One train step.  `scaler` (mmdx.GradScaler, the fp16 C5 path): the loss
     is scaled before the backward (TP:1056), the clip coefficient is taken on the unscaled
     norm and folded with 1/scale into AdamW's gradient scale, an overflow skips the update
@@ -255,8 +272,8 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
         # thread onto the main stream, the text tower (Python-issued) from a worker thread
         # onto the side stream
         z_img, z_txt = towers(lambda: img(x)["embeddings"],
-                              (lambda: txt(input_ids=ids, attention_mask=mask)
-                                          ["embeddings"]))
+                              text_fn or (lambda: txt(input_ids=ids, attention_mask=mask)
+                                                     ["embeddings"]))
         main.wait_stream(side)
         with rng("mmdx/fusion_fwd"):
             logits = fus(z_img, z_txt)["disease_logits"]
@@ -442,7 +459,16 @@ def main():
         XP.STACK_SEGMENT_HOOK = reducer.trunk_segment
     # fp16 (C5): loss scaling with GradScaler semantics (TP:1025-1026, 1056-1061)
     scaler = mmdx.GradScaler() if dtype == torch.float16 else None
-    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler)
+    # MMDX_GRAPH_TEXT=1: the text tower replayed from hipGraphs (capture after build, before
+    # the warm-up; the capture itself runs eagerly on torch's capture stream)
+    text_fn = None
+    graph_text = os.environ.get("MMDX_GRAPH_TEXT", "0") == "1"
+    if graph_text:
+        with torch.cuda.stream(side):
+            text_fn = graph_text_tower(txt, ids, mask)
+        torch.cuda.synchronize()
+    step = make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, scaler=scaler,
+                     text_fn=text_fn)
     timer = StepTimer()
     if vit:   # dominant kernel family: the dense GEMMs of the ViT and BERT encoders
         MF.GEMM_TIMER = timer
@@ -561,7 +587,7 @@ def main():
         "dtype": "fp16" if dtype == torch.float16 else "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
-        "launch": "eager",
+        "launch": "eager" + (" (text tower: hipGraph replay)" if graph_text else ""),
         "stream_priority": "main+text",
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,

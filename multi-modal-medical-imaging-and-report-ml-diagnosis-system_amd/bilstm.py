@@ -51,15 +51,21 @@ class _CoopStatus:
         self.ev.record()
 
     def poll(self, block=False):
-        ev = self.ev
-        if ev is None:
-            return
         if block:
-            ev.synchronize()
-        elif not ev.query():
+            # read the device word itself: a graph-replayed launch (hipGraph capture skips
+            # the per-launch copy) sets it too
+            if int(self.word[0].item()) != 0:
+                self._raise()
+            return
+        ev = self.ev
+        if ev is None or not ev.query():
             return
         if int(self.host[0]) != 0:
-            raise RecurrenceError(
+            self._raise()
+
+    @staticmethod
+    def _raise():
+        raise RecurrenceError(
                 "mmdx BiLSTM: the cooperative recurrence timed out waiting for a peer "
                 "workgroup (mmdx_lstm_fwd status=1); the text tower's outputs and gradients "
                 "of this step are invalid")

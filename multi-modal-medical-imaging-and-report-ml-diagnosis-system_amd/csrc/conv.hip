@@ -577,21 +577,92 @@ static int conv_fwd_bn_eval_t(const mmdx_conv_desc* d, const void* x, const void
 
 // Strided dgrad as sh*sw phase GEMMs (see DgradPhaseK); phases no tap reaches are written
 // as zeros (beta = 0) or left untouched (beta != 0).
+static bool phase_geom(const ConvGeom& g, int a, int b, PhaseGeom& ph) {
+  ph.Hp = g.H > a ? (g.H - a + g.sh - 1) / g.sh : 0;
+  ph.Wp = g.W > b ? (g.W - b + g.sw - 1) / g.sw : 0;
+  if (ph.Hp == 0 || ph.Wp == 0) return false;
+  ph.r0 = (a + g.ph) % g.sh;
+  ph.s0 = (b + g.pw) % g.sw;
+  ph.ntr = ph.r0 < g.R ? (g.R - 1 - ph.r0) / g.sh + 1 : 0;
+  ph.nts = ph.s0 < g.S ? (g.S - 1 - ph.s0) / g.sw + 1 : 0;
+  ph.dr0 = (a + g.ph - ph.r0) / g.sh;
+  ph.ds0 = (b + g.pw - ph.s0) / g.sw;
+  return true;
+}
+
+// bf16 LDS-DMA path: every phase in ONE launch (grid z = phase; each block selects its own
+// phase's geometry, EpiPhase::select).  The sh*sw separate launches each filled a quarter of
+// the chip (layer4's 3x3/2: 4 x 196 tiles of 128 x 128 on 256 CUs) and were the slowest
+// C4 convs per FLOP (isolated 0.175-0.186 of their roofline).
 template <typename T>
-static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_crsk, void* dx,
-                             float beta, hipStream_t st, BnStat bs = BnStat{}) {
+static int conv_dgrad_phases_merged(const ConvGeom& g, const void* dy, const void* w_crsk,
+                                    void* dx, float beta, hipStream_t st, BnStat bs) {
+  DgradPhaseK<T> sa{(const T*)dy, g, PhaseGeom{}, 0};
+  PhaseTapK<T> sb{(const T*)w_crsk, (long)g.R * g.S * g.K, g.C, g.K, g.S, g.sh, g.sw,
+                  PhaseGeom{}};
+  EpiPhase<T> epi{(T*)dx, g.C, 0, g.C, beta, 0, 0, g.H, g.W, 0, 0, g.sh, g.sw};
+  epi.bs = bs;
+  const int N = g.C;
+  int np = 0, mmax = 0, kmax = 0;
+  long tiles128 = 0;
   for (int a = 0; a < g.sh; ++a) {
     for (int b = 0; b < g.sw; ++b) {
       PhaseGeom ph;
-      ph.Hp = g.H > a ? (g.H - a + g.sh - 1) / g.sh : 0;
-      ph.Wp = g.W > b ? (g.W - b + g.sw - 1) / g.sw : 0;
-      if (ph.Hp == 0 || ph.Wp == 0) continue;
-      ph.r0 = (a + g.ph) % g.sh;
-      ph.s0 = (b + g.pw) % g.sw;
-      ph.ntr = ph.r0 < g.R ? (g.R - 1 - ph.r0) / g.sh + 1 : 0;
-      ph.nts = ph.s0 < g.S ? (g.S - 1 - ph.s0) / g.sw + 1 : 0;
-      ph.dr0 = (a + g.ph - ph.r0) / g.sh;
-      ph.ds0 = (b + g.pw - ph.s0) / g.sw;
+      if (!phase_geom(g, a, b, ph)) continue;
+      const int K = ph.ntr * ph.nts * g.K;
+      if (K == 0 && beta != 0.f) continue;
+      MMDX_CHECK_ARG(np < MAX_PHASES, "dgrad phases: more than %d", MAX_PHASES);
+      const int M = g.N * ph.Hp * ph.Wp;
+      sa.phs[np] = sb.phs[np] = ph;
+      sa.Ms[np] = epi.Ms[np] = M;
+      epi.Ks[np] = K;
+      epi.Hps[np] = ph.Hp; epi.Wps[np] = ph.Wp;
+      epi.as[np] = a; epi.bs_[np] = b;
+      epi.tile0s[np] = bs.tile0;
+      bs.tile0 += (M + 127) / 128;  // the next phase's statistics tiles follow this phase's
+      mmax = std::max(mmax, M);
+      kmax = std::max(kmax, K);
+      tiles128 += (long)((M + 127) / 128) * ((N + 127) / 128);
+      ++np;
+    }
+  }
+  if (np == 0) return 0;
+  // 8-wave 256x128 tiles (opt-in) and the 128x64 / 128x128 choice on the whole grid's tiles
+  const long lim = conv8_min_tiles();
+  const long tiles256 = (long)np * ((mmax + 255) / 256) * ((N + 127) / 128);
+  if (lim > 0 && N >= 128 && tiles256 >= lim && kmax >= 128) {
+    hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaK<256, DgradPhaseK<T>, 64, 8>,
+                                         DmaK<128, PhaseTapK<T>, 64, 8>, EpiPhase<T>, 3, bf16,
+                                         512, 4, 2>),
+                       dim3((unsigned)(((mmax + 255) / 256) * ((N + 127) / 128)), 1, np),
+                       dim3(512), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
+  } else if (N <= 64 || tiles128 < kNarrowBelow) {
+    const int nwg = ((mmax + 127) / 128) * ((N + 63) / 64);
+    hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, DgradPhaseK<T>>,
+                                         DmaK<64, PhaseTapK<T>>, EpiPhase<T>, 2>),
+                       dim3(nwg, 1, np), dim3(NT), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
+  } else {
+    const int nwg = ((mmax + 127) / 128) * ((N + 127) / 128);
+    hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, DgradPhaseK<T>>,
+                                         DmaK<128, PhaseTapK<T>>, EpiPhase<T>, 2>),
+                       dim3(nwg, 1, np), dim3(NT), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
+  }
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_crsk, void* dx,
+                             float beta, hipStream_t st, BnStat bs = BnStat{}) {
+  if constexpr (sizeof(T) == 2) {
+    if (dma_geom_ok(g, false, 32, (long)g.N * ((g.H + g.sh - 1) / g.sh) *
+                                       ((g.W + g.sw - 1) / g.sw)))
+      return conv_dgrad_phases_merged<T>(g, dy, w_crsk, dx, beta, st, bs);
+  }
+  for (int a = 0; a < g.sh; ++a) {
+    for (int b = 0; b < g.sw; ++b) {
+      PhaseGeom ph;
+      if (!phase_geom(g, a, b, ph)) continue;
       const int K = ph.ntr * ph.nts * g.K;
       if (K == 0 && beta != 0.f) continue;
       const int M = g.N * ph.Hp * ph.Wp, N = g.C;
@@ -601,21 +672,6 @@ static int conv_dgrad_phases(const ConvGeom& g, const void* dy, const void* w_cr
       epi.bs = bs;
       bs.tile0 += (M + 127) / 128;  // the next phase's tiles follow this phase's
       int rc = -1;
-      if constexpr (sizeof(T) == 2) {
-        if (dma_geom_ok(g, false, 32, M)) {
-          const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-          if (try_conv8(sa, sb, epi, M, N, K, st)) {
-            MMDX_LAUNCH_CHECK();
-            continue;
-          }
-          if (N <= 64 || tiles128 < kNarrowBelow)
-            rc = launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
-          else
-            rc = launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
-          if (rc) return rc;
-          continue;
-        }
-      }
       if (N <= 64) {
         rc = launch<T, 128, 64, KLoad<T, 128, DgradPhaseK<T>>, KLoad<T, 64, PhaseTapK<T>>>(
             sa, sb, epi, M, N, K, 1, K, st);

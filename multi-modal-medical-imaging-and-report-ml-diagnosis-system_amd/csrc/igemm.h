@@ -418,9 +418,17 @@ struct PhaseGeom {
   int dr0, ds0;    // (a + ph - r0) / sh, (b + pw - s0) / sw
 };
 
+// Merged-phase launches (gridDim.z = phases, conv_dgrad_phases): the A / B sources and the
+// epilogue carry every phase's geometry and each block selects its own (select(blockIdx.z))
+// before anything else, so the sh*sw phase GEMMs of a strided dgrad fill the chip as one grid
+// instead of sh*sw launches of a quarter of it each.
+constexpr int MAX_PHASES = 4;
+
 template <typename T>
 struct DgradPhaseK {
   const T* dy; ConvGeom g; PhaseGeom ph; int M;
+  PhaseGeom phs[MAX_PHASES]; int Ms[MAX_PHASES];
+  __device__ void select(int p) { ph = phs[p]; M = Ms[p]; }
   struct RowState { const T* img; int i, j; };
   struct KT { int dr, ds, kb, k0, klim; };
   typedef typename Vec16<T>::type V;
@@ -489,6 +497,8 @@ struct DgradPhaseK {
 template <typename T>
 struct PhaseTapK {
   const T* w; long ld; int C, K, S, sh, sw; PhaseGeom ph;  // w[c][r][s][k], ld = R*S*K
+  PhaseGeom phs[MAX_PHASES];
+  __device__ void select(int p) { ph = phs[p]; }
   typedef const T* RowState;
   struct KT { long kg; int k0, klim; };
   typedef typename Vec16<T>::type V;
@@ -1225,6 +1235,13 @@ struct EpiPhase {
   BnStat bs{};
   static constexpr bool BNSTAT = true;
   static constexpr bool SPLIT = false;
+  // merged-phase launch: phase p's rows, K depth, pixel grid, offset and statistics tiles
+  static constexpr bool PHASED = true;
+  int Ms[MAX_PHASES], Ks[MAX_PHASES], Hps[MAX_PHASES], Wps[MAX_PHASES], as[MAX_PHASES],
+      bs_[MAX_PHASES], tile0s[MAX_PHASES];
+  __device__ void select(int p) {
+    M = Ms[p]; Hp = Hps[p]; Wp = Wps[p]; a = as[p]; b = bs_[p]; bs.tile0 = tile0s[p];
+  }
   __device__ __forceinline__ long bn_off(int m, int n) const { return pix(m) * ldc + n; }
   __device__ __forceinline__ long pix(int m) const {
     const int hw = Hp * Wp;
@@ -1291,6 +1308,11 @@ struct EpiPhase {
     }
     *(O8*)(C + off) = o;
   }
+};
+
+template <class E, class = void> struct IsPhased { static constexpr bool value = false; };
+template <class E> struct IsPhased<E, decltype((void)E::PHASED)> {
+  static constexpr bool value = E::PHASED;
 };
 
 // Bijective XCD-aware remap: blocks that share an A panel land on one XCD's L2.
@@ -1663,10 +1685,23 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   static_assert(NS >= 2 && NS <= 5 && PER_TILE * (NS - 2) <= 63, "stages");
   __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];  // the only LDS object
 
-  const int tiles_n = (N + BN - 1) / BN;
-  const int tiles_m = (M + BM - 1) / BM;
   int tile, zsplit;
-  block_tile(tiles_m * tiles_n, tile, zsplit);
+  if constexpr (IsPhased<Epi>::value) {
+    // merged strided-dgrad phases: blockIdx.z is this block's phase (not a K split)
+    const int ph = blockIdx.z;
+    sa.select(ph);
+    sb.select(ph);
+    epi.select(ph);
+    M = epi.Ms[ph];
+    K = kper = epi.Ks[ph];
+    const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if ((int)blockIdx.x >= nwg) return;  // a phase with fewer tiles than the grid's x extent
+    tile = xcd_swizzle(blockIdx.x, nwg);
+    zsplit = 0;
+  } else {
+    block_tile(((M + BM - 1) / BM) * ((N + BN - 1) / BN), tile, zsplit);
+  }
+  const int tiles_n = (N + BN - 1) / BN;
   if constexpr (Epi::SPLIT) epi.z = zsplit;
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int kbeg = zsplit * kper;

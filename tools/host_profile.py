@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c4")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--idle", action="store_true",
+                    help="profile each step issued onto an idle device (sync between steps)")
     a = ap.parse_args()
     cfg = dict(bench.CONFIGS[a.config])
     dev = torch.device("cuda", 0)
@@ -35,12 +37,22 @@ def main():
     pt = cProfile.Profile()   # the text tower's worker thread (TwoTowerForward)
     pool = step.towers._pool
     pool.submit(pt.enable).result()
-    pr.enable()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    host = (time.perf_counter() - t0) / a.steps
-    pr.disable()
+    host = 0.0
+    if a.idle:
+        for _ in range(a.steps):
+            torch.cuda.synchronize()
+            pr.enable()
+            t0 = time.perf_counter()
+            step()
+            host += (time.perf_counter() - t0) / a.steps
+            pr.disable()
+    else:
+        pr.enable()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        host = (time.perf_counter() - t0) / a.steps
+        pr.disable()
     pool.submit(pt.disable).result()
     torch.cuda.synchronize()
     print(f"host time per step (main thread, wall, device busy): {host * 1e3:.2f} ms")
