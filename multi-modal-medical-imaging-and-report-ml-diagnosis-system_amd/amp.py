@@ -73,7 +73,10 @@ class GradScaler:
         self._device = device
         self._scale = None
         self._tracker = None
-        self._found_inf = None
+        self._init_tracker = 0
+        self._found_inf = None       # the combined overflow flag of the last update()
+        self._opt_inf = {}           # id(optimizer) -> its own found_inf device scalar
+        self._step_infs = {}         # the optimizers checked since the last update()
         self._unscaled = {}
 
     def is_enabled(self):
@@ -82,8 +85,19 @@ class GradScaler:
     def _lazy(self, dev):
         if self._scale is None:
             self._scale = torch.full((1,), self._init_scale, dtype=torch.float32, device=dev)
-            self._tracker = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self._tracker = torch.full((1,), self._init_tracker, dtype=torch.int32, device=dev)
             self._found_inf = torch.zeros((1,), dtype=torch.float32, device=dev)
+
+    def _inf_for(self, optimizer, dev):
+        """optimizer's own found_inf (written by this step's norm pass), recorded for update():
+        with several optimizers the scale backs off if ANY of them overflowed (torch.amp)."""
+        self._lazy(dev)
+        fi = self._opt_inf.get(id(optimizer))
+        if fi is None:
+            fi = self._opt_inf[id(optimizer)] = torch.zeros((1,), dtype=torch.float32,
+                                                           device=dev)
+        self._step_infs[id(optimizer)] = fi
+        return fi
 
     def get_scale(self):
         """Current scale as a Python float (host sync), or 1.0 when disabled."""
@@ -115,9 +129,8 @@ class GradScaler:
         ps = self._params(optimizer)
         if not ps:
             return
-        self._lazy(ps[0].device)
-        grad_norm(ps, 0.0, apply=True, loss_scale=self._scale, unscale_first=True,
-                  found_inf=self._found_inf)
+        fi = self._inf_for(optimizer, ps[0].device)
+        grad_norm(ps, 0.0, apply=True, loss_scale=self._scale, unscale_first=True, found_inf=fi)
         self._unscaled[id(optimizer)] = True
 
     def step(self, optimizer, *args, **kwargs):
@@ -126,24 +139,27 @@ class GradScaler:
         ps = self._params(optimizer)
         if not ps:
             return None
-        self._lazy(ps[0].device)
         if id(optimizer) in self._unscaled:
-            return optimizer.step(*args, found_inf=self._found_inf, **kwargs)
-        _, inv = grad_norm(ps, 0.0, loss_scale=self._scale, found_inf=self._found_inf)
-        return optimizer.step(*args, grad_scale=inv, found_inf=self._found_inf, **kwargs)
+            return optimizer.step(*args, found_inf=self._opt_inf[id(optimizer)], **kwargs)
+        fi = self._inf_for(optimizer, ps[0].device)
+        _, inv = grad_norm(ps, 0.0, loss_scale=self._scale, found_inf=fi)
+        return optimizer.step(*args, grad_scale=inv, found_inf=fi, **kwargs)
 
     def clip_and_step(self, optimizer, max_norm=1.0, unscale_first=False, params=None):
         """clip_grad_norm_(params, max_norm) + step(optimizer) in one norm pass; returns the
         gradient norm (device scalar; unscaled iff unscale_first)."""
         ps = params if params is not None else self._params(optimizer)
+        ps = [p for p in ps if p.grad is not None]
+        if not ps:   # no gradients: nothing to clip or step (clip_grad_norm_ returns 0)
+            return torch.zeros(())
         if not self._enabled:
             norm, s = grad_norm(ps, max_norm)
             optimizer.step(grad_scale=s)
             return norm
-        self._lazy(ps[0].device)
+        fi = self._inf_for(optimizer, ps[0].device)
         norm, s = grad_norm(ps, max_norm, loss_scale=self._scale, unscale_first=unscale_first,
-                            found_inf=self._found_inf)
-        optimizer.step(grad_scale=s, found_inf=self._found_inf)
+                            found_inf=fi)
+        optimizer.step(grad_scale=s, found_inf=fi)
         return norm
 
     def update(self, new_scale=None):
@@ -152,8 +168,14 @@ class GradScaler:
         if new_scale is not None:
             self._scale.fill_(float(new_scale))
         else:
+            infs = list(self._step_infs.values())
+            if not infs:
+                raise AssertionError("No inf checks were recorded prior to update.")
+            # any optimizer's overflow backs the scale off (torch.amp.GradScaler.update)
+            self._found_inf = infs[0] if len(infs) == 1 else torch.stack(infs).amax(0)
             call("mmdx_amp_update_scale", ptr(self._scale), ptr(self._tracker),
                  ptr(self._found_inf), self._growth, self._backoff, self._interval, stream())
+        self._step_infs = {}
         self._unscaled.clear()
 
     def state_dict(self):
@@ -170,6 +192,8 @@ class GradScaler:
         self._growth = float(sd["growth_factor"])
         self._backoff = float(sd["backoff_factor"])
         self._interval = int(sd["growth_interval"])
+        # kept for a scaler whose device state does not exist yet (_lazy starts from it)
+        self._init_tracker = int(sd.get("_growth_tracker", 0))
         if self._scale is not None:
             self._scale.fill_(self._init_scale)
-            self._tracker.fill_(int(sd.get("_growth_tracker", 0)))
+            self._tracker.fill_(self._init_tracker)

@@ -85,23 +85,31 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const mmdx_adamw_tensor* __r
   __shared__ float red[4];
   const mmdx_adamw_tensor d = tab[blockIdx.x];
   float acc = 0.f;
+  bool bad = false;  // a non-finite element (torch's per-element inf/NaN check)
   long i0 = 0;
   if (aligned16(d.g)) {
     const long nv = d.n / 4;
     for (long i = threadIdx.x; i < nv; i += blockDim.x) {
       const f32x4 g = ((const f32x4*)d.g)[i];
+      bad |= !(isfinite(g[0]) && isfinite(g[1]) && isfinite(g[2]) && isfinite(g[3]));
       acc += g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
     }
     i0 = nv * 4;
   }
-  for (long i = i0 + threadIdx.x; i < d.n; i += blockDim.x) acc += d.g[i] * d.g[i];
+  for (long i = i0 + threadIdx.x; i < d.n; i += blockDim.x) {
+    bad |= !isfinite(d.g[i]);
+    acc += d.g[i] * d.g[i];
+  }
   acc = block_sum<256>(acc, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+  bad = __syncthreads_or(bad);
+  // a chunk holding an inf/NaN gradient reports NaN; finite gradients whose squares overflow
+  // report +inf — norm_finalize tells the two apart (found_inf only for the first)
+  if (threadIdx.x == 0) part[blockIdx.x] = bad ? __builtin_nanf("") : acc;
 }
 
 // norm = sqrt(sum of partials); scale = clip coefficient (torch.nn.utils.clip_grad_norm_:
 // min(1, max_norm / (norm + 1e-6))).  AMP form (loss_scale != NULL, torch.amp.GradScaler):
-// the gradients hold loss_scale * g; found_inf = 1 when the sum is inf/NaN; with
+// the gradients hold loss_scale * g; found_inf = 1 when some gradient is inf/NaN; with
 // unscale_first the clip sees the unscaled norm (scaler.unscale_ before the clip), otherwise
 // the scaled one (the reference's order, TP:1056-1060: clip, then scaler.step unscales);
 // scale additionally carries 1/loss_scale, so AdamW's grad_scale does the unscale.
@@ -121,7 +129,10 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const float* __restr
     norm[0] = nrm;
     float s = max_norm > 0.f ? fminf(1.f, max_norm / (nrm + 1e-6f)) : 1.f;
     if (scale) scale[0] = s * inv;
-    if (found_inf) found_inf[0] = isfinite(acc) ? 0.f : 1.f;
+    // found_inf: some gradient element is inf/NaN (its chunk's partial is NaN), as
+    // torch._amp_foreach_non_finite_check_and_unscale_; an overflow of the sum of squares of
+    // finite gradients is not an overflow of the gradients
+    if (found_inf) found_inf[0] = isnan(acc) ? 1.f : 0.f;
   }
 }
 

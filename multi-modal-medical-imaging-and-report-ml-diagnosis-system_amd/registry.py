@@ -50,8 +50,12 @@ def parse_s3_url(url):
 
 def get_image_from_s3(bucket, key):
     """TP:93-96: the object's bytes — read from <MMDX_S3_MIRROR>/<bucket>/<key>."""
-    root = _env_path("MMDX_S3_MIRROR", "S3 (get_image_from_s3)")
-    path = Path(root) / bucket / key
+    root = Path(_env_path("MMDX_S3_MIRROR", "S3 (get_image_from_s3)")).resolve()
+    path = (root / bucket / key).resolve()
+    # bucket / key come from feature-store rows: a '..' or absolute component must not read
+    # outside the mirror
+    if root != path and root not in path.parents:
+        raise ValueError(f"s3://{bucket}/{key} resolves outside the local mirror ({root})")
     if not path.is_file():
         raise FileNotFoundError(f"s3://{bucket}/{key} not in the local mirror ({path})")
     return path.read_bytes()
@@ -102,9 +106,16 @@ class RegistryModel:
         with open(tmp / "model.json", "w") as f:
             json.dump({"name": self.name, "version": self.version, "metrics": self.metrics,
                        "description": self.description}, f, indent=2)
+        # the old version is renamed aside (not deleted) before the new one takes its name,
+        # so a crash at any point leaves either version on disk under a known name
+        old = dst.with_name(f".{dst.name}.old")
+        if old.exists():
+            shutil.rmtree(old)
         if dst.exists():
-            shutil.rmtree(dst)
+            os.replace(dst, old)
         os.replace(tmp, dst)
+        if old.exists():
+            shutil.rmtree(old)
         return self
 
 

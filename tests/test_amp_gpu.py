@@ -126,3 +126,69 @@ def test_scale_forward_backward(dev):
     assert y.item() == 192.0 and x.grad.item() == 256.0
     off = mmdx.GradScaler(enabled=False)
     assert off.scale(x) is x
+
+
+def test_two_optimizers_any_overflow_backs_off(dev):
+    """With two optimizers the scale backs off when EITHER overflowed (torch.amp keeps one
+    found_inf per optimizer and update() takes them all): here the first overflows and the
+    second, stepped last, is clean."""
+    pa = [torch.nn.Parameter(t.clone()) for t in _params(dev)[:2]]
+    pb = [torch.nn.Parameter(t.clone()) for t in _params(dev, 1)[2:]]
+    oa, ob = mmdx.AdamW(pa, lr=1e-3), mmdx.AdamW(pb, lr=1e-3)
+    sc = mmdx.GradScaler(init_scale=1024.0)
+    sc.scale(torch.ones((), device=dev))
+    ga = _grads(0, dev)
+    ga[0][3, 4] = float("nan")
+    for p, g in zip(pa, ga[:2]):
+        p.grad = g * 1024.0
+    for p, g in zip(pb, _grads(0, dev)[2:]):
+        p.grad = g * 1024.0
+    before_b = [p.detach().clone() for p in pb]
+    sc.step(oa)
+    sc.step(ob)
+    sc.update()
+    torch.cuda.synchronize()
+    assert sc.get_scale() == 512.0
+    assert all(not torch.equal(p.detach(), b) for p, b in zip(pb, before_b))  # b stepped
+    with pytest.raises(AssertionError):
+        sc.update()          # nothing checked since the last update (torch's assertion)
+
+
+def test_finite_gradients_whose_squares_overflow_are_not_an_overflow(dev):
+    """found_inf comes from a per-element inf/NaN check, not from the sum of squares: finite
+    gradients of ~1e30 (their squares overflow fp32) do not skip the step."""
+    ps = [torch.nn.Parameter(torch.zeros(64, device=dev))]
+    opt = mmdx.AdamW(ps, lr=1e-3)
+    sc = mmdx.GradScaler(init_scale=1.0)
+    sc.scale(torch.ones((), device=dev))
+    ps[0].grad = torch.full((64,), 1e30, device=dev)
+    sc.step(opt)
+    sc.update()
+    torch.cuda.synchronize()
+    assert float(sc.found_inf.item()) == 0.0
+    assert sc.get_scale() == 1.0
+    assert float(opt.state[ps[0]]["step"].item()) == 1.0
+
+
+def test_state_dict_before_first_use_keeps_the_growth_tracker(dev):
+    """load_state_dict on a scaler that has not created its device state yet keeps the saved
+    growth tracker (two clean steps recorded): the next clean step grows the scale."""
+    dst = mmdx.GradScaler(init_scale=1.0, growth_interval=3)
+    dst.load_state_dict({"scale": 64.0, "growth_factor": 2.0, "backoff_factor": 0.5,
+                         "growth_interval": 3, "_growth_tracker": 2})
+    ps = [torch.nn.Parameter(torch.zeros(8, device=dev))]
+    opt = mmdx.AdamW(ps, lr=1e-3)
+    dst.scale(torch.ones((), device=dev))
+    ps[0].grad = torch.ones(8, device=dev)
+    dst.step(opt)
+    dst.update()               # the 3rd clean step since the saved tracker: grows now
+    torch.cuda.synchronize()
+    assert dst.get_scale() == 128.0
+
+
+def test_clip_and_step_without_gradients(dev):
+    ps = [torch.nn.Parameter(torch.zeros(8, device=dev))]
+    opt = mmdx.AdamW(ps, lr=1e-3)
+    sc = mmdx.GradScaler()
+    norm = sc.clip_and_step(opt, 1.0)
+    assert float(norm) == 0.0

@@ -67,6 +67,12 @@ def test_s3_mirror(tmp_path, monkeypatch):
     assert get_image_from_s3("b", "dir/k.jpg") == b"\xff\xd8abc"
     with pytest.raises(FileNotFoundError):
         get_image_from_s3("b", "missing.jpg")
+    # keys from feature-store rows cannot leave the mirror
+    (tmp_path.parent / "outside.jpg").write_bytes(b"secret")
+    with pytest.raises(ValueError, match="outside the local mirror"):
+        get_image_from_s3("b", "../../outside.jpg")
+    with pytest.raises(ValueError, match="outside the local mirror"):
+        get_image_from_s3("..", "outside.jpg")
     monkeypatch.delenv("MMDX_FEATURES_PARQUET", raising=False)
     with pytest.raises(REG.OfflineServiceError, match="MMDX_FEATURES_PARQUET"):
         mmdx.training_pipeline.load_features_labels_from_feature_store()
@@ -130,3 +136,20 @@ def test_adamw_refuses_late_parameters():
                        1: {"step": torch.tensor(5.0), "exp_avg": torch.zeros(3),
                            "exp_avg_sq": torch.zeros(3)}}
         opt.load_state_dict(sd)
+
+
+def test_registry_save_replaces_a_version_atomically(tmp_path, monkeypatch):
+    """RegistryModel.save over an existing version: the new folder takes the name, the old
+    one is gone, no temporary or renamed-aside folder is left behind."""
+    from mmdx.registry import LocalModelRegistry
+    monkeypatch.setenv("MMDX_MODEL_REGISTRY", str(tmp_path / "registry"))
+    reg = LocalModelRegistry()
+    for content in (b"v1", b"v2"):
+        stage = tmp_path / f"stage_{content.decode()}"
+        stage.mkdir()
+        (stage / "weights.bin").write_bytes(content)
+        rm = reg.create_model("m", version=1)
+        rm.save(str(stage))
+    d = tmp_path / "registry" / "m"
+    assert (d / "1" / "weights.bin").read_bytes() == b"v2"
+    assert sorted(p.name for p in d.iterdir()) == ["1"]
