@@ -428,7 +428,14 @@ template <typename T>
 struct DgradPhaseK {
   const T* dy; ConvGeom g; PhaseGeom ph; int M;
   PhaseGeom phs[MAX_PHASES]; int Ms[MAX_PHASES];
-  __device__ void select(int p) { ph = phs[p]; M = Ms[p]; }
+  // constant indices only (a dynamically indexed by-value kernel argument would be copied to
+  // scratch); p is wave-uniform (blockIdx.z), so this is a scalar branch
+  __device__ void select(int p) {
+    if (p == 0) { ph = phs[0]; M = Ms[0]; }
+    else if (p == 1) { ph = phs[1]; M = Ms[1]; }
+    else if (p == 2) { ph = phs[2]; M = Ms[2]; }
+    else { ph = phs[3]; M = Ms[3]; }
+  }
   struct RowState { const T* img; int i, j; };
   struct KT { int dr, ds, kb, k0, klim; };
   typedef typename Vec16<T>::type V;
@@ -498,7 +505,12 @@ template <typename T>
 struct PhaseTapK {
   const T* w; long ld; int C, K, S, sh, sw; PhaseGeom ph;  // w[c][r][s][k], ld = R*S*K
   PhaseGeom phs[MAX_PHASES];
-  __device__ void select(int p) { ph = phs[p]; }
+  __device__ void select(int p) {  // constant indices (see DgradPhaseK::select)
+    if (p == 0) ph = phs[0];
+    else if (p == 1) ph = phs[1];
+    else if (p == 2) ph = phs[2];
+    else ph = phs[3];
+  }
   typedef const T* RowState;
   struct KT { long kg; int k0, klim; };
   typedef typename Vec16<T>::type V;
@@ -1239,8 +1251,16 @@ struct EpiPhase {
   static constexpr bool PHASED = true;
   int Ms[MAX_PHASES], Ks[MAX_PHASES], Hps[MAX_PHASES], Wps[MAX_PHASES], as[MAX_PHASES],
       bs_[MAX_PHASES], tile0s[MAX_PHASES];
-  __device__ void select(int p) {
-    M = Ms[p]; Hp = Hps[p]; Wp = Wps[p]; a = as[p]; b = bs_[p]; bs.tile0 = tile0s[p];
+  int Kp = 0;  // the selected phase's K depth
+  template <int P> __device__ void select_c() {
+    M = Ms[P]; Kp = Ks[P]; Hp = Hps[P]; Wp = Wps[P]; a = as[P]; b = bs_[P];
+    bs.tile0 = tile0s[P];
+  }
+  __device__ void select(int p) {  // constant indices (see DgradPhaseK::select)
+    if (p == 0) select_c<0>();
+    else if (p == 1) select_c<1>();
+    else if (p == 2) select_c<2>();
+    else select_c<3>();
   }
   __device__ __forceinline__ long bn_off(int m, int n) const { return pix(m) * ldc + n; }
   __device__ __forceinline__ long pix(int m) const {
@@ -1692,8 +1712,8 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     sa.select(ph);
     sb.select(ph);
     epi.select(ph);
-    M = epi.Ms[ph];
-    K = kper = epi.Ks[ph];
+    M = epi.M;
+    K = kper = epi.Kp;
     const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     if ((int)blockIdx.x >= nwg) return;  // a phase with fewer tiles than the grid's x extent
     tile = xcd_swizzle(blockIdx.x, nwg);

@@ -216,9 +216,6 @@ __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma,
 // Row-tiled channel-vector layout for the elementwise BN passes: a 256-thread block covers
 // `tpr` 16-B channel vectors of `rpi` rows; each thread keeps its channels' coefficients in
 // registers for every row it visits (no per-element index math or coefficient reloads).
-// row iterations whose loads one thread keeps in flight in the apply passes
-constexpr int BN_U = 4;
-
 struct RowTile { int cv, tpr, rpi; };
 __host__ __device__ inline RowTile row_tile(int C, int vec) {
   RowTile t;
@@ -261,44 +258,29 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
   constexpr int VEC = Vec16<T>::N;
   const RowTile rt = row_tile(C, VEC);
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
-  const long stride = (long)gridDim.x * rt.rpi;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
     float sc[VEC], sh[VEC];
     load_coef<VEC>(scale + j * VEC, sc);
     load_coef<VEC>(shift + j * VEC, sh);
-    // BN_U row iterations at a time, every load issued before the first is consumed: one
-    // 16-B load per lane in flight held the pass at ~4.3 TB/s (HBM latency x bytes in flight)
-    for (long r0 = (long)blockIdx.x * rt.rpi + ro; r0 < rows; r0 += BN_U * stride) {
-      V v[BN_U], rr[BN_U];
+    for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
+      const long i = r * rt.cv + j;
+      const V v = ((const V*)x)[i];
+      V rr{};
+      if (res) rr = ((const V*)res)[i];
+      V o;
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long r = r0 + u * stride;
-        rr[u] = V{};
-        if (r < rows) {
-          v[u] = ((const V*)x)[r * rt.cv + j];
-          if (res) rr[u] = ((const V*)res)[r * rt.cv + j];
-        }
+      for (int e = 0; e < VEC; ++e) {
+        float f = to_f(v[e]) * sc[e] + sh[e];
+        if (res) f += to_f(rr[e]);
+        if (relu) f = fmaxf(f, 0.f);
+        o[e] = from_f<T>(f);
       }
+      ((V*)y)[i] = o;
+      if (mask) {
+        unsigned b = 0;
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long r = r0 + u * stride;
-        if (r >= rows) break;
-        const long i = r * rt.cv + j;
-        V o;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          float f = to_f(v[u][e]) * sc[e] + sh[e];
-          if (res) f += to_f(rr[u][e]);
-          if (relu) f = fmaxf(f, 0.f);
-          o[e] = from_f<T>(f);
-        }
-        ((V*)y)[i] = o;
-        if (mask) {
-          unsigned b = 0;
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) b |= (to_f(o[e]) > 0.f ? 1u : 0u) << e;
-          mask[i] = (uint8_t)b;
-        }
+        for (int e = 0; e < VEC; ++e) b |= (to_f(o[e]) > 0.f ? 1u : 0u) << e;
+        mask[i] = (uint8_t)b;
       }
     }
   }
@@ -341,35 +323,21 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
     }
   }
   if (c0 < C) {
-    // BN_U rows' loads in flight per thread; accumulated in the same row order as one at a
-    // time (bit-identical sums)
-    for (long rb = r0 + ty; rb < r1; rb += BN_U * rt) {
-      V vx[BN_U], vd[BN_U], vy[BN_U];
-      unsigned mb[BN_U];
+    for (long r = r0 + ty; r < r1; r += rt) {
+      const V vx = *(const V*)(x + r * C + c0);
+      const V vd = dy.row(r, c0);
+      V vy{};
+      unsigned mb = 0;
+      if (relu && mask) mb = mask[r * (C / VEC) + c0 / VEC];
+      else if (relu && !mask_x) vy = *(const V*)(y + r * C + c0);
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long r = rb + u * rt;
-        vy[u] = V{};
-        mb[u] = 0;
-        if (r < r1) {
-          vx[u] = *(const V*)(x + r * C + c0);
-          vd[u] = dy.row(r, c0);
-          if (relu && mask) mb[u] = mask[r * (C / VEC) + c0 / VEC];
-          else if (relu && !mask_x) vy[u] = *(const V*)(y + r * C + c0);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        if (rb + u * rt >= r1) break;
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-          float g = to_f(vd[u][j]);
-          const float a = mask_x ? to_f(vx[u][j]) * sc[j] + sh[j] : to_f(vy[u][j]);
-          const bool pos = mask ? ((mb[u] >> j) & 1u) != 0 : a > 0.f;
-          if (relu && !pos) g = 0.f;
-          sg[j] += g;
-          sgx[j] += g * (to_f(vx[u][j]) - mu[j]) * rs[j];
-        }
+      for (int j = 0; j < VEC; ++j) {
+        float g = to_f(vd[j]);
+        const float a = mask_x ? to_f(vx[j]) * sc[j] + sh[j] : to_f(vy[j]);
+        const bool pos = mask ? ((mb >> j) & 1u) != 0 : a > 0.f;
+        if (relu && !pos) g = 0.f;
+        sg[j] += g;
+        sgx[j] += g * (to_f(vx[j]) - mu[j]) * rs[j];
       }
     }
   }
@@ -450,7 +418,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   constexpr int VEC = Vec16<T>::N;
   const RowTile rt = row_tile(C, VEC);
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
-  const long stride = (long)gridDim.x * rt.rpi;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
     float ca[VEC], cb[VEC], ck[VEC], sc[VEC], sh[VEC];
     load_coef<VEC>(coef + j * VEC, ca);
@@ -458,41 +425,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     load_coef<VEC>(coef + 2 * C + j * VEC, ck);
     load_coef<VEC>(coef + 3 * C + j * VEC, sc);
     load_coef<VEC>(coef + 4 * C + j * VEC, sh);
-    // BN_U row iterations at a time, all loads issued first (as bn_apply_kernel)
-    for (long r0 = (long)blockIdx.x * rt.rpi + ro; r0 < rows; r0 += BN_U * stride) {
-      V vx[BN_U], vd[BN_U], vy[BN_U];
-      unsigned mb[BN_U];
+    for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
+      const long i = r * rt.cv + j;
+      const V vx = ((const V*)x)[i];
+      const V vd = dy.row(r, j * VEC);
+      V vy{};
+      unsigned mb = 0;
+      if (relu && mask) mb = mask[i];
+      else if (relu && !mask_x) vy = ((const V*)y)[i];
+      V o, og;
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long r = r0 + u * stride;
-        vy[u] = V{};
-        mb[u] = 0;
-        if (r < rows) {
-          const long i = r * rt.cv + j;
-          vx[u] = ((const V*)x)[i];
-          vd[u] = dy.row(r, j * VEC);
-          if (relu && mask) mb[u] = mask[i];
-          else if (relu && !mask_x) vy[u] = ((const V*)y)[i];
-        }
+      for (int e = 0; e < VEC; ++e) {
+        float g = to_f(vd[e]);
+        const float a = mask_x ? to_f(vx[e]) * sc[e] + sh[e] : to_f(vy[e]);
+        const bool pos = mask ? ((mb >> e) & 1u) != 0 : a > 0.f;
+        if (relu && !pos) g = 0.f;
+        o[e] = from_f<T>(ca[e] * g + cb[e] + ck[e] * to_f(vx[e]));
+        og[e] = from_f<T>(g);
       }
-#pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long r = r0 + u * stride;
-        if (r >= rows) break;
-        const long i = r * rt.cv + j;
-        V o, og;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          float g = to_f(vd[u][e]);
-          const float a = mask_x ? to_f(vx[u][e]) * sc[e] + sh[e] : to_f(vy[u][e]);
-          const bool pos = mask ? ((mb[u] >> e) & 1u) != 0 : a > 0.f;
-          if (relu && !pos) g = 0.f;
-          o[e] = from_f<T>(ca[e] * g + cb[e] + ck[e] * to_f(vx[u][e]));
-          og[e] = from_f<T>(g);
-        }
-        ((V*)dx)[i] = o;
-        if (dres) ((V*)dres)[i] = og;
-      }
+      ((V*)dx)[i] = o;
+      if (dres) ((V*)dres)[i] = og;
     }
   }
 }
