@@ -971,11 +971,17 @@ struct EpiStore {
     if (acc_src) v += acc_at(m, n);
     C[off] = from_f<OutT>(v);
   }
-  // Block-uniform: every 8-column chunk can take one 16-B (bf16) / 2x16-B (fp32) store.
+  // Block-uniform: every 8-column chunk can take one 16-B (bf16) / 2x16-B (fp32) store —
+  // with a bias (8 consecutive fp32 per chunk), an addend row, a pre-activation copy and a
+  // ReLU / GELU activation too (the forward Linear layers of the BERT / ViT stacks all carry
+  // a bias; the per-element epilogue stored them 2 bytes at a time)
   __device__ __forceinline__ bool vec8_ok() const {
-    return !bias && !addend && ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
-           ((!preact && act == ACT_NONE) ||
-            (act == ACT_GELU_BWD && !acc_src && ((uintptr_t)preact & 15) == 0));
+    if (ldc % 8 != 0 || ((uintptr_t)C & 15) != 0) return false;
+    if (bias && ((uintptr_t)bias & 15) != 0) return false;
+    if (addend && ((uintptr_t)addend & 15) != 0) return false;
+    if (preact && ((uintptr_t)preact & 15) != 0) return false;
+    if (act == ACT_GELU_BWD) return !acc_src && preact;
+    return !(acc_src && (bias || addend || preact || act != ACT_NONE));
   }
   // 8 consecutive columns n..n+7 of row m (vec8_ok() checked by the caller)
   __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
@@ -1001,7 +1007,48 @@ struct EpiStore {
       *(O8*)(C + off) = o;
       return;
     }
-    if (acc_src) {  // 8 columns = one mask byte (bf16) or two (fp32)
+    if (bias || addend || preact || act != ACT_NONE) {
+      // the general form, in apply()'s order: alpha*acc + bias + addend -> preact copy ->
+      // activation -> + beta*C
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = alpha * lo[j];
+        v[j + 4] = alpha * hi[j];
+      }
+      if (bias) {
+        const f32x4 b0 = *(const f32x4*)(bias + n), b1 = *(const f32x4*)(bias + n + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] += b0[j];
+          v[j + 4] += b1[j];
+        }
+      }
+      if (addend) {
+        const f32x4 a0 = *(const f32x4*)(addend + off), a1 = *(const f32x4*)(addend + off + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] += a0[j];
+          v[j + 4] += a1[j];
+        }
+      }
+      if (preact) {
+        O8 pr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pr[j] = from_f<OutT>(v[j]);
+        *(O8*)(preact + off) = pr;
+      }
+      O8 c{};
+      if (beta != 0.f) c = *(const O8*)(C + off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = v[j];
+        if (act == ACT_RELU) x = fmaxf(x, 0.f);
+        else if (act == ACT_GELU) x = gelu_erf(x);
+        if (beta != 0.f) x += beta * to_f(c[j]);
+        o[j] = from_f<OutT>(x);
+      }
+    } else if (acc_src) {  // 8 columns = one mask byte (bf16) or two (fp32)
       const O8 c = *(const O8*)(acc_src + off);
       constexpr int VM = 16 / (int)sizeof(OutT);
 #pragma unroll

@@ -91,6 +91,42 @@ def test_gemm_gelu_bwd_epilogue(dev, dt, MNK, beta):
     assert torch.equal(Pd.float().cpu(), P), "the pre-activation input was written"
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("act", ["none", "relu", "gelu"])
+@pytest.mark.parametrize("ldc_pad", [0, 1])
+def test_gemm_epilogue_bias_addend_preact(dev, dt, act, ldc_pad):
+    """C = act(A B^T + bias + addend) + beta C with the pre-activation copied out — the
+    16-B-per-8-columns epilogue (ldc % 8 == 0) and the per-element one (ldc odd) against a
+    float64 reference of the same rounded operands; 16-bit outputs."""
+    M, N, K = 300, 256, 192
+    ldc = N + ldc_pad
+    g = torch.Generator().manual_seed(11 + ldc_pad)
+    A, B = torch.randn(M, K, generator=g) / 8, torch.randn(N, K, generator=g) / 8
+    bias, add = torch.randn(N, generator=g), torch.randn(M, ldc, generator=g)
+    C0 = torch.randn(M, ldc, generator=g)
+    Ad, Bd = A.to(dev, dt), B.to(dev, dt)
+    C = C0.to(dev, dt)
+    pre = torch.full((M, ldc), 7.0, device=dev).to(dt)
+    code = {"none": L.ACT_NONE, "relu": L.ACT_RELU, "gelu": L.ACT_GELU}[act]
+    L.call("mmdx_gemm", L.dtype_code(dt), M, N, K, Ad.data_ptr(), K, 1, Bd.data_ptr(), K, 1,
+           C.data_ptr(), ldc, L.dtype_code(dt), bias.to(dev).data_ptr(),
+           add.to(dev).data_ptr(), code, 1.0, 0.5, pre.data_ptr(),
+           *_ws(dt, M, N, K, dev), L.stream())
+    torch.cuda.synchronize()
+    Ar, Br = Ad.double().cpu(), Bd.double().cpu()
+    z = Ar @ Br.T + bias.double() + add[:, :N].double()
+    y = {"none": z, "relu": z.clamp(min=0), "gelu": tF.gelu(z)}[act]
+    ref = y + 0.5 * C0.to(dt).double()[:, :N]
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    for what, got, want in (("C", C, ref), ("preact", pre, z)):
+        got = got.double().cpu()
+        err = ((got[:, :N] - want).abs().max() / want.abs().max()).item()
+        assert err <= tol, (what, err)
+    if ldc_pad:   # the padding column is never written
+        assert torch.equal(C.cpu()[:, N:], C0.to(dt)[:, N:])
+        assert torch.all(pre.float().cpu()[:, N:] == 7.0)
+
+
 def _ws(dt, M, N, K, dev):
     n = L.lib().mmdx_gemm_workspace_size(L.dtype_code(dt), M, N, K)
     w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
