@@ -1,0 +1,326 @@
+// Dense 16-bit GEMM, 256 x 256 tiles, 8 waves in two staggered groups ("ping-pong"), the K loop
+// cut into 4 phases per 64-deep K tile.  Used by gemm_dense.hip for the Linear layers of the
+// BERT / ViT stacks (C5) where the 4-wave 128 x 128 kernel of igemm.h leaves the MFMA pipe
+// idle at every K-tile barrier.
+//
+// Block: 512 threads = waves w = 0..7 on a 2 x 4 grid, wave (wr = w / 4, wc = w % 4) owns rows
+// wr*128 .. +127 and columns wc*64 .. +63 of the tile (acc[8][4] of 16 x 16 MFMA tiles).
+// LDS: two stages of four 16-KB half-tile images (A rows 0-127, A rows 128-255, B rows 0-127,
+// B rows 128-255), each filled by 16 LDS-DMA instructions (buffer_load ... lds, 1 KiB per
+// wave-instruction, two per wave).  Wave group wr reads only A half wr; wave wc reads only B
+// half wc / 2.
+//
+// Phases of K tile t (stage s = t % 2), per wave: R = LDS fragment reads + this phase's
+// DMA issue, then s_barrier, the MFMA cluster, s_barrier:
+//   p0: A(t+1) half 0 -> stage s^1 | read A rows 0-63 (8 x b128), B cols 0-31 (4)  | 16 MFMA
+//   p1: A(t+1) half 1 -> stage s^1 | read B cols 32-63 (4)                          | 16 MFMA
+//   p2: B(t+2) half 0 -> stage s   | read A rows 64-127 (8)                         | 16 MFMA
+//   p3: B(t+2) half 1 -> stage s   | vmcnt: everything but B(t+2) landed            | 16 MFMA
+// Group 1 executes one extra s_barrier before its first phase, so its R sections run while
+// group 0 is in an MFMA cluster and vice versa: on every SIMD (one wave of each group) one wave
+// feeds the MFMA pipe while the other reads LDS and issues DMAs.
+// Hazards (all by construction, every wave executes the same barrier count):
+//   RAW: a wave's DMAs of tile t+1 (A: p0/p1 of tile t, B: p2/p3 of tile t-1) are retired by
+//     its counted vmcnt in p3 of tile t before that phase's barrier; the other group passes
+//     that barrier before its first read of tile t+1 (one or more barriers later).
+//   WAR: B halves of stage s are last read in p1 of tile t and refilled from p2 on; A halves of
+//     stage s^1 last read in p2 of tile t-1, refilled in p0/p1 of tile t; each R section
+//     drains its LDS reads (lgkmcnt(0)) before its barrier, so no read is pending when the
+//     other group's next R section issues a DMA.
+// Epilogue: the fp32 tile staged through LDS in two 128-column passes (igemm.h epilogue_pass).
+#pragma once
+
+#include "igemm.h"
+
+namespace mmdx {
+
+// K-major operand (element (r, k) at base[r * ld + k]): half image [128 rows][64 k], 128-B
+// rows, logical chunk c of row r at slot c ^ (r & 7) (conflict-free b128 fragment reads).
+// DMA instruction j (0, 1) of wave w fills rows (j * 8 + w) * 8 .. +7 of the half.
+template <typename T>
+struct HalfK {
+  typedef DenseK<T> Src;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int off[2][2];   // [half][j]: byte offset of this lane's chunk at k = 0, or -1 (row >= R)
+  int coff;        // k offset of this lane's chunk within the K tile
+  __device__ void init(const Src& s, int row0, int lane, int wid) {
+    const int rr = lane >> 3, slot = lane & 7;
+    coff = (slot ^ rr) * 8;
+    rsrc = dma_rsrc(s.base, s.bbytes());
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = row0 + h * 128 + (j * 8 + wid) * 8 + rr;
+        off[h][j] = r < s.R ? (int)(((long)r * s.ld + coff) * (long)sizeof(T)) : -1;
+      }
+  }
+  __device__ void issue(char* img, int h, int k0, int klim, int wid) const {
+    const bool kok = k0 + coff < klim;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = kok && off[h][j] >= 0;
+      dma16(rsrc, img + (j * 8 + wid) * 1024,
+            ok ? (unsigned)(off[h][j] + k0 * (int)sizeof(T)) : DMA_OOB);
+    }
+  }
+  // rows r16 .. r16+15 of the half, k = ks .. ks+31: lane (i, g) gets row r16+i, k ks+8g..+7
+  __device__ static bf16x8 frag(const char* img, int r16, int ks, int lane) {
+    const int row = r16 + (lane & 15);
+    const int c = (ks >> 3) + (lane >> 4);
+    return *(const bf16x8*)(img + row * 128 + ((c ^ (row & 7)) << 4));
+  }
+};
+
+// R-major operand (element (r, k) at base[k * ld + r], R % 8 == 0): half image [64 k][128
+// rows], one 256-B line per k (16 chunks of 8 rows), chunk slots XOR-swizzled per k so the
+// ds_read_b64_tr_b16 fragment reads hit every bank once (igemm.h DmaR, ROWS = 128).  DMA
+// instruction j of wave w fills k-lines (j * 8 + w) * 4 .. +3.
+template <typename T>
+struct HalfR {
+  typedef DenseR<T> Src;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int off[2][2];   // [half][j]: byte offset of this lane's 8 rows at k = its k-line, or -1
+  int kl[2];       // this lane's k-line (within the K tile) per j
+  int ldb;         // bytes per k step (ld * sizeof(T))
+  __device__ static int sw(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+  __device__ void init(const Src& s, int row0, int lane, int wid) {
+    const int slot = lane & 15;
+    rsrc = dma_rsrc(s.base, s.bbytes());
+    ldb = (int)(s.ld * (long)sizeof(T));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      kl[j] = (j * 8 + wid) * 4 + (lane >> 4);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = row0 + h * 128 + (slot ^ sw(kl[j])) * 8;
+        off[h][j] = r < s.R ? (int)(((long)kl[j] * s.ld + r) * (long)sizeof(T)) : -1;
+      }
+    }
+  }
+  __device__ void issue(char* img, int h, int k0, int klim, int wid) const {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = off[h][j] >= 0 && k0 + kl[j] < klim;
+      dma16(rsrc, img + (j * 8 + wid) * 1024,
+            ok ? (unsigned)(off[h][j] + k0 * ldb) : DMA_OOB);
+    }
+  }
+  __device__ static bf16x8 frag(const char* img, int r16, int ks, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = ks + 8 * g + q;
+    const int col = r16 + 4 * p;
+    const int o = (((col >> 3) ^ sw(k)) << 4) + ((col >> 2) & 1) * 8;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + k * 256 + o));
+    const s16x4 hi =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (k + 4) * 256 + o));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
+
+template <typename ET>
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (std::is_same<ET, f16>::value)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// one phase's MFMA cluster: acc[I0 .. I0+3][J0, J0+1] += a[4][2] x b[2][2] (two 32-deep k steps)
+template <typename ET, int I0, int J0>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
+                                              const bf16x8 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[I0 + i][J0 + j] = mfma16<ET>(a[i][s], b[j][s], acc[I0 + i][J0 + j]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <class OP>
+__device__ __forceinline__ void read_a4(bf16x8 (&a)[4][2], const char* img, int r0, int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i][s] = OP::frag(img, r0 + i * 16, s * 32, lane);
+}
+
+template <class OP>
+__device__ __forceinline__ void read_b2(bf16x8 (&b)[2][2], const char* img, int c0, int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j][s] = OP::frag(img, c0 + j * 16, s * 32, lane);
+}
+
+__device__ __forceinline__ void lds_drain_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <class OA, class OB, class Epi, typename ET, int SCHED = 1>
+__global__ __launch_bounds__(512, 2) void gemm8ph_kernel(typename OA::Src sa, typename OB::Src sb,
+                                                         Epi epi, int M, int N, int K, int kper) {
+  constexpr int BM = 256, BN = 256, HALF = 16384, STAGE = 4 * HALF;
+  constexpr int WM = 2, WN = 4, WTM = 128, WTN = 64, RM = 8, RN = 4, NTH = 512;
+  constexpr int RED = 16;              // floats per column of reg_stats scratch (>= WM * 3)
+  constexpr int CH = 128, LDC = CH + 4; // two column passes of the fp32 tile
+  constexpr int EPI_BYTES = BM * LDC * 4 + RED * BN * 4;
+  constexpr int LDS_BYTES = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];  // the only LDS object
+
+  int tile, zsplit;
+  block_tile(((M + BM - 1) / BM) * ((N + BN - 1) / BN), tile, zsplit);
+  const int tiles_n = (N + BN - 1) / BN;
+  if constexpr (Epi::SPLIT) epi.z = zsplit;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int kbeg = zsplit * kper;
+  const int kend = min(K, kbeg + kper);
+  const int nt = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
+  const int lane = threadIdx.x & 63,
+            wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wr = wid >> 2, wc = wid & 3;
+
+  OA oa;
+  OB ob;
+  oa.init(sa, tm * BM, lane, wid);
+  ob.init(sb, tn * BN, lane, wid);
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // image h of stage s: A halves 0, 1 then B halves 0, 1
+#define IMG(s, h) (lds + (s) * STAGE + (h) * HALF)
+  if (nt > 0) {
+    oa.issue(IMG(0, 0), 0, kbeg, kend, wid);
+    oa.issue(IMG(0, 1), 1, kbeg, kend, wid);
+    ob.issue(IMG(0, 2), 0, kbeg, kend, wid);
+    ob.issue(IMG(0, 3), 1, kbeg, kend, wid);
+  }
+  if (nt > 1) {
+    ob.issue(IMG(1, 2), 0, kbeg + 64, kend, wid);
+    if constexpr (SCHED == 0) {
+      ob.issue(IMG(1, 3), 1, kbeg + 64, kend, wid);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      ob.issue(IMG(1, 3), 1, kbeg + 64, kend, wid);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 one barrier behind
+
+  const int bc = (wc & 1) * 64;  // this wave's columns within its B half
+  for (int t = 0; t < nt; ++t) {
+    const int s = t & 1;
+    const int k1 = kbeg + (t + 1) * 64, k2 = kbeg + (t + 2) * 64;
+    const char* ai = IMG(s, wr);
+    const char* bi = IMG(s, 2 + (wc >> 1));
+    bf16x8 a[4][2], b0[2][2], b1[2][2];
+    if constexpr (SCHED == 0) {
+      // p0
+      if (t + 1 < nt) oa.issue(IMG(s ^ 1, 0), 0, k1, kend, wid);
+      read_a4<OA>(a, ai, 0, lane);
+      read_b2<OB>(b0, bi, bc, lane);
+      lds_drain_barrier();
+      mfma_quadrant<ET, 0, 0>(acc, a, b0);
+      __builtin_amdgcn_s_barrier();
+      // p1
+      if (t + 1 < nt) oa.issue(IMG(s ^ 1, 1), 1, k1, kend, wid);
+      read_b2<OB>(b1, bi, bc + 32, lane);
+      lds_drain_barrier();
+      mfma_quadrant<ET, 0, 2>(acc, a, b1);
+      __builtin_amdgcn_s_barrier();
+      // p2
+      if (t + 2 < nt) ob.issue(IMG(s, 2), 0, k2, kend, wid);
+      read_a4<OA>(a, ai, 64, lane);
+      lds_drain_barrier();
+      mfma_quadrant<ET, 4, 2>(acc, a, b1);
+      __builtin_amdgcn_s_barrier();
+      // p3
+      if (t + 2 < nt) {
+        ob.issue(IMG(s, 3), 1, k2, kend, wid);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      mfma_quadrant<ET, 4, 0>(acc, a, b0);
+      __builtin_amdgcn_s_barrier();
+    } else {
+      // B(t+2) half 0 at p3 of tile t, half 1 at p0 of tile t+1: every DMA lands in a region
+      // whose last reads were drained by an lgkmcnt one barrier earlier in both groups, so
+      // the LDS reads of an R section may stay in flight across its barrier
+      // p0
+      if (t + 1 < nt) {
+        if (t >= 1) ob.issue(IMG(s ^ 1, 3), 1, kbeg + (t + 1) * 64, kend, wid);
+        oa.issue(IMG(s ^ 1, 0), 0, k1, kend, wid);
+      }
+      read_a4<OA>(a, ai, 0, lane);
+      read_b2<OB>(b0, bi, bc, lane);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<ET, 0, 0>(acc, a, b0);
+      __builtin_amdgcn_s_barrier();
+      // p1
+      if (t + 1 < nt) oa.issue(IMG(s ^ 1, 1), 1, k1, kend, wid);
+      read_b2<OB>(b1, bi, bc + 32, lane);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<ET, 0, 2>(acc, a, b1);
+      __builtin_amdgcn_s_barrier();
+      // p2
+      read_a4<OA>(a, ai, 64, lane);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<ET, 4, 2>(acc, a, b1);
+      __builtin_amdgcn_s_barrier();
+      // p3: B(t+2) half 0; retire everything older (A(t+1), B(t+1))
+      if (t + 2 < nt) {
+        ob.issue(IMG(s, 2), 0, k2, kend, wid);
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      mfma_quadrant<ET, 4, 0>(acc, a, b0);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+#undef IMG
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // unstagger: equal barrier counts
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float* cst = (float*)lds;
+  float* red = cst + BM * LDC;
+  if constexpr (Epi::REG_STATS)
+    epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wr, wc, lane);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h > 0) __syncthreads();
+    if ((wc * WTN) / CH == h) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cst[(wr * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wc * WTN - h * CH + j * 16 +
+                (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    epilogue_pass<BM, CH, LDC, NTH>(epi, cst, tm * BM, tn * BN + h * CH);
+  }
+}
+
+}  // namespace mmdx
