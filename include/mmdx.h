@@ -264,7 +264,7 @@ enum {
   /* transformer layer stacks (BERT / ViT encoders, one plan per stack and direction) */
   MMDX_OP_GEMM, MMDX_OP_ATTN_FWD, MMDX_OP_ATTN_BWD, MMDX_OP_LN_FWD, MMDX_OP_LN_BWD,
   MMDX_OP_GELU_BWD, MMDX_OP_BIAS_GRAD, MMDX_OP_ADD, MMDX_OP_DROPOUT_FWD, MMDX_OP_DROPOUT_BWD,
-  MMDX_OP_AXPBY
+  MMDX_OP_AXPBY, MMDX_OP_ATTN_FWD_LSE, MMDX_OP_ATTN_BWD_LSE
 };
 typedef struct {
   int op, dtype, stream;
@@ -442,6 +442,22 @@ size_t mmdx_attention_workspace_size(int dtype, int B, int L, int H);
 int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs, const void* dout,
                        const int64_t* mask, int B, int L, int H, float scale, float p_drop,
                        void* dqkv, void* workspace, size_t ws_bytes, void* stream);
+/* Flash-style variant (16-bit dtypes, no score bias / causal mask): the forward saves the
+ * row log-sum-exp lse [B, H, L] fp32 instead of P, and rng[0] (device uint64) receives the
+ * dropout stream's base (seed and *counter as the launch read them).  The backward
+ * recomputes P from Q, K and lse, the keep bits from the same hash, and the softmax row term
+ * rowsum(P o dP) as dO . out (out = the forward's output, which the attention output
+ * projection keeps anyway), so no [B, H, L, L] tensor is written or read.  The workspace
+ * holds that row term ([B, H, L] fp32).  Same arguments and results otherwise.
+ * Replaces: BertSelfAttention / torchvision MultiheadAttention as above (TP:360, vit_b_16). */
+int mmdx_attention_fwd_lse(int dtype, const void* qkv, const int64_t* mask, int B, int L,
+                           int H, float scale, float p_drop, uint64_t seed, uint64_t* counter,
+                           void* out, float* lse, uint64_t* rng, void* stream);
+size_t mmdx_attention_lse_workspace_size(int dtype, int B, int L, int H);
+int mmdx_attention_bwd_lse(int dtype, const void* qkv, const void* out, const float* lse,
+                           const uint64_t* rng, const void* dout, const int64_t* mask, int B,
+                           int L, int H, float scale, float p_drop, void* dqkv,
+                           void* workspace, size_t ws_bytes, void* stream);
 
 /* LSTM recurrence for one layer, both directions (build-defined C3/C4 tower).
  * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);

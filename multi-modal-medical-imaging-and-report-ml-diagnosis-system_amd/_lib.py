@@ -56,7 +56,7 @@ class PlanOp(C.Structure):
  OP_STEM_PAIR_PACK, OP_STEM_PAIR_GRAD, OP_CONV_PACK_MULTI, OP_CONV_FWD_BNEVAL,
  OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK, OP_BN_BWD_MASKED_DY,
  OP_GEMM, OP_ATTN_FWD, OP_ATTN_BWD, OP_LN_FWD, OP_LN_BWD, OP_GELU_BWD, OP_BIAS_GRAD, OP_ADD,
- OP_DROPOUT_FWD, OP_DROPOUT_BWD, OP_AXPBY) = range(1, 37)
+ OP_DROPOUT_FWD, OP_DROPOUT_BWD, OP_AXPBY, OP_ATTN_FWD_LSE, OP_ATTN_BWD_LSE) = range(1, 39)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -138,6 +138,11 @@ SIGNATURES = {
                                     vp, vp]),
     "mmdx_attention_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_attention_bwd": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp, vp, sz, vp]),
+    "mmdx_attention_fwd_lse": (i32, [i32, vp, vp, i32, i32, i32, f32, f32, u64, vp, vp, vp, vp,
+                                     vp]),
+    "mmdx_attention_lse_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_attention_bwd_lse": (i32, [i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp,
+                                     vp, sz, vp]),
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp, i64, i32, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_fwd_workspace_size": (sz, [i32, i32, i32, i32]),

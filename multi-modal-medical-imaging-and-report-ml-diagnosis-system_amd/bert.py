@@ -110,16 +110,14 @@ class _BertLayerFn(torch.autograd.Function):
         F.gemm(x, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, bias=bqkv, compute_dtype=T)
         att = torch.empty((M, D), dtype=T, device=dev)
         keep = any(ctx.needs_input_grad)
-        probs = (torch.empty((B, Hn, Ls, Ls), dtype=torch.float32, device=dev)
-                 if keep else None)
         scale = 1.0 / math.sqrt(D // Hn)
         # BertSelfAttention's dropout on attention_probs (train mode), fused in the kernel
         pa = float(cfg.p_attn) if (cfg.training and keep) else 0.0
         if pa > 0:
             _SEED[0] += 1
-        call("mmdx_attention_fwd", L.dtype_code(T), ptr(qkv), ptr(mask), B, Ls, Hn, float(scale),
-             pa, L.dropout_seed(_SEED[0]) if pa > 0 else 0, ptr(L.rng_counter(dev)), ptr(att),
-             ptr(probs), stream())
+        ctx.attn = F.attention_fwd(qkv, mask, B, Ls, Hn, scale, pa,
+                                   L.dropout_seed(_SEED[0]) if pa > 0 else 0,
+                                   L.rng_counter(dev), att, keep)
         woc = F.cast(wo, T)
         a = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(att, D, True, woc, D, True, M, D, D, a, D, bias=bo, compute_dtype=T)
@@ -142,7 +140,7 @@ class _BertLayerFn(torch.autograd.Function):
             _SEED[0] += 1
             f2, m2 = _dropout_fwd(f2, p, _SEED[0])
         h2, xs2, mu2, rs2 = _ln_fwd(f2, h1, g2, b2, eps)
-        ctx.save_for_backward(x, mask, wqkv, qkv, probs, att, woc, xs1, mu1, rs1, g1, h1, wic,
+        ctx.save_for_backward(x, mask, wqkv, qkv, att, woc, xs1, mu1, rs1, g1, h1, wic,
                               pre, f, wo2c, xs2, mu2, rs2, g2)
         ctx.m1, ctx.m2, ctx.p, ctx.pa = m1, m2, p, pa
         ctx.dims = (B, Ls, D, Hn, I, scale)
@@ -150,7 +148,7 @@ class _BertLayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2):
-        (x, mask, wqkv, qkv, probs, att, woc, xs1, mu1, rs1, g1, h1, wic, pre, f, wo2c, xs2, mu2,
+        (x, mask, wqkv, qkv, att, woc, xs1, mu1, rs1, g1, h1, wic, pre, f, wo2c, xs2, mu2,
          rs2, g2) = ctx.saved_tensors
         B, Ls, D, Hn, I, scale = ctx.dims
         T = x.dtype
@@ -182,10 +180,7 @@ class _BertLayerFn(torch.autograd.Function):
         F.gemm(dY1, D, False, att, D, False, D, D, M, dWo, D, compute_dtype=T)
         dbo = F._bias_grad(dY1, M, D, torch.empty(D, dtype=torch.float32, device=dev))
         dqkv = torch.empty((M, 3 * D), dtype=T, device=dev)
-        n = L.lib().mmdx_attention_workspace_size(L.dtype_code(T), B, Ls, Hn)
-        w = _ws(n, dev)
-        call("mmdx_attention_bwd", L.dtype_code(T), ptr(qkv), ptr(probs), ptr(datt), ptr(mask),
-             B, Ls, Hn, float(scale), float(ctx.pa), ptr(dqkv), ptr(w), n, stream())
+        F.attention_bwd(qkv, ctx.attn, att, datt, mask, B, Ls, Hn, scale, ctx.pa, dqkv)
         dWqkv = torch.empty((3 * D, D), dtype=torch.float32, device=dev)
         F.gemm(dqkv, 3 * D, False, x, D, False, 3 * D, D, M, dWqkv, D, compute_dtype=T)
         dbqkv = F._bias_grad(dqkv, M, 3 * D, torch.empty(3 * D, dtype=torch.float32, device=dev))

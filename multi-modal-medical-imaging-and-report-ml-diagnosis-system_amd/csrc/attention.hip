@@ -535,7 +535,8 @@ template <typename T, int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd16_kernel(
     const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bias,
     int causal, int L, int H, float scale, float p_drop, uint64_t seed,
-    const uint64_t* __restrict__ ctr, T* __restrict__ out, float* __restrict__ probs) {
+    const uint64_t* __restrict__ ctr, T* __restrict__ out, float* __restrict__ probs,
+    float* __restrict__ lse, uint64_t* __restrict__ rng_out) {
   typedef MfmaOp<T> Op;
   typedef typename Op::frag_t F;
   static_assert(Op::FRAG == 8 && Op::KS == 32, "16-bit MFMA 16x16x32 operands");
@@ -603,6 +604,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd16_kernel(
   sum += __shfl_xor(sum, 16, 64);
   sum += __shfl_xor(sum, 32, 64);
   const float inv = 1.f / sum;
+  // flash-style save (mmdx_attention_fwd_lse): the row log-sum-exp instead of P
+  if (lse && g == 0 && q < L) lse[((long)b * H + h) * L + q] = mx + __logf(sum);
   float* pbase = probs ? probs + (((long)b * H + h) * L) * L : nullptr;
   const bool vec_p = (L & 3) == 0;
   // L % 4 != 0: the lane's 4 keys are not a 16-B aligned run of a row; the wave transposes
@@ -610,9 +613,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd16_kernel(
   float* pscr = madd + LP + wid * 16 * LDP;
   const bool drop = p_drop > 0.f;
   const float keep_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
-  const uint64_t rbase = drop ? seed * 0x9E3779B97F4A7C15ULL + (ctr ? ctr[0] << 32 : 0ull) +
-                                    (((uint64_t)b * H + h) * L) * (uint64_t)L
-                              : 0ull;
+  const uint64_t rb0 = seed * 0x9E3779B97F4A7C15ULL + (ctr ? ctr[0] << 32 : 0ull);
+  if (rng_out && blockIdx.x == 0 && threadIdx.x == 0) rng_out[0] = rb0;  // for the backward
+  const uint64_t rbase = drop ? rb0 + (((uint64_t)b * H + h) * L) * (uint64_t)L : 0ull;
   F pf[MAXKT / 2];
 #pragma unroll
   for (int j = 0; j < MAXKT; ++j) {
@@ -863,6 +866,220 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_kv16_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Flash-style backward (16-bit; mmdx_attention_bwd_lse): nothing of size L^2 is saved or
+// exchanged.  P is recomputed from Q, K and the forward's row log-sum-exp, the dropout keep
+// bits from the counter hash (the forward left the stream's base in rng[0]), and the row term
+// rowsum(P o dP) of the softmax gradient is D = dO . O (with dropout: sum_k P'_k dP'_k, the
+// same number), so each kernel makes one pass:
+//   A (per query block, swapped products as attn_bwd_q16_kernel): D, then per key-tile pair
+//     S^T = K Q^T and dP'^T = V dO^T, dS = P o (keep * dP' / (1-p) - D), dQ^T += K^T dS^T;
+//     D is left in the workspace for B.
+//   B (per key block, one key per lane column): per 32-query chunk S = Q K^T and
+//     dP' = dO V^T as two 16-query tiles (queries g*4+r and 16+g*4+r of the lane: the MFMA
+//     k order of the next products, matched by the permuted transposed reads of Q / dO),
+//     P' and dS formed in registers, dV^T += dO^T P', dK^T += Q^T dS.
+// K (A) and Q, dO (B) are staged once per block as [LP][LDT] images: plain 16-B reads give
+// the S / dP operands, ds_read_b64_tr_b16 the transposed ones.
+// ---------------------------------------------------------------------------------------
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_q16_lse_kernel(
+    const T* __restrict__ qkv, const T* __restrict__ outp, const float* __restrict__ lse,
+    const uint64_t* __restrict__ rng, const T* __restrict__ dout, const int64_t* __restrict__ mask,
+    int L, int H, float scale, float p_drop, float* __restrict__ Dg, T* __restrict__ dqkv) {
+  typedef MfmaOp<T> Op;
+  typedef typename Op::frag_t F;
+  constexpr int QB = NW * 16;
+  const int LP = (L + 31) & ~31;
+  const int nkt = LP / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Vs = (T*)smem_raw;               // [LP][LDR]  A operand rows of dP^T
+  T* Ks = Vs + LP * LDR;              // [LP][LDT]  A operand rows of S^T / transposed K^T
+  float* madd = (float*)(Ks + LP * LDT);   // [LP]
+  int qb, h, b;
+  attn_block((L + QB - 1) / QB, H, qb, h, b);
+  const int q0 = qb * QB;
+  const long row_ld = 3L * H * HD;
+  const T* base = qkv + (long)b * L * row_ld + h * HD;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ql = lane & 15, g = lane >> 4;
+  const int q = q0 + wid * 16 + ql;
+  const bool idle = q0 + wid * 16 >= L;
+  F qf[2], of[2];
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    qf[k] = of[k] = F{};
+    if (q < L) {
+      qf[k] = *(const F*)(base + (long)q * row_ld + k * 32 + g * 8);
+      const long orow = ((long)b * L + q) * H * HD + h * HD + k * 32 + g * 8;
+      of[k] = *(const F*)(dout + orow);
+      const F ov = *(const F*)(outp + orow);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot += (float)of[k][e] * (float)ov[e];
+    }
+  }
+  dot += __shfl_xor(dot, 16, 64);
+  dot += __shfl_xor(dot, 32, 64);
+  stage_pair<T, 4, false, false>(Vs, LDR, base + 2L * H * HD, Ks, LDT, base + (long)H * HD,
+                                 row_ld, LP, L, NW * 64);
+  for (int k = threadIdx.x; k < LP; k += NW * 64)
+    madd[k] = k < L ? (mask && mask[(long)b * L + k] == 0 ? MASK_NEG : 0.f) : -INFINITY;
+  __syncthreads();   // the only barrier
+  if (idle) return;
+  if (g == 0 && q < L) Dg[((long)b * H + h) * L + q] = dot;
+  const float lq = q < L ? lse[((long)b * H + h) * L + q] : 0.f;
+  const bool drop = p_drop > 0.f;
+  const float keep_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
+  const uint64_t rbase = drop ? rng[0] + (((uint64_t)b * H + h) * L) * (uint64_t)L : 0ull;
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < MAXKT / 2; ++t) {
+    if (2 * t >= nkt) continue;
+    F df;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int j = 2 * t + h2;
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, tp = st;
+      const T* ak = Ks + (j * 16 + ql) * LDT + g * 8;
+      const T* av = Vs + (j * 16 + ql) * LDR + g * 8;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        st = Op::mma(Op::ld(ak + k * 32), qf[k], st);
+        tp = Op::mma(Op::ld(av + k * 32), of[k], tp);
+      }
+      const f32x4 ma = *(const f32x4*)(madd + j * 16 + g * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = j * 16 + g * 4 + r;
+        const float p = __expf(st[r] * scale + ma[r] - lq);
+        bool keep = true;
+        if (drop) {
+          const float u = (attn_hash64(rbase + (uint64_t)q * L + key) >> 8) * (1.f / 16777216.f);
+          keep = u >= p_drop;
+        }
+        const float dp = keep ? tp[r] * keep_scale : 0.f;
+        df[h2 * 4 + r] = from_f<T>(p * (dp - dot));
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const F kf = join_frag<T>(tr_read4(Ks, 2 * t * 16 + g * 4, dt * 16),
+                                tr_read4(Ks, (2 * t + 1) * 16 + g * 4, dt * 16));
+      o[dt] = Op::mma(kf, df, o[dt]);
+    }
+  }
+  if (q < L) {
+    T* drow = dqkv + ((long)b * L + q) * 3 * H * HD + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+      store4<T>(drow + dt * 16 + g * 4, o[dt][0] * scale, o[dt][1] * scale, o[dt][2] * scale,
+                o[dt][3] * scale);
+  }
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_kv16_lse_kernel(
+    const T* __restrict__ qkv, const float* __restrict__ lse, const uint64_t* __restrict__ rng,
+    const T* __restrict__ dout, const int64_t* __restrict__ mask, const float* __restrict__ Dg,
+    int L, int H, float scale, float p_drop, T* __restrict__ dqkv) {
+  typedef MfmaOp<T> Op;
+  typedef typename Op::frag_t F;
+  constexpr int KB = NW * 16;
+  const int LP = (L + 31) & ~31;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* Qs = (T*)smem_raw;               // [LP][LDT]
+  T* Os = Qs + LP * LDT;              // [LP][LDT]  dO
+  float* ls = (float*)(Os + LP * LDT);   // [LP] lse (0 beyond L)
+  float* ds_ = ls + LP;                  // [LP] D
+  int kb, h, b;
+  attn_block((L + KB - 1) / KB, H, kb, h, b);
+  const int k0 = kb * KB;
+  const long row_ld = 3L * H * HD;
+  const T* base = qkv + (long)b * L * row_ld + h * HD;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, kl = lane & 15, g = lane >> 4;
+  const int key = k0 + wid * 16 + kl;
+  const bool idle = k0 + wid * 16 >= L;
+  const bool kok = key < L;
+  F kf[2], vf[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    kf[k] = vf[k] = F{};
+    if (kok) {
+      kf[k] = *(const F*)(base + (long)key * row_ld + (long)H * HD + k * 32 + g * 8);
+      vf[k] = *(const F*)(base + (long)key * row_ld + 2L * H * HD + k * 32 + g * 8);
+    }
+  }
+  stage_rows<T, 4, false>(Qs, LDT, base, row_ld, LP, L, NW * 64);
+  stage_rows<T, 4, false>(Os, LDT, dout + (long)b * L * H * HD + h * HD, (long)H * HD, LP, L,
+                          NW * 64);
+  const long hq = ((long)b * H + h) * L;
+  for (int i = threadIdx.x; i < LP; i += NW * 64) {
+    ls[i] = i < L ? lse[hq + i] : 0.f;
+    ds_[i] = i < L ? Dg[hq + i] : 0.f;
+  }
+  __syncthreads();   // the only barrier
+  if (idle) return;
+  const float mk = kok ? (mask && mask[(long)b * L + key] == 0 ? MASK_NEG : 0.f) : -INFINITY;
+  const bool drop = p_drop > 0.f;
+  const float keep_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
+  const uint64_t rbase = drop ? rng[0] + (uint64_t)hq * (uint64_t)L : 0ull;
+  f32x4 dv[HD / 16], dk[HD / 16];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int qs = 0; qs < LP; qs += 32) {
+    F pf, sf;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, tp = st;
+      const T* aq = Qs + (qs + 16 * u + kl) * LDT + g * 8;
+      const T* ao = Os + (qs + 16 * u + kl) * LDT + g * 8;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        st = Op::mma(Op::ld(aq + k * 32), kf[k], st);   // S[q][key]
+        tp = Op::mma(Op::ld(ao + k * 32), vf[k], tp);   // dP'[q][key]
+      }
+      const int qr0 = qs + 16 * u + g * 4;
+      const f32x4 lq = *(const f32x4*)(ls + qr0);
+      const f32x4 dq = *(const f32x4*)(ds_ + qr0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qr0 + r;
+        const float p = __expf(st[r] * scale + mk - lq[r]);
+        bool keep = true;
+        if (drop) {
+          const float uu =
+              (attn_hash64(rbase + (uint64_t)qq * L + key) >> 8) * (1.f / 16777216.f);
+          keep = uu >= p_drop;
+        }
+        const float dp = keep ? tp[r] * keep_scale : 0.f;
+        pf[u * 4 + r] = from_f<T>(keep ? p * keep_scale : 0.f);
+        sf[u * 4 + r] = from_f<T>(p * (dp - dq[r]));
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const F of = join_frag<T>(tr_read4(Os, qs + g * 4, dt * 16),
+                                tr_read4(Os, qs + 16 + g * 4, dt * 16));
+      dv[dt] = Op::mma(of, pf, dv[dt]);
+      const F qf = join_frag<T>(tr_read4(Qs, qs + g * 4, dt * 16),
+                                tr_read4(Qs, qs + 16 + g * 4, dt * 16));
+      dk[dt] = Op::mma(qf, sf, dk[dt]);
+    }
+  }
+  if (kok) {
+    T* row = dqkv + ((long)b * L + key) * 3 * H * HD + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      store4<T>(row + (long)H * HD + dt * 16 + g * 4, dk[dt][0] * scale, dk[dt][1] * scale,
+                dk[dt][2] * scale, dk[dt][3] * scale);
+      store4<T>(row + 2L * H * HD + dt * 16 + g * 4, dv[dt][0], dv[dt][1], dv[dt][2],
+                dv[dt][3]);
+    }
+  }
+}
+
 static size_t smem16(int L, int nw) {
   const size_t LP = (L + 31) & ~31;
   return LP * (LDR + LDT) * 2 + (LP + (size_t)nw * 16 * LDP) * sizeof(float);
@@ -926,7 +1143,8 @@ extern "C" int mmdx_attention_fwd_ex(int dtype, const void* qkv, const int64_t* 
         const int qb = nw * 16;
         hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
                            (const T*)qkv, mask, bias, causal, L, H, scale, p_drop, seed,
-                           (const uint64_t*)counter, (T*)out, probs);
+                           (const uint64_t*)counter, (T*)out, probs, (float*)nullptr,
+                           (uint64_t*)nullptr);
       };
       if (fwd16_nw() == 8) launch(attn_fwd16_kernel<T, 8>, 8);
       else launch(attn_fwd16_kernel<T, 4>, 4);
@@ -993,6 +1211,73 @@ extern "C" int mmdx_attention_bwd(int dtype, const void* qkv, const float* probs
       hipLaunchKernelGGL(kv16, dim3((L + 127) / 128 * H * B), dim3(512),
                          sm, st, (const T*)qkv, probs, (const T*)dout, (const T*)ws, L, H,
                          scale, keep_scale, (T*)dqkv);
+    }
+  });
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_attention_fwd_lse(int dtype, const void* qkv, const int64_t* mask, int B,
+                                      int L, int H, float scale, float p_drop, uint64_t seed,
+                                      uint64_t* counter, void* out, float* lse, uint64_t* rng,
+                                      void* stream) {
+  MMDX_CHECK_ARG(dtype != F32, "attention (lse): 16-bit compute dtypes only");
+  MMDX_CHECK_ARG(B > 0 && H > 0 && L > 0 && L <= 16 * MAXKT, "attention: L=%d > 256", L);
+  MMDX_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f && lse && rng,
+                 "attention (lse): bad dropout p=%g or missing lse / rng", (double)p_drop);
+  hipStream_t st = (hipStream_t)stream;
+  MMDX_DISPATCH(dtype, {
+    if constexpr (!std::is_same<T, float>::value) {
+      auto launch = [&](auto kern, int nw) {
+        const size_t sm = smem16(L, nw);
+        mmdx_lds_max_once((const void*)kern);
+        const int qb = nw * 16;
+        hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
+                           (const T*)qkv, mask, (const float*)nullptr, 0, L, H, scale, p_drop,
+                           seed, (const uint64_t*)counter, (T*)out, (float*)nullptr, lse, rng);
+      };
+      if (fwd16_nw() == 8) launch(attn_fwd16_kernel<T, 8>, 8);
+      else launch(attn_fwd16_kernel<T, 4>, 4);
+    }
+  });
+  if (p_drop > 0.f && counter)
+    hipLaunchKernelGGL(attn_counter_incr_kernel, dim3(1), dim3(1), 0, st, counter);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t mmdx_attention_lse_workspace_size(int dtype, int B, int L, int H) {
+  (void)dtype;
+  return (size_t)B * H * L * sizeof(float);   // D = rowsum(dO o O)
+}
+
+extern "C" int mmdx_attention_bwd_lse(int dtype, const void* qkv, const void* out,
+                                      const float* lse, const uint64_t* rng, const void* dout,
+                                      const int64_t* mask, int B, int L, int H, float scale,
+                                      float p_drop, void* dqkv, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  MMDX_CHECK_ARG(dtype != F32, "attention bwd (lse): 16-bit compute dtypes only");
+  MMDX_CHECK_ARG(B > 0 && H > 0 && L > 0 && L <= 16 * MAXKT && lse && rng && out &&
+                     p_drop >= 0.f && p_drop < 1.f,
+                 "attention bwd (lse): bad args");
+  MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_attention_lse_workspace_size(dtype, B, L, H),
+                 "attention bwd (lse): workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int LP = (L + 31) & ~31;
+  MMDX_DISPATCH(dtype, {
+    if constexpr (!std::is_same<T, float>::value) {
+      const size_t sma = (size_t)LP * (LDR + LDT) * sizeof(T) + (size_t)LP * sizeof(float);
+      auto qk = attn_bwd_q16_lse_kernel<T, 8>;
+      mmdx_lds_max_once((const void*)qk);
+      hipLaunchKernelGGL(qk, dim3((L + 127) / 128 * H * B), dim3(512), sma, st, (const T*)qkv,
+                         (const T*)out, lse, rng, (const T*)dout, mask, L, H, scale, p_drop,
+                         (float*)ws, (T*)dqkv);
+      const size_t smb = (size_t)LP * LDT * 2 * sizeof(T) + (size_t)LP * 2 * sizeof(float);
+      auto kv = attn_bwd_kv16_lse_kernel<T, 8>;
+      mmdx_lds_max_once((const void*)kv);
+      hipLaunchKernelGGL(kv, dim3((L + 127) / 128 * H * B), dim3(512), smb, st, (const T*)qkv,
+                         lse, rng, (const T*)dout, mask, (const float*)ws, L, H, scale, p_drop,
+                         (T*)dqkv);
     }
   });
   MMDX_LAUNCH_CHECK();

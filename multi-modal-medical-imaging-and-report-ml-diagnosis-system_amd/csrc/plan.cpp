@@ -165,6 +165,18 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
       return mmdx_attention_bwd(o.dtype, P(o, 0, ext), (const float*)P(o, 1, ext), P(o, 2, ext),
                                 (const int64_t*)P(o, 3, ext), o.i[0], o.i[1], o.i[2], o.f[0],
                                 o.f[1], P(o, 4, ext), P(o, 5, ext), (size_t)o.l[0], s);
+    case MMDX_OP_ATTN_FWD_LSE:
+      // i: B, L, H; f: scale, p_drop; l: seed; p: qkv, mask, counter, out, lse, rng
+      return mmdx_attention_fwd_lse(o.dtype, P(o, 0, ext), (const int64_t*)P(o, 1, ext), o.i[0],
+                                    o.i[1], o.i[2], o.f[0], o.f[1], (uint64_t)o.l[0],
+                                    (uint64_t*)P(o, 2, ext), P(o, 3, ext), (float*)P(o, 4, ext),
+                                    (uint64_t*)P(o, 5, ext), s);
+    case MMDX_OP_ATTN_BWD_LSE:
+      // i: B, L, H; f: scale, p_drop; l: ws_bytes; p: qkv, out, lse, rng, dout, mask, dqkv, ws
+      return mmdx_attention_bwd_lse(o.dtype, P(o, 0, ext), P(o, 1, ext), (const float*)P(o, 2, ext),
+                                    (const uint64_t*)P(o, 3, ext), P(o, 4, ext),
+                                    (const int64_t*)P(o, 5, ext), o.i[0], o.i[1], o.i[2], o.f[0],
+                                    o.f[1], P(o, 6, ext), P(o, 7, ext), (size_t)o.l[0], s);
     case MMDX_OP_LN_FWD:
       // i: D; l: rows; f: eps; p: x, residual, gamma, beta, y, sum_out, mean, rstd
       return mmdx_layernorm_fwd(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],

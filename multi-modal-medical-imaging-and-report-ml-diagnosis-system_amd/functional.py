@@ -7,6 +7,8 @@ compute dtype of activations is fp32 (parity path) or bf16 (throughput path).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -31,6 +33,48 @@ class _NoTimer:
 
 # bench.py installs a HIP-event timer here to measure the dense GEMM launches (C5 roofline).
 GEMM_TIMER = _NoTimer()
+
+
+def attn_flash(T) -> bool:
+    """The flash-style attention path (mmdx_attention_fwd_lse / _bwd_lse: row log-sum-exp
+    saved, P recomputed in the backward) for the 16-bit compute dtypes; MMDX_ATTN_FLASH=0
+    saves P [B,H,L,L] fp32 instead (the previous path, kept for A/B runs)."""
+    return T != torch.float32 and os.environ.get("MMDX_ATTN_FLASH", "1") != "0"
+
+
+def attention_fwd(qkv, mask, B, Ls, H, scale, p_drop, seed, counter, out, keep):
+    """Self-attention forward of the eager per-layer nodes (BERT, ViT): returns what
+    attention_bwd needs besides qkv / out — (lse, rng) on the flash-style path, (probs,)
+    otherwise ((None,) when nothing is kept for a backward)."""
+    T = qkv.dtype
+    dev = qkv.device
+    if keep and attn_flash(T):
+        lse = torch.empty((B, H, Ls), dtype=torch.float32, device=dev)
+        rng = torch.empty(1, dtype=torch.int64, device=dev)
+        call("mmdx_attention_fwd_lse", L.dtype_code(T), ptr(qkv), ptr(mask), B, Ls, H,
+             float(scale), float(p_drop), seed, ptr(counter), ptr(out), ptr(lse), ptr(rng),
+             stream())
+        return (lse, rng)
+    probs = torch.empty((B, H, Ls, Ls), dtype=torch.float32, device=dev) if keep else None
+    call("mmdx_attention_fwd", L.dtype_code(T), ptr(qkv), ptr(mask), B, Ls, H, float(scale),
+         float(p_drop), seed, ptr(counter), ptr(out), ptr(probs), stream())
+    return (probs,)
+
+
+def attention_bwd(qkv, saved, out, dout, mask, B, Ls, H, scale, p_drop, dqkv):
+    T = qkv.dtype
+    dc = L.dtype_code(T)
+    if len(saved) == 2:
+        n = L.lib().mmdx_attention_lse_workspace_size(dc, B, Ls, H)
+        w = torch.empty(max(1, n), dtype=torch.uint8, device=qkv.device)
+        call("mmdx_attention_bwd_lse", dc, ptr(qkv), ptr(out), ptr(saved[0]), ptr(saved[1]),
+             ptr(dout), ptr(mask), B, Ls, H, float(scale), float(p_drop), ptr(dqkv), ptr(w), n,
+             stream())
+        return
+    n = L.lib().mmdx_attention_workspace_size(dc, B, Ls, H)
+    w = torch.empty(max(1, n), dtype=torch.uint8, device=qkv.device)
+    call("mmdx_attention_bwd", dc, ptr(qkv), ptr(saved[0]), ptr(dout), ptr(mask), B, Ls, H,
+         float(scale), float(p_drop), ptr(dqkv), ptr(w), n, stream())
 
 
 def gemm_cost(M, N, K, dt, c_dt, beta=0.0, act=L.ACT_NONE, preact=None):

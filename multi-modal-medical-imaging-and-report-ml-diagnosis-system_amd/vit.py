@@ -133,11 +133,9 @@ class _VitBlockFn(torch.autograd.Function):
         qkv = torch.empty((M, 3 * D), dtype=T, device=dev)
         F.gemm(u1, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, bias=b_in, compute_dtype=T)
         keep = any(ctx.needs_input_grad)
-        probs = torch.empty((N, heads, S, S), dtype=torch.float32, device=dev) if keep else None
         scale = 1.0 / math.sqrt(D // heads)
         att = torch.empty((M, D), dtype=T, device=dev)
-        call("mmdx_attention_fwd", L.dtype_code(T), ptr(qkv), None, N, S, heads, float(scale),
-             0.0, 0, None, ptr(att), ptr(probs), stream())
+        ctx.attn = F.attention_fwd(qkv, None, N, S, heads, scale, 0.0, 0, None, att, keep)
         woc = F.cast(w_out, T)
         o = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(att, D, True, woc, D, True, M, D, D, o, D, bias=b_out, compute_dtype=T)
@@ -152,14 +150,14 @@ class _VitBlockFn(torch.autograd.Function):
         out = _copy(a)  # out = a + f W2^T + b2 (residual accumulated in the GEMM epilogue)
         F.gemm(f, I, True, w2c, I, True, M, D, I, out, D, bias=bb2, beta=1.0, compute_dtype=T)
         if keep:
-            ctx.save_for_backward(x, u1, mu1, rs1, g1, wqkv, qkv, probs, att, woc, a, u2, mu2,
+            ctx.save_for_backward(x, u1, mu1, rs1, g1, wqkv, qkv, att, woc, a, u2, mu2,
                                   rs2, g2, w1c, pre, f, w2c)
         ctx.dims = (N, S, D, I, heads, scale)
         return out.reshape(N, S, D)
 
     @staticmethod
     def backward(ctx, dout):
-        (x, u1, mu1, rs1, g1, wqkv, qkv, probs, att, woc, a, u2, mu2, rs2, g2, w1c, pre, f,
+        (x, u1, mu1, rs1, g1, wqkv, qkv, att, woc, a, u2, mu2, rs2, g2, w1c, pre, f,
          w2c) = ctx.saved_tensors
         N, S, D, I, heads, scale = ctx.dims
         T = x.dtype
@@ -186,10 +184,7 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm(da, D, False, att, D, False, D, D, M, dWo, D, compute_dtype=T)
         dbo = _colsum(da, M, D)
         dqkv = torch.empty((M, 3 * D), dtype=T, device=dev)
-        n = L.lib().mmdx_attention_workspace_size(L.dtype_code(T), N, S, heads)
-        w = L.workspace(n, dev)
-        call("mmdx_attention_bwd", L.dtype_code(T), ptr(qkv), ptr(probs), ptr(datt), None, N, S,
-             heads, float(scale), 0.0, ptr(dqkv), ptr(w), n, stream())
+        F.attention_bwd(qkv, ctx.attn, att, datt, None, N, S, heads, scale, 0.0, dqkv)
         dWqkv = torch.empty((3 * D, D), dtype=torch.float32, device=dev)
         F.gemm(dqkv, 3 * D, False, u1, D, False, 3 * D, D, M, dWqkv, D, compute_dtype=T)
         dbqkv = _colsum(dqkv, M, 3 * D)

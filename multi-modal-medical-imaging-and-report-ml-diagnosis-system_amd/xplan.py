@@ -93,14 +93,28 @@ class _Rec:
                        l=(lda, ldb, ldc, n), f=(1.0, beta),
                        p=(A, B, C, bias, None, preact, self._ws(n)))
 
-    def attn_fwd(self, qkv, mask, B, Ls, H, scale, p_drop, seed, counter, out, probs):
+    def attn_fwd(self, qkv, mask, B, Ls, H, scale, p_drop, seed, counter, out):
+        """Returns what the backward needs besides qkv / out: the row log-sum-exp and the
+        dropout stream base (flash-style, 16-bit) or the saved probabilities [B,H,L,L]."""
+        if F.attn_flash(self.T):
+            lse, rng = self.buf((B, H, Ls), _F32), self.buf((1,), torch.int64)
+            self.ops.add(L.OP_ATTN_FWD_LSE, self.dt, i=(B, Ls, H), f=(scale, p_drop),
+                         l=(seed,), p=(qkv, mask, counter, out, lse, rng))
+            return ("lse", lse, rng)
+        probs = self.buf((B, H, Ls, Ls), _F32)
         self.ops.add(L.OP_ATTN_FWD, self.dt, i=(B, Ls, H), f=(scale, p_drop), l=(seed,),
                      p=(qkv, mask, counter, out, probs))
+        return ("probs", probs)
 
-    def attn_bwd(self, qkv, probs, dout, mask, B, Ls, H, scale, p_drop, dqkv):
+    def attn_bwd(self, qkv, saved, out, dout, mask, B, Ls, H, scale, p_drop, dqkv):
+        if saved[0] == "lse":
+            n = L.lib().mmdx_attention_lse_workspace_size(self.dt, B, Ls, H)
+            self.ops.add(L.OP_ATTN_BWD_LSE, self.dt, i=(B, Ls, H), f=(scale, p_drop), l=(n,),
+                         p=(qkv, out, saved[1], saved[2], dout, mask, dqkv, self._ws(n)))
+            return
         n = L.lib().mmdx_attention_workspace_size(self.dt, B, Ls, H)
         self.ops.add(L.OP_ATTN_BWD, self.dt, i=(B, Ls, H), f=(scale, p_drop), l=(n,),
-                     p=(qkv, probs, dout, mask, dqkv, self._ws(n)))
+                     p=(qkv, saved[1], dout, mask, dqkv, self._ws(n)))
 
     def ln_fwd(self, x, res, g, b, eps, rows, D, y, xsum, mean, rstd):
         self.ops.add(L.OP_LN_FWD, self.dt, i=(D,), l=(rows,), f=(eps,),
@@ -232,10 +246,9 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
             rf.axpby(D, 1.0, bb, 0.0, None, bqkv[j * D:(j + 1) * D])
         qkv = rf.buf((M, 3 * D))
         rf.gemm(x, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, T, bias=bqkv)
-        probs = rf.buf((B, Hn, Ls, Ls), _F32)
         att = rf.buf((M, D))
-        rf.attn_fwd(qkv, mask, B, Ls, Hn, scale, pa, _seed(0xA770 + 7919 * li) if pa > 0 else 0,
-                    counter, att, probs)
+        probs = rf.attn_fwd(qkv, mask, B, Ls, Hn, scale, pa,
+                            _seed(0xA770 + 7919 * li) if pa > 0 else 0, counter, att)
         woc = rf.buf((D, D))
         rf.cast_weight(wo, woc)
         a = rf.buf((M, D))
@@ -324,7 +337,7 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         rb.gemm(dY1, D, True, s["woc"], D, False, M, D, D, datt, D, T)
         rb.gemm(dY1, D, False, s["att"], D, False, D, D, M, gx(o["wo"]), D, _F32)
         rb.colsum(dY1, M, D, gx(o["bo"]))
-        rb.attn_bwd(s["qkv"], s["probs"], datt, mask, B, Ls, Hn, scale, pa, dqkv)
+        rb.attn_bwd(s["qkv"], s["probs"], s["att"], datt, mask, B, Ls, Hn, scale, pa, dqkv)
         xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)  # the stack input
         rb.gemm(dqkv, 3 * D, False, xin, D, False, 3 * D, D, M, gx(o["wqkv"]), D, _F32)
         rb.colsum(dqkv, M, 3 * D, gx(o["bqkv"]))
@@ -359,9 +372,8 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         rf.cast_weight(w_in, wqkv)
         qkv = rf.buf((M, 3 * D))
         rf.gemm(u1, D, True, wqkv, D, True, M, 3 * D, D, qkv, 3 * D, T, bias=b_in)
-        probs = rf.buf((N, heads, S, S), _F32)
         att = rf.buf((M, D))
-        rf.attn_fwd(qkv, None, N, S, heads, scale, 0.0, 0, None, att, probs)
+        probs = rf.attn_fwd(qkv, None, N, S, heads, scale, 0.0, 0, None, att)
         woc = rf.buf((D, D))
         rf.cast_weight(w_out, woc)
         o_ = rf.buf((M, D))
@@ -417,7 +429,7 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         rb.gemm(DA, D, True, s["woc"], D, False, M, D, D, datt, D, T)
         rb.gemm(DA, D, False, s["att"], D, False, D, D, M, gx(o[4]), D, _F32)
         rb.colsum(DA, M, D, gx(o[5]))
-        rb.attn_bwd(s["qkv"], s["probs"], datt, None, N, S, heads, scale, 0.0, dqkv)
+        rb.attn_bwd(s["qkv"], s["probs"], s["att"], datt, None, N, S, heads, scale, 0.0, dqkv)
         rb.gemm(dqkv, 3 * D, False, s["u1"], D, False, 3 * D, D, M, gx(o[2]), D, _F32)
         rb.colsum(dqkv, M, 3 * D, gx(o[3]))
         rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, du1, D, T)
