@@ -264,7 +264,8 @@ enum {
   /* transformer layer stacks (BERT / ViT encoders, one plan per stack and direction) */
   MMDX_OP_GEMM, MMDX_OP_ATTN_FWD, MMDX_OP_ATTN_BWD, MMDX_OP_LN_FWD, MMDX_OP_LN_BWD,
   MMDX_OP_GELU_BWD, MMDX_OP_BIAS_GRAD, MMDX_OP_ADD, MMDX_OP_DROPOUT_FWD, MMDX_OP_DROPOUT_BWD,
-  MMDX_OP_AXPBY, MMDX_OP_ATTN_FWD_LSE, MMDX_OP_ATTN_BWD_LSE
+  MMDX_OP_AXPBY, MMDX_OP_ATTN_FWD_LSE, MMDX_OP_ATTN_BWD_LSE, MMDX_OP_LN_FWD_DROP,
+  MMDX_OP_LN_BWD_DROP
 };
 typedef struct {
   int op, dtype, stream;
@@ -365,6 +366,24 @@ int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, long rows, i
                        void* dx, float* dgamma, float* dbeta, float beta_acc,
                        void* workspace, size_t ws_bytes, void* stream);
 size_t mmdx_layernorm_workspace_size(long rows, int D);
+/* LayerNorm(dropout(x) + residual) in one pass (BertSelfOutput / BertOutput in train mode):
+ * element e of x is kept with the keep bit mmdx_dropout_fwd would draw for it (seed,
+ * *counter), scaled by 1/(1-p) and rounded to dtype as that kernel stores it, so the outputs
+ * are bit-identical to mmdx_dropout_fwd + mmdx_layernorm_fwd with neither the dropped tensor
+ * nor its mask written.  rng[0] (device uint64) receives the stream base for the backward;
+ * counter (may be NULL) is incremented after the launch.
+ * Replaces: BertSelfOutput.dropout + LayerNorm, BertOutput.dropout + LayerNorm (TP:360). */
+int mmdx_layernorm_fwd_dropout(int dtype, const void* x, const void* residual, long rows,
+                               int D, const float* gamma, const float* beta, float eps, float p,
+                               uint64_t seed, uint64_t* counter, void* y, void* sum_out,
+                               float* save_mean, float* save_rstd, uint64_t* rng, void* stream);
+/* mmdx_layernorm_bwd plus dx_drop = the dropout backward of dx with the keep bits of rng[0]
+ * (bit-identical to mmdx_dropout_bwd on dx and the forward's mask). */
+int mmdx_layernorm_bwd_dropout(int dtype, const void* xsum, const void* dy, long rows, int D,
+                               const float* gamma, const float* save_mean,
+                               const float* save_rstd, float p, const uint64_t* rng, void* dx,
+                               void* dx_drop, float* dgamma, float* dbeta, float beta_acc,
+                               void* workspace, size_t ws_bytes, void* stream);
 /* GELU backward from the pre-activation: dx = dy * gelu'(pre) */
 int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n, void* dx,
                   void* stream);

@@ -71,6 +71,37 @@ def _ln_fwd(x, res, gamma, beta, eps):
     return y, xs, mean, rstd
 
 
+def _ln_fwd_drop(x, res, gamma, beta, eps, p, seed):
+    """LayerNorm(dropout(x) + res) in one pass; returns (y, xsum, mean, rstd, rng)."""
+    D = x.shape[-1]
+    rows = x.numel() // D
+    y = torch.empty_like(x)
+    xs = torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rng = torch.empty(1, dtype=torch.int64, device=x.device)
+    call("mmdx_layernorm_fwd_dropout", L.dtype_code(x.dtype), ptr(x), ptr(res), rows, D,
+         ptr(gamma), ptr(beta), float(eps), float(p), L.dropout_seed(seed),
+         ptr(L.rng_counter(x.device)), ptr(y), ptr(xs), ptr(mean), ptr(rstd), ptr(rng), stream())
+    return y, xs, mean, rstd, rng
+
+
+def _ln_bwd_drop(xs, dy, gamma, mean, rstd, p, rng):
+    """(d xsum, its dropout backward, dgamma, dbeta)."""
+    D = xs.shape[-1]
+    rows = xs.numel() // D
+    dx = torch.empty_like(xs)
+    dxd = torch.empty_like(xs)
+    dg = torch.empty(D, dtype=torch.float32, device=xs.device)
+    db = torch.empty(D, dtype=torch.float32, device=xs.device)
+    n = L.lib().mmdx_layernorm_workspace_size(rows, D)
+    w = _ws(n, xs.device)
+    call("mmdx_layernorm_bwd_dropout", L.dtype_code(xs.dtype), ptr(xs), ptr(dy), rows, D,
+         ptr(gamma), ptr(mean), ptr(rstd), float(p), ptr(rng), ptr(dx), ptr(dxd), ptr(dg),
+         ptr(db), 0.0, ptr(w), n, stream())
+    return dx, dxd, dg, db
+
+
 def _dropout_fwd(x, p, seed):
     y = torch.empty_like(x)
     m = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
@@ -122,10 +153,11 @@ class _BertLayerFn(torch.autograd.Function):
         a = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(att, D, True, woc, D, True, M, D, D, a, D, bias=bo, compute_dtype=T)
         m1 = None
-        if p > 0 and cfg.training:
+        if p > 0 and cfg.training:   # dropout inside the LayerNorm pass (keep bits in m1)
             _SEED[0] += 1
-            a, m1 = _dropout_fwd(a, p, _SEED[0])
-        h1, xs1, mu1, rs1 = _ln_fwd(a, x, g1, b1, eps)
+            h1, xs1, mu1, rs1, m1 = _ln_fwd_drop(a, x, g1, b1, eps, p, _SEED[0])
+        else:
+            h1, xs1, mu1, rs1 = _ln_fwd(a, x, g1, b1, eps)
         wic = F.cast(wi, T)
         I = wi.shape[0]
         f = torch.empty((M, I), dtype=T, device=dev)
@@ -138,8 +170,9 @@ class _BertLayerFn(torch.autograd.Function):
         m2 = None
         if p > 0 and cfg.training:
             _SEED[0] += 1
-            f2, m2 = _dropout_fwd(f2, p, _SEED[0])
-        h2, xs2, mu2, rs2 = _ln_fwd(f2, h1, g2, b2, eps)
+            h2, xs2, mu2, rs2, m2 = _ln_fwd_drop(f2, h1, g2, b2, eps, p, _SEED[0])
+        else:
+            h2, xs2, mu2, rs2 = _ln_fwd(f2, h1, g2, b2, eps)
         ctx.save_for_backward(x, mask, wqkv, qkv, att, woc, xs1, mu1, rs1, g1, h1, wic,
                               pre, f, wo2c, xs2, mu2, rs2, g2)
         ctx.m1, ctx.m2, ctx.p, ctx.pa = m1, m2, p, pa
@@ -156,8 +189,11 @@ class _BertLayerFn(torch.autograd.Function):
         M = B * Ls
         dh2 = F.cast(dh2.contiguous().reshape(M, D), T)
         # LN2: X = d(f2 + h1)
-        X, dg2, db2 = _ln_bwd(xs2, dh2, g2, mu2, rs2)
-        dX2 = _dropout_bwd(X, ctx.m2, ctx.p) if ctx.m2 is not None else X
+        if ctx.m2 is not None:
+            X, dX2, dg2, db2 = _ln_bwd_drop(xs2, dh2, g2, mu2, rs2, ctx.p, ctx.m2)
+        else:
+            X, dg2, db2 = _ln_bwd(xs2, dh2, g2, mu2, rs2)
+            dX2 = X
         # FFN down: f2 = f Wo2^T + bo2
         # dpre = (dX2 Wo2) * gelu'(pre): the GELU backward in the GEMM epilogue
         dpre = torch.empty((M, I), dtype=T, device=dev)
@@ -172,8 +208,11 @@ class _BertLayerFn(torch.autograd.Function):
         # X := dpre Wi + X  (residual into h1)
         F.gemm(dpre, I, True, wic, D, False, M, D, I, X, D, beta=1.0, compute_dtype=T)
         # LN1: Y = d(a + x)
-        Y, dg1, db1 = _ln_bwd(xs1, X, g1, mu1, rs1)
-        dY1 = _dropout_bwd(Y, ctx.m1, ctx.p) if ctx.m1 is not None else Y
+        if ctx.m1 is not None:
+            Y, dY1, dg1, db1 = _ln_bwd_drop(xs1, X, g1, mu1, rs1, ctx.p, ctx.m1)
+        else:
+            Y, dg1, db1 = _ln_bwd(xs1, X, g1, mu1, rs1)
+            dY1 = Y
         datt = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dY1, D, True, woc, D, False, M, D, D, datt, D, compute_dtype=T)
         dWo = torch.empty((D, D), dtype=torch.float32, device=dev)

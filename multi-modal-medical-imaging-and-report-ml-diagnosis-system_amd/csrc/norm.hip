@@ -555,17 +555,42 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
 // One wave per row; D <= 64 * LN_MAXV * VEC handled from registers (two-pass stats).
 constexpr int LN_MAXV = 4;
 
-template <typename T>
+// Dropout on the x input (DROP; BertSelfOutput / BertOutput: LayerNorm(dropout(dense) + res)):
+// element e = row * D + c of x is kept when hash(base + e) >= p, base = seed * phi +
+// (counter << 32) as mmdx_dropout_fwd draws it, and the kept value is rounded to T after the
+// 1 / (1 - p) scale as that kernel stores it — so the normalised rows are bit-identical to
+// mmdx_dropout_fwd followed by mmdx_layernorm_fwd, without the dropped tensor or its mask.
+__device__ __forceinline__ uint32_t ln_drop_hash(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ bool ln_keep(uint64_t base, long e, float p) {
+  return (ln_drop_hash(base + (uint64_t)e) >> 8) * (1.f / 16777216.f) >= p;
+}
+
+template <typename T, bool DROP = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
                                                      const T* __restrict__ res, long rows, int D,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
                                                      T* __restrict__ y, T* __restrict__ xsum,
-                                                     float* smean, float* srstd) {
+                                                     float* smean, float* srstd, float p = 0.f,
+                                                     uint64_t seed = 0,
+                                                     const uint64_t* __restrict__ ctr = nullptr,
+                                                     uint64_t* __restrict__ rng_out = nullptr) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   const int lane = threadIdx.x & 63;
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  uint64_t dbase = 0;
+  float dscale = 1.f;
+  if constexpr (DROP) {
+    dbase = seed * 0x9E3779B97F4A7C15ULL + (ctr ? ctr[0] << 32 : 0ull);
+    dscale = 1.f / (1.f - p);
+    if (rng_out && blockIdx.x == 0 && threadIdx.x == 0) rng_out[0] = dbase;
+  }
   if (row >= rows) return;
   const int nv = D / VEC;
   float v[LN_MAXV][VEC];
@@ -579,7 +604,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
       if (res) b = *(const V*)(res + row * D + vi * VEC);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        v[i][j] = to_f(a[j]) + (res ? to_f(b[j]) : 0.f);
+        float av = to_f(a[j]);
+        if constexpr (DROP)
+          av = to_f(from_f<T>(ln_keep(dbase, row * D + vi * VEC + j, p) ? av * dscale : 0.f));
+        v[i][j] = av + (res ? to_f(b[j]) : 0.f);
         s += v[i][j];
       }
       if (xsum) {
@@ -636,14 +664,19 @@ static int ln_bwd_rpw() {   // MMDX_LN_BWD_RPW = 4 | 8 (default 8)
 // dx per row; per-block partial dgamma/dbeta -> part[blk][2][D]
 // MV: 16-B vectors per lane (ceil(D / VEC / 64)), a template argument so the register arrays
 // are sized for D (MV everywhere held 194 VGPRs at D = 768: two waves per SIMD)
-template <typename T, int MV>
+// DROP: dx_drop = dropout's backward of the stored dx (the same keep bits from rng[0], the
+// base the forward left): mmdx_dropout_bwd's result, bit for bit, without the mask tensor.
+template <typename T, int MV, bool DROP = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
                                                      const T* __restrict__ dy, long rows, int D,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ smean,
                                                      const float* __restrict__ srstd,
                                                      T* __restrict__ dx,
-                                                     float* __restrict__ part, int rpw) {
+                                                     float* __restrict__ part, int rpw,
+                                                     float p = 0.f,
+                                                     const uint64_t* __restrict__ rng = nullptr,
+                                                     T* __restrict__ dx_drop = nullptr) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2][D]
@@ -712,6 +745,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
 #pragma unroll
         for (int j = 0; j < VEC; ++j) o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2));
         *(V*)(dx + row * D + vi * VEC) = o;
+        if constexpr (DROP) {
+          const uint64_t dbase = rng[0];
+          const float dscale = 1.f / (1.f - p);
+          V od;
+#pragma unroll
+          for (int j = 0; j < VEC; ++j)
+            od[j] = from_f<T>(ln_keep(dbase, row * D + vi * VEC + j, p) ? to_f(o[j]) * dscale
+                                                                         : 0.f);
+          *(V*)(dx_drop + row * D + vi * VEC) = od;
+        }
       }
     }
   }
@@ -901,15 +944,40 @@ extern "C" int mmdx_layernorm_fwd(int dtype, const void* x, const void* residual
   return 0;
 }
 
+__global__ void ln_counter_incr_kernel(uint64_t* c) { c[0] += 1; }
+
+extern "C" int mmdx_layernorm_fwd_dropout(int dtype, const void* x, const void* residual,
+                                          long rows, int D, const float* gamma,
+                                          const float* beta, float eps, float p, uint64_t seed,
+                                          uint64_t* counter, void* y, void* sum_out,
+                                          float* save_mean, float* save_rstd, uint64_t* rng,
+                                          void* stream) {
+  const int VEC = dtype == F32 ? 4 : 8;
+  MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC && gamma && beta,
+                 "layernorm: D=%d unsupported", D);
+  MMDX_CHECK_ARG(p >= 0.f && p < 1.f && rng, "layernorm dropout: p=%g / rng", (double)p);
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (int)((rows + 3) / 4);
+  MMDX_DISPATCH(dtype, hipLaunchKernelGGL((ln_fwd_kernel<T, true>), dim3(blocks), dim3(256), 0,
+                                          st, (const T*)x, (const T*)residual, rows, D, gamma,
+                                          beta, eps, (T*)y, (T*)sum_out, save_mean, save_rstd, p,
+                                          seed, (const uint64_t*)counter, rng));
+  if (counter)
+    hipLaunchKernelGGL(ln_counter_incr_kernel, dim3(1), dim3(1), 0, st, counter);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" size_t mmdx_layernorm_workspace_size(long rows, int D) {
   const long nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   return (size_t)nblk * 2 * D * sizeof(float);
 }
 
-extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, long rows, int D,
-                                  const float* gamma, const float* save_mean,
-                                  const float* save_rstd, void* dx, float* dgamma, float* dbeta,
-                                  float beta_acc, void* ws, size_t ws_bytes, void* stream) {
+static int layernorm_bwd_t(int dtype, const void* xsum, const void* dy, long rows, int D,
+                           const float* gamma, const float* save_mean, const float* save_rstd,
+                           void* dx, float* dgamma, float* dbeta, float beta_acc, void* ws,
+                           size_t ws_bytes, float p, const uint64_t* rng, void* dx_drop,
+                           void* stream) {
   const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC, "layernorm bwd: D=%d", D);
   const int rpw = ln_bwd_rpw();
@@ -919,19 +987,47 @@ extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, l
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = 8 * (size_t)D * sizeof(float);
   const int mv = (D / VEC + 63) / 64;
+  const bool drop = dx_drop != nullptr;
   MMDX_DISPATCH(dtype, {
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), shm, st, (const T*)xsum, (const T*)dy,
-                         rows, D, gamma, save_mean, save_rstd, (T*)dx, (float*)ws, rpw);
+                         rows, D, gamma, save_mean, save_rstd, (T*)dx, (float*)ws, rpw, p, rng,
+                         (T*)dx_drop);
     };
-    if (mv == 1) launch(ln_bwd_kernel<T, 1>);
-    else if (mv == 2) launch(ln_bwd_kernel<T, 2>);
-    else if (mv == 3) launch(ln_bwd_kernel<T, 3>);
-    else launch(ln_bwd_kernel<T, 4>);
+    if (drop) {
+      if (mv == 1) launch(ln_bwd_kernel<T, 1, true>);
+      else if (mv == 2) launch(ln_bwd_kernel<T, 2, true>);
+      else if (mv == 3) launch(ln_bwd_kernel<T, 3, true>);
+      else launch(ln_bwd_kernel<T, 4, true>);
+    } else {
+      if (mv == 1) launch(ln_bwd_kernel<T, 1>);
+      else if (mv == 2) launch(ln_bwd_kernel<T, 2>);
+      else if (mv == 3) launch(ln_bwd_kernel<T, 3>);
+      else launch(ln_bwd_kernel<T, 4>);
+    }
   });
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 31) / 32, 2), dim3(32 * LN_FIN_LANES), 0,
                      st,
                      (const float*)ws, (int)nblk, D, dgamma, dbeta, beta_acc);
   MMDX_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, long rows, int D,
+                                  const float* gamma, const float* save_mean,
+                                  const float* save_rstd, void* dx, float* dgamma, float* dbeta,
+                                  float beta_acc, void* ws, size_t ws_bytes, void* stream) {
+  return layernorm_bwd_t(dtype, xsum, dy, rows, D, gamma, save_mean, save_rstd, dx, dgamma,
+                         dbeta, beta_acc, ws, ws_bytes, 0.f, nullptr, nullptr, stream);
+}
+
+extern "C" int mmdx_layernorm_bwd_dropout(int dtype, const void* xsum, const void* dy, long rows,
+                                          int D, const float* gamma, const float* save_mean,
+                                          const float* save_rstd, float p, const uint64_t* rng,
+                                          void* dx, void* dx_drop, float* dgamma, float* dbeta,
+                                          float beta_acc, void* ws, size_t ws_bytes,
+                                          void* stream) {
+  MMDX_CHECK_ARG(p >= 0.f && p < 1.f && rng && dx_drop, "layernorm bwd dropout: bad args");
+  return layernorm_bwd_t(dtype, xsum, dy, rows, D, gamma, save_mean, save_rstd, dx, dgamma,
+                         dbeta, beta_acc, ws, ws_bytes, p, rng, dx_drop, stream);
 }

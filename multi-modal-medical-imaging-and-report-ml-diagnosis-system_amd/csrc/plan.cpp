@@ -190,6 +190,23 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                                 (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
                                 (const float*)P(o, 4, ext), P(o, 5, ext), (float*)P(o, 6, ext),
                                 (float*)P(o, 7, ext), o.f[0], P(o, 8, ext), (size_t)o.l[1], s);
+    case MMDX_OP_LN_FWD_DROP:
+      // i: D; l: rows, seed; f: eps, p; p: x, residual, gamma, beta, y, sum_out, mean, rstd,
+      // counter, rng
+      return mmdx_layernorm_fwd_dropout(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
+                                        (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
+                                        o.f[0], o.f[1], (uint64_t)o.l[1], (uint64_t*)P(o, 8, ext),
+                                        P(o, 4, ext), P(o, 5, ext), (float*)P(o, 6, ext),
+                                        (float*)P(o, 7, ext), (uint64_t*)P(o, 9, ext), s);
+    case MMDX_OP_LN_BWD_DROP:
+      // i: D; l: rows, ws_bytes; f: beta_acc, p; p: xsum, dy, gamma, mean, rstd, dx, dgamma,
+      // dbeta, ws, rng, dx_drop
+      return mmdx_layernorm_bwd_dropout(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
+                                        (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
+                                        (const float*)P(o, 4, ext), o.f[1],
+                                        (const uint64_t*)P(o, 9, ext), P(o, 5, ext),
+                                        P(o, 10, ext), (float*)P(o, 6, ext), (float*)P(o, 7, ext),
+                                        o.f[0], P(o, 8, ext), (size_t)o.l[1], s);
     case MMDX_OP_GELU_BWD:  // l: n; p: pre, dy, dx
       return mmdx_gelu_bwd(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], P(o, 2, ext), s);
     case MMDX_OP_BIAS_GRAD:  // i: N; l: M, ws_bytes; f: beta_acc; p: dy, db, ws

@@ -120,6 +120,18 @@ class _Rec:
         self.ops.add(L.OP_LN_FWD, self.dt, i=(D,), l=(rows,), f=(eps,),
                      p=(x, res, g, b, y, xsum, mean, rstd))
 
+    def ln_fwd_drop(self, x, res, g, b, eps, p, seed, counter, rows, D, y, xsum, mean, rstd):
+        """LayerNorm(dropout(x) + res); returns the dropout stream base buffer (rng)."""
+        rng = self.buf((1,), torch.int64)
+        self.ops.add(L.OP_LN_FWD_DROP, self.dt, i=(D,), l=(rows, seed), f=(eps, p),
+                     p=(x, res, g, b, y, xsum, mean, rstd, counter, rng))
+        return rng
+
+    def ln_bwd_drop(self, xsum, dy, g, mean, rstd, p, rng, rows, D, dx, dx_drop, dg, db):
+        n = L.lib().mmdx_layernorm_workspace_size(rows, D)
+        self.ops.add(L.OP_LN_BWD_DROP, self.dt, i=(D,), l=(rows, n), f=(0.0, p),
+                     p=(xsum, dy, g, mean, rstd, dx, dg, db, self._ws(n), rng, dx_drop))
+
     def ln_bwd(self, xsum, dy, g, mean, rstd, rows, D, dx, dg, db):
         n = L.lib().mmdx_layernorm_workspace_size(rows, D)
         self.ops.add(L.OP_LN_BWD, self.dt, i=(D,), l=(rows, n), f=(0.0,),
@@ -253,14 +265,16 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         rf.cast_weight(wo, woc)
         a = rf.buf((M, D))
         rf.gemm(att, D, True, woc, D, True, M, D, D, a, D, T, bias=bo)
+        # BertSelfOutput: LayerNorm(dropout(a) + x), the dropout inside the LayerNorm pass
+        # (no dropped tensor, no mask: the backward redraws the keep bits from rng)
         m1 = None
-        if p > 0:
-            ad, m1 = rf.buf((M, D)), rf.buf((M, D), torch.uint8)
-            rf.dropout_fwd(a, M * D, p, _seed(0xD401 + 7919 * li), counter, ad, m1)
-            a = ad
         h1, xs1 = rf.buf((M, D)), rf.buf((M, D))
         mu1, rs1 = rf.buf((M,), _F32), rf.buf((M,), _F32)
-        rf.ln_fwd(a, x, g1, b1, eps, M, D, h1, xs1, mu1, rs1)
+        if p > 0:
+            m1 = rf.ln_fwd_drop(a, x, g1, b1, eps, p, _seed(0xD401 + 7919 * li), counter, M, D,
+                                h1, xs1, mu1, rs1)
+        else:
+            rf.ln_fwd(a, x, g1, b1, eps, M, D, h1, xs1, mu1, rs1)
         wic = rf.buf((I, D))
         rf.cast_weight(wi, wic)
         f, pre = rf.buf((M, I)), rf.buf((M, I))
@@ -271,13 +285,13 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         f2 = rf.buf((M, D))
         rf.gemm(f, I, True, wo2c, I, True, M, D, I, f2, D, T, bias=bo2)
         m2 = None
-        if p > 0:
-            fd, m2 = rf.buf((M, D)), rf.buf((M, D), torch.uint8)
-            rf.dropout_fwd(f2, M * D, p, _seed(0xD402 + 7919 * li), counter, fd, m2)
-            f2 = fd
         h2, xs2 = rf.buf((M, D)), rf.buf((M, D))
         mu2, rs2 = rf.buf((M,), _F32), rf.buf((M,), _F32)
-        rf.ln_fwd(f2, h1, g2, b2, eps, M, D, h2, xs2, mu2, rs2)
+        if p > 0:   # BertOutput: LayerNorm(dropout(f2) + h1)
+            m2 = rf.ln_fwd_drop(f2, h1, g2, b2, eps, p, _seed(0xD402 + 7919 * li), counter, M,
+                                D, h2, xs2, mu2, rs2)
+        else:
+            rf.ln_fwd(f2, h1, g2, b2, eps, M, D, h2, xs2, mu2, rs2)
         saves.append(dict(x=x, wqkv=wqkv, qkv=qkv, probs=probs, att=att, woc=woc, xs1=xs1,
                           mu1=mu1, rs1=rs1, h1=h1, wic=wic, pre=pre, f=f, wo2c=wo2c, xs2=xs2,
                           mu2=mu2, rs2=rs2, m1=m1, m2=m2))
@@ -317,11 +331,13 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         s, o = saves[li], offs[li]
         g1 = params[li * _BERT_NP + 8]
         g2 = params[li * _BERT_NP + 14]
-        rb.ln_bwd(s["xs2"], dh, g2, s["mu2"], s["rs2"], M, D, X, gx(o["g2"]), gx(o["b2"]))
         dX2 = X
         if p > 0:
-            rb.dropout_bwd(X, s["m2"], M * D, p, DX2)
+            rb.ln_bwd_drop(s["xs2"], dh, g2, s["mu2"], s["rs2"], p, s["m2"], M, D, X, DX2,
+                           gx(o["g2"]), gx(o["b2"]))
             dX2 = DX2
+        else:
+            rb.ln_bwd(s["xs2"], dh, g2, s["mu2"], s["rs2"], M, D, X, gx(o["g2"]), gx(o["b2"]))
         rb.gemm(dX2, D, True, s["wo2c"], I, False, M, I, D, dpre, I, T, act=L.ACT_GELU_BWD,
                 preact=s["pre"])
         rb.gemm(dX2, D, False, s["f"], I, False, D, I, M, gx(o["wo2"]), I, _F32)
@@ -329,11 +345,13 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         rb.gemm(dpre, I, False, s["h1"], D, False, I, D, M, gx(o["wi"]), D, _F32)
         rb.colsum(dpre, M, I, gx(o["bi"]))
         rb.gemm(dpre, I, True, s["wic"], D, False, M, D, I, X, D, T, beta=1.0)
-        rb.ln_bwd(s["xs1"], X, g1, s["mu1"], s["rs1"], M, D, Y, gx(o["g1"]), gx(o["b1"]))
         dY1 = Y
         if p > 0:
-            rb.dropout_bwd(Y, s["m1"], M * D, p, DY1)
+            rb.ln_bwd_drop(s["xs1"], X, g1, s["mu1"], s["rs1"], p, s["m1"], M, D, Y, DY1,
+                           gx(o["g1"]), gx(o["b1"]))
             dY1 = DY1
+        else:
+            rb.ln_bwd(s["xs1"], X, g1, s["mu1"], s["rs1"], M, D, Y, gx(o["g1"]), gx(o["b1"]))
         rb.gemm(dY1, D, True, s["woc"], D, False, M, D, D, datt, D, T)
         rb.gemm(dY1, D, False, s["att"], D, False, D, D, M, gx(o["wo"]), D, _F32)
         rb.colsum(dY1, M, D, gx(o["bo"]))

@@ -55,9 +55,13 @@ def test_bert_stack_plan_structure(p):
     _check_layout(pl, params)
     # per layer: 3 (q, k, v) + out + FFN up + FFN down weights cast; GEMMs fwd 4, bwd 8
     _check_ops(pl, 6 * 2, 2, 4, 8)
-    drop = sum(o.op == L.OP_DROPOUT_FWD for o in _ops(pl.fwd))
-    assert drop == (4 if p > 0 else 0)
-    seeds = [o.l[1] for o in _ops(pl.fwd) if o.op == L.OP_DROPOUT_FWD]
+    # hidden dropout inside the two LayerNorm passes per layer (forward and backward), no
+    # separate dropout launch or mask; attention-probability dropout inside the attention op
+    fwd, bwd = _ops(pl.fwd), _ops(pl.bwd)
+    assert not any(o.op in (L.OP_DROPOUT_FWD, L.OP_DROPOUT_BWD) for o in fwd + bwd)
+    assert sum(o.op == L.OP_LN_FWD_DROP for o in fwd) == (4 if p > 0 else 0)
+    assert sum(o.op == L.OP_LN_BWD_DROP for o in bwd) == (4 if p > 0 else 0)
+    seeds = [o.l[1] for o in fwd if o.op == L.OP_LN_FWD_DROP]
     assert len(set(seeds)) == len(seeds), "two dropout ops share a seed"
 
 
