@@ -31,7 +31,7 @@ static SplitPlan plan_dense(int dtype, int M, int N, int K) {
 
 template <typename OutT>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                     EpiStore<OutT> epi) {
+                                     EpiStore<OutT, true> epi) {
   const long total = (long)M * N;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
@@ -48,7 +48,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
 template <typename OutT>
 __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ ws,
                                                              int splits, int M, int N,
-                                                             EpiStore<OutT> epi) {
+                                                             EpiStore<OutT, true> epi) {
   const int total4 = M * N / 4, n4 = N / 4;
   const f32x4* w = (const f32x4*)ws;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
@@ -224,7 +224,7 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
   const SplitPlan p = plan_dense(sizeof(T) == 2 ? BF16 : F32, M, N, K);  // BF16 = any 16-bit
   MMDX_CHECK_ARG(lda >= (ak ? K : M) && ldb >= (bk ? K : N) && ldc >= N,
                  "mmdx_gemm: leading dimension too small");
-  EpiStore<OutT> epi{(OutT*)C, ldc, M, N, bias, addend, act, alpha, beta, (OutT*)preact};
+  EpiStore<OutT, true> epi{(OutT*)C, ldc, M, N, bias, addend, act, alpha, beta, (OutT*)preact};
   if (p.splits == 1) return dispatch_major<T>(p, A, lda, ak, B, ldb, bk, epi, M, N, K, st);
   const size_t need = (size_t)p.splits * M * N * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "mmdx_gemm: workspace %zu < %zu", ws_bytes, need);

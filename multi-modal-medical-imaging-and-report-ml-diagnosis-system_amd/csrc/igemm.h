@@ -892,7 +892,11 @@ __device__ __forceinline__ void bn_stat_store(const BnStat& b, float* sg, float*
   }
 }
 
-template <typename OutT>
+// VEC_EPI: the 16-B-per-8-columns epilogue also for bias / addend / pre-activation / ReLU /
+// GELU (the dense GEMMs of gemm_dense.hip).  The conv instantiations keep the lean form
+// (their epilogues never carry those): the extra branch cost the C4 step 2.3 % when it was
+// compiled into every conv kernel (8955 vs 8750 samples/s, tools/lab_ab3c4.sh).
+template <typename OutT, bool VEC_EPI = false>
 struct EpiStore {
   OutT* C; long ldc; int M, N;
   const float* bias;    // [N] or null
@@ -976,6 +980,10 @@ struct EpiStore {
   // ReLU / GELU activation too (the forward Linear layers of the BERT / ViT stacks all carry
   // a bias; the per-element epilogue stored them 2 bytes at a time)
   __device__ __forceinline__ bool vec8_ok() const {
+    if constexpr (!VEC_EPI)
+      return !bias && !addend && ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
+             ((!preact && act == ACT_NONE) ||
+              (act == ACT_GELU_BWD && !acc_src && ((uintptr_t)preact & 15) == 0));
     if (ldc % 8 != 0 || ((uintptr_t)C & 15) != 0) return false;
     if (bias && ((uintptr_t)bias & 15) != 0) return false;
     if (addend && ((uintptr_t)addend & 15) != 0) return false;
@@ -1007,7 +1015,7 @@ struct EpiStore {
       *(O8*)(C + off) = o;
       return;
     }
-    if (bias || addend || preact || act != ACT_NONE) {
+    if (VEC_EPI && (bias || addend || preact || act != ACT_NONE)) {
       // the general form, in apply()'s order: alpha*acc + bias + addend -> preact copy ->
       // activation -> + beta*C
       float v[8];
