@@ -8,6 +8,20 @@ namespace mmdx {
 
 struct SplitPlan { int bm, bn, splits, kper; };
 
+// Split-K target: about this many (tile, split) blocks for grids of < 256 tiles (read once;
+// MMDX_SPLITK_TARGET for A/B runs).  Every split writes an fp32 M x N slab that the reduce
+// reads back, so the target trades slab traffic against idle CUs: C5 (paired, two boxes)
+// 128 / 192 / 256 / 512 / 1024 -> 2379 / 2539 / 2587-2656 / 2609 / 2529 samples/s, C4
+// neutral (tools/lab_splitk{,2}.sh, profiles/r04_splitk_sweep.txt).
+static long splitk_target() {
+  static const long v = [] {
+    const char* e = getenv("MMDX_SPLITK_TARGET");
+    const long t = e ? atol(e) : 0L;
+    return t >= 64 ? t : 256L;
+  }();
+  return v;
+}
+
 // Tile + split-K choice; shared by the workspace query and the launch so both agree.
 static SplitPlan plan_dense(int dtype, int M, int N, int K) {
   SplitPlan p;
@@ -18,7 +32,7 @@ static SplitPlan plan_dense(int dtype, int M, int N, int K) {
   const int ktiles = (K + BK - 1) / BK;
   int s = 1;
   if (tiles < 256 && ktiles >= 8) {
-    s = (int)((512 + tiles - 1) / tiles);
+    s = (int)((splitk_target() + tiles - 1) / tiles);
     s = std::min(s, ktiles / 4);
     s = std::max(s, 1);
   }

@@ -280,23 +280,34 @@ __global__ void gelu_bwd_kernel(const T* __restrict__ pre, const T* __restrict__
   GRID_STRIDE(i, n) dx[i] = from_f<T>(to_f(dy[i]) * gelu_erf_grad(to_f(pre[i])));
 }
 
-constexpr int BG_ROWS = 256;
+constexpr int BG_ROWS = 256;     // the most rows a pass-1 block takes
+constexpr int BG_ROWS_MIN = 32;  // the fewest (sizes the workspace)
+// rows per pass-1 block: enough blocks to cover the chip (>= 1024) at N = 768 as at 3072 —
+// with a fixed 256 rows a C5 bias gradient ([8192, 768] fp16) ran as 64 blocks, 1.4 TB/s
+static int bias_grad_rows(long M, int N, int vec) {
+  const long nx = (N / vec + 63) / 64;
+  const long nb_target = (1024 + nx - 1) / nx;
+  long rows = (M + nb_target - 1) / nb_target;
+  rows = (rows + 3) / 4 * 4;
+  return (int)std::max<long>(BG_ROWS_MIN, std::min<long>(BG_ROWS, rows));
+}
 // Column sums of dY [M][N] (bias gradients) in two deterministic passes.  Pass 1: a block
-// owns 64 16-B column vectors x BG_ROWS rows; its 4 row lanes stride the rows with vector
+// owns 64 16-B column vectors x `rows` rows; its 4 row lanes stride the rows with vector
 // loads (a wave reads 1 KB of one row), then combine through LDS into one partial row.
 // (The first version summed one column per thread with 2-B loads and serial adds: 63 us per
 // call, 6.9 ms per C5 step.)
 template <typename T>
 __global__ __launch_bounds__(256) void bias_grad_partial_kernel(const T* __restrict__ dy,
                                                                 long M, int N,
-                                                                float* __restrict__ part) {
+                                                                float* __restrict__ part,
+                                                                int rows) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   __shared__ float red[4][64 * VEC];
   const int cv = threadIdx.x & 63, lane = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + cv;          // column vector
   const bool ok = j < N / VEC;
-  const long r0 = (long)blockIdx.y * BG_ROWS, r1 = min(M, r0 + BG_ROWS);
+  const long r0 = (long)blockIdx.y * rows, r1 = min(M, r0 + rows);
   float acc[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
@@ -323,10 +334,10 @@ __global__ __launch_bounds__(256) void bias_grad_partial_kernel(const T* __restr
 // N not a multiple of the vector width: one column per thread
 template <typename T>
 __global__ void bias_grad_partial_scalar_kernel(const T* __restrict__ dy, long M, int N,
-                                                float* __restrict__ part) {
+                                                float* __restrict__ part, int rows) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  const long r0 = (long)blockIdx.y * BG_ROWS, r1 = min(M, r0 + BG_ROWS);
+  const long r0 = (long)blockIdx.y * rows, r1 = min(M, r0 + rows);
   float acc = 0.f;
   for (long r = r0; r < r1; ++r) acc += to_f(dy[r * N + n]);
   part[(long)blockIdx.y * N + n] = acc;
@@ -532,24 +543,25 @@ extern "C" int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n,
 }
 
 extern "C" size_t mmdx_bias_grad_workspace_size(long M, int N) {
-  return (size_t)((M + BG_ROWS - 1) / BG_ROWS) * N * sizeof(float);
+  return (size_t)((M + BG_ROWS_MIN - 1) / BG_ROWS_MIN) * N * sizeof(float);
 }
 
 extern "C" int mmdx_bias_grad(int dtype, const void* dy, long M, int N, float* db,
                               float beta_acc, void* ws, size_t ws_bytes, void* stream) {
-  const int nb = (int)((M + BG_ROWS - 1) / BG_ROWS);
+  const int vec = dtype == F32 ? 4 : 8;
+  const int rows = bias_grad_rows(M, N, vec);
+  const int nb = (int)((M + rows - 1) / rows);
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_bias_grad_workspace_size(M, N),
                  "bias_grad: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  const int vec = dtype == F32 ? 4 : 8;
   if (N % vec == 0 && ((uintptr_t)dy & 15) == 0)
     DISPATCH_T(dtype, hipLaunchKernelGGL(bias_grad_partial_kernel<T>,
                                          dim3((N / vec + 63) / 64, nb), dim3(256), 0, st,
-                                         (const T*)dy, M, N, (float*)ws));
+                                         (const T*)dy, M, N, (float*)ws, rows));
   else
     DISPATCH_T(dtype, hipLaunchKernelGGL(bias_grad_partial_scalar_kernel<T>,
                                          dim3((N + 255) / 256, nb), dim3(256), 0, st,
-                                         (const T*)dy, M, N, (float*)ws));
+                                         (const T*)dy, M, N, (float*)ws, rows));
   hipLaunchKernelGGL(bias_grad_finalize_kernel, dim3((N + 63) / 64), dim3(256), 0, st,
                      (const float*)ws, nb, N, db, beta_acc);
   MMDX_LAUNCH_CHECK();
