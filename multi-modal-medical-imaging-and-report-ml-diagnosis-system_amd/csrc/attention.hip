@@ -532,7 +532,7 @@ __device__ __forceinline__ void store4(T* dst, float a, float b, float c, float 
 }
 
 template <typename T, int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd16_kernel(
+__global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 8 / NW) void attn_fwd16_kernel(
     const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bias,
     int causal, int L, int H, float scale, float p_drop, uint64_t seed,
     const uint64_t* __restrict__ ctr, T* __restrict__ out, float* __restrict__ probs,
@@ -1095,6 +1095,18 @@ static int fwd16_nw() {
   }();
   return nw;
 }
+// the flash-style forward's block: 8 waves (128 queries); MMDX_ATTN_FWD_NW = 4 | 16 selects
+// 64 / 256 (16 waves = one block per ViT head, K and V staged once instead of twice: C5
+// 2631 / 2640 vs 2653 / 2664 samples/s with 8, paired, tools/lab_attnnw.sh)
+static int fwd16_lse_nw(int L) {
+  (void)L;
+  static const int nw = [] {
+    const char* e = getenv("MMDX_ATTN_FWD_NW");
+    const int v = e ? atoi(e) : 0;
+    return v == 4 || v == 16 ? v : 8;
+  }();
+  return nw;
+}
 static int bwd16_nw() {   // the same for the dQ kernel; MMDX_ATTN_BWD_NW=4 selects 64
   static const int nw = [] {
     const char* e = getenv("MMDX_ATTN_BWD_NW");
@@ -1229,14 +1241,18 @@ extern "C" int mmdx_attention_fwd_lse(int dtype, const void* qkv, const int64_t*
   MMDX_DISPATCH(dtype, {
     if constexpr (!std::is_same<T, float>::value) {
       auto launch = [&](auto kern, int nw) {
-        const size_t sm = smem16(L, nw);
+        // (no probability tiles to transpose: the K / V images and the key mask only)
+        const size_t LP = (L + 31) & ~31;
+        const size_t sm = LP * (LDR + LDT) * sizeof(T) + LP * sizeof(float);
         mmdx_lds_max_once((const void*)kern);
         const int qb = nw * 16;
         hipLaunchKernelGGL(kern, dim3((L + qb - 1) / qb * H * B), dim3(nw * 64), sm, st,
                            (const T*)qkv, mask, (const float*)nullptr, 0, L, H, scale, p_drop,
                            seed, (const uint64_t*)counter, (T*)out, (float*)nullptr, lse, rng);
       };
-      if (fwd16_nw() == 8) launch(attn_fwd16_kernel<T, 8>, 8);
+      const int nw = fwd16_lse_nw(L);
+      if (nw == 16) launch(attn_fwd16_kernel<T, 16>, 16);
+      else if (nw == 8) launch(attn_fwd16_kernel<T, 8>, 8);
       else launch(attn_fwd16_kernel<T, 4>, 4);
     }
   });
