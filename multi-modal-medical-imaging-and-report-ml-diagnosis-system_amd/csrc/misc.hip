@@ -542,12 +542,49 @@ extern "C" int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n,
   return 0;
 }
 
+// MMDX_BIAS_GRAD_GEMM=1 (16-bit dY with M, N multiples of 8): db = 1^T dY as a 1 x N x M
+// GEMM on the MFMA core (a ones row in the workspace as A, dY read R-major as B, split-K over
+// the M rows into fp32 slabs + the split-K reduce, beta = beta_acc).  Tested
+// (test_kernels_gpu.py::test_bias_grad) but off: in the C5 step it ran slower than the two
+// column-sum passes below (2624 / 2624 vs 2647 / 2655 samples/s, paired) — its ~200 blocks
+// of mostly idle 64 x 128 MFMA tiles hold CUs the other tower's kernels want.
+static bool bias_grad_gemm_ok(int dtype, long M, int N) {
+  static const bool on = [] {
+    const char* e = getenv("MMDX_BIAS_GRAD_GEMM");
+    return e && atoi(e) == 1;
+  }();
+  return on && dtype != F32 && M % 8 == 0 && N % 8 == 0 && M < (1L << 30);
+}
+static size_t bias_grad_ones_bytes(long M) { return ((size_t)M * 2 + 255) & ~(size_t)255; }
+
+template <typename T>
+__global__ void fill_ones_kernel(T* __restrict__ p, long n) {
+  GRID_STRIDE(i, n) p[i] = from_f<T>(1.f);
+}
+
 extern "C" size_t mmdx_bias_grad_workspace_size(long M, int N) {
-  return (size_t)((M + BG_ROWS_MIN - 1) / BG_ROWS_MIN) * N * sizeof(float);
+  const size_t cs = (size_t)((M + BG_ROWS_MIN - 1) / BG_ROWS_MIN) * N * sizeof(float);
+  // the GEMM form's workspace (the split plan depends on the dtype class only through the
+  // K tile, the same for bf16 and f16)
+  const size_t gm = M < (1L << 30) ? bias_grad_ones_bytes(M) +
+                                         mmdx_gemm_workspace_size(BF16, 1, N, (int)M)
+                                   : 0;
+  return std::max(cs, gm);
 }
 
 extern "C" int mmdx_bias_grad(int dtype, const void* dy, long M, int N, float* db,
                               float beta_acc, void* ws, size_t ws_bytes, void* stream) {
+  if (bias_grad_gemm_ok(dtype, M, N) && ((uintptr_t)dy & 15) == 0 && ws &&
+      ws_bytes >= mmdx_bias_grad_workspace_size(M, N)) {
+    hipStream_t st = (hipStream_t)stream;
+    char* ones = (char*)ws;
+    const size_t ob = bias_grad_ones_bytes(M);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(fill_ones_kernel<T>, dim3(grid_for(M)), dim3(256), 0,
+                                         st, (T*)ones, M));
+    MMDX_LAUNCH_CHECK();
+    return mmdx_gemm(dtype, 1, N, (int)M, ones, M, 1, dy, N, 0, db, N, F32, nullptr, nullptr,
+                     0, 1.f, beta_acc, nullptr, ones + ob, ws_bytes - ob, stream);
+  }
   const int vec = dtype == F32 ? 4 : 8;
   const int rows = bias_grad_rows(M, N, vec);
   const int nb = (int)((M + rows - 1) / rows);

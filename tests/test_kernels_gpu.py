@@ -127,6 +127,29 @@ def test_gemm_epilogue_bias_addend_preact(dev, dt, act, ldc_pad):
         assert torch.all(pre.float().cpu()[:, N:] == 7.0)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N", [(8192, 768), (12608, 3072), (300, 130), (64, 2304), (1000, 13),
+                                 (8, 8)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_bias_grad(dev, dt, M, N, beta):
+    """Bias gradients = column sums of dY [M, N] (the two-pass column-sum kernels; with
+    MMDX_BIAS_GRAD_GEMM=1 and 16-bit M, N % 8 == 0 the 1 x N x M GEMM against a ones row),
+    accumulated onto db when beta = 1, against float64 sums of the same rounded values."""
+    g = torch.Generator().manual_seed(M + N)
+    dy = torch.randn(M, N, generator=g).to(dev, dt)
+    db0 = torch.randn(N, generator=g).to(dev)
+    db = db0.clone()
+    n = L.lib().mmdx_bias_grad_workspace_size(M, N)
+    w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    L.call("mmdx_bias_grad", L.dtype_code(dt), dy.data_ptr(), M, N, db.data_ptr(), beta,
+           w.data_ptr(), n, L.stream())
+    torch.cuda.synchronize()
+    ref = dy.double().cpu().sum(0) + beta * db0.double().cpu()
+    bound = 2e-6 * dy.double().abs().cpu().sum(0) + 1e-6 * db0.double().abs().cpu() + 1e-12
+    err = (db.double().cpu() - ref).abs()
+    assert (err <= bound).all(), (err / bound).max().item()
+
+
 def _ws(dt, M, N, K, dev):
     n = L.lib().mmdx_gemm_workspace_size(L.dtype_code(dt), M, N, K)
     w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
