@@ -57,7 +57,7 @@ class PlanOp(C.Structure):
  OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK, OP_BN_BWD_MASKED_DY,
  OP_GEMM, OP_ATTN_FWD, OP_ATTN_BWD, OP_LN_FWD, OP_LN_BWD, OP_GELU_BWD, OP_BIAS_GRAD, OP_ADD,
  OP_DROPOUT_FWD, OP_DROPOUT_BWD, OP_AXPBY, OP_ATTN_FWD_LSE, OP_ATTN_BWD_LSE, OP_LN_FWD_DROP,
- OP_LN_BWD_DROP) = range(1, 41)
+ OP_LN_BWD_DROP, OP_GEMM_BIAS_GRAD) = range(1, 42)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
@@ -118,6 +118,9 @@ SIGNATURES = {
     "mmdx_layernorm_bwd": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, f32, vp, sz,
                                  vp]),
     "mmdx_layernorm_workspace_size": (sz, [i64, i32]),
+    "mmdx_gemm_bias_grad_workspace_size": (sz, [i32, i32, i32, i32]),
+    "mmdx_gemm_bias_grad": (i32, [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, i32, vp, vp, sz,
+                                  vp]),
     "mmdx_layernorm_fwd_dropout": (i32, [i32, vp, vp, i64, i32, vp, vp, f32, f32, u64, vp, vp,
                                          vp, vp, vp, vp, vp]),
     "mmdx_layernorm_bwd_dropout": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, f32, vp, vp, vp, vp,

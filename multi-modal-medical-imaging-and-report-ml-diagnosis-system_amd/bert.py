@@ -200,11 +200,11 @@ class _BertLayerFn(torch.autograd.Function):
         F.gemm(dX2, D, True, wo2c, I, False, M, I, D, dpre, I, act=L.ACT_GELU_BWD, preact=pre,
                compute_dtype=T)
         dWo2 = torch.empty((D, I), dtype=torch.float32, device=dev)
-        F.gemm(dX2, D, False, f, I, False, D, I, M, dWo2, I, compute_dtype=T)
-        dbo2 = F._bias_grad(dX2, M, D, torch.empty(D, dtype=torch.float32, device=dev))
+        dbo2 = torch.empty(D, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dX2, D, f, I, D, I, M, dWo2, I, dbo2, compute_dtype=T)
         dWi = torch.empty((I, D), dtype=torch.float32, device=dev)
-        F.gemm(dpre, I, False, h1, D, False, I, D, M, dWi, D, compute_dtype=T)
-        dbi = F._bias_grad(dpre, M, I, torch.empty(I, dtype=torch.float32, device=dev))
+        dbi = torch.empty(I, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dpre, I, h1, D, I, D, M, dWi, D, dbi, compute_dtype=T)
         # X := dpre Wi + X  (residual into h1)
         F.gemm(dpre, I, True, wic, D, False, M, D, I, X, D, beta=1.0, compute_dtype=T)
         # LN1: Y = d(a + x)
@@ -216,13 +216,13 @@ class _BertLayerFn(torch.autograd.Function):
         datt = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dY1, D, True, woc, D, False, M, D, D, datt, D, compute_dtype=T)
         dWo = torch.empty((D, D), dtype=torch.float32, device=dev)
-        F.gemm(dY1, D, False, att, D, False, D, D, M, dWo, D, compute_dtype=T)
-        dbo = F._bias_grad(dY1, M, D, torch.empty(D, dtype=torch.float32, device=dev))
+        dbo = torch.empty(D, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dY1, D, att, D, D, D, M, dWo, D, dbo, compute_dtype=T)
         dqkv = torch.empty((M, 3 * D), dtype=T, device=dev)
         F.attention_bwd(qkv, ctx.attn, att, datt, mask, B, Ls, Hn, scale, ctx.pa, dqkv)
         dWqkv = torch.empty((3 * D, D), dtype=torch.float32, device=dev)
-        F.gemm(dqkv, 3 * D, False, x, D, False, 3 * D, D, M, dWqkv, D, compute_dtype=T)
-        dbqkv = F._bias_grad(dqkv, M, 3 * D, torch.empty(3 * D, dtype=torch.float32, device=dev))
+        dbqkv = torch.empty(3 * D, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dqkv, 3 * D, x, D, 3 * D, D, M, dWqkv, D, dbqkv, compute_dtype=T)
         # Y := dqkv Wqkv + Y  (residual into x)
         F.gemm(dqkv, 3 * D, True, wqkv, D, False, M, D, 3 * D, Y, D, beta=1.0, compute_dtype=T)
         dx = Y.reshape(B, Ls, D)

@@ -143,7 +143,7 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
     const bool oka = va && (AK ? K % 8 == 0 : M % 8 == 0) && abytes < (1L << 31);
     const bool okb = vb && (BKm ? K % 8 == 0 : N % 8 == 0) && bbytes < (1L << 31);
     if (oka && okb) {
-      if constexpr (BM == 128 && BN == 128) {
+      if constexpr (BM == 128 && BN == 128 && !HasBiasSum<Epi>::value) {
         const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
         long lim256 = gemm256_min_tiles();
         if (AK && BKm && lim256 == 0) lim256 = gemm256_fwd_min_tiles();
@@ -263,9 +263,90 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
   return 0;
 }
 
+// dW = A B with A = dY^T and B = X both R-major (the weight gradient of a Linear layer), plus
+// its bias gradient db = row sums of A, fused into the split-K GEMM (EpiPartialBias) and
+// reduced over the splits here; bias partials follow the fp32 slabs in the workspace.
+__global__ void bias_part_reduce_kernel(const float* __restrict__ bpart, int splits, int M,
+                                        float* __restrict__ db) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += bpart[(long)z * M + m];
+  db[m] = s;
+}
+
+static bool wgrad_bias_fused_on() {   // MMDX_WGRAD_BIAS_FUSED=0: GEMM + column-sum kernels
+  static const bool on = [] {
+    const char* e = getenv("MMDX_WGRAD_BIAS_FUSED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+template <typename T, typename OutT>
+static int gemm_wgrad_bias_typed(const SplitPlan& p, int M, int N, int K, const void* A, long lda,
+                                 const void* B, long ldb, void* C, long ldc, float* db,
+                                 void* ws, hipStream_t st) {
+  EpiPartialBias part{};
+  part.ws = (float*)ws;
+  part.M = M;
+  part.N = N;
+  part.bpart = (float*)ws + (size_t)p.splits * M * N;
+  int rc = dispatch_tile<T, false, false>(p, A, lda, B, ldb, part, M, N, K, st);
+  if (rc) return rc;
+  EpiStore<OutT, true> epi{(OutT*)C, ldc, M, N, nullptr, nullptr, ACT_NONE, 1.f, 0.f, nullptr};
+  const long total = (long)M * N;
+  const int blocks = (int)std::min<long>((total / 4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(splitk_reduce4_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
+                     (const float*)ws, p.splits, M, N, epi);
+  hipLaunchKernelGGL(bias_part_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, st,
+                     (const float*)part.bpart, p.splits, M, db);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace mmdx
 
 using namespace mmdx;
+
+extern "C" size_t mmdx_gemm_bias_grad_workspace_size(int dtype, int M, int N, int K) {
+  const SplitPlan p = plan_dense(dtype, M, N, K);
+  const size_t fused = p.splits > 1 ? (size_t)p.splits * ((size_t)M * N + M) * sizeof(float) : 0;
+  const size_t plain = std::max(mmdx_gemm_workspace_size(dtype, M, N, K),
+                                mmdx_bias_grad_workspace_size(K, M));
+  return std::max(fused, plain);
+}
+
+extern "C" int mmdx_gemm_bias_grad(int dtype, int M, int N, int K, const void* A, long lda,
+                                   const void* B, long ldb, void* C, long ldc, int c_dtype,
+                                   float* db, void* ws, size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(lda >= M && ldb >= N && ldc >= N && db, "gemm bias grad: bad arguments");
+  MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_gemm_bias_grad_workspace_size(dtype, M, N, K),
+                 "gemm bias grad: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const SplitPlan p = plan_dense(dtype, M, N, K);
+  const long abytes = (long)K * lda * 2, bbytes = (long)K * ldb * 2;
+  const bool fused = wgrad_bias_fused_on() && dtype != F32 && p.splits > 1 && p.bm == 128 &&
+                     M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+                     ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+                     abytes < (1L << 31) && bbytes < (1L << 31);
+  if (fused) {
+    if (dtype == F16) {
+      if (c_dtype == F32)
+        return gemm_wgrad_bias_typed<f16, float>(p, M, N, K, A, lda, B, ldb, C, ldc, db, ws, st);
+      return gemm_wgrad_bias_typed<f16, f16>(p, M, N, K, A, lda, B, ldb, C, ldc, db, ws, st);
+    }
+    if (c_dtype == F32)
+      return gemm_wgrad_bias_typed<bf16, float>(p, M, N, K, A, lda, B, ldb, C, ldc, db, ws, st);
+    return gemm_wgrad_bias_typed<bf16, bf16>(p, M, N, K, A, lda, B, ldb, C, ldc, db, ws, st);
+  }
+  // the GEMM, then the column sums of dY = A^T ([K][lda], M columns)
+  MMDX_CHECK_ARG(lda == M, "gemm bias grad: unfused path needs lda == M");
+  int rc = mmdx_gemm(dtype, M, N, K, A, lda, 0, B, ldb, 0, C, ldc, c_dtype, nullptr, nullptr,
+                     ACT_NONE, 1.f, 0.f, nullptr, ws, ws_bytes, stream);
+  if (rc) return rc;
+  return mmdx_bias_grad(dtype, A, K, M, db, 0.f, ws, ws_bytes, stream);
+}
 
 extern "C" size_t mmdx_gemm_workspace_size(int dtype, int M, int N, int K) {
   const SplitPlan p = plan_dense(dtype, M, N, K);

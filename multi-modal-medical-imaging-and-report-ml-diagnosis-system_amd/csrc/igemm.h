@@ -1385,6 +1385,20 @@ struct EpiPhase {
   }
 };
 
+// Bias gradient fused into a weight-gradient GEMM (A R-major = dY^T): the blocks of column
+// tile 0 also multiply their A fragments by a ones operand (one extra MFMA per A fragment
+// and 32-deep k step, waves of column group 0 only), which leaves the row sums of A — the
+// column sums of dY over this K split — in a 16 x 16 accumulator per row tile; they are
+// stored to bpart[z][M] and reduced over the splits by gemm_dense.hip.
+struct EpiPartialBias : EpiPartial {
+  float* bpart;   // [splits][M]
+  static constexpr bool BIAS_SUM = true;
+};
+template <class E, class = void> struct HasBiasSum { static constexpr bool value = false; };
+template <class E> struct HasBiasSum<E, decltype((void)E::BIAS_SUM)> {
+  static constexpr bool value = E::BIAS_SUM;
+};
+
 template <class E, class = void> struct IsPhased { static constexpr bool value = false; };
 template <class E> struct IsPhased<E, decltype((void)E::PHASED)> {
   static constexpr bool value = E::PHASED;
@@ -1797,6 +1811,21 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient (EpiPartialBias): row sums of A in the column-tile-0 blocks
+  constexpr bool BSUM = HasBiasSum<Epi>::value;
+  static_assert(!BSUM || FRAG_FIRST, "bias sums ride the fragments-first K loop");
+  const bool bias_blk = BSUM && tn == 0 && wn == 0;   // wave-uniform
+  f32x4 bsum[BSUM ? RM : 1];
+#pragma unroll
+  for (int i = 0; i < (BSUM ? RM : 1); ++i) bsum[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if constexpr (std::is_same<ET, f16>::value)
+      ones8[e] = __builtin_bit_cast(bf16, (f16)1.0f);
+    else
+      ones8[e] = (bf16)1.0f;
+  }
 
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t) {
@@ -1871,6 +1900,22 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j],
                                                                    acc[i][j], 0, 0, 0);
           }
+      if constexpr (BSUM) {
+        if (bias_blk) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int i = 0; i < RM; ++i) {
+              if constexpr (std::is_same<ET, f16>::value)
+                bsum[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                    __builtin_bit_cast(f16x8, af[s][i]), __builtin_bit_cast(f16x8, ones8),
+                    bsum[i], 0, 0, 0);
+              else
+                bsum[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], ones8, bsum[i], 0,
+                                                                   0, 0);
+            }
+        }
+      }
       continue;
     }
     if (t + NS - 1 < nt) {  // its stage was consumed in iteration t-1 by every wave
@@ -1902,6 +1947,19 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (BSUM) {
+    // every column of a bsum tile holds the row sums: lanes 0, 16, 32, 48 store rows
+    // (lane >> 4) * 4 + r of each row tile
+    if (bias_blk && (lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = tm * BM + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          if (m < M) epi.bpart[(long)zsplit * M + m] = bsum[i][r];
+        }
+    }
+  }
 
   float* cst = (float*)lds_raw;
   float* red = cst + BM * LDC;

@@ -155,6 +155,11 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
                        P(o, 1, ext), o.l[1], o.i[4], P(o, 2, ext), o.l[2], o.i[5],
                        (const float*)P(o, 3, ext), (const float*)P(o, 4, ext), o.i[6], o.f[0],
                        o.f[1], P(o, 5, ext), P(o, 6, ext), (size_t)o.l[3], s);
+    case MMDX_OP_GEMM_BIAS_GRAD:
+      // i: M, N, K, c_dtype; l: lda, ldb, ldc, ws_bytes; p: A, B, C, db, ws
+      return mmdx_gemm_bias_grad(o.dtype, o.i[0], o.i[1], o.i[2], P(o, 0, ext), o.l[0],
+                                 P(o, 1, ext), o.l[1], P(o, 2, ext), o.l[2], o.i[3],
+                                 (float*)P(o, 3, ext), P(o, 4, ext), (size_t)o.l[3], s);
     case MMDX_OP_ATTN_FWD:
       // i: B, L, H; f: scale, p_drop; l: seed; p: qkv, mask, counter, out, probs
       return mmdx_attention_fwd(o.dtype, P(o, 0, ext), (const int64_t*)P(o, 1, ext), o.i[0],

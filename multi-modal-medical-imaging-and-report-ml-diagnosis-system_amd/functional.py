@@ -103,6 +103,18 @@ def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, Cout, ldc, *, bias=None, a
     return Cout
 
 
+def gemm_wgrad_bias(dY, ldy, X, ldx, M, N, K, dW, ldw, db, *, compute_dtype=None):
+    """dW[M,N] = dY^T X (both R-major: dY [K][ldy], X [K][ldx]) and db[M] = column sums of
+    dY, in one launch sequence (mmdx_gemm_bias_grad)."""
+    dt = L.dtype_code(compute_dtype if compute_dtype is not None else dY.dtype)
+    ws_n = L.lib().mmdx_gemm_bias_grad_workspace_size(dt, M, N, K)
+    ws = L.workspace(ws_n, dW.device)
+    with GEMM_TIMER(gemm_cost(M, N, K, dt, L.dtype_code(dW.dtype), 0.0, L.ACT_NONE, None)):
+        call("mmdx_gemm_bias_grad", dt, M, N, K, ptr(dY), ldy, ptr(X), ldx, ptr(dW), ldw,
+             L.dtype_code(dW.dtype), ptr(db), ptr(ws), ws_n, stream())
+    return dW, db
+
+
 def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """Device cast through the mmdx kernel (fp32 master weights -> compute dtype)."""
     if x.dtype == dtype:

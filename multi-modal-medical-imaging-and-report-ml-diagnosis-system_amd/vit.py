@@ -169,11 +169,11 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm(dO, D, True, w2c, I, False, M, I, D, dpre, I, act=L.ACT_GELU_BWD, preact=pre,
                compute_dtype=T)
         dW2 = torch.empty((D, I), dtype=torch.float32, device=dev)
-        F.gemm(dO, D, False, f, I, False, D, I, M, dW2, I, compute_dtype=T)
-        dbb2 = _colsum(dO, M, D)
+        dbb2 = torch.empty(D, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dO, D, f, I, D, I, M, dW2, I, dbb2, compute_dtype=T)
         dW1 = torch.empty((I, D), dtype=torch.float32, device=dev)
-        F.gemm(dpre, I, False, u2, D, False, I, D, M, dW1, D, compute_dtype=T)
-        dbb1 = _colsum(dpre, M, I)
+        dbb1 = torch.empty(I, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dpre, I, u2, D, I, D, M, dW1, D, dbb1, compute_dtype=T)
         du2 = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dpre, I, True, w1c, D, False, M, D, I, du2, D, compute_dtype=T)
         da_ln, dg2, db2 = _ln_bwd(a, du2, g2, mu2, rs2)
@@ -181,13 +181,13 @@ class _VitBlockFn(torch.autograd.Function):
         datt = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(da, D, True, woc, D, False, M, D, D, datt, D, compute_dtype=T)
         dWo = torch.empty((D, D), dtype=torch.float32, device=dev)
-        F.gemm(da, D, False, att, D, False, D, D, M, dWo, D, compute_dtype=T)
-        dbo = _colsum(da, M, D)
+        dbo = torch.empty(D, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(da, D, att, D, D, D, M, dWo, D, dbo, compute_dtype=T)
         dqkv = torch.empty((M, 3 * D), dtype=T, device=dev)
         F.attention_bwd(qkv, ctx.attn, att, datt, None, N, S, heads, scale, 0.0, dqkv)
         dWqkv = torch.empty((3 * D, D), dtype=torch.float32, device=dev)
-        F.gemm(dqkv, 3 * D, False, u1, D, False, 3 * D, D, M, dWqkv, D, compute_dtype=T)
-        dbqkv = _colsum(dqkv, M, 3 * D)
+        dbqkv = torch.empty(3 * D, dtype=torch.float32, device=dev)
+        F.gemm_wgrad_bias(dqkv, 3 * D, u1, D, 3 * D, D, M, dWqkv, D, dbqkv, compute_dtype=T)
         du1 = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dqkv, 3 * D, True, wqkv, D, False, M, D, 3 * D, du1, D, compute_dtype=T)
         dx_ln, dg1, db1 = _ln_bwd(x, du1, g1, mu1, rs1)

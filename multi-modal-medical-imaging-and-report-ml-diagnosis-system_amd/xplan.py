@@ -93,6 +93,13 @@ class _Rec:
                        l=(lda, ldb, ldc, n), f=(1.0, beta),
                        p=(A, B, C, bias, None, preact, self._ws(n)))
 
+    def gemm_wgrad_bias(self, dY, ldy, X, ldx, M, N, K, dW, ldw, db):
+        """dW = dY^T X (fp32) and db = column sums of dY (mmdx_gemm_bias_grad)."""
+        n = L.lib().mmdx_gemm_bias_grad_workspace_size(self.dt, M, N, K)
+        self.ops.timed(F.gemm_cost(M, N, K, self.dt, L.F32, 0.0, L.ACT_NONE, None),
+                       L.OP_GEMM_BIAS_GRAD, dtype=self.dt, i=(M, N, K, L.F32),
+                       l=(ldy, ldx, ldw, n), p=(dY, X, dW, db, self._ws(n)))
+
     def attn_fwd(self, qkv, mask, B, Ls, H, scale, p_drop, seed, counter, out):
         """Returns what the backward needs besides qkv / out: the row log-sum-exp and the
         dropout stream base (flash-style, 16-bit) or the saved probabilities [B,H,L,L]."""
@@ -340,10 +347,8 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
             rb.ln_bwd(s["xs2"], dh, g2, s["mu2"], s["rs2"], M, D, X, gx(o["g2"]), gx(o["b2"]))
         rb.gemm(dX2, D, True, s["wo2c"], I, False, M, I, D, dpre, I, T, act=L.ACT_GELU_BWD,
                 preact=s["pre"])
-        rb.gemm(dX2, D, False, s["f"], I, False, D, I, M, gx(o["wo2"]), I, _F32)
-        rb.colsum(dX2, M, D, gx(o["bo2"]))
-        rb.gemm(dpre, I, False, s["h1"], D, False, I, D, M, gx(o["wi"]), D, _F32)
-        rb.colsum(dpre, M, I, gx(o["bi"]))
+        rb.gemm_wgrad_bias(dX2, D, s["f"], I, D, I, M, gx(o["wo2"]), I, gx(o["bo2"]))
+        rb.gemm_wgrad_bias(dpre, I, s["h1"], D, I, D, M, gx(o["wi"]), D, gx(o["bi"]))
         rb.gemm(dpre, I, True, s["wic"], D, False, M, D, I, X, D, T, beta=1.0)
         dY1 = Y
         if p > 0:
@@ -353,12 +358,10 @@ def _build_bert(params, B, Ls, D, Hn, I, eps, p, pa, T, dev):
         else:
             rb.ln_bwd(s["xs1"], X, g1, s["mu1"], s["rs1"], M, D, Y, gx(o["g1"]), gx(o["b1"]))
         rb.gemm(dY1, D, True, s["woc"], D, False, M, D, D, datt, D, T)
-        rb.gemm(dY1, D, False, s["att"], D, False, D, D, M, gx(o["wo"]), D, _F32)
-        rb.colsum(dY1, M, D, gx(o["bo"]))
+        rb.gemm_wgrad_bias(dY1, D, s["att"], D, D, D, M, gx(o["wo"]), D, gx(o["bo"]))
         rb.attn_bwd(s["qkv"], s["probs"], s["att"], datt, mask, B, Ls, Hn, scale, pa, dqkv)
         xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)  # the stack input
-        rb.gemm(dqkv, 3 * D, False, xin, D, False, 3 * D, D, M, gx(o["wqkv"]), D, _F32)
-        rb.colsum(dqkv, M, 3 * D, gx(o["bqkv"]))
+        rb.gemm_wgrad_bias(dqkv, 3 * D, xin, D, 3 * D, D, M, gx(o["wqkv"]), D, gx(o["bqkv"]))
         rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, Y, D, T, beta=1.0)
         dh = Y
         pl.cut_after_layers(li, nl, lambda j: offs[j]["wqkv"] if j < nl else G.n)
@@ -437,19 +440,15 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         g2 = params[li * _VIT_NP + 6]
         rb.gemm(dO, D, True, s["w2c"], I, False, M, I, D, dpre, I, T, act=L.ACT_GELU_BWD,
                 preact=s["pre"])
-        rb.gemm(dO, D, False, s["f"], I, False, D, I, M, gx(o[10]), I, _F32)
-        rb.colsum(dO, M, D, gx(o[11]))
-        rb.gemm(dpre, I, False, s["u2"], D, False, I, D, M, gx(o[8]), D, _F32)
-        rb.colsum(dpre, M, I, gx(o[9]))
+        rb.gemm_wgrad_bias(dO, D, s["f"], I, D, I, M, gx(o[10]), I, gx(o[11]))
+        rb.gemm_wgrad_bias(dpre, I, s["u2"], D, I, D, M, gx(o[8]), D, gx(o[9]))
         rb.gemm(dpre, I, True, s["w1c"], D, False, M, D, I, du2, D, T)
         rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, da_ln, gx(o[6]), gx(o[7]))
         rb.add(dO, da_ln, M * D, DA)
         rb.gemm(DA, D, True, s["woc"], D, False, M, D, D, datt, D, T)
-        rb.gemm(DA, D, False, s["att"], D, False, D, D, M, gx(o[4]), D, _F32)
-        rb.colsum(DA, M, D, gx(o[5]))
+        rb.gemm_wgrad_bias(DA, D, s["att"], D, D, D, M, gx(o[4]), D, gx(o[5]))
         rb.attn_bwd(s["qkv"], s["probs"], s["att"], datt, None, N, S, heads, scale, 0.0, dqkv)
-        rb.gemm(dqkv, 3 * D, False, s["u1"], D, False, 3 * D, D, M, gx(o[2]), D, _F32)
-        rb.colsum(dqkv, M, 3 * D, gx(o[3]))
+        rb.gemm_wgrad_bias(dqkv, 3 * D, s["u1"], D, 3 * D, D, M, gx(o[2]), D, gx(o[3]))
         rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, du1, D, T)
         xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)
         rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, dx_ln, gx(o[0]), gx(o[1]))

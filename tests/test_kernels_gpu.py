@@ -150,6 +150,30 @@ def test_bias_grad(dev, dt, M, N, beta):
     assert (err <= bound).all(), (err / bound).max().item()
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(768, 3072, 8192), (2304, 768, 12608), (768, 768, 1000),
+                                   (520, 130, 64), (3072, 768, 256)])
+def test_gemm_wgrad_bias(dev, dt, M, N, K):
+    """dW = dY^T X and db = column sums of dY (mmdx_gemm_bias_grad; 16-bit split-K grids fuse
+    the sums into the GEMM's column-tile-0 blocks, the rest runs GEMM + column sums)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    dY = (torch.randn(K, M, generator=g) / 4).to(dev, dt)
+    X = (torch.randn(K, N, generator=g) / 4).to(dev, dt)
+    dW = torch.full((M, N), float("nan"), device=dev)
+    db = torch.full((M,), float("nan"), device=dev)
+    n = L.lib().mmdx_gemm_bias_grad_workspace_size(L.dtype_code(dt), M, N, K)
+    w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    L.call("mmdx_gemm_bias_grad", L.dtype_code(dt), M, N, K, dY.data_ptr(), M, X.data_ptr(), N,
+           dW.data_ptr(), N, L.F32, db.data_ptr(), w.data_ptr(), n, L.stream())
+    torch.cuda.synchronize()
+    a, b = dY.double().cpu(), X.double().cpu()
+    _close(dW, a.T @ b, dt if dt != torch.float32 else torch.float32, "dW")
+    ref = a.sum(0)
+    bound = 2e-6 * a.abs().sum(0) + 1e-12
+    assert ((db.double().cpu() - ref).abs() <= bound).all(), \
+        ((db.double().cpu() - ref).abs() / bound).max().item()
+
+
 def _ws(dt, M, N, K, dev):
     n = L.lib().mmdx_gemm_workspace_size(L.dtype_code(dt), M, N, K)
     w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)

@@ -42,7 +42,10 @@ def _check_ops(pl, n_weights, n_layers, gemm_fwd, gemm_bwd):
         for j in range(12):
             assert not (o.ext[j] == -1 and o.p[j] == 1), "unpatched workspace placeholder"
     assert sum(o.op == L.OP_GEMM for o in fwd) == gemm_fwd * n_layers
-    assert sum(o.op == L.OP_GEMM for o in bwd) == gemm_bwd * n_layers
+    # the four weight gradients per layer carry their bias gradients (no column-sum ops)
+    assert sum(o.op == L.OP_GEMM_BIAS_GRAD for o in bwd) == 4 * n_layers
+    assert sum(o.op == L.OP_GEMM for o in bwd) == (gemm_bwd - 4) * n_layers
+    assert not any(o.op == L.OP_BIAS_GRAD for o in bwd)
     assert not any(o.op == L.OP_GELU_BWD for o in bwd), "GELU backward not fused"
     assert sum(o.op == L.OP_EVENT for o in fwd) == 2 * len(pl.fwd.conv_names)
 
