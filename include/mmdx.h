@@ -62,6 +62,14 @@ size_t mmdx_gemm_workspace_size(int dtype, int M, int N, int K);
  * (fp32, unsplit grids, unaligned operands, MMDX_WGRAD_BIAS_FUSED=0) mmdx_gemm followed by
  * mmdx_bias_grad (needs lda == M).
  * Replaces: the weight and bias gradients of nn.Linear in the BERT / ViT layers (TP:360). */
+/* mmdx_gemm plus a residual [M][ldc] of C's dtype added last (after the activation and
+ * beta*C): C = act(alpha*A B^T + bias) + beta*C + residual; residual must not alias C.
+ * Replaces: the residual adds of torchvision's EncoderBlock (x + mlp(ln_2(x)), vit_b_16). */
+int mmdx_gemm_res(int dtype, int M, int N, int K, const void* A, long lda, int a_kmajor,
+                  const void* B, long ldb, int b_kmajor, void* C, long ldc, int c_dtype,
+                  const float* bias, const float* addend, int act, float alpha, float beta,
+                  void* preact, const void* residual, void* workspace, size_t ws_bytes,
+                  void* stream);
 size_t mmdx_gemm_bias_grad_workspace_size(int dtype, int M, int N, int K);
 int mmdx_gemm_bias_grad(int dtype, int M, int N, int K, const void* A, long lda, const void* B,
                         long ldb, void* C, long ldc, int c_dtype, float* db, void* workspace,

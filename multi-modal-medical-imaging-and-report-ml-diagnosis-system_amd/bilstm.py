@@ -156,9 +156,10 @@ class _LSTMLayerFn(torch.autograd.Function):
         call("mmdx_lstm_bwd", L.dtype_code(T), ptr(whh), ptr(hout), ptr(cs), ptr(gs), ptr(dh), B,
              Ls, H, ptr(dxg), ptr(dwhh), ptr(ws), n, stream())
         dwih = torch.empty((2 * G4, In), dtype=torch.float32, device=dev)
-        F.gemm(dxg, 2 * G4, False, x.reshape(M, In), In, False, 2 * G4, In, M, dwih, In,
-               compute_dtype=T)
-        db = F._bias_grad(dxg, M, 2 * G4, torch.empty(2 * G4, dtype=torch.float32, device=dev))
+        db = torch.empty(2 * G4, dtype=torch.float32, device=dev)
+        # dW_ih and the (shared) bias gradient in one launch sequence
+        F.gemm_wgrad_bias(dxg, 2 * G4, x.reshape(M, In), In, 2 * G4, In, M, dwih, In, db,
+                          compute_dtype=T)
         db2 = torch.empty_like(db)
         call("mmdx_axpby", 2 * G4, 1.0, ptr(db), 0.0, None, ptr(db2), stream())
         dx = None

@@ -234,11 +234,12 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
                       long ldb, int bk, void* C, long ldc, const float* bias,
                       const float* addend, int act,
                       float alpha, float beta, void* preact, void* ws, size_t ws_bytes,
-                      hipStream_t st) {
+                      hipStream_t st, const void* res = nullptr) {
   const SplitPlan p = plan_dense(sizeof(T) == 2 ? BF16 : F32, M, N, K);  // BF16 = any 16-bit
   MMDX_CHECK_ARG(lda >= (ak ? K : M) && ldb >= (bk ? K : N) && ldc >= N,
                  "mmdx_gemm: leading dimension too small");
   EpiStore<OutT, true> epi{(OutT*)C, ldc, M, N, bias, addend, act, alpha, beta, (OutT*)preact};
+  epi.res = (const OutT*)res;
   if (p.splits == 1) return dispatch_major<T>(p, A, lda, ak, B, ldb, bk, epi, M, N, K, st);
   const size_t need = (size_t)p.splits * M * N * sizeof(float);
   MMDX_CHECK_ARG(ws && ws_bytes >= need, "mmdx_gemm: workspace %zu < %zu", ws_bytes, need);
@@ -353,31 +354,51 @@ extern "C" size_t mmdx_gemm_workspace_size(int dtype, int M, int N, int K) {
   return p.splits > 1 ? (size_t)p.splits * M * N * sizeof(float) : 0;
 }
 
-extern "C" int mmdx_gemm(int dtype, int M, int N, int K, const void* A, long lda, int a_kmajor,
+static int gemm_entry(int dtype, int M, int N, int K, const void* A, long lda, int a_kmajor,
                          const void* B, long ldb, int b_kmajor, void* C, long ldc, int c_dtype,
                          const float* bias, const float* addend, int act, float alpha,
                          float beta, void* preact, void* workspace, size_t ws_bytes,
-                         void* stream) {
+                         void* stream, const void* res) {
   MMDX_CHECK_ARG(M > 0 && N > 0 && K > 0, "mmdx_gemm: empty problem M=%d N=%d K=%d", M, N, K);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == F32) {
     MMDX_CHECK_ARG(c_dtype == F32, "mmdx_gemm: fp32 compute needs fp32 output");
     return gemm_typed<float, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
-                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st, res);
   }
   if (dtype == F16) {
     if (c_dtype == F32)
       return gemm_typed<f16, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
-                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+                                    addend, act, alpha, beta, preact, workspace, ws_bytes, st, res);
     MMDX_CHECK_ARG(c_dtype == F16, "mmdx_gemm: fp16 compute writes fp16 or fp32");
     return gemm_typed<f16, f16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
-                                addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+                                addend, act, alpha, beta, preact, workspace, ws_bytes, st, res);
   }
   MMDX_CHECK_ARG(dtype == BF16, "mmdx_gemm: bad dtype %d", dtype);
   MMDX_CHECK_ARG(c_dtype == F32 || c_dtype == BF16, "mmdx_gemm: bf16 compute writes bf16/fp32");
   if (c_dtype == F32)
     return gemm_typed<bf16, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias,
-                                   addend, act, alpha, beta, preact, workspace, ws_bytes, st);
+                                   addend, act, alpha, beta, preact, workspace, ws_bytes, st, res);
   return gemm_typed<bf16, bf16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, bias, addend, act,
-                                alpha, beta, preact, workspace, ws_bytes, st);
+                                alpha, beta, preact, workspace, ws_bytes, st, res);
+}
+
+extern "C" int mmdx_gemm(int dtype, int M, int N, int K, const void* A, long lda, int a_kmajor,
+                         const void* B, long ldb, int b_kmajor, void* C, long ldc, int c_dtype,
+                         const float* bias, const float* addend, int act, float alpha,
+                         float beta, void* preact, void* workspace, size_t ws_bytes,
+                         void* stream) {
+  return gemm_entry(dtype, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, c_dtype, bias,
+                    addend, act, alpha, beta, preact, workspace, ws_bytes, stream, nullptr);
+}
+
+extern "C" int mmdx_gemm_res(int dtype, int M, int N, int K, const void* A, long lda,
+                             int a_kmajor, const void* B, long ldb, int b_kmajor, void* C,
+                             long ldc, int c_dtype, const float* bias, const float* addend,
+                             int act, float alpha, float beta, void* preact,
+                             const void* residual, void* workspace, size_t ws_bytes,
+                             void* stream) {
+  MMDX_CHECK_ARG(residual != C, "mmdx_gemm_res: the residual must not alias C");
+  return gemm_entry(dtype, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, c_dtype, bias,
+                    addend, act, alpha, beta, preact, workspace, ws_bytes, stream, residual);
 }

@@ -911,6 +911,9 @@ struct EpiStore {
   // gradient a residual unit's identity path adds, without materialising it
   const OutT* acc_src = nullptr;
   const uint8_t* acc_mask = nullptr;
+  // optional residual [M][ldc] (OutT) added last, as beta*C with beta 1 would add a copy of
+  // it (ViT's out = a + f W2^T + b2 without copying a into C first)
+  const OutT* res = nullptr;
   static constexpr bool BNSTAT = true;
   static constexpr bool SPLIT = false;
   __device__ __forceinline__ long bn_off(int m, int n) const { return (long)m * ldc + n; }
@@ -972,6 +975,7 @@ struct EpiStore {
     if (act == ACT_RELU) v = fmaxf(v, 0.f);
     else if (act == ACT_GELU) v = gelu_erf(v);
     if (beta != 0.f) v += beta * to_f(C[off]);
+    if (res) v += to_f(res[off]);
     if (acc_src) v += acc_at(m, n);
     C[off] = from_f<OutT>(v);
   }
@@ -981,15 +985,16 @@ struct EpiStore {
   // a bias; the per-element epilogue stored them 2 bytes at a time)
   __device__ __forceinline__ bool vec8_ok() const {
     if constexpr (!VEC_EPI)
-      return !bias && !addend && ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
+      return !bias && !addend && !res && ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
              ((!preact && act == ACT_NONE) ||
               (act == ACT_GELU_BWD && !acc_src && ((uintptr_t)preact & 15) == 0));
     if (ldc % 8 != 0 || ((uintptr_t)C & 15) != 0) return false;
     if (bias && ((uintptr_t)bias & 15) != 0) return false;
     if (addend && ((uintptr_t)addend & 15) != 0) return false;
     if (preact && ((uintptr_t)preact & 15) != 0) return false;
-    if (act == ACT_GELU_BWD) return !acc_src && preact;
-    return !(acc_src && (bias || addend || preact || act != ACT_NONE));
+    if (res && ((uintptr_t)res & 15) != 0) return false;
+    if (act == ACT_GELU_BWD) return !acc_src && !res && preact;
+    return !(acc_src && (bias || addend || preact || res || act != ACT_NONE));
   }
   // 8 consecutive columns n..n+7 of row m (vec8_ok() checked by the caller)
   __device__ __forceinline__ void apply8_fast(int m, int n, f32x4 lo, f32x4 hi) const {
@@ -1015,7 +1020,7 @@ struct EpiStore {
       *(O8*)(C + off) = o;
       return;
     }
-    if (VEC_EPI && (bias || addend || preact || act != ACT_NONE)) {
+    if (VEC_EPI && (bias || addend || preact || res || act != ACT_NONE)) {
       // the general form, in apply()'s order: alpha*acc + bias + addend -> preact copy ->
       // activation -> + beta*C
       float v[8];
@@ -1046,14 +1051,16 @@ struct EpiStore {
         for (int j = 0; j < 8; ++j) pr[j] = from_f<OutT>(v[j]);
         *(O8*)(preact + off) = pr;
       }
-      O8 c{};
+      O8 c{}, rr{};
       if (beta != 0.f) c = *(const O8*)(C + off);
+      if (res) rr = *(const O8*)(res + off);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float x = v[j];
         if (act == ACT_RELU) x = fmaxf(x, 0.f);
         else if (act == ACT_GELU) x = gelu_erf(x);
         if (beta != 0.f) x += beta * to_f(c[j]);
+        if (res) x += to_f(rr[j]);
         o[j] = from_f<OutT>(x);
       }
     } else if (acc_src) {  // 8 columns = one mask byte (bf16) or two (fp32)
@@ -1178,7 +1185,7 @@ struct EpiStore {
     if (m >= M) return;
     const long off = (long)m * ldc + n;
     const bool fast = n + 4 <= N && (off & 3) == 0 && !bias && !addend && !preact &&
-                      act == ACT_NONE && !acc_src;
+                      act == ACT_NONE && !acc_src && !res;
     if (!fast) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) apply(m, n + j, v[j]);

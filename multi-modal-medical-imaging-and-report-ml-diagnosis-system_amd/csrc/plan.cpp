@@ -151,6 +151,13 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_GEMM:
       // i: M, N, K, a_kmajor, b_kmajor, c_dtype, act; l: lda, ldb, ldc, ws_bytes;
       // f: alpha, beta; p: A, B, C, bias, addend, preact, ws
+      // (p[7]: optional residual, mmdx_gemm_res)
+      if (P(o, 7, ext))
+        return mmdx_gemm_res(o.dtype, o.i[0], o.i[1], o.i[2], P(o, 0, ext), o.l[0], o.i[3],
+                             P(o, 1, ext), o.l[1], o.i[4], P(o, 2, ext), o.l[2], o.i[5],
+                             (const float*)P(o, 3, ext), (const float*)P(o, 4, ext), o.i[6],
+                             o.f[0], o.f[1], P(o, 5, ext), P(o, 7, ext), P(o, 6, ext),
+                             (size_t)o.l[3], s);
       return mmdx_gemm(o.dtype, o.i[0], o.i[1], o.i[2], P(o, 0, ext), o.l[0], o.i[3],
                        P(o, 1, ext), o.l[1], o.i[4], P(o, 2, ext), o.l[2], o.i[5],
                        (const float*)P(o, 3, ext), (const float*)P(o, 4, ext), o.i[6], o.f[0],

@@ -91,15 +91,25 @@ def gemm_cost(M, N, K, dt, c_dt, beta=0.0, act=L.ACT_NONE, preact=None):
 
 # ----------------------------------------------------------------------------- primitives
 def gemm(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, Cout, ldc, *, bias=None, addend=None,
-         act=L.ACT_NONE, alpha=1.0, beta=0.0, preact=None, compute_dtype=None):
-    """C[M,N] = act(alpha * A.B^T + bias) + beta*C on the MFMA implicit-GEMM core."""
+         act=L.ACT_NONE, alpha=1.0, beta=0.0, preact=None, compute_dtype=None, residual=None):
+    """C[M,N] = act(alpha * A.B^T + bias) + beta*C (+ residual) on the MFMA implicit-GEMM
+    core."""
     dt = L.dtype_code(compute_dtype if compute_dtype is not None else A.dtype)
     ws_n = L.lib().mmdx_gemm_workspace_size(dt, M, N, K)
     ws = L.workspace(ws_n, Cout.device)
-    with GEMM_TIMER(gemm_cost(M, N, K, dt, L.dtype_code(Cout.dtype), beta, act, preact)):
-        call("mmdx_gemm", dt, M, N, K, ptr(A), lda, int(a_kmajor), ptr(B), ldb, int(b_kmajor),
-             ptr(Cout), ldc, L.dtype_code(Cout.dtype), ptr(bias), ptr(addend), act,
-             float(alpha), float(beta), ptr(preact), ptr(ws), ws_n, stream())
+    cost = gemm_cost(M, N, K, dt, L.dtype_code(Cout.dtype),
+                     1.0 if residual is not None else beta, act, preact)
+    with GEMM_TIMER(cost):
+        if residual is not None:
+            call("mmdx_gemm_res", dt, M, N, K, ptr(A), lda, int(a_kmajor), ptr(B), ldb,
+                 int(b_kmajor), ptr(Cout), ldc, L.dtype_code(Cout.dtype), ptr(bias),
+                 ptr(addend), act, float(alpha), float(beta), ptr(preact), ptr(residual),
+                 ptr(ws), ws_n, stream())
+        else:
+            call("mmdx_gemm", dt, M, N, K, ptr(A), lda, int(a_kmajor), ptr(B), ldb,
+                 int(b_kmajor), ptr(Cout), ldc, L.dtype_code(Cout.dtype), ptr(bias),
+                 ptr(addend), act, float(alpha), float(beta), ptr(preact), ptr(ws), ws_n,
+                 stream())
     return Cout
 
 

@@ -147,8 +147,8 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm(u2, D, True, w1c, D, True, M, I, D, f, I, bias=bb1, act=L.ACT_GELU, preact=pre,
                compute_dtype=T)
         w2c = F.cast(w2, T)
-        out = _copy(a)  # out = a + f W2^T + b2 (residual accumulated in the GEMM epilogue)
-        F.gemm(f, I, True, w2c, I, True, M, D, I, out, D, bias=bb2, beta=1.0, compute_dtype=T)
+        out = torch.empty_like(a)  # out = a + f W2^T + b2 (the residual read by the epilogue)
+        F.gemm(f, I, True, w2c, I, True, M, D, I, out, D, bias=bb2, residual=a, compute_dtype=T)
         if keep:
             ctx.save_for_backward(x, u1, mu1, rs1, g1, wqkv, qkv, att, woc, a, u2, mu2,
                                   rs2, g2, w1c, pre, f, w2c)

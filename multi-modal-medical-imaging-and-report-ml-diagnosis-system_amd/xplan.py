@@ -85,13 +85,15 @@ class _Rec:
         self.ops.add(L.OP_AXPBY, i=(), l=(n,), f=(a, b), p=(x, y, out))
 
     def gemm(self, A, lda, akm, B, ldb, bkm, M, N, K, C, ldc, c_dtype, bias=None, act=0,
-             preact=None, beta=0.0):
+             preact=None, beta=0.0, residual=None):
+        """residual: a [M][ldc] tensor of C's dtype added last (mmdx_gemm_res)."""
         n = L.lib().mmdx_gemm_workspace_size(self.dt, M, N, K)
-        self.ops.timed(F.gemm_cost(M, N, K, self.dt, L.dtype_code(c_dtype), beta, act, preact),
+        self.ops.timed(F.gemm_cost(M, N, K, self.dt, L.dtype_code(c_dtype),
+                                   1.0 if residual is not None else beta, act, preact),
                        L.OP_GEMM, dtype=self.dt,
                        i=(M, N, K, int(akm), int(bkm), L.dtype_code(c_dtype), act),
                        l=(lda, ldb, ldc, n), f=(1.0, beta),
-                       p=(A, B, C, bias, None, preact, self._ws(n)))
+                       p=(A, B, C, bias, None, preact, self._ws(n), residual))
 
     def gemm_wgrad_bias(self, dY, ldy, X, ldx, M, N, K, dW, ldw, db):
         """dW = dY^T X (fp32) and db = column sums of dY (mmdx_gemm_bias_grad)."""
@@ -409,9 +411,8 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
                 preact=pre)
         w2c = rf.buf((D, I))
         rf.cast_weight(w2, w2c)
-        out = rf.buf((M, D))
-        rf.copy(a, out, M * D)
-        rf.gemm(f, I, True, w2c, I, True, M, D, I, out, D, T, bias=bb2, beta=1.0)
+        out = rf.buf((M, D))   # out = a + f W2^T + b2, the residual read by the epilogue
+        rf.gemm(f, I, True, w2c, I, True, M, D, I, out, D, T, bias=bb2, residual=a)
         saves.append(dict(x=x, u1=u1, mu1=mu1, rs1=rs1, wqkv=wqkv, qkv=qkv, probs=probs,
                           att=att, woc=woc, a=a, u2=u2, mu2=mu2, rs2=rs2, w1c=w1c, pre=pre,
                           f=f, w2c=w2c))

@@ -174,6 +174,35 @@ def test_gemm_wgrad_bias(dev, dt, M, N, K):
         ((db.double().cpu() - ref).abs() / bound).max().item()
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("M,N,K,ldc", [(300, 256, 192, 256), (300, 256, 192, 257),
+                                       (37, 768, 3072, 768), (12608, 768, 64, 768)])
+def test_gemm_residual(dev, dt, M, N, K, ldc):
+    """mmdx_gemm_res: C = A B^T + bias + residual equals the copy-then-beta-1 form bit for bit
+    (vector and per-element epilogues, split-K through the reduce: K 3072 on a small grid)."""
+    g = torch.Generator().manual_seed(M + N + K + ldc)
+    A = (torch.randn(M, K, generator=g) / 8).to(dev, dt)
+    B = (torch.randn(N, K, generator=g) / 8).to(dev, dt)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = torch.randn(M, ldc, generator=g).to(dev, dt)
+    n = L.lib().mmdx_gemm_workspace_size(L.dtype_code(dt), M, N, K)
+    w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    C1 = torch.full((M, ldc), 3.0, device=dev).to(dt)
+    L.call("mmdx_gemm_res", L.dtype_code(dt), M, N, K, A.data_ptr(), K, 1, B.data_ptr(), K, 1,
+           C1.data_ptr(), ldc, L.dtype_code(dt), bias.data_ptr(), None, L.ACT_NONE, 1.0, 0.0,
+           None, res.data_ptr(), w.data_ptr(), n, L.stream())
+    C0 = res.clone()
+    L.call("mmdx_gemm", L.dtype_code(dt), M, N, K, A.data_ptr(), K, 1, B.data_ptr(), K, 1,
+           C0.data_ptr(), ldc, L.dtype_code(dt), bias.data_ptr(), None, L.ACT_NONE, 1.0, 1.0,
+           None, w.data_ptr(), n, L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(C1[:, :N], C0[:, :N])
+    if ldc > N:
+        assert torch.all(C1.float()[:, N:] == 3.0)
+    ref = A.double().cpu() @ B.double().cpu().T + bias.double().cpu() + res.double().cpu()[:, :N]
+    _close(C1[:, :N], ref, dt, "gemm residual")
+
+
 def _ws(dt, M, N, K, dev):
     n = L.lib().mmdx_gemm_workspace_size(L.dtype_code(dt), M, N, K)
     w = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)

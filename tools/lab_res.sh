@@ -1,0 +1,14 @@
+# residual-input GEMM (ViT residual without the copy) + the BiLSTM fused bias gradient:
+# tests, then C5 twice and C4 twice
+set -u
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -k "gemm" -x -q --timeout 200 --timeout-method thread > gpurun_out/t_res1.log 2>&1 || { echo "tests1 rc=$?"; tail -30 gpurun_out/t_res1.log; exit 1; }
+tail -1 gpurun_out/t_res1.log
+timeout -k 10 700 python -u -m pytest tests/test_stack_plans_gpu.py tests/test_vit_gpu.py tests/test_text_gpu.py tests/test_benched_path_gpu.py -x -q --timeout 250 --timeout-method thread > gpurun_out/t_res2.log 2>&1 || { echo "tests2 rc=$?"; tail -30 gpurun_out/t_res2.log; exit 1; }
+tail -1 gpurun_out/t_res2.log
+for rep in 1 2; do
+  timeout -k 10 300 python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/res_c5_$rep.log 2>&1 || exit 2
+  echo c5_$rep $(grep -o '"value": [0-9.]*' gpurun_out/res_c5_$rep.log)
+  timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/res_c4_$rep.log 2>&1 || exit 2
+  echo c4_$rep $(grep -o '"value": [0-9.]*' gpurun_out/res_c4_$rep.log)
+done
