@@ -397,6 +397,14 @@ int mmdx_layernorm_fwd_dropout(int dtype, const void* x, const void* residual, l
                                int D, const float* gamma, const float* beta, float eps, float p,
                                uint64_t seed, uint64_t* counter, void* y, void* sum_out,
                                float* save_mean, float* save_rstd, uint64_t* rng, void* stream);
+/* mmdx_layernorm_bwd with a residual branch's gradient added to dx before its one rounding:
+ * dx = LN'(dy) + residual_grad (the pre-LN encoder block's "x + f(LN(x))" backward, vit_b_16);
+ * residual_grad must not alias dx. */
+int mmdx_layernorm_bwd_residual(int dtype, const void* xsum, const void* dy, long rows, int D,
+                                const float* gamma, const float* save_mean,
+                                const float* save_rstd, const void* residual_grad, void* dx,
+                                float* dgamma, float* dbeta, float beta_acc, void* workspace,
+                                size_t ws_bytes, void* stream);
 /* mmdx_layernorm_bwd plus dx_drop = the dropout backward of dx with the keep bits of rng[0]
  * (bit-identical to mmdx_dropout_bwd on dx and the forward's mask). */
 int mmdx_layernorm_bwd_dropout(int dtype, const void* xsum, const void* dy, long rows, int D,

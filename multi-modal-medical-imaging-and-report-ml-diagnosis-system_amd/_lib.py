@@ -118,6 +118,8 @@ SIGNATURES = {
     "mmdx_layernorm_bwd": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, f32, vp, sz,
                                  vp]),
     "mmdx_layernorm_workspace_size": (sz, [i64, i32]),
+    "mmdx_layernorm_bwd_residual": (i32, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp,
+                                          f32, vp, sz, vp]),
     "mmdx_gemm_res": (i32, [i32, i32, i32, i32, vp, i64, i32, vp, i64, i32, vp, i64, i32, vp, vp,
                             i32, f32, f32, vp, vp, vp, sz, vp]),
     "mmdx_gemm_bias_grad_workspace_size": (sz, [i32, i32, i32, i32]),

@@ -676,7 +676,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
                                                      float* __restrict__ part, int rpw,
                                                      float p = 0.f,
                                                      const uint64_t* __restrict__ rng = nullptr,
-                                                     T* __restrict__ dx_drop = nullptr) {
+                                                     T* __restrict__ dx_drop = nullptr,
+                                                     const T* __restrict__ addin = nullptr) {
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2][D]
@@ -742,8 +743,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
       const int vi = lane + i * 64;
       if (vi < nv) {
         V o;
+        if (addin) {   // dx + a residual branch's gradient, one rounding (ViT: da = dO + LN'(.))
+          const V ai = *(const V*)(addin + row * D + vi * VEC);
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2));
+          for (int j = 0; j < VEC; ++j)
+            o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2) + to_f(ai[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2));
+        }
         *(V*)(dx + row * D + vi * VEC) = o;
         if constexpr (DROP) {
           const uint64_t dbase = rng[0];
@@ -977,7 +985,7 @@ static int layernorm_bwd_t(int dtype, const void* xsum, const void* dy, long row
                            const float* gamma, const float* save_mean, const float* save_rstd,
                            void* dx, float* dgamma, float* dbeta, float beta_acc, void* ws,
                            size_t ws_bytes, float p, const uint64_t* rng, void* dx_drop,
-                           void* stream) {
+                           void* stream, const void* addin = nullptr) {
   const int VEC = dtype == F32 ? 4 : 8;
   MMDX_CHECK_ARG(rows > 0 && D % VEC == 0 && D <= 64 * LN_MAXV * VEC, "layernorm bwd: D=%d", D);
   const int rpw = ln_bwd_rpw();
@@ -992,7 +1000,7 @@ static int layernorm_bwd_t(int dtype, const void* xsum, const void* dy, long row
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), shm, st, (const T*)xsum, (const T*)dy,
                          rows, D, gamma, save_mean, save_rstd, (T*)dx, (float*)ws, rpw, p, rng,
-                         (T*)dx_drop);
+                         (T*)dx_drop, (const T*)addin);
     };
     if (drop) {
       if (mv == 1) launch(ln_bwd_kernel<T, 1, true>);
@@ -1019,6 +1027,19 @@ extern "C" int mmdx_layernorm_bwd(int dtype, const void* xsum, const void* dy, l
                                   float beta_acc, void* ws, size_t ws_bytes, void* stream) {
   return layernorm_bwd_t(dtype, xsum, dy, rows, D, gamma, save_mean, save_rstd, dx, dgamma,
                          dbeta, beta_acc, ws, ws_bytes, 0.f, nullptr, nullptr, stream);
+}
+
+extern "C" int mmdx_layernorm_bwd_residual(int dtype, const void* xsum, const void* dy,
+                                           long rows, int D, const float* gamma,
+                                           const float* save_mean, const float* save_rstd,
+                                           const void* residual_grad, void* dx, float* dgamma,
+                                           float* dbeta, float beta_acc, void* ws,
+                                           size_t ws_bytes, void* stream) {
+  MMDX_CHECK_ARG(residual_grad && residual_grad != dx,
+                 "layernorm bwd residual: residual_grad missing or aliasing dx");
+  return layernorm_bwd_t(dtype, xsum, dy, rows, D, gamma, save_mean, save_rstd, dx, dgamma,
+                         dbeta, beta_acc, ws, ws_bytes, 0.f, nullptr, nullptr, stream,
+                         residual_grad);
 }
 
 extern "C" int mmdx_layernorm_bwd_dropout(int dtype, const void* xsum, const void* dy, long rows,

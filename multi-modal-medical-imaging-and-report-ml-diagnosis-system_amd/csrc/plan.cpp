@@ -198,6 +198,15 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_LN_BWD:
       // i: D; l: rows, ws_bytes; f: beta_acc; p: xsum, dy, gamma, mean, rstd, dx, dgamma,
       // dbeta, ws
+      // (p[9]: optional residual-branch gradient added to dx, mmdx_layernorm_bwd_residual)
+      if (P(o, 9, ext))
+        return mmdx_layernorm_bwd_residual(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
+                                           (const float*)P(o, 2, ext),
+                                           (const float*)P(o, 3, ext),
+                                           (const float*)P(o, 4, ext), P(o, 9, ext),
+                                           P(o, 5, ext), (float*)P(o, 6, ext),
+                                           (float*)P(o, 7, ext), o.f[0], P(o, 8, ext),
+                                           (size_t)o.l[1], s);
       return mmdx_layernorm_bwd(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
                                 (const float*)P(o, 2, ext), (const float*)P(o, 3, ext),
                                 (const float*)P(o, 4, ext), P(o, 5, ext), (float*)P(o, 6, ext),

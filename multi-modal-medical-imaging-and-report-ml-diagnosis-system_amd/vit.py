@@ -44,7 +44,8 @@ def _ln(x, res, g, b, want_sum):
     return y, s, mean, rstd
 
 
-def _ln_bwd(xs, dy, g, mean, rstd):
+def _ln_bwd(xs, dy, g, mean, rstd, addin=None):
+    """LayerNorm backward; addin: a residual branch's gradient added to dx (one pass)."""
     D = xs.shape[-1]
     rows = xs.numel() // D
     dx = torch.empty_like(xs)
@@ -52,8 +53,13 @@ def _ln_bwd(xs, dy, g, mean, rstd):
     db = torch.empty(D, dtype=torch.float32, device=xs.device)
     n = L.lib().mmdx_layernorm_workspace_size(rows, D)
     w = L.workspace(n, xs.device)
-    call("mmdx_layernorm_bwd", L.dtype_code(xs.dtype), ptr(xs), ptr(dy), rows, D, ptr(g),
-         ptr(mean), ptr(rstd), ptr(dx), ptr(dg), ptr(db), 0.0, ptr(w), n, stream())
+    if addin is not None:
+        call("mmdx_layernorm_bwd_residual", L.dtype_code(xs.dtype), ptr(xs), ptr(dy), rows, D,
+             ptr(g), ptr(mean), ptr(rstd), ptr(addin), ptr(dx), ptr(dg), ptr(db), 0.0, ptr(w),
+             n, stream())
+    else:
+        call("mmdx_layernorm_bwd", L.dtype_code(xs.dtype), ptr(xs), ptr(dy), rows, D, ptr(g),
+             ptr(mean), ptr(rstd), ptr(dx), ptr(dg), ptr(db), 0.0, ptr(w), n, stream())
     return dx, dg, db
 
 
@@ -176,8 +182,7 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm_wgrad_bias(dpre, I, u2, D, I, D, M, dW1, D, dbb1, compute_dtype=T)
         du2 = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dpre, I, True, w1c, D, False, M, D, I, du2, D, compute_dtype=T)
-        da_ln, dg2, db2 = _ln_bwd(a, du2, g2, mu2, rs2)
-        da = _add(dO, da_ln)
+        da, dg2, db2 = _ln_bwd(a, du2, g2, mu2, rs2, addin=dO)   # dO + LN2'(du2)
         datt = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(da, D, True, woc, D, False, M, D, D, datt, D, compute_dtype=T)
         dWo = torch.empty((D, D), dtype=torch.float32, device=dev)
@@ -190,8 +195,7 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm_wgrad_bias(dqkv, 3 * D, u1, D, 3 * D, D, M, dWqkv, D, dbqkv, compute_dtype=T)
         du1 = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dqkv, 3 * D, True, wqkv, D, False, M, D, 3 * D, du1, D, compute_dtype=T)
-        dx_ln, dg1, db1 = _ln_bwd(x, du1, g1, mu1, rs1)
-        dx = _add(da, dx_ln)
+        dx, dg1, db1 = _ln_bwd(x, du1, g1, mu1, rs1, addin=da)
         return (dx.reshape(N, S, D), None, dg1, db1, dWqkv, dbqkv, dWo, dbo, dg2, db2, dW1,
                 dbb1, dW2, dbb2)
 

@@ -141,10 +141,11 @@ class _Rec:
         self.ops.add(L.OP_LN_BWD_DROP, self.dt, i=(D,), l=(rows, n), f=(0.0, p),
                      p=(xsum, dy, g, mean, rstd, dx, dg, db, self._ws(n), rng, dx_drop))
 
-    def ln_bwd(self, xsum, dy, g, mean, rstd, rows, D, dx, dg, db):
+    def ln_bwd(self, xsum, dy, g, mean, rstd, rows, D, dx, dg, db, addin=None):
+        """addin: a residual branch's gradient added to dx (mmdx_layernorm_bwd_residual)."""
         n = L.lib().mmdx_layernorm_workspace_size(rows, D)
         self.ops.add(L.OP_LN_BWD, self.dt, i=(D,), l=(rows, n), f=(0.0,),
-                     p=(xsum, dy, g, mean, rstd, dx, dg, db, self._ws(n)))
+                     p=(xsum, dy, g, mean, rstd, dx, dg, db, self._ws(n), addin))
 
     def gelu_bwd(self, pre, dy, n, dx):
         self.ops.add(L.OP_GELU_BWD, self.dt, l=(n,), p=(pre, dy, dx))
@@ -423,8 +424,8 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
     # backward: ext 0 = upstream gradient, 1 = gradient buffer, 3 = the stack input
     rb = _Rec(pl.arena, dev, T, pl.bwd)
     dpre = rb.buf((M, I))
-    du2, da_ln, DA = rb.buf((M, D)), rb.buf((M, D)), rb.buf((M, D))
-    datt, dqkv, du1, dx_ln = rb.buf((M, D)), rb.buf((M, 3 * D)), rb.buf((M, D)), rb.buf((M, D))
+    du2, DA = rb.buf((M, D)), rb.buf((M, D))
+    datt, dqkv, du1 = rb.buf((M, D)), rb.buf((M, 3 * D)), rb.buf((M, D))
     DX = rb.buf((M, D))
     G = pl.grads
     offs = []
@@ -444,16 +445,15 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         rb.gemm_wgrad_bias(dO, D, s["f"], I, D, I, M, gx(o[10]), I, gx(o[11]))
         rb.gemm_wgrad_bias(dpre, I, s["u2"], D, I, D, M, gx(o[8]), D, gx(o[9]))
         rb.gemm(dpre, I, True, s["w1c"], D, False, M, D, I, du2, D, T)
-        rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, da_ln, gx(o[6]), gx(o[7]))
-        rb.add(dO, da_ln, M * D, DA)
+        # da = dO + LN2'(du2): the residual branch's gradient added inside the LN backward
+        rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, DA, gx(o[6]), gx(o[7]), addin=dO)
         rb.gemm(DA, D, True, s["woc"], D, False, M, D, D, datt, D, T)
         rb.gemm_wgrad_bias(DA, D, s["att"], D, D, D, M, gx(o[4]), D, gx(o[5]))
         rb.attn_bwd(s["qkv"], s["probs"], s["att"], datt, None, N, S, heads, scale, 0.0, dqkv)
         rb.gemm_wgrad_bias(dqkv, 3 * D, s["u1"], D, 3 * D, D, M, gx(o[2]), D, gx(o[3]))
         rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, du1, D, T)
         xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)
-        rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, dx_ln, gx(o[0]), gx(o[1]))
-        rb.add(DA, dx_ln, M * D, DX)
+        rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, DX, gx(o[0]), gx(o[1]), addin=DA)
         dO = DX
         pl.cut_after_layers(li, nl, lambda j: offs[j][0] if j < nl else G.n)
     pl.dx = DX

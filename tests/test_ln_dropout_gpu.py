@@ -69,3 +69,38 @@ def test_layernorm_dropout_fused_equals_unfused(dev, dt, rows, D, p):
     # the drop rate is p (binomial 6-sigma band)
     frac = 1.0 - mask.float().mean().item()
     assert abs(frac - p) <= 6 * (p * (1 - p) / mask.numel()) ** 0.5
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+def test_layernorm_bwd_residual(dev, dt):
+    """mmdx_layernorm_bwd_residual: dx = LN'(dy) + residual_grad in one rounding, gamma / beta
+    gradients unchanged (equal to mmdx_layernorm_bwd's bit for bit)."""
+    rows, D = 197, 768
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(rows, D, generator=g).to(dev, dt)
+    dy = torch.randn(rows, D, generator=g).to(dev, dt)
+    r = torch.randn(rows, D, generator=g).to(dev, dt)
+    gam = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    bet = torch.zeros(D, device=dev)
+    dc = L.dtype_code(dt)
+    st = L.stream()
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    L.call("mmdx_layernorm_fwd", dc, x.data_ptr(), None, rows, D, gam.data_ptr(), bet.data_ptr(),
+           1e-6, y.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(), st)
+    n = L.lib().mmdx_layernorm_workspace_size(rows, D)
+    ws = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    dx0, dx1 = torch.empty_like(x), torch.empty_like(x)
+    dg0, db0, dg1, db1 = (torch.empty(D, device=dev) for _ in range(4))
+    L.call("mmdx_layernorm_bwd", dc, x.data_ptr(), dy.data_ptr(), rows, D, gam.data_ptr(),
+           mean.data_ptr(), rstd.data_ptr(), dx0.data_ptr(), dg0.data_ptr(), db0.data_ptr(), 0.0,
+           ws.data_ptr(), n, st)
+    L.call("mmdx_layernorm_bwd_residual", dc, x.data_ptr(), dy.data_ptr(), rows, D,
+           gam.data_ptr(), mean.data_ptr(), rstd.data_ptr(), r.data_ptr(), dx1.data_ptr(),
+           dg1.data_ptr(), db1.data_ptr(), 0.0, ws.data_ptr(), n, st)
+    torch.cuda.synchronize()
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    want = dx0.double() + r.double()   # dx0 is rounded once already: allow two roundings
+    u = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11, torch.float32: 2.0 ** -24}[dt]
+    bound = 2 * u * (dx0.double().abs() + r.double().abs() + want.abs()) + 1e-30
+    assert ((dx1.double() - want).abs() <= bound).all()
