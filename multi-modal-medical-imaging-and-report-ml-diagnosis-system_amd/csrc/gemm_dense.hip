@@ -62,7 +62,18 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, i
 template <typename OutT>
 __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ ws,
                                                              int splits, int M, int N,
-                                                             EpiStore<OutT, true> epi) {
+                                                             EpiStore<OutT, true> epi,
+                                                             const float* __restrict__ bpart =
+                                                                 nullptr,
+                                                             float* __restrict__ db = nullptr) {
+  // fused wgrad + bias (gemm_wgrad_bias_typed): the bias partials [splits][M] are reduced by
+  // the same launch, in split order
+  if (db)
+    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
+      float sb = 0.f;
+      for (int z = 0; z < splits; ++z) sb += bpart[(long)z * M + m];
+      db[m] = sb;
+    }
   const int total4 = M * N / 4, n4 = N / 4;
   const f32x4* w = (const f32x4*)ws;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
@@ -266,15 +277,8 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
 
 // dW = A B with A = dY^T and B = X both R-major (the weight gradient of a Linear layer), plus
 // its bias gradient db = row sums of A, fused into the split-K GEMM (EpiPartialBias) and
-// reduced over the splits here; bias partials follow the fp32 slabs in the workspace.
-__global__ void bias_part_reduce_kernel(const float* __restrict__ bpart, int splits, int M,
-                                        float* __restrict__ db) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += bpart[(long)z * M + m];
-  db[m] = s;
-}
+// reduced over the splits by the split-K reduce launch; bias partials follow the fp32 slabs
+// in the workspace.
 
 static bool wgrad_bias_fused_on() {   // MMDX_WGRAD_BIAS_FUSED=0: GEMM + column-sum kernels
   static const bool on = [] {
@@ -299,9 +303,7 @@ static int gemm_wgrad_bias_typed(const SplitPlan& p, int M, int N, int K, const 
   const long total = (long)M * N;
   const int blocks = (int)std::min<long>((total / 4 + 255) / 256, 8192);
   hipLaunchKernelGGL(splitk_reduce4_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
-                     (const float*)ws, p.splits, M, N, epi);
-  hipLaunchKernelGGL(bias_part_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, st,
-                     (const float*)part.bpart, p.splits, M, db);
+                     (const float*)ws, p.splits, M, N, epi, (const float*)part.bpart, db);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
