@@ -715,6 +715,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
       dv[i] = dn[i];
     }
     if (rr + 1 < rpw && row + 1 < rows) fetch(row + 1);
+    // the residual branch's gradient is loaded here, not at the store: a load issued after
+    // the row's wave sums left its whole latency exposed on every row (C5 -1.5 %)
+    V ai[MV];
+    if (addin) {
+#pragma unroll
+      for (int i = 0; i < MV; ++i) {
+        const int vi = lane + i * 64;
+        if (vi < nv) ai[i] = *(const V*)(addin + row * D + vi * VEC);
+      }
+    }
     float xh[MV][VEC], g[MV][VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -744,10 +754,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ xs,
       if (vi < nv) {
         V o;
         if (addin) {   // dx + a residual branch's gradient, one rounding (ViT: da = dO + LN'(.))
-          const V ai = *(const V*)(addin + row * D + vi * VEC);
 #pragma unroll
           for (int j = 0; j < VEC; ++j)
-            o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2) + to_f(ai[j]));
+            o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2) + to_f(ai[i][j]));
         } else {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) o[j] = from_f<T>(rstd * (g[i][j] - s1 - xh[i][j] * s2));

@@ -182,7 +182,12 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm_wgrad_bias(dpre, I, u2, D, I, D, M, dW1, D, dbb1, compute_dtype=T)
         du2 = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dpre, I, True, w1c, D, False, M, D, I, du2, D, compute_dtype=T)
-        da, dg2, db2 = _ln_bwd(a, du2, g2, mu2, rs2, addin=dO)   # dO + LN2'(du2)
+        from .xplan import VIT_LN_ADDIN
+        if VIT_LN_ADDIN:   # dO + LN2'(du2) in one pass (xplan._build_vit's choice)
+            da, dg2, db2 = _ln_bwd(a, du2, g2, mu2, rs2, addin=dO)
+        else:
+            da_ln, dg2, db2 = _ln_bwd(a, du2, g2, mu2, rs2)
+            da = _add(dO, da_ln)
         datt = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(da, D, True, woc, D, False, M, D, D, datt, D, compute_dtype=T)
         dWo = torch.empty((D, D), dtype=torch.float32, device=dev)
@@ -195,7 +200,11 @@ class _VitBlockFn(torch.autograd.Function):
         F.gemm_wgrad_bias(dqkv, 3 * D, u1, D, 3 * D, D, M, dWqkv, D, dbqkv, compute_dtype=T)
         du1 = torch.empty((M, D), dtype=T, device=dev)
         F.gemm(dqkv, 3 * D, True, wqkv, D, False, M, D, 3 * D, du1, D, compute_dtype=T)
-        dx, dg1, db1 = _ln_bwd(x, du1, g1, mu1, rs1, addin=da)
+        if VIT_LN_ADDIN:
+            dx, dg1, db1 = _ln_bwd(x, du1, g1, mu1, rs1, addin=da)
+        else:
+            dx_ln, dg1, db1 = _ln_bwd(x, du1, g1, mu1, rs1)
+            dx = _add(da, dx_ln)
         return (dx.reshape(N, S, D), None, dg1, db1, dWqkv, dbqkv, dWo, dbo, dg2, db2, dW1,
                 dbb1, dW2, dbb2)
 

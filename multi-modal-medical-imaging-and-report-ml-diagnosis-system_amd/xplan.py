@@ -30,6 +30,9 @@ from . import functional as F
 from .resnet import _Arena, _Ext, _OpList, _Token, plan_cache_get
 
 _WS_TOKEN = 0x1   # placeholder operand for the plan's workspace (patched when sized)
+# ViT backward: residual-branch gradient added inside the LayerNorm backward (1, default) or
+# by a separate add pass (0); read by vit.py's eager path too
+VIT_LN_ADDIN = os.environ.get("MMDX_VIT_LN_ADDIN", "1") == "1"
 _F32 = torch.float32
 
 
@@ -424,7 +427,7 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
     # backward: ext 0 = upstream gradient, 1 = gradient buffer, 3 = the stack input
     rb = _Rec(pl.arena, dev, T, pl.bwd)
     dpre = rb.buf((M, I))
-    du2, DA = rb.buf((M, D)), rb.buf((M, D))
+    du2, DA, da_ln = rb.buf((M, D)), rb.buf((M, D)), rb.buf((M, D))
     datt, dqkv, du1 = rb.buf((M, D)), rb.buf((M, 3 * D)), rb.buf((M, D))
     DX = rb.buf((M, D))
     G = pl.grads
@@ -446,14 +449,25 @@ def _build_vit(params, N, S, D, heads, I, eps, T, dev):
         rb.gemm_wgrad_bias(dpre, I, s["u2"], D, I, D, M, gx(o[8]), D, gx(o[9]))
         rb.gemm(dpre, I, True, s["w1c"], D, False, M, D, I, du2, D, T)
         # da = dO + LN2'(du2): the residual branch's gradient added inside the LN backward
-        rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, DA, gx(o[6]), gx(o[7]), addin=dO)
+        # (mmdx_layernorm_bwd_residual; MMDX_VIT_LN_ADDIN=0: a separate add pass).  Within the
+        # box-to-box spread on C5: -0.8 % and +1.2 % against the add pass on two boxes, paired
+        # (profiles/r04_c5_ab_ln_addin.txt)
+        if VIT_LN_ADDIN:
+            rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, DA, gx(o[6]), gx(o[7]), addin=dO)
+        else:
+            rb.ln_bwd(s["a"], du2, g2, s["mu2"], s["rs2"], M, D, da_ln, gx(o[6]), gx(o[7]))
+            rb.add(dO, da_ln, M * D, DA)
         rb.gemm(DA, D, True, s["woc"], D, False, M, D, D, datt, D, T)
         rb.gemm_wgrad_bias(DA, D, s["att"], D, D, D, M, gx(o[4]), D, gx(o[5]))
         rb.attn_bwd(s["qkv"], s["probs"], s["att"], datt, None, N, S, heads, scale, 0.0, dqkv)
         rb.gemm_wgrad_bias(dqkv, 3 * D, s["u1"], D, 3 * D, D, M, gx(o[2]), D, gx(o[3]))
         rb.gemm(dqkv, 3 * D, True, s["wqkv"], D, False, M, D, 3 * D, du1, D, T)
         xin = s["x"] if not isinstance(s["x"], _Ext) else _Ext(3)
-        rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, DX, gx(o[0]), gx(o[1]), addin=DA)
+        if VIT_LN_ADDIN:
+            rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, DX, gx(o[0]), gx(o[1]), addin=DA)
+        else:
+            rb.ln_bwd(xin, du1, g1, s["mu1"], s["rs1"], M, D, da_ln, gx(o[0]), gx(o[1]))
+            rb.add(DA, da_ln, M * D, DX)
         dO = DX
         pl.cut_after_layers(li, nl, lambda j: offs[j][0] if j < nl else G.n)
     pl.dx = DX
