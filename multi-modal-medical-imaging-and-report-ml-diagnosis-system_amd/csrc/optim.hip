@@ -16,6 +16,9 @@ __global__ void step_incr_kernel(float* step, const float* found_inf) {
   step[0] += 1.f;
 }
 
+// 16-B vectors per thread per loop iteration of the AdamW update
+constexpr int ADAMW_U = 4;
+
 __device__ __forceinline__ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // p <- p*(1-lr*wd); m <- lerp(m, g, 1-b1); v <- b2*v + (1-b2) g^2;
@@ -46,9 +49,45 @@ __global__ __launch_bounds__(256) void adamw_kernel(const mmdx_adamw_tensor* __r
   long i0 = 0;
   if (aligned16(d.p) && aligned16(d.g) && aligned16(d.m) && aligned16(d.v)) {
     const long nv = n / 4;
-    for (long i = threadIdx.x; i < nv; i += blockDim.x) {
-      f32x4 p = ((f32x4*)d.p)[i], m = ((f32x4*)d.m)[i], v = ((f32x4*)d.v)[i];
-      const f32x4 g = ((const f32x4*)d.g)[i];
+    f32x4* P = (f32x4*)d.p;
+    f32x4* Mv = (f32x4*)d.m;
+    f32x4* Vv = (f32x4*)d.v;
+    const f32x4* G = (const f32x4*)d.g;
+    // ADAMW_U vectors per thread per iteration, all loads issued before any store (the
+    // stores may alias the next iteration's loads as far as the compiler knows, so a
+    // one-vector loop kept one 64-B group of loads in flight per thread)
+    long i = threadIdx.x;
+    for (; i + (ADAMW_U - 1) * (long)blockDim.x < nv; i += ADAMW_U * (long)blockDim.x) {
+      f32x4 p[ADAMW_U], m[ADAMW_U], v[ADAMW_U], g[ADAMW_U];
+#pragma unroll
+      for (int u = 0; u < ADAMW_U; ++u) {
+        const long k = i + u * (long)blockDim.x;
+        p[u] = P[k];
+        m[u] = Mv[k];
+        v[u] = Vv[k];
+        g[u] = G[k];
+      }
+#pragma unroll
+      for (int u = 0; u < ADAMW_U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float pj = p[u][j], mj = m[u][j], vj = v[u][j];
+          adamw_elem(pj, g[u][j] * gs, mj, vj, decay, beta1, beta2, step_size, bc2s, eps);
+          p[u][j] = pj;
+          m[u][j] = mj;
+          v[u][j] = vj;
+        }
+#pragma unroll
+      for (int u = 0; u < ADAMW_U; ++u) {
+        const long k = i + u * (long)blockDim.x;
+        P[k] = p[u];
+        Mv[k] = m[u];
+        Vv[k] = v[u];
+      }
+    }
+    for (; i < nv; i += blockDim.x) {
+      f32x4 p = P[i], m = Mv[i], v = Vv[i];
+      const f32x4 g = G[i];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float pj = p[j], mj = m[j], vj = v[j];
@@ -57,9 +96,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(const mmdx_adamw_tensor* __r
         m[j] = mj;
         v[j] = vj;
       }
-      ((f32x4*)d.p)[i] = p;
-      ((f32x4*)d.m)[i] = m;
-      ((f32x4*)d.v)[i] = v;
+      P[i] = p;
+      Mv[i] = m;
+      Vv[i] = v;
     }
     i0 = nv * 4;
   }

@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import os
+
 import numpy as np
 import torch
 
@@ -19,7 +21,10 @@ from . import _lib as L
 from ._lib import call, ptr, stream
 
 
-CHUNK = 1 << 16  # elements per workgroup descriptor
+# elements per workgroup descriptor (MMDX_ADAMW_CHUNK for A/B runs).  16K: C5's 196 M
+# parameters in 64K chunks were ~3000 blocks, 1.5 rounds of the 2048 resident slots (a
+# half-empty tail); 16K / 8K chunks +0.3 % on C5 and C4, paired (profiles/r04_adamw_ab.txt)
+CHUNK = int(os.environ.get("MMDX_ADAMW_CHUNK", str(1 << 14)))
 
 # Pinned staging buffers cannot be allocated while a stream is capturing a graph, so the
 # eager path keeps a few spares (at most _MAX_SPARES, the largest kept) for a later capture.
