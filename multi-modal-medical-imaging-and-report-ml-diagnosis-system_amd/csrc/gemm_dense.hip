@@ -113,12 +113,16 @@ static long gemm256_min_tiles() {
 // The same threshold for the forward orientation only (both operands k-major: x W^T), where
 // the isolated C5 table has the 256 x 256 tiles 3-8 % ahead on the ViT-B shapes while the
 // backward orientations and the BERT-base shapes lose (profiles/r03n_gemm_bench_f16.txt).
-// Default 400 tiles: the ViT-B QKV and FFN-up GEMMs at 64 images (450 / 600 tiles); C5
-// 2227 / 2234 vs 2204 / 2193 samples/s (profiles/r03u_c5_ab_gemm256fwd.txt); 0 disables
+// Default 90 tiles: every C5 encoder forward GEMM (ViT-B QKV / FFN-up 450 / 600 tiles, ViT-B
+// N = 768 150, BERT-base QKV / FFN-up 288 / 384, BERT-base N = 768 96).  Round 3 set 400 (the
+// ViT-B QKV / FFN-up only; profiles/r03u_c5_ab_gemm256fwd.txt); on the round-4 kernels (vector
+// epilogue, residual input) 400 / 300 / 200 / 140 / 90 / 60 / 30 / 1 gave C5 2772 / 2781 / 2797
+// / 2831 / 2863-2876 / 2877 / 2877 / 2871 samples/s, C4 neutral
+// (profiles/r04_gemm256_fwd_sweep.txt); 0 disables
 static long gemm256_fwd_min_tiles() {
   static const long v = [] {
     const char* e = getenv("MMDX_GEMM256_FWD_MIN");
-    return e ? atol(e) : 400L;
+    return e ? atol(e) : 90L;
   }();
   return v;
 }
