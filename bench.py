@@ -253,10 +253,10 @@ def graph_text_tower(txt, ids, mask):
 def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_bwd=None,
               scaler=None, text_fn=None):
     """One train step.  `scaler` (mmdx.GradScaler, the fp16 C5 path): the loss
-    is scaled before the backward (TP:1056), the clip coefficient is taken on the unscaled
-    norm and folded with 1/scale into AdamW's gradient scale, an overflow skips the update
-    and backs the scale off (TP:1058-1061; the clip sees true gradients, the order
-    torch.amp documents — the reference's loop clips the scaled ones)."""
+    is scaled before the backward (TP:1056), clip_grad_norm_(1.0) is taken on the SCALED
+    gradients as the reference's loop does (TP:1058, before scaler.step unscales them,
+    TP:1060), the clip coefficient is folded with 1/scale into AdamW's gradient scale, and an
+    overflow skips the update and backs the scale off (TP:1060-1061)."""
     import mmdx
     from mmdx import optim as MO
     from mmdx.schedule import TwoTowerForward, two_tower_backward
@@ -291,7 +291,8 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
             reducer.reduce()
         with rng("mmdx/optimizer"):
             if scaler is not None:
-                step.norm = scaler.clip_and_step(opt, 1.0, unscale_first=True, params=params)
+                # the reference's order (TP:1056-1061): clip on the scaled gradients
+                step.norm = scaler.clip_and_step(opt, 1.0, unscale_first=False, params=params)
                 scaler.update()
             else:
                 step.norm, scale = MO.grad_norm(params, 1.0)
@@ -605,9 +606,8 @@ def main():
         "mfma_util_pmc": load_mfma_util(args.config),
         "amp": ({"loss_scaling": "mmdx.GradScaler (init 2^16, growth 2 per 2000 clean steps, "
                                  "backoff 0.5, device-side inf check, overflow skips AdamW)",
-                 "clip_order": "unscale -> clip_grad_norm_(1.0) -> AdamW (torch.amp's "
-                               "documented order); the reference TP:1056-1058 clips the "
-                               "SCALED gradients before scaler.step unscales them"}
+                 "clip_order": "reference (scaled): clip_grad_norm_(1.0) on the SCALED "
+                               "gradients, then scaler.step unscales (TP:1056-1061)"}
                 if scaler is not None else None),
         "roofline": {
             "kernel": ("igemm_dma_kernel (dense GEMMs of the ViT-B/16 and BERT-base encoders, "

@@ -54,14 +54,6 @@ const char* mmdx_last_error(void);
  * TextEncoderTransformer.proj/classifier (TP:365,367), BERT dense layers (TP:360 ->
  * transformers BertModel), fusion_mlp[0] + GELU (TP:534-536), disease_head (TP:542). */
 size_t mmdx_gemm_workspace_size(int dtype, int M, int N, int K);
-/* Weight gradient of a Linear layer with its bias gradient: C = A B for A = dY^T and B = X
- * both R-major (element (m, k) of A at A[k*lda + m]: dY [K tokens][lda]), alpha 1, beta 0,
- * and db[m] = sum_k A(m, k) (the column sums of dY) — for 16-bit split-K problems computed by
- * the GEMM blocks of column tile 0 from their own A fragments (one extra MFMA per fragment
- * against a ones operand) and reduced over the splits, so dY is not read again; otherwise
- * (fp32, unsplit grids, unaligned operands, MMDX_WGRAD_BIAS_FUSED=0) mmdx_gemm followed by
- * mmdx_bias_grad (needs lda == M).
- * Replaces: the weight and bias gradients of nn.Linear in the BERT / ViT layers (TP:360). */
 /* mmdx_gemm plus a residual [M][ldc] of C's dtype added last (after the activation and
  * beta*C): C = act(alpha*A B^T + bias) + beta*C + residual; residual must not alias C.
  * Replaces: the residual adds of torchvision's EncoderBlock (x + mlp(ln_2(x)), vit_b_16). */
@@ -70,6 +62,14 @@ int mmdx_gemm_res(int dtype, int M, int N, int K, const void* A, long lda, int a
                   const float* bias, const float* addend, int act, float alpha, float beta,
                   void* preact, const void* residual, void* workspace, size_t ws_bytes,
                   void* stream);
+/* Weight gradient of a Linear layer with its bias gradient: C = A B for A = dY^T and B = X
+ * both R-major (element (m, k) of A at A[k*lda + m]: dY [K tokens][lda]), alpha 1, beta 0,
+ * and db[m] = sum_k A(m, k) (the column sums of dY) — for 16-bit split-K problems computed by
+ * the GEMM blocks of column tile 0 from their own A fragments (one extra MFMA per fragment
+ * against a ones operand) and reduced over the splits, so dY is not read again; otherwise
+ * (fp32, unsplit grids, unaligned operands, MMDX_WGRAD_BIAS_FUSED=0) mmdx_gemm followed by
+ * mmdx_bias_grad (needs lda == M).
+ * Replaces: the weight and bias gradients of nn.Linear in the BERT / ViT layers (TP:360). */
 size_t mmdx_gemm_bias_grad_workspace_size(int dtype, int M, int N, int K);
 int mmdx_gemm_bias_grad(int dtype, int M, int N, int K, const void* A, long lda, const void* B,
                         long ldb, void* C, long ldc, int c_dtype, float* db, void* workspace,

@@ -9,7 +9,7 @@ The reference's fusion loop enables AMP whenever it runs on a GPU (TP:1025-1026:
 
 Everything stays on the device (no host sync per step): the scale and the growth tracker
 are device scalars, `found_inf` comes out of the same pass that computes the gradient norm
-(mmdx_grad_norm_amp: the sum of squares is inf/NaN iff some gradient is), the unscale rides
+(mmdx_grad_norm_amp: a per-chunk non-finite flag beside the sum of squares), the unscale rides
 in AdamW's `grad_scale`, an overflowed step is skipped inside the AdamW launch
 (mmdx_adamw_multi_amp: no update, no step count), and `update()` is one tiny kernel
 (mmdx_amp_update_scale = torch._amp_update_scale_).
@@ -78,6 +78,7 @@ class GradScaler:
         self._opt_inf = {}           # id(optimizer) -> its own found_inf device scalar
         self._step_infs = {}         # the optimizers checked since the last update()
         self._unscaled = {}
+        self._noop = False           # a step / clip_and_step since the last update() found no grads
 
     def is_enabled(self):
         return self._enabled
@@ -138,6 +139,7 @@ class GradScaler:
             return optimizer.step(*args, **kwargs)
         ps = self._params(optimizer)
         if not ps:
+            self._noop = True
             return None
         if id(optimizer) in self._unscaled:
             return optimizer.step(*args, found_inf=self._opt_inf[id(optimizer)], **kwargs)
@@ -151,6 +153,7 @@ class GradScaler:
         ps = params if params is not None else self._params(optimizer)
         ps = [p for p in ps if p.grad is not None]
         if not ps:   # no gradients: nothing to clip or step (clip_grad_norm_ returns 0)
+            self._noop = True
             return torch.zeros(())
         if not self._enabled:
             norm, s = grad_norm(ps, max_norm)
@@ -170,6 +173,10 @@ class GradScaler:
         else:
             infs = list(self._step_infs.values())
             if not infs:
+                if self._noop:   # the steps since the last update() had no gradients: the
+                    self._noop = False   # scale and the growth tracker stay as they are
+                    self._unscaled.clear()
+                    return
                 raise AssertionError("No inf checks were recorded prior to update.")
             # any optimizer's overflow backs the scale off (torch.amp.GradScaler.update)
             self._found_inf = infs[0] if len(infs) == 1 else torch.stack(infs).amax(0)
@@ -177,6 +184,7 @@ class GradScaler:
                  ptr(self._found_inf), self._growth, self._backoff, self._interval, stream())
         self._step_infs = {}
         self._unscaled.clear()
+        self._noop = False
 
     def state_dict(self):
         if not self._enabled:

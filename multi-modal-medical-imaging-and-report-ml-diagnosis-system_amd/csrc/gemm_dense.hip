@@ -118,13 +118,11 @@ static long gemm256_min_tiles() {
 // ViT-B QKV / FFN-up only; profiles/r03u_c5_ab_gemm256fwd.txt); on the round-4 kernels (vector
 // epilogue, residual input) 400 / 300 / 200 / 140 / 90 / 60 / 30 / 1 gave C5 2772 / 2781 / 2797
 // / 2831 / 2863-2876 / 2877 / 2877 / 2871 samples/s, C4 neutral
-// (profiles/r04_gemm256_fwd_sweep.txt); 0 disables
+// (profiles/r04_gemm256_fwd_sweep.txt); 0 disables.  Read per launch like the other tile
+// knobs, so a test can pin the 4-wave 128 x 128 kernel as its baseline.
 static long gemm256_fwd_min_tiles() {
-  static const long v = [] {
-    const char* e = getenv("MMDX_GEMM256_FWD_MIN");
-    return e ? atol(e) : 90L;
-  }();
-  return v;
+  const char* e = getenv("MMDX_GEMM256_FWD_MIN");
+  return e ? atol(e) : 90L;
 }
 
 // The 256 x 256 tiles with 32-deep K tiles in NS = 3 / 4 stages (MMDX_GEMM256_NS; 0 = the

@@ -993,7 +993,9 @@ struct EpiStore {
     if (addend && ((uintptr_t)addend & 15) != 0) return false;
     if (preact && ((uintptr_t)preact & 15) != 0) return false;
     if (res && ((uintptr_t)res & 15) != 0) return false;
-    if (act == ACT_GELU_BWD) return !acc_src && !res && preact;
+    // the vector GELU-backward branch computes alpha*acc*gelu'(pre) + beta*C only: a bias or
+    // addend takes the per-element path (apply() adds them)
+    if (act == ACT_GELU_BWD) return !acc_src && !res && !bias && !addend && preact;
     return !(acc_src && (bias || addend || preact || res || act != ACT_NONE));
   }
   // 8 consecutive columns n..n+7 of row m (vec8_ok() checked by the caller)

@@ -141,9 +141,11 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const mmdx_adamw_tensor* __r
   }
   acc = block_sum<256>(acc, red);
   bad = __syncthreads_or(bad);
-  // a chunk holding an inf/NaN gradient reports NaN; finite gradients whose squares overflow
-  // report +inf — norm_finalize tells the two apart (found_inf only for the first)
-  if (threadIdx.x == 0) part[blockIdx.x] = bad ? __builtin_nanf("") : acc;
+  // the sum of squares passes through unchanged (an inf gradient gives +inf, a NaN one NaN,
+  // as torch's norm); a chunk holding an inf/NaN element sets the partial's sign bit (a sum of
+  // squares is otherwise >= 0, so the bit is free) — finite gradients whose squares overflow
+  // give +inf without it, and norm_finalize raises found_inf only for the flagged ones
+  if (threadIdx.x == 0) part[blockIdx.x] = bad ? copysignf(acc, -1.f) : acc;
 }
 
 // norm = sqrt(sum of partials); scale = clip coefficient (torch.nn.utils.clip_grad_norm_:
@@ -159,19 +161,31 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const float* __restr
                                                             int unscale_first, float* found_inf) {
   __shared__ float red[4];
   float acc = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
+  bool bad = false;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float v = part[i];
+    bad |= signbit(v);
+    acc += fabsf(v);
+  }
   acc = block_sum<256>(acc, red);
+  bad = __syncthreads_or(bad);
   if (threadIdx.x == 0) {
     float nrm = sqrtf(acc);
     const float inv = loss_scale ? 1.f / loss_scale[0] : 1.f;
     if (loss_scale && unscale_first) nrm *= inv;
     norm[0] = nrm;
-    float s = max_norm > 0.f ? fminf(1.f, max_norm / (nrm + 1e-6f)) : 1.f;
+    // torch.nn.utils.clip_grad_norm_: clamp(max_norm / (norm + 1e-6), max=1) — 0 for an inf
+    // norm, NaN for a NaN one (clamp keeps a NaN; fminf would return 1)
+    float s = 1.f;
+    if (max_norm > 0.f) {
+      const float c = max_norm / (nrm + 1e-6f);
+      s = isnan(c) ? c : fminf(1.f, c);
+    }
     if (scale) scale[0] = s * inv;
-    // found_inf: some gradient element is inf/NaN (its chunk's partial is NaN), as
-    // torch._amp_foreach_non_finite_check_and_unscale_; an overflow of the sum of squares of
-    // finite gradients is not an overflow of the gradients
-    if (found_inf) found_inf[0] = isnan(acc) ? 1.f : 0.f;
+    // found_inf: some gradient element is inf/NaN (its chunk's partial carries the sign
+    // flag), as torch._amp_foreach_non_finite_check_and_unscale_; an overflow of the sum of
+    // squares of finite gradients is not an overflow of the gradients
+    if (found_inf) found_inf[0] = bad ? 1.f : 0.f;
   }
 }
 

@@ -9,6 +9,8 @@ gradients, scaler.step, scaler.update) and in torch's documented order (unscale_
 * The fused `clip_and_step` equals the unfused clip_grad_norm_ + scaler.step sequence.
 * scaler.scale(loss) and its backward multiply by the scale (mmdx_mul_dev_scalar).
 """
+import math
+
 import pytest
 import torch
 
@@ -192,3 +194,33 @@ def test_clip_and_step_without_gradients(dev):
     sc = mmdx.GradScaler()
     norm = sc.clip_and_step(opt, 1.0)
     assert float(norm) == 0.0
+    sc.scale(torch.ones((), device=dev))
+    sc.clip_and_step(opt, 1.0)
+    sc.update()                # a no-gradient step records no inf check: update() keeps state
+    torch.cuda.synchronize()
+    assert sc.get_scale() == 2.0 ** 16
+
+
+@pytest.mark.parametrize("bad", [float("inf"), float("nan")])
+def test_clip_norm_nonfinite_matches_torch(dev, bad):
+    """Without AMP, an inf (NaN) gradient makes clip_grad_norm_ return an inf (NaN) norm and a
+    clip coefficient of 0 (NaN), as torch.nn.utils.clip_grad_norm_ does; the non-finite flag
+    rides beside the sum of squares, not in it."""
+    g = torch.Generator().manual_seed(3)
+    vals = [torch.randn(300, generator=g), torch.randn(17, 5, generator=g)]
+    vals[1][2, 3] = bad
+    mine = [torch.nn.Parameter(v.clone().to(dev)) for v in vals]
+    ref = [torch.nn.Parameter(v.clone().to(dev)) for v in vals]
+    for p, v in zip(mine + ref, vals + vals):
+        p.grad = v.clone().to(dev) * 0.5
+    n_mine = mmdx.clip_grad_norm_(mine, 1.0)
+    n_ref = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    torch.cuda.synchronize()
+    nm, nr = float(n_mine), float(n_ref)
+    assert (math.isinf(nm) and math.isinf(nr)) if bad == float("inf") else \
+        (math.isnan(nm) and math.isnan(nr)), (nm, nr)
+    for a, b in zip(mine, ref):   # the clipped gradients: same finite / inf / NaN pattern
+        ga, gb = a.grad.cpu(), b.grad.cpu()
+        assert torch.equal(torch.isnan(ga), torch.isnan(gb))
+        fin = torch.isfinite(gb)
+        assert torch.equal(ga[fin], gb[fin])

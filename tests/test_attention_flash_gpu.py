@@ -4,9 +4,11 @@ vs the P-saving kernels it replaces on the benched path.
 The forward is the P-saving kernel with the row log-sum-exp written instead of P, so its
 output must be bit-identical to mmdx_attention_fwd's (same dropout mask from the same seed and
 counter).  The backward recomputes P and the keep bits and takes rowsum(P o dP) as dO . O:
-its gradients must match torch's autograd of the same masked, dropped-out attention within
-the 16-bit bar of test_text_gpu.py::test_attention (5e-2 relative), and the P-saving
-backward's within 2e-2 of each other.
+its gradients must match torch's autograd of the same masked, dropped-out attention, and
+the P-saving backward's.  The bars are multiples of the 16-bit unit roundoff u (bf16 2^-8,
+fp16 2^-11), relative to the output's / each gradient's own scale: the kernels round P (and
+dS) to the 16-bit type before each product and the outputs once; the output within 4u of
+torch's fp32, gradients within 8u of torch and 4u of the P-saving kernels.
 """
 import pytest
 import torch
@@ -15,6 +17,8 @@ from mmdx import _lib as L
 from parity_util import rel_err
 
 pytestmark = pytest.mark.gpu
+
+U = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}   # unit roundoff of the 16-bit type
 
 
 def _run(dev, dt, B, Ls, H, masked, pd, seed=77):
@@ -77,8 +81,11 @@ def _run(dev, dt, B, Ls, H, masked, pd, seed=77):
 @pytest.mark.parametrize("masked,pd", [(False, 0.0), (True, 0.0), (True, 0.1)])
 def test_flash_attention(dev, dt, B, Ls, H, masked, pd):
     r = _run(dev, dt, B, Ls, H, masked, pd)
+    u = U[dt]
     assert torch.equal(r["out1"], r["out0"]), "forward output differs from the P-saving kernel"
-    assert rel_err(r["out1"], r["o"]) <= 3e-2
+    eo = rel_err(r["out1"], r["o"])
+    print(f"  out err {eo / u:.2f}u", end="")
+    assert eo <= 4 * u, eo
     ref_lse = torch.logsumexp(r["s"], -1)
     assert (r["lse"].cpu() - ref_lse).abs().max().item() <= 1e-3 * max(1.0, ref_lse.abs().max())
     assert torch.isfinite(r["dq1"]).all()
@@ -93,13 +100,14 @@ def test_flash_attention(dev, dt, B, Ls, H, masked, pd):
         d = r["dq1"].float().cpu()
         assert (d[:, :, 0].abs() <= 0.125 * ds_max * k.abs() + 1e-6).all(), "dQ at L = 1"
         assert (d[:, :, 1].abs() <= 0.125 * ds_max * q.abs() + 1e-6).all(), "dK at L = 1"
-        assert _err(r["dq1"], r["grad"], 2) <= 5e-2
+        assert _err(r["dq1"], r["grad"], 2) <= 8 * u
         return
     for i, name in enumerate("qkv"):
         e = _err(r["dq1"], r["grad"], i)
-        assert e <= 5e-2, f"d{name} vs torch {e}"
         e2 = _err(r["dq1"], r["dq0"].float().cpu(), i)
-        assert e2 <= 2e-2, f"d{name} vs P-saving kernels {e2}"
+        print(f" d{name} {e / u:.2f}u / {e2 / u:.2f}u", end="")
+        assert e <= 8 * u, f"d{name} vs torch {e}"
+        assert e2 <= 4 * u, f"d{name} vs P-saving kernels {e2}"
 
 
 def _err(got, ref, i):
@@ -118,5 +126,6 @@ def test_flash_attention_vit_bert_shapes(dev):
     for Ls, masked, pd in ((197, False, 0.0), (128, True, 0.1)):
         r = _run(dev, torch.float16, 4, Ls, 12, masked, pd)
         assert torch.equal(r["out1"], r["out0"])
+        assert rel_err(r["out1"], r["o"]) <= 4 * U[torch.float16]
         for i in range(3):
-            assert _err(r["dq1"], r["grad"], i) <= 5e-2
+            assert _err(r["dq1"], r["grad"], i) <= 8 * U[torch.float16]

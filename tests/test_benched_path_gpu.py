@@ -42,9 +42,16 @@ checked on its own inputs in test_trunk_launches_gpu.py.
     percentile and the maximum <= 2x autocast's + 1e-2;
   - BERT key biases (exact gradient zero: the softmax cancels them): norm <= 2e-2 (fp32:
     1e-4) x the same layer's query-bias gradient norm;
-  - every other gradient (heads, text towers, ViT / BERT layers): 1 - cos <= max(2e-3,
+  - every other gradient (heads, text towers) of the bf16 configs: 1 - cos <= max(2e-3,
     2x autocast's), norm error <= max(5e-3, 2x autocast's);
-  - the update equals torch AdamW + clip on the step's own (unscaled) gradients (rtol 1e-5);
+  - C5 (fp16, every tensor is in this bin): per tensor 1 - cos <= 3x autocast's + 1e-6 and
+    norm error <= 3x autocast's + 1e-5 — no floor far above what the kernels deliver; logits
+    max / rms error <= 2x autocast's + 1e-5;
+  - the update equals torch AdamW + clip on the step's own gradients (rtol 1e-5) — for C5 in
+    the reference's GradScaler order (TP:1056-1061: clip on the SCALED gradients, then
+    scaler.step unscales), which is what the bench runs; and the C5 update per tensor within
+    3x (+1e-4) of the reference-order torch-autocast oracle's update against the same order
+    applied to the fp32 oracle's gradients;
   - fp16 + GradScaler: no overflow at the first step (the update must happen); the fp16
     error bar is torch's own fp16 autocast of the oracle module on the GPU (CPU fp16
     autocast is emulated on the box's host: minutes per step) with torch's GradScaler in
@@ -226,29 +233,45 @@ def _mmdx_step(dev, cfg, dt):
     for n, p in after.items():
         assert torch.isfinite(p).all(), n
     bufs = {n: b.detach().cpu() for n, b in wrap.named_buffers() if "running" in n}
-    inv = 1.0 / scaler.get_scale() if scaler is not None else 1.0  # grads hold scale * g
+    # the loss scale the step used (no overflow at step 1, so update() has not changed it)
+    S = scaler.get_scale() if scaler is not None else None
+    inv = 1.0 / S if scaler is not None else 1.0  # grads hold scale * g
     return {"logits": cap.out["disease_logits"].float().cpu(), "loss": loss.item(),
             "grads": {n: g.float() * inv for n, g in _grads(wrap).items()}, "bufs": bufs,
             "norm": float(step.norm.item()), "before": before, "after": after,
-            "lr": _lr_of(wrap)}
+            "lr": _lr_of(wrap), "loss_scale": S}
 
 
-def _adamw_on_my_grads(m, cfg):
+def _adamw_step(before, grads, cfg, loss_scale=None):
     """torch.optim.AdamW + clip_grad_norm_(1.0) (the oracle's optimizer, TP:1018-1023 /
-    TP:1058) applied on the CPU to the benched step's OWN gradients from the same
-    parameters: the post-step parameters the benched update must reproduce."""
+    TP:1058) applied on the CPU to `grads` (unscaled) from the parameters `before`.  With
+    `loss_scale` S the reference's GradScaler order (TP:1056-1061): the clip sees the SCALED
+    gradients S*g, then scaler.step unscales (exact: S is a power of two) and steps."""
     image, text, _, _ = CFGS[cfg]
     ref = R.RefMultimodal(image, text, bert_layers=12, dropout=0.0)
     md = torch.nn.ModuleDict({"image": ref.image, "text": ref.text, "fusion": ref.fusion})
+    S = float(loss_scale) if loss_scale else 1.0
     with torch.no_grad():
         for n, p in md.named_parameters():
-            p.copy_(m["before"][n])
-            g = m["grads"].get(n)
-            p.grad = None if g is None else g.float().cpu().clone()
+            p.copy_(before[n])
+            g = grads.get(n)
+            p.grad = None if g is None else g.float().cpu().clone() * S
     opt = torch.optim.AdamW(_groups(ref.image, ref.text, ref.fusion), weight_decay=1e-2)
     torch.nn.utils.clip_grad_norm_(md.parameters(), 1.0)
+    if S != 1.0:
+        with torch.no_grad():
+            for p in md.parameters():
+                if p.grad is not None:
+                    p.grad.mul_(1.0 / S)
     opt.step()
     return {n: p.detach().clone() for n, p in md.named_parameters()}
+
+
+def _adamw_on_my_grads(m, cfg):
+    """The post-step parameters the benched update must reproduce: _adamw_step on the
+    benched step's OWN gradients, in the order the bench clips (C5: the reference's scaled
+    order at the step's loss scale)."""
+    return _adamw_step(m["before"], m["grads"], cfg, m.get("loss_scale"))
 
 
 def _check_update(m, o32, cfg):
@@ -345,8 +368,13 @@ def test_benched_step_reduced_precision_vs_oracle(dev, cfg):
     print(f"{cfg} {dt}: logits max-abs {m_max:.3e} (autocast oracle {a_max:.3e}), rms rel "
           f"{m_rms:.3e} ({a_rms:.3e}); loss {m['loss']:.6f} vs {o32['loss']:.6f} "
           f"(autocast {oau['loss']:.6f})")
-    assert m_max <= 1.25 * a_max + 1e-2 * scale
-    assert m_rms <= 1.25 * a_rms + 1e-2
+    c5 = cfg == "c5"
+    if c5:   # fp16: bars relative to fp16 autocast's own error, no large floor
+        assert m_max <= 2 * a_max + 1e-5 * scale, (m_max, a_max)
+        assert m_rms <= 2 * a_rms + 1e-5, (m_rms, a_rms)
+    else:
+        assert m_max <= 1.25 * a_max + 1e-2 * scale
+        assert m_rms <= 1.25 * a_rms + 1e-2
     assert abs(m["loss"] - o32["loss"]) <= 1e-2 * abs(o32["loss"])
     assert set(m["grads"]) == set(o32["grads"]), set(m["grads"]) ^ set(o32["grads"])
     mine = grad_report(m["grads"], o32["grads"])
@@ -395,10 +423,18 @@ def test_benched_step_reduced_precision_vs_oracle(dev, cfg):
                 va = float(np.percentile([auto[n][j] for n in bn], q))
                 if vm > k * va + 1e-2:
                     bad.append(("bn", f"p{q} {what}", vm, va))
+    ratio = []
     for n in rest:
         (c, r), (ca, ra) = mine[n], auto[n]
-        if c > max(2e-3, 2 * ca) or r > max(5e-3, 2 * ra):
+        if c5:
+            ratio.append((c / max(ca, 1e-12), n))
+            if c > 3 * ca + 1e-6 or r > 3 * ra + 1e-5:
+                bad.append(("other", n, c, ca, r, ra))
+        elif c > max(2e-3, 2 * ca) or r > max(5e-3, 2 * ra):
             bad.append(("other", n, c, ca, r, ra))
+    if ratio:
+        print(f"  C5 per-tensor 1-cos / autocast's: median {np.median([q for q, _ in ratio]):.2f}"
+              f", max {max(ratio)}")
     for kind, names in (("trunk", trunk), ("bn", bn), ("other", rest)):
         if names:
             print(f"  {kind} ({len(names)}): worst 1-cos "
@@ -411,11 +447,27 @@ def test_benched_step_reduced_precision_vs_oracle(dev, cfg):
     want = _adamw_on_my_grads(m, cfg)
     for n, w in want.items():
         torch.testing.assert_close(m["after"][n], w, rtol=1e-5, atol=1e-7, msg=n)
-    up_m = _update_report(m, o32, m["before"])
-    up_a = _update_report({"after": oau["after"]}, o32, m["before"])
-    print(f"  update vs fp32 oracle: median 1-cos "
-          f"{np.median([c for c, _ in up_m.values()]):.2e} (autocast "
-          f"{np.median([c for c, _ in up_a.values()]):.2e})")
+    if c5:
+        # the update against the reference-order oracle: torch autocast + GradScaler clips the
+        # scaled gradients (TP:1056-1061) as the bench now does; both are measured against the
+        # same order applied to the fp32 oracle's gradients at the same loss scale
+        want32 = {"after": _adamw_step(m["before"], o32["grads"], cfg, m["loss_scale"])}
+        up_m = _update_report(m, want32, m["before"])
+        up_a = _update_report({"after": oau["after"]}, want32, m["before"])
+        # (the BERT key biases' exact gradient is 0: their updates are noise on every side)
+        badu = [(n, c, up_a[n][0]) for n, (c, _) in up_m.items()
+                if n not in zero and c > 3 * up_a[n][0] + 1e-4]
+        print(f"  update vs reference-order fp32: median 1-cos "
+              f"{np.median([c for c, _ in up_m.values()]):.2e} (autocast + GradScaler "
+              f"{np.median([c for c, _ in up_a.values()]):.2e}), worst "
+              f"{max((c, n) for n, (c, _) in up_m.items())}")
+        assert not badu, badu[:10]
+    else:
+        up_m = _update_report(m, o32, m["before"])
+        up_a = _update_report({"after": oau["after"]}, o32, m["before"])
+        print(f"  update vs fp32 oracle: median 1-cos "
+              f"{np.median([c for c, _ in up_m.values()]):.2e} (autocast "
+              f"{np.median([c for c, _ in up_a.values()]):.2e})")
 
 
 @pytest.mark.parametrize("case,image", [("c1", "e1.jpg"), ("c1_e2", "e2.jpg")])

@@ -67,23 +67,31 @@ def test_gemm_gelu_preact_beta(dev, dt):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("MNK,beta", [((96, 256, 128), 0.0), ((200, 3072, 768), 0.0),
                                       ((37, 130, 64), 0.5), ((4096, 64, 2048), 0.0)])
-def test_gemm_gelu_bwd_epilogue(dev, dt, MNK, beta):
-    """act = MMDX_ACT_GELU_BWD: C = (A B^T) * gelu'(pre) (+ beta C), pre read from `preact`
-    (the FFN backward's fused GELU gradient); vector and scalar epilogues (N % 8 != 0),
-    split-K (K = 2048 on a small grid) through the reduce kernel."""
+@pytest.mark.parametrize("extra", [False, True])
+def test_gemm_gelu_bwd_epilogue(dev, dt, MNK, beta, extra):
+    """act = MMDX_ACT_GELU_BWD: C = (A B^T) * gelu'(pre) (+ bias + addend) (+ beta C), pre
+    read from `preact` (the FFN backward's fused GELU gradient); vector and scalar epilogues
+    (N % 8 != 0), split-K (K = 2048 on a small grid) through the reduce kernel.  `extra` adds
+    a bias and an addend, which the 16-B vector branch does not carry: the epilogue must take
+    the per-element path for them (apply()'s order: gelu' first, then bias, addend)."""
     M, N, K = MNK
     g = torch.Generator().manual_seed(M + N)
     A, B = torch.randn(M, K, generator=g) / 8, torch.randn(N, K, generator=g) / 8
     P = torch.randn(M, N, generator=g)
     C0 = torch.randn(M, N, generator=g)
+    bias, add = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
     Ad, Bd, Pd = A.to(dev, dt), B.to(dev, dt), P.to(dev, dt)
     A, B, P = Ad.float().cpu(), Bd.float().cpu(), Pd.float().cpu()
     x = P.double()
     grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * math.pi) ** 0.5
     ref = (A.double() @ B.double().T) * grad + beta * C0.to(dt).double()
+    if extra:
+        ref = ref + bias.double() + add.double()
     C = C0.to(dev, dt)
+    bd, addd = bias.to(dev), add.to(dev)
     L.call("mmdx_gemm", L.dtype_code(dt), M, N, K, Ad.data_ptr(), K, 1, Bd.data_ptr(), K, 1,
-           C.data_ptr(), N, L.dtype_code(dt), None, None, L.ACT_GELU_BWD, 1.0, beta,
+           C.data_ptr(), N, L.dtype_code(dt), bd.data_ptr() if extra else None,
+           addd.data_ptr() if extra else None, L.ACT_GELU_BWD, 1.0, beta,
            Pd.data_ptr(), *_ws(dt, M, N, K, dev), L.stream())
     torch.cuda.synchronize()
     err = ((C.double().cpu() - ref).abs().max() / ref.abs().max()).item()
@@ -176,10 +184,13 @@ def test_gemm_wgrad_bias(dev, dt, M, N, K):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("M,N,K,ldc", [(300, 256, 192, 256), (300, 256, 192, 257),
-                                       (37, 768, 3072, 768), (12608, 768, 64, 768)])
+                                       (37, 768, 3072, 768), (12608, 768, 64, 768),
+                                       (12608, 768, 3072, 768)])
 def test_gemm_residual(dev, dt, M, N, K, ldc):
     """mmdx_gemm_res: C = A B^T + bias + residual equals the copy-then-beta-1 form bit for bit
-    (vector and per-element epilogues, split-K through the reduce: K 3072 on a small grid)."""
+    (vector and per-element epilogues, split-K through the reduce: K 3072 on a small grid;
+    12608 x 768 x 3072 is the ViT-B FFN-down shape, 150 256 x 256 tiles: the 8-wave forward
+    kernel's residual epilogue under the default MMDX_GEMM256_FWD_MIN)."""
     g = torch.Generator().manual_seed(M + N + K + ldc)
     A = (torch.randn(M, K, generator=g) / 8).to(dev, dt)
     B = (torch.randn(N, K, generator=g) / 8).to(dev, dt)

@@ -1,8 +1,8 @@
-// Lab build of csrc/gemm8ph.h (the 8-wave ping-pong 256 x 256 GEMM) with a C entry point,
-// timed and checked by tools/gemm8ph_lab.py before the kernel is dispatched by mmdx_gemm.
+// Lab build of tools/lab/gemm8ph.h (the 8-wave ping-pong 256 x 256 GEMM; not on the product
+// path until it is dispatched by mmdx_gemm) with a C entry point, timed by tools/gemm8ph_lab.py.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I include \
 //     -o tools/lab/libgemm8ph_lab.so tools/lab/gemm8ph_lab.hip
-#include "../../multi-modal-medical-imaging-and-report-ml-diagnosis-system_amd/csrc/gemm8ph.h"
+#include "gemm8ph.h"
 
 using namespace mmdx;
 
