@@ -85,29 +85,34 @@ def load_traffic(cfg_name, batch):
         except (OSError, ValueError):
             continue
         if t.get("config") == cfg_name and t.get("per_gpu_batch") == batch:
-            best = (t["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+            best = (t["traffic_bytes_per_launch"], os.path.relpath(f, ROOT),
+                    t.get("git_rev", "unstamped"))
     return best
 
 
 def load_mfma_util(cfg_name):
-    """Per-family MFMA utilisation from the newest committed PMC pass (tools/pmc_mfma.py:
-    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), dispatches serialised by
-    the profiler) for the C4 workload, or None."""
+    """Per-family MFMA utilisation from the newest committed PMC pass of this config
+    (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8),
+    dispatches serialised by the profiler; files without a config key are C4's), with the
+    git revision it was measured on, or None."""
     import glob
-    if cfg_name != "c4":
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.json"))):
+        try:
+            with open(f) as fh:
+                t = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if t.get("config", "c4") == cfg_name:
+            best = (f, t)
+    if best is None:
         return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as fh:
-            t = json.load(fh)
-    except (OSError, ValueError):
-        return None
+    f, t = best
     pct = {k: round(100 * v["mfma_util"], 1) for k, v in t.items()
            if isinstance(v, dict) and v.get("mfma_util") is not None
            and k in ("conv_fwd", "conv_dgrad", "conv_wgrad", "conv_all", "gemm")}
-    return {"pct": pct, "source": os.path.relpath(files[-1], ROOT)}
+    return {"pct": pct, "source": os.path.relpath(f, ROOT),
+            "git_rev": t.get("git_rev", "unstamped")}
 
 
 def vit_flops_per_sample(layers=12, S=197, D=768, I=3072, patches=196, kpatch=768):
@@ -623,6 +628,7 @@ def main():
             "traffic": traffic[0] if traffic else None,
             "traffic_unit": "HBM bytes per conv launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)",
             "traffic_source": traffic[1] if traffic else None,
+            "traffic_git_rev": traffic[2] if traffic else None,
             "algorithmic_bytes_per_launch": round(alg_bytes / alg_launches),
             "mfma_achieved_tflops": round(conv_tf, 2),
             "mfma_frac": round(conv_tf / PEAK_BF16_TFLOPS, 4),

@@ -65,9 +65,11 @@ has pmc && step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d 
 has pmc && step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmcw_$tag" \
   -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
 has pmcm && step pmc_mfma 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
-  -d "$R/gpurun_out/pmcm_$tag" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+  -d "$R/gpurun_out/pmcm_$tag" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
+  --config "${PC:-c4}"
 cd "$R"
-has pmcm && python tools/pmc_mfma.py "gpurun_out/pmcm_$tag" -o "gpurun_out/${tag}_mfma_util.json"
+has pmcm && python tools/pmc_mfma.py "gpurun_out/pmcm_$tag" --config "${PC:-c4}" \
+  -o "gpurun_out/${tag}_${PC:-c4}_mfma_util.json"
 has pmc && python tools/pmc_traffic.py "gpurun_out/pmcf_$tag" "gpurun_out/pmcw_$tag" --config c4 \
   --batch 128 -o "gpurun_out/${tag}_conv_traffic.json"
 exit 0

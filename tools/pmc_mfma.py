@@ -43,6 +43,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("-o", "--out", default="")
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--rev", default=os.environ.get("MMDX_GIT_REV", "unstamped"),
+                    help="git revision the counters were measured on (the GPU box has no .git)")
     args = ap.parse_args()
     files = glob.glob(os.path.join(args.dir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -73,6 +76,8 @@ def main():
     out["conv_all"] = {"mfma_util": round(cm / cc, 4) if cc else None,
                        "dispatches": sum(v[2] for v in conv)}
     out["formula"] = "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE / 8), cycle-weighted"
+    out["config"] = args.config
+    out["git_rev"] = args.rev
     for k, v in out.items():
         print(f"{k:12s} {v}")
     if args.out:

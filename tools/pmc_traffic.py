@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--calls-per-step", type=int, default=158,
                     help="conv calls per train step (bench.py's conv_launches_per_step)")
     ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--rev", default=os.environ.get("MMDX_GIT_REV", "unstamped"),
+                    help="git revision the counters were measured on (the GPU box has no .git)")
     a = ap.parse_args()
     f_conv, f_red, n_f, s_f = load(a.fetch_dir, "FETCH_SIZE")
     w_conv, w_red, n_w, s_w = load(a.write_dir, "WRITE_SIZE")
@@ -72,7 +74,8 @@ def main():
     fetch = 2.0 * (f_conv + f_red) * 1024 / calls
     write = (w_conv + w_red) * 1024 / calls
     out = {
-        "config": a.config, "per_gpu_batch": a.batch, "dispatches": n_f, "steps": s_f,
+        "config": a.config, "per_gpu_batch": a.batch, "git_rev": a.rev,
+        "dispatches": n_f, "steps": s_f,
         "calls": calls,
         "kernels": "igemm(_dma)_kernel (Im2colK/DgradK/DgradPhaseK/Im2colR/PointFwdK/PointDgradK/PointWgradR sources) + wgrad_reduce_kernel",
         "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
