@@ -126,6 +126,34 @@ int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void*
  * whatever MMDX_STEM_DIRECT says later; a size the kernels cannot write is an error). */
 int mmdx_conv_fwd_rows(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
                        void* y, float* stat_part, int stat_rows, void* stream);
+/* Train-mode conv whose epilogue also FINALIZES the BatchNorm statistics of its output
+ * (mean / rstd / running-stat update / the apply pass's scale and shift, as mmdx_bn_fwd's
+ * finalize): the blocks write their (mean, M2) slabs to stat_part as mmdx_conv_fwd does, and
+ * the last block of each group of row tiles, then the last group of each column tile, merges
+ * them inside the same launch (ticket counters in `scratch`), so no finalize launch sits
+ * between the conv and its BN apply.  scratch: mmdx_conv_fwd_bnfin_scratch_size(d) bytes, zeroed
+ * once before first use (the counters return to zero after every call).  Convs the fused
+ * kernels do not cover (fp32, the pixel-pair stem, 256-row tiles) run mmdx_conv_fwd and then
+ * mmdx_bn_finalize: the outputs are the same either way.  Follow with mmdx_bn_apply.
+ * Replaces: the BatchNorm2d batch statistics + running-stat update after each backbone conv
+ * (TP:183 / TP:223, train mode). */
+typedef struct {
+  const float* gamma;      /* [K] or NULL (1) */
+  const float* beta;       /* [K] or NULL (0) */
+  float* running_mean;     /* [K] or NULL (no running-stat update) */
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;        /* [K] outputs */
+  float* save_rstd;
+  float* scale;            /* [K]: gamma * rstd */
+  float* shift;            /* [K]: beta - mean * gamma * rstd */
+  void* scratch;
+  size_t scratch_bytes;
+} mmdx_bn_fin;
+size_t mmdx_conv_fwd_bnfin_scratch_size(const mmdx_conv_desc* d);
+int mmdx_conv_fwd_bnfin(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
+                        void* y, float* stat_part, int stat_rows, const mmdx_bn_fin* fin,
+                        void* stream);
 /* Eval-mode conv + BatchNorm2d (running statistics) (+residual) (+ReLU) in one launch:
  * y = act(conv(x, w) * s + t + residual), s = gamma / sqrt(running_var + eps),
  * t = beta - running_mean * s, applied in the conv epilogue on the fp32 accumulators.
@@ -213,6 +241,16 @@ int mmdx_bn_fwd_ex(int dtype, int train, const void* x, long rows, int C,
                    float* save_mean, float* save_rstd,
                    const void* residual, int relu, void* y, uint8_t* relu_mask,
                    void* workspace, size_t ws_bytes, void* stream);
+/* The two halves of the train forward above: the finalize of precomputed slabs (mean,
+ * rstd, running stats, scale = gamma*rstd, shift = beta - mean*scale), and the apply pass
+ * y = act(x*scale + shift (+ residual)) with the optional ReLU bit mask. */
+int mmdx_bn_finalize(const float* stat_part, int stat_blocks, long stat_rows, long rows, int C,
+                     const float* gamma, const float* beta, float* running_mean,
+                     float* running_var, float momentum, float eps, float* save_mean,
+                     float* save_rstd, float* scale, float* shift, void* stream);
+int mmdx_bn_apply(int dtype, const void* x, const void* residual, long rows, int C,
+                  const float* scale, const float* shift, int relu, void* y,
+                  uint8_t* relu_mask, void* stream);
 /* dy: grad w.r.t. y; y: forward output (ReLU mask source).  Writes dx, d_residual
  * (may be NULL), and dgamma/dbeta (fp32, accumulated with beta_acc). */
 int mmdx_bn_bwd(int dtype, int train, const void* x, const void* y, const void* dy,
@@ -285,7 +323,12 @@ enum {
   MMDX_OP_GEMM, MMDX_OP_ATTN_FWD, MMDX_OP_ATTN_BWD, MMDX_OP_LN_FWD, MMDX_OP_LN_BWD,
   MMDX_OP_GELU_BWD, MMDX_OP_BIAS_GRAD, MMDX_OP_ADD, MMDX_OP_DROPOUT_FWD, MMDX_OP_DROPOUT_BWD,
   MMDX_OP_AXPBY, MMDX_OP_ATTN_FWD_LSE, MMDX_OP_ATTN_BWD_LSE, MMDX_OP_LN_FWD_DROP,
-  MMDX_OP_LN_BWD_DROP, MMDX_OP_GEMM_BIAS_GRAD
+  MMDX_OP_LN_BWD_DROP, MMDX_OP_GEMM_BIAS_GRAD,
+  /* conv + fused BN finalize (i: stat_rows; l: scratch (absolute), scratch_bytes; f: momentum,
+   * eps; p: x, w, y, stat_part, gamma, beta, running_mean, running_var, save_mean, save_rstd,
+   * scale, shift) and the BN apply pass (i: C, relu; l: rows; p: x, residual, scale, shift, y,
+   * relu_mask) */
+  MMDX_OP_CONV_FWD_BNFIN, MMDX_OP_BN_APPLY
 };
 typedef struct {
   int op, dtype, stream;

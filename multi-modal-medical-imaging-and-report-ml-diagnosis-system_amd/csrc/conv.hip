@@ -2,6 +2,7 @@
 // Replaces every nn.Conv2d of the torchvision ResNet trunk that ImageEncoderCNN wraps
 // (training_pipeline.py:178-183, run through _backbone_forward_grad TP:285-289).
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "igemm.h"
@@ -334,12 +335,16 @@ static bool fold_probe_on() {
   return e && atoi(e) != 0;
 }
 
+// fin_ok (optional): set when the launched kernel is one whose epilogue runs the fused BN
+// finalize tail (the LDS-DMA kernel with 128-row tiles; EpiStore::fin)
 template <typename T, class SA, class Epi>
 static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int N, int K,
-                         hipStream_t st, bool dma_ok) {
+                         hipStream_t st, bool dma_ok, bool* fin_ok = nullptr) {
   DenseK<T> sb{(const T*)w, K, N, true};
+  if (fin_ok) *fin_ok = false;
   if constexpr (DmaOk<SA>::value) {
     if (dma_ok && fold_probe_on()) {
+      if (fin_ok) *fin_ok = true;
       const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
       const int bn = (N <= 64 || tiles128 < kNarrowBelow) ? 64 : 128;
       const int nwg = ((M + 127) / 128) * ((N + bn - 1) / bn);
@@ -361,6 +366,7 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
       }
       // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
       const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+      if (fin_ok) *fin_ok = true;
       if (const int ns32 = conv_bk32_stages()) {
         if (N <= 64 || tiles128 < kNarrowBelow)
           launch_dma32<128, 64>(sa, sb, epi, M, N, K, ns32, st);
@@ -385,13 +391,15 @@ template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
                      hipStream_t st, float* stats = nullptr, bool dma_ok = false,
                      const BnStat& bs = BnStat{}, const void* acc_src = nullptr,
-                     const uint8_t* acc_mask = nullptr) {
+                     const uint8_t* acc_mask = nullptr, const BnFinArgs* fin = nullptr,
+                     bool* fin_ok = nullptr) {
   EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
                   (float2*)stats};
   epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
   epi.acc_src = (const T*)acc_src;
   epi.acc_mask = acc_mask;
-  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok);
+  if (fin) epi.fin = *fin;
+  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok, fin_ok);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -528,11 +536,15 @@ static int stem_direct_fwd(const ConvGeom& g, const void* x, const void* w, void
 
 // stat_rows: the rows per statistics slab the caller sized `stats` for (128; 2*Q selects the
 // direct stem kernel, which writes one slab per block); without stats the env knob decides
+// fin / fin_ok: the fused BN finalize (mmdx_conv_fwd_bnfin); fin_ok reports whether the
+// launched kernel ran it
 template <typename T>
 static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
-                      float* stats, int stat_rows, hipStream_t st) {
+                      float* stats, int stat_rows, hipStream_t st,
+                      const BnFinArgs* fin = nullptr, bool* fin_ok = nullptr) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
+  if (fin_ok) *fin_ok = false;
   const bool direct = stem_direct_geom(g) && std::is_same<T, bf16>::value &&
                       (stats ? stat_rows == STEM_PB * g.Q : stem_direct_on());
   MMDX_CHECK_ARG(!stats || direct || stat_rows == 128,
@@ -542,14 +554,37 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
     if (direct) return stem_direct_fwd(g, x, w, y, stats, st);
   if (g.C % KTile<T>::BK == 0 && is_pointwise(g))  // x itself is the [M][C] A operand
     return conv_gemm<T>(PointFwdK<T>{{(const T*)x, g.C, M, true}}, w, y, M, N, K, 0.f, st,
-                        stats, dma_geom_ok(g, false, 32, M));
+                        stats, dma_geom_ok(g, false, 32, M), BnStat{}, nullptr, nullptr, fin,
+                        fin_ok);
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
-                        dma_geom_ok(g, false, 32, M));
+                        dma_geom_ok(g, false, 32, M), BnStat{}, nullptr, nullptr, fin, fin_ok);
   // channel count a power of two: the LDS-DMA kernel decodes each lane's tap itself
   const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
   Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
-  return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64, M));
+  return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64, M),
+                      BnStat{}, nullptr, nullptr, fin, fin_ok);
+}
+
+// Fused-finalize layout: row tiles (128 rows) in groups of ~sqrt(tiles) (each merge reads at
+// most 64 slabs per channel: bnfin_merge's 32 per thread x 2 threads per channel at BN = 128);
+// scratch = [tiles_n (BN 64) column counters + tiles_n x ngroups group counters] (u32, padded
+// to 256 B) + [N][ngroups] group slabs.  0 groups: too many row tiles for the fused merge.
+struct BnFinLayout { int group, ngroups; size_t ctr_bytes, bytes; };
+static BnFinLayout bnfin_layout(const ConvGeom& g) {
+  BnFinLayout L{0, 0, 0, 0};
+  const long M = (long)g.N * g.P * g.Q;
+  const long tiles_m = (M + 127) / 128;
+  long G = 1;
+  while (G * G < tiles_m) ++G;
+  const long ng = (tiles_m + G - 1) / G;
+  if (G > 64 || ng > 64) return L;
+  const long tiles_n = (g.K + 63) / 64;
+  L.group = (int)G;
+  L.ngroups = (int)ng;
+  L.ctr_bytes = (size_t)((tiles_n + tiles_n * ng) * 4 + 255) / 256 * 256;
+  L.bytes = L.ctr_bytes + (size_t)g.K * ng * sizeof(float2);
+  return L;
 }
 
 template <typename T>
@@ -889,9 +924,31 @@ __global__ __launch_bounds__(512, 1) void stem_direct_wgrad_kernel(
               acc[a][b][j];
 }
 
+// The im2col^T operand of the 3x3 / strided weight gradients in the row-quartered LDS image
+// (DmaRq: one pixel state per lane; MMDX_WGRAD_RQ=0 restores DmaR for A/B runs)
+static bool wgrad_rq_on() {
+  const char* e = getenv("MMDX_WGRAD_RQ");   // read per launch: tests / A-B runs switch it
+  return !(e && atoi(e) == 0);
+}
+
 template <typename T, class SB>
 static int wgrad_dma(const WgradPlan& p, const DenseR<T>& sa, const SB& sb, const EpiPartial& epi,
                      int M, int N, int K, hipStream_t st) {
+  if constexpr (std::is_same<SB, Im2colR<T>>::value) {
+    if (p.bm != 256 && wgrad_rq_on()) {
+      if (p.bm == 128 && p.bn == 128)
+        return launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaRq<128, SB>>(
+            sa, sb, epi, M, N, K, p.splits, p.kper, st);
+      if (p.bm == 128)
+        return launch_dma_ops<128, 64, DmaR<128, DenseR<T>>, DmaRq<64, SB>>(
+            sa, sb, epi, M, N, K, p.splits, p.kper, st);
+      if (p.bn == 128)
+        return launch_dma_ops<64, 128, DmaR<64, DenseR<T>>, DmaRq<128, SB>>(
+            sa, sb, epi, M, N, K, p.splits, p.kper, st);
+      return launch_dma_ops<64, 64, DmaR<64, DenseR<T>>, DmaRq<64, SB>>(sa, sb, epi, M, N, K,
+                                                                       p.splits, p.kper, st);
+    }
+  }
   if (p.bm == 256) {
     const int nwg = ((M + 255) / 256) * ((N + 127) / 128);
     hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaR<256, DenseR<T>, 64, 8>, DmaR<128, SB, 64, 8>,
@@ -1041,6 +1098,58 @@ extern "C" int mmdx_conv_fwd_rows(int dtype, const mmdx_conv_desc* d, const void
   if (dtype == BF16)
     return conv_fwd_t<bf16>(d, x, w, y, stat_part, stat_rows, (hipStream_t)stream);
   return conv_fwd_t<float>(d, x, w, y, stat_part, stat_rows, (hipStream_t)stream);
+}
+
+extern "C" size_t mmdx_conv_fwd_bnfin_scratch_size(const mmdx_conv_desc* d) {
+  const BnFinLayout L = bnfin_layout(geom(d));
+  return std::max<size_t>(L.bytes, 256);
+}
+
+extern "C" int mmdx_conv_fwd_bnfin(int dtype, const mmdx_conv_desc* d, const void* x,
+                                   const void* w, void* y, float* stat_part, int stat_rows,
+                                   const mmdx_bn_fin* fin, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_fwd_bnfin: fp16 is the C5 path only");
+  MMDX_CHECK_ARG(fin && stat_part && fin->save_mean && fin->save_rstd && fin->scale &&
+                     fin->shift,
+                 "conv fwd bnfin: statistics, outputs and the finalize arguments are required");
+  const ConvGeom g = geom(d);
+  const long M = (long)g.N * g.P * g.Q;
+  MMDX_CHECK_ARG(M < (1L << 31), "conv fwd bnfin: N*P*Q too large");
+  hipStream_t st = (hipStream_t)stream;
+  const BnFinLayout L = bnfin_layout(g);
+  const bool fusable = dtype == BF16 && L.group > 0 && fin->scratch &&
+                       fin->scratch_bytes >= L.bytes && stat_rows == 128;
+  BnFinArgs fa;
+  if (fusable) {
+    fa.ctr = (unsigned*)fin->scratch;
+    fa.gpart = (float2*)((char*)fin->scratch + L.ctr_bytes);
+    fa.group = L.group;
+    fa.ngroups = L.ngroups;
+    fa.gamma = fin->gamma;
+    fa.beta = fin->beta;
+    fa.rmean = fin->running_mean;
+    fa.rvar = fin->running_var;
+    fa.momentum = fin->momentum;
+    fa.eps = fin->eps;
+    fa.save_mean = fin->save_mean;
+    fa.save_rstd = fin->save_rstd;
+    fa.scale = fin->scale;
+    fa.shift = fin->shift;
+  }
+  bool done = false;
+  int rc;
+  if (dtype == BF16)
+    rc = conv_fwd_t<bf16>(d, x, w, y, stat_part, stat_rows, st, fusable ? &fa : nullptr, &done);
+  else
+    rc = conv_fwd_t<float>(d, x, w, y, stat_part, stat_rows, st);
+  if (rc) return rc;
+  if (fusable && done) return 0;
+  // not fused here (fp32, the direct stem, 256-row tiles, too many row tiles): the finalize
+  // launch over the same slabs
+  const long blocks = (M + stat_rows - 1) / stat_rows;
+  return mmdx_bn_finalize(stat_part, (int)blocks, stat_rows, M, g.K, fin->gamma, fin->beta,
+                          fin->running_mean, fin->running_var, fin->momentum, fin->eps,
+                          fin->save_mean, fin->save_rstd, fin->scale, fin->shift, stream);
 }
 
 extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,

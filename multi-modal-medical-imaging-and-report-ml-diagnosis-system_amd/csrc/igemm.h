@@ -194,6 +194,8 @@ struct DenseR {
   __device__ int roff(RowState rs, int k, int klim) const {
     return rs >= 0 && k < klim ? (int)(((long)k * ld + rs) * sizeof(T)) : -1;
   }
+  // DmaRq: every row of every ROWS-row tile is in range (quarters share one validity test)
+  __device__ bool rows_one_tap(int rows) const { return R % rows == 0; }
 };
 
 // x^T of a pointwise conv in its weight gradient (named apart from DenseR, see PointFwdK)
@@ -635,6 +637,9 @@ struct Im2colR {
                     (unsigned)iw < (unsigned)g.W;
     return ok ? (l.off + rs.toff) * (int)sizeof(T) : -1;
   }
+  // DmaRq: a ROWS-row tile lies in one filter tap (C % ROWS == 0, so tiles start on a tap and
+  // every row is in range): its quarters share the pixel's bounds test
+  __device__ bool rows_one_tap(int rows) const { return g.C % rows == 0; }
   // pixel k -> (n, p, q) by float reciprocals (k < 2^23: one correction step is exact)
   __device__ int roff(const RowState& rs, int k, int klim) const {
     if (rs.r < 0 || k >= klim) return -1;
@@ -892,6 +897,152 @@ __device__ __forceinline__ void bn_stat_store(const BnStat& b, float* sg, float*
   }
 }
 
+// Train-mode BatchNorm finalize fused into the producing conv (TP:223 / TP:206: batch
+// statistics, running-stat update, the apply pass's per-channel scale / shift), replacing the
+// separate bn_finalize launch between the conv and its BN apply on the critical stream.
+// Every block writes its per-128-row (mean, M2) slab as before, write-through (sc1: 8-B
+// agent-scope atomic stores), drains, and takes a ticket on its column tile's group counter;
+// the block that draws the group's last ticket merges the group's `group` slabs into one group
+// slab (also sc1), then takes a ticket on the column tile's counter, and the last group merges
+// the `ngroups` group slabs and finalises the tile's BN columns.  Both merges are the exact
+// two-level decomposition mean = sum n_b mean_b / n, M2 = sum M2_b + n_b (mean_b - mean)^2 in a
+// fixed slab order, so the result does not depend on which block arrives last (deterministic).
+// The last arriver of each counter resets it (the scratch is zeroed once by its owner, and
+// mmdx_conv_fwd_bnfin re-zeroes it only on request).  Hand-off form: cdna_hip_programming.md
+// §6 G16 (sc1 payload + relaxed agent ticket; every load of a slab an sc1 load).
+struct BnFinArgs {
+  unsigned* ctr = nullptr;   // [tiles_n] column counters, then [tiles_n][ngroups] group counters
+  float2* gpart = nullptr;   // [N][ngroups] group (mean, M2)
+  int group = 1, ngroups = 1;
+  const float *gamma = nullptr, *beta = nullptr;
+  float *rmean = nullptr, *rvar = nullptr;
+  float momentum = 0.1f, eps = 1e-5f;
+  float *save_mean = nullptr, *save_rstd = nullptr, *scale = nullptr, *shift = nullptr;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long bnfin_gu64;
+__device__ __forceinline__ void bnfin_store(float2* p, float2 v) {  // 8-B sc1 store
+  __hip_atomic_store((bnfin_gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 bnfin_load(const float2* p) {     // 8-B sc1 load
+  return __builtin_bit_cast(float2, __hip_atomic_load((bnfin_gu64*)p, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// the slab-merge of one level: channel c's `cnt` slabs src[c*ld + b0 + i] (i < cnt), slab i
+// holding nrows(b0 + i) rows; TPC threads per channel (256 / BN), slab i on sub-thread i % TPC,
+// at most 32 slabs per thread (the host keeps group and ngroups <= 32 * TPC); partial sums
+// combined through `red` (2 * 256 floats) in a fixed order.  Returns (n, mean, M2) on every
+// thread of the channel.
+constexpr int BNFIN_PER = 32;
+template <int BN, class NRows>
+__device__ __forceinline__ void bnfin_merge(const float2* src, long ld, int b0, int cnt,
+                                            bool cok, NRows nrows, float* red, float& n_out,
+                                            float& mean_out, float& m2_out) {
+  constexpr int TPC = NT / BN;
+  const int col = threadIdx.x % BN, sub = threadIdx.x / BN;
+  float2 v[BNFIN_PER];
+  float nb[BNFIN_PER];
+#pragma unroll
+  for (int i = 0; i < BNFIN_PER; ++i) {
+    const int b = sub + TPC * i;
+    const bool ok = cok && b < cnt;
+    v[i] = ok ? bnfin_load(src + (long)col * ld + b0 + b) : make_float2(0.f, 0.f);
+    nb[i] = ok ? nrows(b0 + b) : 0.f;
+  }
+  float sn = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < BNFIN_PER; ++i) {
+    sn += nb[i];
+    s1 += nb[i] * v[i].x;
+  }
+  red[threadIdx.x] = sn;
+  red[NT + threadIdx.x] = s1;
+  __syncthreads();
+  float n = 0.f, t1 = 0.f;
+#pragma unroll
+  for (int q = 0; q < TPC; ++q) {
+    n += red[q * BN + col];
+    t1 += red[NT + q * BN + col];
+  }
+  const float mean = n > 0.f ? t1 / n : 0.f;
+  __syncthreads();
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < BNFIN_PER; ++i) {
+    const float d = v[i].x - mean;
+    s2 += nb[i] > 0.f ? v[i].y + nb[i] * d * d : 0.f;
+  }
+  red[threadIdx.x] = s2;
+  __syncthreads();
+  float m2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < TPC; ++q) m2 += red[q * BN + col];
+  __syncthreads();
+  n_out = n;
+  mean_out = mean;
+  m2_out = m2;
+}
+
+// The ticketed tail of a conv block whose epilogue wrote its (mean, M2) slab `tm` of column
+// tile `tn` (slabs of 128 rows: BM = 128).  `lds` is free scratch (>= 2 KiB + 16 B).
+template <int BN>
+__device__ void bnfin_tail(const BnFinArgs& f, const float2* part, int M, int N, int tm, int tn,
+                           char* lds) {
+  const int tiles_m = (M + 127) / 128, tiles_n = (N + BN - 1) / BN;
+  const int grp = tm / f.group;
+  const int g0 = grp * f.group, gcnt = min(f.group, tiles_m - g0);
+  unsigned* c1 = f.ctr + tiles_n + (long)tn * f.ngroups + grp;
+  unsigned* c2 = f.ctr + tn;
+  int* flag = (int*)lds;
+  float* red = (float*)(lds + 16);
+  // every wave's slab (and output) stores have landed before the ticket (R1: all storing waves
+  // drain, then the workgroup barrier, then ONE lane's relaxed agent-scope add)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)(gcnt - 1);
+  __syncthreads();
+  if (!*flag) return;
+  if (threadIdx.x == 0) __hip_atomic_store(c1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the ticket
+  const int col = threadIdx.x % BN;
+  const int c = tn * BN + col;
+  const bool cok = c < N;
+  float n, mean, m2;
+  bnfin_merge<BN>(part + (long)tn * BN * tiles_m, tiles_m, g0, gcnt, cok,
+                  [&](int b) { return (float)min(128, M - b * 128); }, red, n, mean, m2);
+  if (cok && threadIdx.x < BN) bnfin_store(f.gpart + (long)c * f.ngroups + grp, make_float2(mean, m2));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)(f.ngroups - 1);
+  __syncthreads();
+  if (!*flag) return;
+  if (threadIdx.x == 0) __hip_atomic_store(c2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int G = f.group;
+  bnfin_merge<BN>(f.gpart + (long)tn * BN * f.ngroups, f.ngroups, 0, f.ngroups, cok,
+                  [&](int g) { return (float)min(G * 128, M - g * G * 128); }, red, n, mean, m2);
+  if (!cok || threadIdx.x >= BN) return;
+  // bn_finalize_kernel's expressions (norm.hip): var, rstd, running stats, scale / shift
+  const float var = m2 / (float)M;
+  const float rstd = rsqrtf(var + f.eps);
+  f.save_mean[c] = mean;
+  f.save_rstd[c] = rstd;
+  if (f.rmean) {
+    const float unb = M > 1 ? m2 / (float)(M - 1) : var;
+    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
+    f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unb;
+  }
+  const float gm = f.gamma ? f.gamma[c] : 1.f;
+  f.scale[c] = gm * rstd;
+  f.shift[c] = (f.beta ? f.beta[c] : 0.f) - mean * gm * rstd;
+}
+
 // VEC_EPI: the 16-B-per-8-columns epilogue also for bias / addend / pre-activation / ReLU /
 // GELU (the dense GEMMs of gemm_dense.hip).  The conv instantiations keep the lean form
 // (their epilogues never carry those): the extra branch cost the C4 step 2.3 % when it was
@@ -906,6 +1057,7 @@ struct EpiStore {
   OutT* preact;         // optional copy of the pre-activation value, ld = ldc
   float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [N][tiles_m]
   BnStat bs{};          // optional fused consumer-BN backward statistics (bs.part != null)
+  BnFinArgs fin{};      // optional fused BN finalize of `stats` (fin.ctr != null; BM = 128)
   // optional masked accumulation source (beta must be 0): C = acc + (bit ? acc_src : 0), bit
   // from a 1-bit ReLU mask ([M][N / VEC] bytes, bit e of byte n / VEC = column n) — the
   // gradient a residual unit's identity path adds, without materialising it
@@ -1179,8 +1331,8 @@ struct EpiStore {
         nn = tot;
       }
       if (nn > 0.f || SLABS == 1)
-        stats[(long)(tn * BN + col) * ((M + SLAB - 1) / SLAB) + tm * SLABS + slab] =
-            make_float2(mu, mm);
+        bnfin_store(stats + (long)(tn * BN + col) * ((M + SLAB - 1) / SLAB) + tm * SLABS + slab,
+                    make_float2(mu, mm));  // write-through: a fused finalize may read it
     }
   }
   __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
@@ -1406,6 +1558,11 @@ struct EpiPartialBias : EpiPartial {
 template <class E, class = void> struct HasBiasSum { static constexpr bool value = false; };
 template <class E> struct HasBiasSum<E, decltype((void)E::BIAS_SUM)> {
   static constexpr bool value = E::BIAS_SUM;
+};
+
+template <class E, class = void> struct HasBnFin { static constexpr bool value = false; };
+template <class E> struct HasBnFin<E, decltype((void)std::declval<E>().fin, void())> {
+  static constexpr bool value = true;
 };
 
 template <class E, class = void> struct IsPhased { static constexpr bool value = false; };
@@ -1706,7 +1863,84 @@ struct DmaR {
         (lds_s16x4*)(stage + k * (ROWS * 2) + o));
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (lds_s16x4*)(stage + (k + 4) * (ROWS * 2) + o));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
+
+// R-major operand in a row-QUARTERED LDS image (BK = 64): the tile's ROWS rows are kept as
+// QN = ROWS / 32 sub-images [64 k][32 rows] (64-B k-lines, 4 KiB each).  Wave w's instruction
+// j fills k-lines 16w .. 16w+15 of quarter j (1 KiB, lane-linear: lane L -> k-line 16w + L/4,
+// 16-B slot L % 4), so a lane serves ONE k-line (one pixel of the im2col^T operand) in all
+// of its QN instructions: one pixel state per lane, stepped once per K tile, instead of DmaR's
+// QN independent k-lines per lane (the im2col^T stepping and bounds tests were ~60 of the ~110
+// VALU per K tile of the 3x3 weight-gradient loop, ~5 VALU per MFMA: PMC r05).
+// When the tile's rows lie in one filter tap (C % ROWS == 0) the quarters share the pixel's
+// validity and their offsets differ by 32 rows: one bounds test per lane per K tile.
+// Slot swizzle: physical slot = logical ^ 2*((k >> 3) & 1), so the two 16-lane groups of a
+// ds_read_b64_tr_b16 half-wave (k-lines k..k+3 and k+8..k+11, 32 B each) cover all 64 banks.
+template <int ROWS, class Src>
+struct DmaRq {
+  static constexpr int BK = 64;
+  static constexpr bool RMAJOR = true;
+  static constexpr int NW = NT / 64;
+  static constexpr int QN = ROWS / 32;           // quarters (32-row sub-images)
+  static constexpr int INSTR = QN;               // DMAs per wave per stage (one per quarter)
+  static constexpr int BYTES = BK * ROWS * 2;
+  static_assert(ROWS == 64 || ROWS == 128, "quartered R-major tile rows");
+  static_assert(NW == 4, "16 k-lines per wave");
+  static_assert(Src::STEP, "lane-stepping source");
+  typedef Src SrcT;
+  __amdgpu_buffer_rsrc_t rsrc;
+  typename Src::RowState rs[QN];
+  typename Src::Lane ln;
+  int kk;        // this lane's k-line within the K tile
+  bool same;     // every quarter in the pixel's one tap: one bounds test (block-uniform)
+  __device__ static int swq(int k) { return ((k >> 3) & 1) << 1; }
+  __device__ void init(const Src& s, int row0, int lane, int wid, int kbeg) {
+    rsrc = dma_rsrc(s.bbase(), s.bbytes());
+    kk = wid * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ swq(kk);          // logical 16-B chunk this lane fetches
+#pragma unroll
+    for (int j = 0; j < QN; ++j) rs[j] = s.row(row0 + 32 * j + lc * 8);
+    ln = s.lane_at(kbeg + kk);
+    same = s.rows_one_tap(ROWS);
+  }
+  __device__ void issue(const Src& s, char* stage, int k0, int klim, int wid) {
+    if (k0 + BK <= klim)
+      issue_t<false>(s, stage, k0, klim, wid);
+    else
+      issue_t<true>(s, stage, k0, klim, wid);
+  }
+  template <bool CHECK_K>
+  __device__ void issue_t(const Src& s, char* stage, int k0, int klim, int wid) {
+    char* dst = stage + wid * 1024;
+    if (same) {
+      const int o = s.template roff_at<CHECK_K>(rs[0], ln, k0 + kk, klim);
+#pragma unroll
+      for (int j = 0; j < QN; ++j)
+        dma16(rsrc, dst + j * 4096, o >= 0 ? (unsigned)(o + j * 32 * (int)sizeof(bf16)) : DMA_OOB);
+    } else {
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int o = s.template roff_at<CHECK_K>(rs[j], ln, k0 + kk, klim);
+        dma16(rsrc, dst + j * 4096, o >= 0 ? (unsigned)o : DMA_OOB);
+      }
+    }
+    s.lane_step(ln);
+  }
+  // as DmaR::frag: lane 4q+p of 16-lane group g reads k-line ks+8g+q (and +4), columns
+  // r16+4p..+3 (8 B inside one 16-B slot of quarter r16/32)
+  __device__ static bf16x8 frag(const char* stage, int r16, int ks, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = ks + 8 * g + q;
+    const int col = r16 + 4 * p;
+    const int cq = col & 31;
+    const char* base = stage + (col >> 5) * 4096 + ((col >> 2) & 1) * 8;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(base + k * 64 + (((cq >> 3) ^ swq(k)) << 4)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(base + (k + 4) * 64 + (((cq >> 3) ^ swq(k + 4)) << 4)));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 };
@@ -2047,6 +2281,12 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     return;
   }
   epilogue_pass<BM, CH, LDC, NTH>(epi, cst, tm * BM, tn * BN);
+  if constexpr (HasBnFin<Epi>::value && BM == 128 && NTH == NT) {
+    if (epi.fin.ctr != nullptr && epi.stats != nullptr) {
+      __syncthreads();  // the staging tile's readers are done with the LDS
+      bnfin_tail<BN>(epi.fin, epi.stats, M, N, tm, tn, lds_raw);
+    }
+  }
 }
 
 // Loader bundles (give the kernel template one type per operand).

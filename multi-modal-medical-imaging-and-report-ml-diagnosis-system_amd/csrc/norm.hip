@@ -857,6 +857,56 @@ extern "C" int mmdx_bn_fwd_ex(int dtype, int train, const void* x, long rows, in
                          residual, relu, y, ws, ws_bytes, st, relu_mask);
 }
 
+// The finalize alone (slabs from a conv epilogue -> mean / rstd / running stats / scale /
+// shift) and the apply alone: the two halves of mmdx_bn_fwd_ex's train forward, for callers
+// whose conv did not finalize its own statistics (mmdx_conv_fwd_bnfin's fallback) and for the
+// apply pass behind one that did.
+extern "C" int mmdx_bn_finalize(const float* stat_part, int stat_blocks, long stat_rows,
+                                long rows, int C, const float* gamma, const float* beta,
+                                float* running_mean, float* running_var, float momentum,
+                                float eps, float* save_mean, float* save_rstd, float* scale,
+                                float* shift, void* stream) {
+  MMDX_CHECK_ARG(stat_part && stat_blocks > 0 && stat_rows > 0 && rows > 0 && C > 0 &&
+                     (long)stat_blocks * stat_rows >= rows && save_mean && save_rstd && scale &&
+                     shift,
+                 "bn finalize: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (stat_blocks > fin_wide())
+    hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
+                       (const float2*)stat_part, stat_blocks, rows, stat_rows, C, gamma, beta,
+                       running_mean, running_var, momentum, eps, save_mean, save_rstd, scale,
+                       shift);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0, st,
+                       (const float2*)stat_part, stat_blocks, rows, stat_rows, C, gamma, beta,
+                       running_mean, running_var, momentum, eps, save_mean, save_rstd, scale,
+                       shift);
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mmdx_bn_apply(int dtype, const void* x, const void* residual, long rows, int C,
+                             const float* scale, const float* shift, int relu, void* y,
+                             uint8_t* relu_mask, void* stream) {
+  MMDX_CHECK_ARG(dtype != F16, "mmdx_bn_apply: fp16 is the C5 path only");
+  MMDX_CHECK_ARG(x && y && scale && shift && rows > 0 && C > 0, "bn apply: bad args");
+  MMDX_CHECK_ARG(!relu_mask || relu, "bn apply: a ReLU mask needs relu");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == BF16) {
+    MMDX_CHECK_ARG(C % 8 == 0, "bn apply: C=%d must be a multiple of 8", C);
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(grid_rows(rows, C, 8)), dim3(256), 0, st,
+                       (const bf16*)x, (const bf16*)residual, rows, C, scale, shift, relu,
+                       (bf16*)y, relu ? relu_mask : nullptr);
+  } else {
+    MMDX_CHECK_ARG(C % 4 == 0, "bn apply: C=%d must be a multiple of 4", C);
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_rows(rows, C, 4)), dim3(256), 0, st,
+                       (const float*)x, (const float*)residual, rows, C, scale, shift, relu,
+                       (float*)y, relu ? relu_mask : nullptr);
+  }
+  MMDX_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int mmdx_bn_fwd(int dtype, int train, const void* x, long rows, int C,
                            const float* stat_part, int stat_blocks, long stat_rows,
                            const float* gamma, const float* beta, float* running_mean,

@@ -7,8 +7,9 @@ counter).  The backward recomputes P and the keep bits and takes rowsum(P o dP) 
 its gradients must match torch's autograd of the same masked, dropped-out attention, and
 the P-saving backward's.  The bars are multiples of the 16-bit unit roundoff u (bf16 2^-8,
 fp16 2^-11), relative to the output's / each gradient's own scale: the kernels round P (and
-dS) to the 16-bit type before each product and the outputs once; the output within 4u of
-torch's fp32, gradients within 8u of torch and 4u of the P-saving kernels.
+dS) to the 16-bit type before each product and the outputs once; the output within 2u of
+torch's fp32, gradients within 4u of torch and of the P-saving kernels (measured on the test's
+cases: 1.3u, 2.1u and 2.4u at most, gpurun_out r05).
 """
 import pytest
 import torch
@@ -85,7 +86,7 @@ def test_flash_attention(dev, dt, B, Ls, H, masked, pd):
     assert torch.equal(r["out1"], r["out0"]), "forward output differs from the P-saving kernel"
     eo = rel_err(r["out1"], r["o"])
     print(f"  out err {eo / u:.2f}u", end="")
-    assert eo <= 4 * u, eo
+    assert eo <= 2 * u, eo
     ref_lse = torch.logsumexp(r["s"], -1)
     assert (r["lse"].cpu() - ref_lse).abs().max().item() <= 1e-3 * max(1.0, ref_lse.abs().max())
     assert torch.isfinite(r["dq1"]).all()
@@ -100,13 +101,13 @@ def test_flash_attention(dev, dt, B, Ls, H, masked, pd):
         d = r["dq1"].float().cpu()
         assert (d[:, :, 0].abs() <= 0.125 * ds_max * k.abs() + 1e-6).all(), "dQ at L = 1"
         assert (d[:, :, 1].abs() <= 0.125 * ds_max * q.abs() + 1e-6).all(), "dK at L = 1"
-        assert _err(r["dq1"], r["grad"], 2) <= 8 * u
+        assert _err(r["dq1"], r["grad"], 2) <= 4 * u
         return
     for i, name in enumerate("qkv"):
         e = _err(r["dq1"], r["grad"], i)
         e2 = _err(r["dq1"], r["dq0"].float().cpu(), i)
         print(f" d{name} {e / u:.2f}u / {e2 / u:.2f}u", end="")
-        assert e <= 8 * u, f"d{name} vs torch {e}"
+        assert e <= 4 * u, f"d{name} vs torch {e}"
         assert e2 <= 4 * u, f"d{name} vs P-saving kernels {e2}"
 
 
@@ -126,6 +127,6 @@ def test_flash_attention_vit_bert_shapes(dev):
     for Ls, masked, pd in ((197, False, 0.0), (128, True, 0.1)):
         r = _run(dev, torch.float16, 4, Ls, 12, masked, pd)
         assert torch.equal(r["out1"], r["out0"])
-        assert rel_err(r["out1"], r["o"]) <= 4 * U[torch.float16]
+        assert rel_err(r["out1"], r["o"]) <= 2 * U[torch.float16]
         for i in range(3):
-            assert _err(r["dq1"], r["grad"], i) <= 8 * U[torch.float16]
+            assert _err(r["dq1"], r["grad"], i) <= 4 * U[torch.float16]

@@ -1,0 +1,147 @@
+"""GPU: the BatchNorm finalize fused into the producing conv (mmdx_conv_fwd_bnfin) against the
+conv + separate finalize it replaces (mmdx_conv_fwd + mmdx_bn_finalize on the same slabs), and
+the apply pass alone (mmdx_bn_apply) against mmdx_bn_fwd_ex's apply.
+
+The fused merge is the same exact decomposition (mean = sum n_b mean_b / n, M2 = sum M2_b +
+n_b (mean_b - mean)^2) taken in two levels (groups of row tiles, then groups), so the
+statistics agree to fp32 rounding (rel 2e-6), the conv output is bit-identical, and two calls
+on the same inputs give bit-identical statistics (the merge order does not depend on which
+block arrives last; the ticket counters return to zero).  Shapes: ResNet-50 C4 convs at
+B = 128 (3136 row tiles: 56 groups of 56), a ragged M, BN = 64 and 128 column tiles, and the
+paths that fall back to the separate finalize (fp32, the pixel-pair stem).
+"""
+import ctypes
+
+import pytest
+import torch
+
+from mmdx import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # N, H, W, C, K, k, s, p
+    (128, 56, 56, 64, 64, 1, 1, 0),     # layer1 conv1: 3136 row tiles, BN = 64
+    (128, 56, 56, 64, 256, 1, 1, 0),    # layer1 conv3: 4 column tiles of 64 / 2 of 128
+    (128, 14, 14, 256, 256, 3, 1, 1),   # layer3 3x3: 196 row tiles
+    (128, 7, 7, 512, 2048, 1, 1, 0),    # layer4 conv3: 49 row tiles, 16 column tiles
+    (3, 13, 11, 64, 128, 3, 2, 1),      # ragged M (126 rows: one partial tile)
+    (7, 9, 9, 128, 64, 3, 1, 1),        # 567 rows: 5 tiles, last one partial
+]
+
+
+def _desc(N, H, W, C, K, k, s, p):
+    P = (H + 2 * p - k) // s + 1
+    Q = (W + 2 * p - k) // s + 1
+    return L.ConvDesc(N, H, W, C, K, k, k, s, s, p, p, P, Q), P, Q
+
+
+def _run(dev, dt, case, fused, seed=0):
+    N, H, W, C, K, k, s, p = case
+    d, P, Q = _desc(*case)
+    g = torch.Generator().manual_seed(seed + sum(case))
+    x = torch.randn(N, H, W, C, generator=g).to(dev, dt)
+    wm = (torch.randn(K, C, k, k, generator=g) * 0.05).to(dev)
+    wk = torch.empty(K, k, k, C, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", L.dtype_code(dt), d, C, L.ptr(wm), L.ptr(wk), None,
+           L.stream())
+    gamma = torch.rand(K, generator=g).to(dev) + 0.5
+    beta = torch.randn(K, generator=g).to(dev)
+    rm0 = torch.randn(K, generator=g).to(dev) * 0.1
+    rv0 = torch.rand(K, generator=g).to(dev) + 0.5
+    rows = N * P * Q
+    rpb = 128
+    nst = (rows + rpb - 1) // rpb
+    part = torch.empty(K, nst, 2, device=dev)
+    y = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    out = {n: torch.full((K,), float("nan"), device=dev)
+           for n in ("mean", "rstd", "scale", "shift")}
+    rm, rv = rm0.clone(), rv0.clone()
+    if fused:
+        nsc = L.lib().mmdx_conv_fwd_bnfin_scratch_size(d)
+        scratch = torch.zeros(nsc, dtype=torch.uint8, device=dev)
+        fin = L.BnFin(L.ptr(gamma), L.ptr(beta), L.ptr(rm), L.ptr(rv), 0.1, 1e-5,
+                      L.ptr(out["mean"]), L.ptr(out["rstd"]), L.ptr(out["scale"]),
+                      L.ptr(out["shift"]), L.ptr(scratch), nsc)
+        L.call("mmdx_conv_fwd_bnfin", L.dtype_code(dt), d, L.ptr(x), L.ptr(wk), L.ptr(y),
+               L.ptr(part), rpb, ctypes.byref(fin), L.stream())
+    else:
+        scratch = None
+        L.call("mmdx_conv_fwd_rows", L.dtype_code(dt), d, L.ptr(x), L.ptr(wk), L.ptr(y),
+               L.ptr(part), rpb, L.stream())
+        L.call("mmdx_bn_finalize", L.ptr(part), nst, rpb, rows, K, L.ptr(gamma), L.ptr(beta),
+               L.ptr(rm), L.ptr(rv), 0.1, 1e-5, L.ptr(out["mean"]), L.ptr(out["rstd"]),
+               L.ptr(out["scale"]), L.ptr(out["shift"]), L.stream())
+    torch.cuda.synchronize()
+    out.update(y=y, rm=rm, rv=rv, scratch=scratch)
+    return out
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_conv_fwd_bnfin_matches_separate_finalize(dev, case, dt):
+    if dt == torch.float32 and case[0] == 128 and case[1] >= 56:
+        pytest.skip("fp32 at the layer-1 size: the fallback path is covered by the others")
+    a = _run(dev, dt, case, True)
+    b = _run(dev, dt, case, False)
+    assert torch.equal(a["y"], b["y"])
+    for n in ("mean", "rstd", "scale", "shift", "rm", "rv"):
+        ref = b[n].double()
+        err = ((a[n].double() - ref).abs() / ref.abs().clamp(min=1e-3)).max().item()
+        assert err <= 2e-6, (n, err)
+    if a["scratch"] is not None:   # every ticket counter is back at zero
+        nctr = a["scratch"][:256].view(torch.int32)
+        assert int(nctr.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("case", CASES[:3])
+def test_conv_fwd_bnfin_deterministic(dev, case):
+    """Same inputs twice through the same scratch: bit-identical statistics (the merge order
+    is fixed, whichever block draws the last ticket)."""
+    a = _run(dev, torch.bfloat16, case, True, seed=5)
+    b = _run(dev, torch.bfloat16, case, True, seed=5)
+    for n in ("mean", "rstd", "scale", "shift", "rm", "rv"):
+        assert torch.equal(a[n], b[n]), n
+
+
+@pytest.mark.parametrize("relu,res", [(1, False), (1, True), (0, False)])
+def test_bn_apply_matches_bn_fwd(dev, relu, res):
+    """mmdx_bn_apply with the finalize's scale / shift == mmdx_bn_fwd_ex's own finalize +
+    apply on the same conv statistics slabs, bit for bit (output and ReLU mask)."""
+    case = (128, 14, 14, 256, 256, 3, 1, 1)
+    N, H, W, C, K, k, s, p = case
+    d, P, Q = _desc(*case)
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, dt)
+    wm = (torch.randn(K, C, k, k, generator=g) * 0.05).to(dev)
+    wk = torch.empty(K, k, k, C, dtype=dt, device=dev)
+    L.call("mmdx_conv_pack_weight", L.BF16, d, C, L.ptr(wm), L.ptr(wk), None, L.stream())
+    rows = N * P * Q
+    nst = (rows + 127) // 128
+    part = torch.empty(K, nst, 2, device=dev)
+    yc = torch.empty(N, P, Q, K, dtype=dt, device=dev)
+    L.call("mmdx_conv_fwd_rows", L.BF16, d, L.ptr(x), L.ptr(wk), L.ptr(yc), L.ptr(part), 128,
+           L.stream())
+    gamma = torch.rand(K, generator=g).to(dev) + 0.5
+    beta = torch.randn(K, generator=g).to(dev)
+    r = torch.randn(N, P, Q, K, generator=g).to(dev, dt) if res else None
+    st = {n: torch.empty(K, device=dev) for n in ("mean", "rstd", "scale", "shift", "m0", "r0")}
+    L.call("mmdx_bn_finalize", L.ptr(part), nst, 128, rows, K, L.ptr(gamma), L.ptr(beta), None,
+           None, 0.1, 1e-5, L.ptr(st["mean"]), L.ptr(st["rstd"]), L.ptr(st["scale"]),
+           L.ptr(st["shift"]), L.stream())
+    y0 = torch.empty_like(yc)
+    m0 = torch.empty(rows, K // 8, dtype=torch.uint8, device=dev) if relu else None
+    wsn = L.lib().mmdx_bn_workspace_size(rows, K)
+    ws = torch.empty(wsn, dtype=torch.uint8, device=dev)
+    L.call("mmdx_bn_fwd_ex", L.BF16, 1, L.ptr(yc), rows, K, L.ptr(part), nst, 128, L.ptr(gamma),
+           L.ptr(beta), None, None, 0.1, 1e-5, L.ptr(st["m0"]), L.ptr(st["r0"]), L.ptr(r), relu,
+           L.ptr(y0), L.ptr(m0), L.ptr(ws), wsn, L.stream())
+    y1 = torch.empty_like(yc)
+    m1 = torch.empty_like(m0) if relu else None
+    L.call("mmdx_bn_apply", L.BF16, L.ptr(yc), L.ptr(r), rows, K, L.ptr(st["scale"]),
+           L.ptr(st["shift"]), relu, L.ptr(y1), L.ptr(m1), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(st["mean"], st["m0"]) and torch.equal(st["rstd"], st["r0"])
+    assert torch.equal(y0, y1)
+    if relu:
+        assert torch.equal(m0, m1)
