@@ -21,6 +21,7 @@
 // The epilogue stages the fp32 accumulators through LDS and stores 4 outputs per lane.
 #pragma once
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 

@@ -800,9 +800,11 @@ TRUNK_GRAD_HOOK = None
 TRUNK_SEGMENT_HOOK = None
 
 # Train-mode BN statistics finalized inside the producing conv launch (mmdx_conv_fwd_bnfin) and
-# the BN forward reduced to its apply pass; MMDX_BN_FIN=0: conv, then finalize + apply (read
-# when a plan is built — A/B runs).
-BN_FIN_FUSED = os.environ.get("MMDX_BN_FIN", "1") != "0"
+# the BN forward reduced to its apply pass (MMDX_BN_FIN=1; read when a plan is built).  Off by
+# default: the ticket drain at the end of every conv block and the last blocks' serial slab
+# merges added 0.78 ms/step of conv time against the 0.47 ms of finalize launches they remove
+# (C4 8733 / 8725 vs 8818 / 8817 samples/s paired).
+BN_FIN_FUSED = os.environ.get("MMDX_BN_FIN", "0") == "1"
 
 # Downsample branch of the forward on the side stream (False: in order on the main stream;
 # read when a plan is built — for A/B runs, tools/step_probe.py --ds-main).

