@@ -308,6 +308,27 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
     return step
 
 
+def capture_step(step):
+    """`step` recorded once into a hipGraph (torch.cuda.graph, relaxed capture: the text
+    tower is issued from its worker thread onto the joined side stream); the returned
+    callable replays it.  Inputs, parameters, gradients and optimizer state keep their
+    addresses between replays; the dropout counters and the AdamW step count live on the
+    device, so every replay is a fresh step."""
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, capture_error_mode="relaxed"):
+        out = step()
+    torch.cuda.synchronize()
+
+    def replay():
+        g.replay()
+        return out
+    replay.graph = g
+    replay.norm = step.norm
+    replay.towers = step.towers
+    return replay
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -484,6 +505,14 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # MMDX_GRAPH_STEP=1: the whole train step (both towers, backward, clip, AdamW) captured
+    # into one hipGraph after the warm-up and replayed per step (no per-kernel host issue)
+    graph_step = os.environ.get("MMDX_GRAPH_STEP", "0") == "1"
+    if graph_step:
+        step = capture_step(step)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
     if dp:
         dist.barrier()
     # Conv (dominant-family) launch durations: HIP events around every conv launch of the
@@ -593,7 +622,8 @@ def main():
         "dtype": "fp16" if dtype == torch.float16 else "bf16",
         "data": "synthetic (U[0,1) ImageNet-normalised 224x224 images, 128-token [CLS]..[SEP] "
                 "reports, Bernoulli(0.15) labels); random-init weights",
-        "launch": "eager" + (" (text tower: hipGraph replay)" if graph_text else ""),
+        "launch": ("hipGraph (whole step)" if graph_step else
+                   "eager" + (" (text tower: hipGraph replay)" if graph_text else "")),
         "stream_priority": "main+text",
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,

@@ -14,6 +14,8 @@ runs after the all-reduce, so every rank clips identically.
 from __future__ import annotations
 
 import os
+import sys
+import time
 
 import torch
 import torch.distributed as dist
@@ -21,6 +23,22 @@ import torch.distributed as dist
 from .trace import rng
 
 BUCKET_BYTES = 64 << 20
+# whole flat gradient buffers below this travel in the packed buckets (see _launch)
+SMALL_ARENA_BYTES = 16 << 20
+
+# MMDX_DP_TRACE=1: per step, the collectives issued (kind, elements, dtype) and the host time
+# of launch() / finish(); the 8th step's record is printed to stderr (tools/lab/r05_rccl.sh)
+_TRACE = ({"calls": [], "host": [], "step": 0}
+          if os.environ.get("MMDX_DP_TRACE", "0") == "1" else None)
+
+
+def _trace_step():
+    _TRACE["step"] += 1
+    if _TRACE["step"] == 8:
+        print("[dp-trace] collectives:", _TRACE["calls"], file=sys.stderr)
+        print("[dp-trace] host ms:", [(k, round(v * 1e3, 3)) for k, v in _TRACE["host"]],
+              file=sys.stderr)
+    _TRACE["calls"], _TRACE["host"] = [], []
 
 
 class GradAllReducer:
@@ -39,7 +57,8 @@ class GradAllReducer:
     """
 
     def __init__(self, params, world_size: int | None = None, bucket_bytes: int = BUCKET_BYTES,
-                 group=None, bucket_dtype: torch.dtype | None = None, rehearse: bool = False):
+                 group=None, bucket_dtype: torch.dtype | None = None, rehearse: bool = False,
+                 small_arena_bytes: int = SMALL_ARENA_BYTES):
         self.params = [p for p in params if p.requires_grad]
         self.world = world_size or dist.get_world_size(group)
         # rehearse: run every collective even in a 1-rank group (RCCL on one GPU exercises
@@ -50,6 +69,7 @@ class GradAllReducer:
         self._avg = (self.active and dist.is_initialized()
                      and dist.get_backend(group) == "nccl")
         self.bucket_bytes = bucket_bytes
+        self.small_arena_bytes = small_arena_bytes
         self.group = group
         # packed buckets may travel in bf16 (MMDX_DP_BUCKET_DTYPE=bf16: half the xGMI bytes
         # for C5's ~800 MB of per-tensor gradients; RCCL sums in bf16, the mean is taken in
@@ -79,7 +99,7 @@ class GradAllReducer:
             return
         part = buf[lo:hi]
         with rng("mmdx/allreduce/trunk_segment"):
-            work = dist.all_reduce(part, op=self._op(part), group=self.group, async_op=True)
+            work = self._all_reduce(part, "segment")
         self._pending.append((None, part, work, None))
         off = buf.storage_offset()
         self._regions.setdefault(_store_key(buf), []).append((off + lo, off + hi))
@@ -103,21 +123,20 @@ class GradAllReducer:
             with torch.cuda.stream(self._comm):
                 self._comm.wait_event(event)
                 tmp = view.clone()
-                work = dist.all_reduce(tmp, op=self._op(tmp), group=self.group,
-                                       async_op=True)
+                work = self._all_reduce(tmp, "region")
             tmp.record_stream(torch.cuda.current_stream(buf.device))
         else:
             tmp = view.clone()
-            work = dist.all_reduce(tmp, op=self._op(tmp), group=self.group, async_op=True)
+            work = self._all_reduce(tmp, "region")
         self._pending.append((None, tmp, work, view))
         off = buf.storage_offset()
         self._regions.setdefault(_store_key(buf), []).append((off + lo, off + hi))
 
-    def _buckets(self, grads):
+    def _buckets(self, pairs):
         plan, cur, size = [], [], 0
         # reverse parameter order ~ order in which backward produces the gradients
-        for g in reversed(grads):
-            cur.append(g)
+        for p, g in reversed(pairs):
+            cur.append((p, g))
             size += g.numel() * g.element_size()
             if size >= self.bucket_bytes:
                 plan.append(cur)
@@ -130,44 +149,57 @@ class GradAllReducer:
         """Start the all-reduce of these parameters' gradients (default: all remaining)."""
         if not self.active:
             return
+        t0 = time.perf_counter()
         with rng("mmdx/allreduce/launch"):
             self._launch(params)
+        if _TRACE is not None:
+            _TRACE["host"].append(("launch", time.perf_counter() - t0))
 
     def _launch(self, params):
         ps = self.params if params is None else [p for p in params if p.requires_grad]
-        grads = []
+        pairs = []
         for p in ps:
             if id(p) in self._launched or p.grad is None:
                 continue
             self._launched.add(id(p))
-            grads.append(p.grad)
+            pairs.append((p, p.grad))
         # Gradients that together tile one whole flat buffer (the ResNet trunk's gradient
-        # arena) are reduced in place on that buffer, minus what launch_region already
-        # started.  They are found by their shared STORAGE: autograd stores a returned view
-        # detached (.grad._base is None), so the view relation itself does not survive.
+        # arena, the encoder stacks') are reduced in place on that buffer, minus what
+        # launch_region already started.  They are found by their shared STORAGE: autograd
+        # stores a returned view detached (.grad._base is None), so the view relation itself
+        # does not survive.  Small flat buffers (the BiLSTM's per-layer weight and bias
+        # pairs, a few MB each) join the packed bucket instead: one collective per ~64 MB,
+        # not one per buffer (each costs ~20 us of host issue at the end of the backward).
         by_store = {}
-        for g in grads:
-            by_store.setdefault(_store_key(g), []).append(g)
+        for p, g in pairs:
+            by_store.setdefault(_store_key(g), []).append((p, g))
         loose = []
-        for key, gs in by_store.items():
+        for key, pgs in by_store.items():
+            gs = [g for _, g in pgs]
             # a buffer that launch_region already started is the trunk's arena even when
             # frozen parameters leave gaps in it (their slots are reduced too, unused): the
             # rest must not also travel through the packed buckets
-            flat = _whole_buffer(gs, allow_gaps=key in self._regions)
-            if flat is None:
-                loose += gs
+            started = key in self._regions
+            flat = _whole_buffer(gs, allow_gaps=started)
+            if flat is None or (not started and
+                                flat.numel() * flat.element_size() < self.small_arena_bytes):
+                loose += pgs
                 continue
             for a, z in _complement(self._regions.get(key, []), flat.numel()):
                 part = flat[a:z]   # what launch_region left
-                work = dist.all_reduce(part, op=self._op(part), group=self.group,
-                                       async_op=True)
+                work = self._all_reduce(part, "arena")
                 self._pending.append((None, part, work, None))
         for bucket in self._buckets(loose):
-            flat = torch._utils._flatten_dense_tensors(bucket)
+            flat = torch._utils._flatten_dense_tensors([g for _, g in bucket])
             if self.bucket_dtype is not None and flat.dtype != self.bucket_dtype:
                 flat = flat.to(self.bucket_dtype)
-            work = dist.all_reduce(flat, op=self._op(flat), group=self.group, async_op=True)
+            work = self._all_reduce(flat, f"bucket[{len(bucket)}]")
             self._pending.append((bucket, flat, work, None))
+
+    def _all_reduce(self, t, kind):
+        if _TRACE is not None:
+            _TRACE["calls"].append((kind, t.numel(), str(t.dtype)))
+        return dist.all_reduce(t, op=self._op(t), group=self.group, async_op=True)
 
     def _op(self, t):
         # averaged in the collective for fp32 with RCCL; bf16 buckets sum in bf16 and take
@@ -176,8 +208,12 @@ class GradAllReducer:
         return dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
 
     def finish(self):
+        t0 = time.perf_counter()
         with rng("mmdx/allreduce/finish"):
             self._finish()
+        if _TRACE is not None:
+            _TRACE["host"].append(("finish", time.perf_counter() - t0))
+            _trace_step()
 
     def _finish(self):
         inv = 1.0 / self.world
@@ -198,10 +234,12 @@ class GradAllReducer:
             if dest is not None:
                 dest.copy_(flat)
             if bucket is not None:
-                # one multi-tensor launch instead of a copy kernel per gradient (C4: ~200
-                # per step, 0.65 ms of serialized copies after the backward)
-                torch._foreach_copy_(list(bucket),
-                                     list(torch._utils._unflatten_dense_tensors(flat, bucket)))
+                # the averaged bucket becomes the gradients: each .grad is rebound to its view
+                # of `flat` (no copy back; the foreach copy it replaces was ~70 us of the
+                # stream's tail at C4, after every other backward kernel)
+                views = torch._utils._unflatten_dense_tensors(flat, [g for _, g in bucket])
+                for (p, _), v in zip(bucket, views):
+                    p.grad = v
         self._pending = []
         self._launched = set()
         self._regions = {}

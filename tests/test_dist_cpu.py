@@ -69,10 +69,10 @@ def _worker_frozen(rank, world, port, out):
     params[0].grad = flat[:120].view(40, 3).detach()
     params[2].grad = torch.randn(16, generator=g)
     params[3].grad = torch.randn(5, 5, generator=g)
-    red = GradAllReducer(params, world, bucket_bytes=64)
+    red = GradAllReducer(params, world, bucket_bytes=64, small_arena_bytes=0)
     red.trunk_hook(flat, [(60, 120, None)])
     red.launch()
-    assert all(b is None or id(params[0].grad) not in {id(t) for t in b}
+    assert all(b is None or id(params[0].grad) not in {id(g) for _, g in b}
                for b, *_ in red._pending), "arena gradient in a packed bucket"
     red.finish()
     out[rank] = [params[0].grad.clone(), params[2].grad.clone(), params[3].grad.clone()]
@@ -117,7 +117,7 @@ def _worker_flat(rank, world, port, out, region=0, detach=False):
         assert params[0].grad._base is None
     params[2].grad = torch.randn(16, generator=g)
     params[3].grad = torch.randn(5, 5, generator=g)
-    red = GradAllReducer(params, world, bucket_bytes=64)
+    red = GradAllReducer(params, world, bucket_bytes=64, small_arena_bytes=0)
     if region == 1:  # the buffer's tail first (the trunk's last layer)
         red.launch_region(flat, 100, flat.numel())
     elif region == 2:  # per-layer slices in backward order (resnet.TRUNK_GRAD_HOOK)
@@ -128,7 +128,7 @@ def _worker_flat(rank, world, port, out, region=0, detach=False):
     red.launch([params[2]])
     red.launch()
     arena = {id(params[0].grad), id(params[1].grad)}
-    assert all(b is None or not arena & {id(t) for t in b} for b, *_ in red._pending), \
+    assert all(b is None or not arena & {id(g) for _, g in b} for b, *_ in red._pending), \
         "arena gradients went through a packed bucket"
     red.finish()
     if not detach:
@@ -146,6 +146,52 @@ def test_grad_allreduce_flat_base_and_early_launch_gloo(region, detach):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker_flat, args=(world, port, out, region, detach), nprocs=world, join=True)
+    exp = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(200 + r)
+        flat = torch.randn(127, generator=g)
+        exp.append([flat[:120].view(40, 3), flat[120:127], torch.randn(16, generator=g),
+                    torch.randn(5, 5, generator=g)])
+    mean = [(a + b) / 2 for a, b in zip(*exp)]
+    for r in range(world):
+        for got, want in zip(out[r], mean):
+            assert torch.allclose(got, want, atol=1e-6)
+
+
+def _worker_small_arena(rank, world, port, out):
+    """A whole flat buffer below small_arena_bytes (the BiLSTM's per-layer weight / bias
+    pairs) travels in the packed bucket with the loose gradients — one collective — and every
+    .grad is rebound to its view of the averaged bucket."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx import dist as D
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in SHAPES2]
+    g = torch.Generator().manual_seed(200 + rank)
+    flat = torch.randn(127, generator=g)
+    params[0].grad = flat[:120].view(40, 3).detach()
+    params[1].grad = flat[120:127].detach()
+    params[2].grad = torch.randn(16, generator=g)
+    params[3].grad = torch.randn(5, 5, generator=g)
+    red = D.GradAllReducer(params, world)
+    calls = []
+    real = red._all_reduce
+    red._all_reduce = lambda t, kind: (calls.append(kind), real(t, kind))[1]
+    red.reduce()
+    assert calls == ["bucket[4]"], calls
+    assert all(p.grad.untyped_storage().data_ptr() != flat.untyped_storage().data_ptr()
+               for p in params[:2])
+    assert len({p.grad.untyped_storage().data_ptr() for p in params}) == 1
+    out[rank] = [p.grad.clone() for p in params]
+    dist.destroy_process_group()
+
+
+def test_small_arena_packed_gloo():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_small_arena, args=(world, port, out), nprocs=world, join=True)
     exp = []
     for r in range(world):
         g = torch.Generator().manual_seed(200 + r)
@@ -237,12 +283,12 @@ def _worker_stack(rank, world, port, out, sizes, regions):
         p.grad = flat[o:o + n].detach()
         o += n
     params[-1].grad = torch.randn(9, generator=g)
-    red = GradAllReducer(params, world, bucket_bytes=64)
+    red = GradAllReducer(params, world, bucket_bytes=64, small_arena_bytes=0)
     for lo, hi in regions:
         red.trunk_segment(flat, lo, hi)
     red.launch()
     stack = {id(p.grad) for p in params[:-1]}
-    assert all(b is None or not stack & {id(t) for t in b} for b, *_ in red._pending)
+    assert all(b is None or not stack & {id(g) for _, g in b} for b, *_ in red._pending)
     red.finish()
     out[rank] = [p.grad.clone() for p in params]
     dist.destroy_process_group()

@@ -163,7 +163,7 @@ def _rccl_worker(port, out, early):
         trunk_p = {id(p) for p in img.backbone.parameters()}
     trunk = {id(p.grad) for p in params if id(p) in trunk_p and p.grad is not None}
     red.launch()
-    packed = sum(1 for b, *_ in red._pending if b is not None for t in b if id(t) in trunk)
+    packed = sum(1 for b, *_ in red._pending if b is not None for _, t in b if id(t) in trunk)
     red.finish()
     torch.cuda.synchronize()
     bad = []
