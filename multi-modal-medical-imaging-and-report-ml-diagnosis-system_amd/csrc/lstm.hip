@@ -18,6 +18,15 @@ constexpr int LSTM_RB = 16;   // batch rows per workgroup
 constexpr int LSTM_NW = 8;    // waves per workgroup
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+// The bf16 recurrences' gate functions: v_exp + v_rcp (1 ulp each) instead of an IEEE divide
+// and the libm tanh, whose VALU sequences made the cell update 3.7 of a 9.9 us step (probe,
+// tools/lab/lstm_probe.py).  Absolute error <= ~1e-7, far below the bf16 rounding of h.
+__device__ __forceinline__ float sigm_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+__device__ __forceinline__ float tanh_fast(float x) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
+}
 
 // acc[j] += A[16 rows][K] (LDS, row base a_row = &A[lane&15][(lane>>4)*FRAG]) x B fragments
 //           streamed from global (L2-resident weights): this lane's fragment of tile j at
@@ -121,13 +130,14 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
       const int e = threadIdx.x + i * LSTM_NW * 64;
       const int row = e / H, u = e - row * H;
       const int b = b0 + row;
-      const float gi = sigm(sg[row * G4 + u]);
-      const float gf = sigm(sg[row * G4 + H + u]);
-      const float gg = tanhf(sg[row * G4 + 2 * H + u]);
-      const float go = sigm(sg[row * G4 + 3 * H + u]);
+      constexpr bool fast = sizeof(T) == 2;
+      const float gi = fast ? sigm_fast(sg[row * G4 + u]) : sigm(sg[row * G4 + u]);
+      const float gf = fast ? sigm_fast(sg[row * G4 + H + u]) : sigm(sg[row * G4 + H + u]);
+      const float gg = fast ? tanh_fast(sg[row * G4 + 2 * H + u]) : tanhf(sg[row * G4 + 2 * H + u]);
+      const float go = fast ? sigm_fast(sg[row * G4 + 3 * H + u]) : sigm(sg[row * G4 + 3 * H + u]);
       const float c = gf * creg[i] + gi * gg;
       creg[i] = c;
-      const float h = go * tanhf(c);
+      const float h = go * (fast ? tanh_fast(c) : tanhf(c));
       sh[row * LDH + u] = from_f<T>(h);
       if (b < B) {
         hout[((long)b * L + t) * 2 * H + dir * H + u] = from_f<T>(h);
@@ -210,7 +220,7 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
         const float gi = gv[i][0], gf = gv[i][1], gg = gv[i][2], go = gv[i][3];
         const float c = cv[i];
         const float dh = dhv[i] + sdh[row * H + u];
-        const float tc = tanhf(c);
+        const float tc = sizeof(T) == 2 ? tanh_fast(c) : tanhf(c);
         const float dc = dh * go * (1.f - tc * tc) + dcn[i];
         const float d_o = dh * tc;
         dgi = dc * gg * gi * (1.f - gi);
@@ -271,6 +281,8 @@ constexpr int COOP_LDH = COOP_H + 8;       // padded h row (bf16): conflict-free
 constexpr int COOP_SC1 = 16;               // buffer instruction aux: sc1 (write-through / L1 bypass)
 constexpr long COOP_SPIN_MAX = 1L << 26;   // default bounded wait (~2 s): a lost peer ends the kernel
 constexpr int COOP_DEBUG_DROP_PEER = 1;    // debug flag: workgroup 0 of direction 0 never signals
+constexpr int COOP_DEBUG_TIMING = 2;       // debug flag: per-step phase timestamps (lab probe)
+constexpr int COOP_TS_PHASES = 8;          // timestamps per (workgroup, step)
 
 typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
 
@@ -293,7 +305,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
     const float* __restrict__ xg, const bf16* __restrict__ whh, int B, int L,
     bf16* __restrict__ hout, float* __restrict__ csave, float* __restrict__ gsave,
     bf16* __restrict__ hx, unsigned* __restrict__ ctr, int* __restrict__ status, long spin_max,
-    int debug) {
+    int debug, unsigned long long* __restrict__ tst) {
   constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
   constexpr int NROWS = 64 * RT;
   static_assert(RT == 1 || RT == 2, "row tiles per wave");
@@ -337,19 +349,51 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
   bf16* hxd = hx + (long)dir * 2 * B * H;
   const __amdgpu_buffer_rsrc_t hrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)hxd, (short)0, 2 * B * H * 2, 0x00020000);
-  for (int s = 0; s < L; ++s) {
-    const int t = dir == 0 ? s : L - 1 - s;
-    // this step's input-projection operands: independent of h, in flight during the wait
-    float xv[RT][4][4];
+  // lab probe (COOP_DEBUG_TIMING): thread 0 stamps the 100 MHz realtime clock at the phase
+  // boundaries of every step, [group][dir][blk][step][phase]
+  unsigned long long* tsw =
+      tst ? tst + ((long)(blockIdx.z * 2 + dir) * COOP_NB + blk) * L * COOP_TS_PHASES : nullptr;
+#define COOP_STAMP(k)                                                                       \
+  do {                                                                                      \
+    if (tsw && threadIdx.x == 0) tsw[s * COOP_TS_PHASES + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  // The input-projection operands of step s+1 and the backward's saves of step s-1 are issued
+  // while step s's gates run: issued right after the publish (as before round 5) they sat in
+  // front of the next wait's counter poll in thread 0's memory queue, so the last workgroup to
+  // publish also saw the counter last (4.4 us behind its peers) and stayed last every step
+  // (probe: tools/lab/lstm_probe.py).  Only the poll and the h loads touch memory between a
+  // publish and the next step's gates.
+#define COOP_LOAD_XV(XV, TT)                                                                 \
+  do {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < RT; ++i)                                            \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                           \
+      const int b = rb0 + (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;                           \
+      const float* xp = xg + (((long)min(b, B - 1) * L + (TT)) * 2 + dir) * G4 + ucol;        \
+      _Pragma("unroll") for (int g = 0; g < 4; ++g) XV[i][r][g] = xp[g * H];                  \
+    }                                                                                        \
+  } while (0)
+  float xv[RT][4][4];
+  COOP_LOAD_XV(xv, dir == 0 ? 0 : L - 1);
+  float hv[RT][4], cv[RT][4], gv[RT][4][4];   // step s-1's outputs, saved during step s
+  int tprev = 0;
+  auto save = [&](int tt) {
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rb0 + (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
-        const float* xp = xg + (((long)min(b, B - 1) * L + t) * 2 + dir) * G4 + ucol;
+        if (b >= B) continue;
+        hout[((long)b * L + tt) * 2 * H + dir * H + ucol] = from_f<bf16>(hv[i][r]);
+        const long sidx = ((long)dir * L + tt) * B + b;
+        csave[sidx * H + ucol] = cv[i][r];
+        float* gp = gsave + sidx * G4;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) xv[i][r][g] = xp[g * H];
+        for (int g = 0; g < 4; ++g) gp[g * H + ucol] = gv[i][r][g];
       }
+  };
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    COOP_STAMP(0);
     // wait until every workgroup of this direction has published h_{t-1}.  The wait is
     // bounded: a peer that never arrives (not co-resident, lost) makes the waiter set the
     // sticky status word and every workgroup leave, so the grid always drains; the host
@@ -379,6 +423,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       __syncthreads();
       if (*sgiveup) return;
     }
+    COOP_STAMP(1);
     // h_{t-1} -> LDS (zeros at the first step); sc1 loads: the producers' sc1 stores are
     // visible to them without an L1 invalidate
     // All of a thread's chunks are requested before any is written to LDS: one memory round
@@ -410,7 +455,11 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       for (int i = 0; i < HCH; ++i) *(coop_v4u*)(hdst + i * 16 * COOP_LDH) = coop_v4u{0u, 0u, 0u, 0u};
     }
     __syncthreads();
-    float hv[RT][4], cv[RT][4], gv[RT][4][4];
+    COOP_STAMP(2);
+    if (s > 0) save(tprev);
+    float xn[RT][4][4];
+    if (s + 1 < L) COOP_LOAD_XV(xn, dir == 0 ? s + 1 : L - 2 - s);
+    COOP_STAMP(3);
     // every W fragment is read from LDS once per step, for all of the wave's row tiles
     constexpr int IB = RT;
 #pragma unroll
@@ -441,13 +490,13 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
         const f32x4* acc = accs[ii];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float gi = sigm(acc[0][r] + xv[i][r][0]);
-          const float gf = sigm(acc[1][r] + xv[i][r][1]);
-          const float gg = tanhf(acc[2][r] + xv[i][r][2]);
-          const float go = sigm(acc[3][r] + xv[i][r][3]);
+          const float gi = sigm_fast(acc[0][r] + xv[i][r][0]);
+          const float gf = sigm_fast(acc[1][r] + xv[i][r][1]);
+          const float gg = tanh_fast(acc[2][r] + xv[i][r][2]);
+          const float go = sigm_fast(acc[3][r] + xv[i][r][3]);
           const float c = gf * creg[i][r] + gi * gg;
           creg[i][r] = c;
-          const bf16 h = from_f<bf16>(go * tanhf(c));
+          const bf16 h = from_f<bf16>(go * tanh_fast(c));
           hv[i][r] = (float)h;
           cv[i][r] = c;
           gv[i][r][0] = gi; gv[i][r][1] = gf; gv[i][r][2] = gg; gv[i][r][3] = go;
@@ -457,7 +506,9 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       }
     }
     __syncthreads();
-    // publish h_t: 16-B sc1 stores of the [B][32] slice, drain, one agent atomic add
+    COOP_STAMP(4);
+    // publish h_t: 16-B sc1 stores of the [B][32] slice, drain, one agent atomic add (the
+    // drain also covers the saves and operand loads issued above, long since complete)
     if (s + 1 < L) {
       const int par_out = (s & 1) * B * H * 2;
       const int nrow = min(NROWS, B - rb0);
@@ -472,21 +523,18 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
       if (threadIdx.x == 0 && !((debug & COOP_DEBUG_DROP_PEER) && blk == 0 && dir == 0))
         __hip_atomic_fetch_add(myctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // saves for the backward (overlap the next step's wait)
+    COOP_STAMP(5);
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = rb0 + (rg + 4 * i) * 16 + (lane >> 4) * 4 + r;
-        if (b >= B) continue;
-        hout[((long)b * L + t) * 2 * H + dir * H + ucol] = from_f<bf16>(hv[i][r]);
-        const long sidx = ((long)dir * L + t) * B + b;
-        csave[sidx * H + ucol] = cv[i][r];
-        float* gp = gsave + sidx * G4;
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) gp[g * H + ucol] = gv[i][r][g];
-      }
+        for (int g = 0; g < 4; ++g) xv[i][r][g] = xn[i][r][g];
+    tprev = t;
   }
+  save(tprev);   // the last step's outputs
+#undef COOP_LOAD_XV
+#undef COOP_STAMP
 }
 
 // W_hh [2][4H][H] -> the backward's B-operand fragments, [2][H/16][4H/KS][64 lanes][FRAG]:
@@ -543,6 +591,13 @@ extern "C" size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H) {
   return (size_t)2 * 2 * B * H * 2 + 256;
 }
 
+// debug_flags & COOP_DEBUG_TIMING (lab probe): the phase timestamps follow the workspace,
+// [groups][2][COOP_NB][L][COOP_TS_PHASES] x u64 (the caller passes a larger workspace)
+static size_t coop_timing_bytes(int B, int L) {
+  const int groups = B <= 128 ? 1 : (B + 127) / 128;
+  return (size_t)groups * 2 * COOP_NB * L * COOP_TS_PHASES * 8;
+}
+
 // The cooperative forward needs its 2 x COOP_NB x groups workgroups resident at once: one per
 // CU (~140 KB of LDS each) on distinct CUs.  Checked once per device and kernel variant: the
 // device must have at least that many CUs and the kernel must fit one block per CU.  The
@@ -580,6 +635,13 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
     bf16* hx = (bf16*)ws;
     unsigned* ctr = (unsigned*)((char*)ws + (size_t)2 * 2 * B * H * 2);
     const long spin_max = spin_limit > 0 ? spin_limit : COOP_SPIN_MAX;
+    unsigned long long* tst = nullptr;
+    if (debug_flags & COOP_DEBUG_TIMING) {
+      MMDX_CHECK_ARG(ws_bytes >= need + coop_timing_bytes(B, L),
+                     "lstm fwd: the timing probe needs %zu more workspace bytes",
+                     coop_timing_bytes(B, L));
+      tst = (unsigned long long*)((char*)ws + need);
+    }
     hipLaunchKernelGGL(lstm_coop_ctr_zero_kernel, dim3(1), dim3(64), 0, st, ctr);
     // B > 128: independent groups of 128 rows (grid z), each with W_hh in LDS (RT = 2)
     const int groups = B <= 128 ? 1 : (B + 127) / 128;
@@ -590,7 +652,7 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
                    "lstm fwd: the cooperative recurrence cannot be co-resident here");       \
     hipLaunchKernelGGL(lstm_fwd_coop_kernel<RT>, grid, dim3(512), 0, st, (const float*)xg,   \
                        (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr,   \
-                       status, spin_max, debug_flags);                                       \
+                       status, spin_max, debug_flags, tst);                                  \
   } while (0)
     if (B <= 64)
       COOP_LAUNCH(1);
