@@ -552,7 +552,8 @@ int mmdx_attention_bwd_lse(int dtype, const void* qkv, const void* out, const fl
 /* LSTM recurrence for one layer, both directions (build-defined C3/C4 tower).
  * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);
  * w_hh: [2][4H][H] compute dtype; h_out: [B, L, 2H]; saved c: [2, L, B, H] fp32,
- * gates: [2, L, B, 4H] fp32 post-activation (for backward). */
+ * gates: [2, L, B, H, 4] fp32 post-activation, the four gates of a unit adjacent (for
+ * backward). */
 /* Workspace for the cooperative bf16 forward (H = 256, B <= 256): h exchange + counters.
  * 0 when that path does not apply (then ws may be NULL and the batch-partitioned kernel
  * runs).
@@ -561,7 +562,9 @@ int mmdx_attention_bwd_lse(int dtype, const void* qkv, const void* out, const fl
  * ~2 s) — every workgroup then leaves and the outputs are invalid.  The kernel never clears
  * it; the caller copies it to the host at a sync point and raises (bilstm.py).  A non-zero
  * status on entry makes the kernel leave at its first wait.  debug_flags bit 0 (tests
- * only): workgroup 0 of direction 0 never signals, forcing the timeout path.
+ * only): workgroup 0 of direction 0 never signals, forcing the timeout path; bit 1 (lab
+ * probe, tools/lab/lstm_probe.py): per-step phase timestamps after the workspace (the
+ * caller passes [groups][2][8][L][8] u64 more).
  * Returns -22 if the device cannot hold the cooperative grid resident. */
 size_t mmdx_lstm_fwd_workspace_size(int dtype, int B, int L, int H);
 int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
@@ -569,10 +572,15 @@ int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int
                   size_t ws_bytes, int* status, long spin_limit, int debug_flags,
                   void* stream);
 size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H);
+/* Backward.  status (may be NULL): the forward's device status word; with it, bf16, H = 256
+ * and B <= 512 run the cooperative recurrence (4 workgroups per 16-row block and direction
+ * exchanging dG slices, W_hh^T held in registers), whose bounded wait sets *status = 2 when
+ * a peer never arrives within spin_limit polls (<= 0: the default).  NULL: the
+ * batch-partitioned kernel.  Both give bit-identical outputs. */
 int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                   const float* gates_save, const void* dh_out, int B, int L, int H,
-                  void* dxg, float* dw_hh, void* workspace, size_t ws_bytes,
-                  void* stream);
+                  void* dxg, float* dw_hh, void* workspace, size_t ws_bytes, int* status,
+                  long spin_limit, void* stream);
 
 /* ---------------------------------------------------------------- T5 report head
  * (TP:545-618 cond_proj + T5ForConditionalGeneration, TP:983-991 /

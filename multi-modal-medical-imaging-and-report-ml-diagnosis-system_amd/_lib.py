@@ -171,7 +171,7 @@ SIGNATURES = {
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp, i64, i32, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_fwd_workspace_size": (sz, [i32, i32, i32, i32]),
-    "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
+    "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp, i64, vp]),
     "mmdx_patchify": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
     "mmdx_vit_tokens_fwd": (i32, [i32, vp, vp, vp, i32, i32, i32, vp, vp]),
     "mmdx_vit_tokens_bwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from types import SimpleNamespace
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -30,7 +32,8 @@ class RecurrenceError(RuntimeError):
 
 
 class _CoopStatus:
-    """Sticky device status word of the cooperative forward recurrence (mmdx_lstm_fwd).
+    """Sticky device status word of the cooperative recurrences (mmdx_lstm_fwd sets 1,
+    mmdx_lstm_bwd 2).
 
     After every cooperative launch the word is copied (async, same stream) into pinned host
     memory behind an event.  `poll()` raises RecurrenceError once a completed copy shows a
@@ -54,21 +57,24 @@ class _CoopStatus:
         if block:
             # read the device word itself: a graph-replayed launch (hipGraph capture skips
             # the per-launch copy) sets it too
-            if int(self.word[0].item()) != 0:
-                self._raise()
+            code = int(self.word[0].item())
+            if code != 0:
+                self._raise(code)
             return
         ev = self.ev
         if ev is None or not ev.query():
             return
-        if int(self.host[0]) != 0:
-            self._raise()
+        code = int(self.host[0])
+        if code != 0:
+            self._raise(code)
 
     @staticmethod
-    def _raise():
+    def _raise(code):
+        which = "mmdx_lstm_bwd" if code == 2 else "mmdx_lstm_fwd"
         raise RecurrenceError(
-                "mmdx BiLSTM: the cooperative recurrence timed out waiting for a peer "
-                "workgroup (mmdx_lstm_fwd status=1); the text tower's outputs and gradients "
-                "of this step are invalid")
+                f"mmdx BiLSTM: the cooperative recurrence timed out waiting for a peer "
+                f"workgroup ({which} status={code}); the text tower's outputs and gradients "
+                f"of this step are invalid")
 
     def reset(self):
         self.word.zero_()
@@ -95,6 +101,10 @@ def check_recurrence(block=True):
 
 # debug knobs of the cooperative forward (tests force the timeout path through these)
 DEBUG = {"spin_limit": 0, "flags": 0}
+
+# the cooperative recurrent backward (mmdx_lstm_bwd with a status word; MMDX_LSTM_BWD_COOP=0:
+# the batch-partitioned kernel, for A/B runs — bit-identical outputs)
+BWD_COOP = os.environ.get("MMDX_LSTM_BWD_COOP", "1") != "0"
 
 
 def _cat_cast(ws, T, dev):
@@ -153,8 +163,14 @@ class _LSTMLayerFn(torch.autograd.Function):
         dwhh = torch.empty((2 * G4, H), dtype=torch.float32, device=dev)
         n = L.lib().mmdx_lstm_workspace_size(L.dtype_code(T), B, Ls, H)
         ws = L.workspace(n, dev)
+        # the cooperative backward (bf16, H 256) shares the forward's sticky status word
+        fw = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(T), B, Ls, H)
+        status = coop_status(dev) if fw and BWD_COOP else None
         call("mmdx_lstm_bwd", L.dtype_code(T), ptr(whh), ptr(hout), ptr(cs), ptr(gs), ptr(dh), B,
-             Ls, H, ptr(dxg), ptr(dwhh), ptr(ws), n, stream())
+             Ls, H, ptr(dxg), ptr(dwhh), ptr(ws), n, ptr(status.word) if status else None,
+             int(DEBUG["spin_limit"]), stream())
+        if status is not None:
+            status.after_launch()
         dwih = torch.empty((2 * G4, In), dtype=torch.float32, device=dev)
         db = torch.empty(2 * G4, dtype=torch.float32, device=dev)
         # dW_ih and the (shared) bias gradient in one launch sequence

@@ -143,11 +143,8 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_fwd_kernel(
         hout[((long)b * L + t) * 2 * H + dir * H + u] = from_f<T>(h);
         const long sidx = (((long)dir * L + t) * B + b);
         csave[sidx * H + u] = c;
-        float* gp = gsave + sidx * G4;
-        gp[u] = gi;
-        gp[H + u] = gf;
-        gp[2 * H + u] = gg;
-        gp[3 * H + u] = go;
+        // gates saved interleaved per unit ([2][L][B][H][4]): one 16-B store / load each
+        *(f32x4*)(gsave + (sidx * H + u) * 4) = f32x4{gi, gf, gg, go};
       }
     }
     __syncthreads();
@@ -197,9 +194,9 @@ __global__ __launch_bounds__(LSTM_NW * 64) void lstm_bwd_kernel(
       const int row = e / H, u = e - row * H;
       const int b = min(b0 + row, B - 1);
       const long sidx = ((long)dir * L + t) * B + b;
-      const float* gp = gsave + sidx * G4;
+      const f32x4 g4 = *(const f32x4*)(gsave + (sidx * H + u) * 4);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gv[i][g] = gp[g * H + u];
+      for (int g = 0; g < 4; ++g) gv[i][g] = g4[g];
       cv[i] = csave[sidx * H + u];
       dhv[i] = to_f(dhout[((long)b * L + t) * 2 * H + dir * H + u]);
       if (has_prev) {
@@ -296,8 +293,8 @@ constexpr int COOP_WLDS_BYTES = 2 * 4 * (COOP_H / 32) * 64 * 16;  // [ug][g][ks]
 // Zeroes the cooperative recurrence's step counters ahead of its launch.  A kernel rather than
 // hipMemsetAsync: the launch sequence captured into a hipGraph is then kernel nodes only,
 // ordered on the stream like any other launch.
-__global__ void lstm_coop_ctr_zero_kernel(unsigned* __restrict__ ctr) {
-  if (threadIdx.x < 16) ctr[threadIdx.x] = 0u;
+__global__ void lstm_coop_ctr_zero_kernel(unsigned* __restrict__ ctr, int n) {
+  if ((int)threadIdx.x < n) ctr[threadIdx.x] = 0u;
 }
 
 template <int RT>
@@ -386,9 +383,8 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
         hout[((long)b * L + tt) * 2 * H + dir * H + ucol] = from_f<bf16>(hv[i][r]);
         const long sidx = ((long)dir * L + tt) * B + b;
         csave[sidx * H + ucol] = cv[i][r];
-        float* gp = gsave + sidx * G4;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) gp[g * H + ucol] = gv[i][r][g];
+        *(f32x4*)(gsave + (sidx * H + ucol) * 4) =
+            f32x4{gv[i][r][0], gv[i][r][1], gv[i][r][2], gv[i][r][3]};
       }
   };
   for (int s = 0; s < L; ++s) {
@@ -559,6 +555,206 @@ __global__ void lstm_pack_whh_kernel(const T* __restrict__ w, int H, T* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Cooperative recurrent backward (bf16, H = 256).  The batch-partitioned lstm_bwd_kernel
+// streams all of W_hh (512 KB) from L2 into every workgroup at every step (7.9 us per step,
+// L2-bound).  Here a group of CB_NU workgroups shares each 16-row block of one direction: a
+// workgroup owns CB_UB hidden units, holds its W_hh^T columns in REGISTERS for all L steps
+// (wave w: one 16-unit tile, 32 k-step fragments = 128 VGPRs; one wave per SIMD) and per step
+//   1. forms dG for (16 rows, its units, 4 gates) elementwise in the MFMA accumulator layout
+//      (lane: rows 4*(lane>>4) + r, unit lane & 15) from dh_out + its own dh_next,
+//   2. writes its dG slice into the step's A image in LDS and publishes it (16-B sc1 stores,
+//      drained, one agent counter add: cdna_hip_programming.md §6 G16) next to the plain
+//      dxg stores of the same chunks,
+//   3. waits for its peers' slices (sc1 loads into the A image) and
+//   4. runs dh_next[16][its units] = dG[16][4H] . W_hh[4H][its units] on MFMA.
+// The arithmetic is the batch-partitioned kernel's: the same bf16 dG A operand, the same packed
+// B fragments, the same k order, so the outputs are bit-identical (tests/test_text_gpu.py).
+// The A image is 16 rows x 1024 bf16 with the 16-B chunk index XORed with the row (row < 16:
+// conflict-free fragment reads without padding).  The exchange buffer is double-buffered by
+// step parity; a slot is rewritten two steps later, after every peer has published the step
+// in between (which it does only after reading this one).  Bounded wait like the forward's.
+// ---------------------------------------------------------------------------------------
+constexpr int CB_RB = 16;                   // batch rows per group
+constexpr int CB_NU = 4;                    // workgroups per (row block, direction)
+constexpr int CB_NT = 256;                  // threads: 4 waves, one 16-unit tile each
+constexpr int CB_UB = COOP_H / CB_NU;       // units per workgroup (4 waves x 16)
+constexpr int CB_G4 = 4 * COOP_H;
+constexpr int CB_NKS = CB_G4 / 32;          // k-steps of the dh contraction
+constexpr int CB_MAX_GROUPS = 32;           // row blocks per direction (B <= 512)
+
+__device__ __forceinline__ int cb_swz(int row, int col) {  // bf16 element offset in the A image
+  return row * CB_G4 + ((((col >> 3) ^ row) << 3) | (col & 7));
+}
+
+__global__ __launch_bounds__(CB_NT, 1) void lstm_bwd_coop_kernel(
+    const bf16* __restrict__ whp, const bf16* __restrict__ hout, const float* __restrict__ csave,
+    const float* __restrict__ gsave, const bf16* __restrict__ dhout, int B, int L,
+    bf16* __restrict__ dxg, bf16* __restrict__ hprev, bf16* __restrict__ xbuf,
+    unsigned* __restrict__ ctr, int* __restrict__ status, long spin_max,
+    unsigned long long* __restrict__ tst) {
+  constexpr int H = COOP_H;
+  __shared__ __attribute__((aligned(16))) bf16 sA[CB_RB * CB_G4];
+  __shared__ int sgiveup;
+  const int j = blockIdx.x, dir = blockIdx.y, rb = blockIdx.z, nrb = gridDim.z;
+  const int b0 = rb * CB_RB;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int unit = j * CB_UB + wid * 16 + (lane & 15);
+  // this wave's B fragments (tile j*8 + wid of lstm_pack_whh_kernel's layout), all k-steps
+  bf16x8 wf[CB_NKS];
+  {
+    const bf16* wp = whp + ((long)(dir * (H / 16) + j * (CB_UB / 16) + wid) * CB_NKS) * 512 +
+                     lane * 8;
+#pragma unroll
+    for (int ks = 0; ks < CB_NKS; ++ks) wf[ks] = *(const bf16x8*)(wp + ks * 512);
+  }
+  unsigned* myctr = ctr + dir * nrb + rb;
+  bf16* xb = xbuf + (long)(dir * nrb + rb) * 2 * CB_RB * CB_G4;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, 2 * CB_RB * CB_G4 * 2, 0x00020000);
+  // operands of one step for this lane's 4 (row, unit) elements
+  f32x4 gq[4];
+  float cq[4], cpq[4], dhq[4];
+  bf16 hpq[4];
+  auto load_ops = [&](int ss) {
+    const int tt = dir == 0 ? ss : L - 1 - ss;
+    const int tpp = dir == 0 ? tt - 1 : tt + 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = min(b0 + (lane >> 4) * 4 + r, B - 1);
+      const long sidx = ((long)dir * L + tt) * B + b;
+      gq[r] = *(const f32x4*)(gsave + (sidx * H + unit) * 4);
+      cq[r] = csave[sidx * H + unit];
+      dhq[r] = to_f(dhout[((long)b * L + tt) * 2 * H + dir * H + unit]);
+      if (ss > 0) {
+        cpq[r] = csave[(((long)dir * L + tpp) * B + b) * H + unit];
+        hpq[r] = hout[((long)b * L + tpp) * 2 * H + dir * H + unit];
+      } else {
+        cpq[r] = 0.f;
+        hpq[r] = from_f<bf16>(0.f);
+      }
+    }
+  };
+  float dcn[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dhn = f32x4{0.f, 0.f, 0.f, 0.f};
+  // lab probe (MMDX_LSTM_BWD_PROBE): [group][dir][wg][step][phase] realtime stamps
+  unsigned long long* tsw =
+      tst ? tst + ((long)(rb * 2 + dir) * CB_NU + j) * L * COOP_TS_PHASES : nullptr;
+#define CB_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (tsw && threadIdx.x == 0) tsw[(L - 1 - s) * COOP_TS_PHASES + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  load_ops(L - 1);
+  for (int s = L - 1; s >= 0; --s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    CB_STAMP(0);
+    // 1. dG of this lane's elements -> the A image (rows >= B contribute zeros)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = (lane >> 4) * 4 + r, b = b0 + row;
+      float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
+      if (b < B) {
+        const float gi = gq[r][0], gf = gq[r][1], gg = gq[r][2], go = gq[r][3];
+        const float c = cq[r];
+        const float dh = dhq[r] + dhn[r];
+        const float tc = tanh_fast(c);
+        const float dc = dh * go * (1.f - tc * tc) + dcn[r];
+        const float d_o = dh * tc;
+        dgi = dc * gg * gi * (1.f - gi);
+        dgf = dc * cpq[r] * gf * (1.f - gf);
+        dgg = dc * gi * (1.f - gg * gg);
+        dgo = d_o * go * (1.f - go);
+        dcn[r] = dc * gf;
+        hprev[((long)dir * B * L + (long)b * L + t) * H + unit] = hpq[r];
+      }
+      sA[cb_swz(row, unit)] = from_f<bf16>(dgi);
+      sA[cb_swz(row, H + unit)] = from_f<bf16>(dgf);
+      sA[cb_swz(row, 2 * H + unit)] = from_f<bf16>(dgg);
+      sA[cb_swz(row, 3 * H + unit)] = from_f<bf16>(dgo);
+    }
+    __syncthreads();
+    CB_STAMP(1);
+    // 2. this workgroup's slice (16 rows x 4 gates x CB_UB units, 16-B chunks) -> dxg, and to
+    //    the exchange slot of this step's parity for the peers
+    const bool more = s > 0;
+    constexpr int OWN = CB_RB * 4 * (CB_UB / 8);     // chunks of the own slice
+#pragma unroll
+    for (int q = threadIdx.x; q < OWN; q += CB_NT) {
+      const int row = q / (4 * (CB_UB / 8)), rem = q - row * (4 * (CB_UB / 8));
+      const int g = rem / (CB_UB / 8), c8 = rem - g * (CB_UB / 8);
+      const int col = g * H + j * CB_UB + c8 * 8;
+      const coop_v4u v = *(const coop_v4u*)(sA + cb_swz(row, col));
+      const int b = b0 + row;
+      if (b < B) *(coop_v4u*)(dxg + (((long)b * L + t) * 2 + dir) * CB_G4 + col) = v;
+      if (more)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, xrs, ((s & 1) * CB_RB * CB_G4 + row * CB_G4 + col) * 2, 0, COOP_SC1);
+    }
+    if (!more) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(myctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CB_STAMP(2);
+    // 3. wait for the peers' slices of this step (monotonic: CB_NU per step published)
+    if (threadIdx.x == 0) {
+      const unsigned target = (unsigned)(CB_NU * (L - s));
+      long spins = 0;
+      int giveup = 0;
+      while (__hip_atomic_load(myctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        ++spins;
+        if (spins > spin_max) {
+          __hip_atomic_store(status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          giveup = 1;
+          break;
+        }
+        if ((spins & 255) == 0 &&
+            __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          giveup = 1;
+          break;
+        }
+      }
+      sgiveup = giveup;
+    }
+    __syncthreads();
+    if (sgiveup) return;
+    CB_STAMP(3);
+    // peers' chunks (every chunk of the row block not owned here), loaded before any LDS write,
+    // then the next step's operands (independent of the chain) behind them
+    constexpr int ALL = CB_RB * CB_G4 / 8;           // chunks of the whole row block
+    constexpr int PER = ALL / CB_NT;                 // per thread
+    coop_v4u pv[PER];
+    int pofs[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = threadIdx.x + i * CB_NT;
+      const int row = q / (CB_G4 / 8), col = (q - row * (CB_G4 / 8)) * 8;
+      const bool peer = ((col % H) / CB_UB) != j;
+      pofs[i] = peer ? cb_swz(row, col) : -1;
+      pv[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          xrs, peer ? ((s & 1) * CB_RB * CB_G4 + row * CB_G4 + col) * 2 : DMA_OOB, 0, COOP_SC1);
+    }
+    load_ops(s - 1);
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (pofs[i] >= 0) *(coop_v4u*)(sA + pofs[i]) = pv[i];
+    __syncthreads();
+    CB_STAMP(4);
+    // 4. dh_next for this wave's 16 units
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < CB_NKS; ++ks) {
+      const bf16x8 af = *(const bf16x8*)(sA + cb_swz(lane & 15, ks * 32 + (lane >> 4) * 8));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks], acc, 0, 0, 0);
+    }
+    dhn = acc;
+    __syncthreads();   // the A image is rewritten by the next step's dG
+    CB_STAMP(5);
+  }
+#undef CB_STAMP
+}
+
 template <typename T>
 static int lstm_fwd_t(const void* xg, const void* whh, int B, int L, int H, void* hout,
                       float* cs, float* gs, hipStream_t st) {
@@ -642,7 +838,7 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
                      coop_timing_bytes(B, L));
       tst = (unsigned long long*)((char*)ws + need);
     }
-    hipLaunchKernelGGL(lstm_coop_ctr_zero_kernel, dim3(1), dim3(64), 0, st, ctr);
+    hipLaunchKernelGGL(lstm_coop_ctr_zero_kernel, dim3(1), dim3(64), 0, st, ctr, 16);
     // B > 128: independent groups of 128 rows (grid z), each with W_hh in LDS (RT = 2)
     const int groups = B <= 128 ? 1 : (B + 127) / 128;
     const dim3 grid(COOP_NB, 2, groups);
@@ -666,18 +862,55 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
   return lstm_fwd_t<float>(xg, w_hh, B, L, H, h_out, c_save, gates_save, st);
 }
 
-extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
+// The cooperative backward applies to bf16, H = 256, B <= 16 * CB_MAX_GROUPS when the caller
+// passes a status word; its 2 x CB_NU x ceil(B / 16) workgroups must fit the device at once.
+template <int Dummy = 0>
+static bool coop_bwd_resident(int groups) {
+  static std::atomic<int> ok[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  int v = ok[dev].load(std::memory_order_relaxed);
+  if (v == 0) {
+    int per_cu = 0, cus = 0;
+    const bool q =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_coop_kernel, CB_NT, 0) ==
+            hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+    v = (q && per_cu >= 1) ? cus : -1;
+    ok[dev].store(v, std::memory_order_relaxed);
+  }
+  return v > 0 && v >= 2 * CB_NU * groups;
+}
+
+static bool coop_bwd_ok(int dtype, int B, int H) {
+  return dtype == BF16 && H == COOP_H && B <= CB_RB * CB_MAX_GROUPS;
+}
+
+static size_t lstm_bwd_base_bytes(int dtype, int B, int L, int H) {
   const size_t es = dtype == BF16 ? 2 : 4;
   // fragment-packed W_hh + shifted hidden states + dW_hh GEMM split-K scratch
   return 2 * (size_t)4 * H * H * es + 2 * (size_t)B * L * H * es +
          2 * mmdx_gemm_workspace_size(dtype, 4 * H, H, B * L) + 256;
 }
 
+extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
+  size_t n = lstm_bwd_base_bytes(dtype, B, L, H);
+  if (coop_bwd_ok(dtype, B, H)) {
+    // + the cooperative backward's dG exchange [2 dir][groups][2 parity][16][4H] bf16 and
+    //   its step counters [2 dir][groups]
+    const size_t groups = (B + CB_RB - 1) / CB_RB;
+    n = ((n + 255) & ~(size_t)255) + 2 * groups * 2 * CB_RB * CB_G4 * 2 + 256;
+  }
+  return n;
+}
+
 extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                              const float* gates_save, const void* dh_out, int B, int L, int H,
-                             void* dxg, float* dw_hh, void* ws, size_t ws_bytes, void* stream) {
+                             void* dxg, float* dw_hh, void* ws, size_t ws_bytes, int* status,
+                             long spin_limit, void* stream) {
   MMDX_CHECK_ARG(dtype != F16, "mmdx_lstm_bwd: fp16 is the C5 path only");
   MMDX_CHECK_ARG(H == 128 || H == 256, "lstm bwd: hidden size %d unsupported", H);
+  MMDX_CHECK_ARG(B > 0 && L > 0, "lstm bwd: bad args");
   MMDX_CHECK_ARG(ws && ws_bytes >= mmdx_lstm_workspace_size(dtype, B, L, H),
                  "lstm bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
@@ -689,21 +922,48 @@ extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, con
   w += 2 * (size_t)B * L * H * es;
   w = (char*)(((uintptr_t)w + 255) & ~(uintptr_t)255);
   const size_t gws = mmdx_gemm_workspace_size(dtype, 4 * H, H, B * L);
-  dim3 grid((B + LSTM_RB - 1) / LSTM_RB, 2);
   const long tw = 2L * 4 * H * H;
   const int tb = (int)std::min<long>((tw + 255) / 256, 4096);
+  const int groups = (B + CB_RB - 1) / CB_RB;
+  if (status && coop_bwd_ok(dtype, B, H)) {
+    MMDX_CHECK_ARG(coop_bwd_resident(groups),
+                   "lstm bwd: the cooperative recurrence cannot be co-resident here");
+    char* x = (char*)ws + ((lstm_bwd_base_bytes(dtype, B, L, H) + 255) & ~(size_t)255);
+    bf16* xbuf = (bf16*)x;
+    unsigned* ctr = (unsigned*)(x + 2 * (size_t)groups * 2 * CB_RB * CB_G4 * 2);
+    const long spin_max = spin_limit > 0 ? spin_limit : COOP_SPIN_MAX;
+    hipLaunchKernelGGL(lstm_pack_whh_kernel<bf16>, dim3(tb), dim3(256), 0, st,
+                       (const bf16*)w_hh, H, (bf16*)whp);
+    hipLaunchKernelGGL(lstm_coop_ctr_zero_kernel, dim3(1), dim3(64), 0, st, ctr, 2 * groups);
+    // lab probe (tools/lab/lstm_probe.py): MMDX_LSTM_BWD_PROBE=1 stamps the phases into the
+    // [groups][2][CB_NU][L][8] u64 that follow the workspace (the caller passes them)
+    unsigned long long* tst = nullptr;
+    const char* pe = getenv("MMDX_LSTM_BWD_PROBE");
+    if (pe && atoi(pe) != 0) {
+      const size_t tb2 = (size_t)groups * 2 * CB_NU * L * COOP_TS_PHASES * 8;
+      MMDX_CHECK_ARG(ws_bytes >= mmdx_lstm_workspace_size(dtype, B, L, H) + tb2,
+                     "lstm bwd: the timing probe needs %zu more workspace bytes", tb2);
+      tst = (unsigned long long*)((char*)ws + mmdx_lstm_workspace_size(dtype, B, L, H));
+    }
+    hipLaunchKernelGGL(lstm_bwd_coop_kernel, dim3(CB_NU, 2, groups), dim3(CB_NT), 0, st,
+                       (const bf16*)whp, (const bf16*)h_out, c_save, gates_save,
+                       (const bf16*)dh_out, B, L, (bf16*)dxg, (bf16*)hprev, xbuf, ctr, status,
+                       spin_max, tst);
+  } else {
+    dim3 grid((B + LSTM_RB - 1) / LSTM_RB, 2);
 #define LSTM_BWD(T, HH)                                                                         \
   hipLaunchKernelGGL(lstm_pack_whh_kernel<T>, dim3(tb), dim3(256), 0, st, (const T*)w_hh, HH,  \
                      (T*)whp);                                                                  \
   hipLaunchKernelGGL((lstm_bwd_kernel<T, HH>), grid, dim3(LSTM_NW * 64), 0, st,                 \
                      (const T*)whp, (const T*)h_out, c_save, gates_save, (const T*)dh_out, B,  \
                      L, (T*)dxg, (T*)hprev)
-  if (dtype == BF16) {
-    if (H == 256) { LSTM_BWD(bf16, 256); } else { LSTM_BWD(bf16, 128); }
-  } else {
-    if (H == 256) { LSTM_BWD(float, 256); } else { LSTM_BWD(float, 128); }
-  }
+    if (dtype == BF16) {
+      if (H == 256) { LSTM_BWD(bf16, 256); } else { LSTM_BWD(bf16, 128); }
+    } else {
+      if (H == 256) { LSTM_BWD(float, 256); } else { LSTM_BWD(float, 128); }
+    }
 #undef LSTM_BWD
+  }
   MMDX_LAUNCH_CHECK();
   // dW_hh[d] = sum_rows dG[:, d]^T hprev[d]   ([4H] x [H] over B*L rows)
   for (int d = 0; d < 2; ++d) {

@@ -207,6 +207,48 @@ def test_lstm_coop_forward_matches_partitioned(dev, B):
         assert (a - b).abs().mean().item() <= 1e-4
 
 
+@pytest.mark.parametrize("B", [128, 200, 40])
+def test_lstm_coop_backward_matches_partitioned(dev, B):
+    """The cooperative bf16 backward (4 workgroups per 16-row block and direction, W_hh^T in
+    registers, dG slices exchanged through a counter) against the batch-partitioned kernel on
+    the same saved forward: same bf16 dG operand, packed fragments and k order, so dG (dxg)
+    and dW_hh agree to the last bit except where the compiler contracted a multiply-add
+    differently (<= one bf16 ulp of dG); B = 200 and 40 leave a ragged last row block."""
+    H, Ls = 256, 24
+    bf = L.dtype_code(torch.bfloat16)
+    g = torch.Generator().manual_seed(B + 1)
+    xg = (torch.randn(B * Ls, 2 * 4 * H, generator=g) * 0.5).to(dev)
+    whh = (torch.randn(2 * 4 * H, H, generator=g) * 0.05).to(dev, torch.bfloat16)
+    dh = (torch.randn(B, Ls, 2 * H, generator=g) * 0.1).to(dev, torch.bfloat16)
+    hout = torch.empty(B, Ls, 2 * H, dtype=torch.bfloat16, device=dev)
+    cs = torch.empty(2, Ls, B, H, device=dev)
+    gs = torch.empty(2, Ls, B, H, 4, device=dev)
+    n = L.lib().mmdx_lstm_fwd_workspace_size(bf, B, Ls, H)
+    ws = torch.empty(n, dtype=torch.uint8, device=dev)
+    status = torch.zeros(4, dtype=torch.int32, device=dev)
+    L.call("mmdx_lstm_fwd", bf, xg.data_ptr(), whh.data_ptr(), B, Ls, H, hout.data_ptr(),
+           cs.data_ptr(), gs.data_ptr(), ws.data_ptr(), n, status.data_ptr(), 0, 0, L.stream())
+    outs = []
+    for coop in (True, False):
+        dxg = torch.full((B * Ls, 2 * 4 * H), float("nan"), dtype=torch.bfloat16, device=dev)
+        dwhh = torch.empty(2 * 4 * H, H, device=dev)
+        nb = L.lib().mmdx_lstm_workspace_size(bf, B, Ls, H)
+        wsb = torch.empty(nb, dtype=torch.uint8, device=dev)
+        L.call("mmdx_lstm_bwd", bf, whh.data_ptr(), hout.data_ptr(), cs.data_ptr(),
+               gs.data_ptr(), dh.data_ptr(), B, Ls, H, dxg.data_ptr(), dwhh.data_ptr(),
+               wsb.data_ptr(), nb, status.data_ptr() if coop else None, 0, L.stream())
+        torch.cuda.synchronize()
+        assert int(status[0]) == 0
+        outs.append((dxg.float(), dwhh))
+    (a_dg, a_dw), (b_dg, b_dw) = outs
+    assert torch.isfinite(a_dg).all() and torch.isfinite(a_dw).all()
+    ulp = b_dg.abs() * 2.0 ** -7 + 1e-30
+    assert ((a_dg - b_dg).abs() <= ulp).all(), (a_dg - b_dg).abs().max().item()
+    same = (a_dg == b_dg).float().mean().item()
+    assert same >= 0.99, same
+    assert (a_dw - b_dw).abs().max().item() <= 1e-2 * b_dw.abs().max().item()
+
+
 def test_lstm_coop_lost_peer_raises(dev):
     """A peer workgroup that never signals (debug flag: workgroup 0 of direction 0 drops its
     signals) makes the cooperative recurrence time out: every workgroup leaves (the launch

@@ -39,7 +39,7 @@ def main():
     whh = (torch.randn((2 * G4, H), generator=g, device=dev) * 0.05).to(torch.bfloat16)
     hout = torch.empty((B, Ls, 2 * H), dtype=torch.bfloat16, device=dev)
     cs = torch.empty((2, Ls, B, H), dtype=torch.float32, device=dev)
-    gs = torch.empty((2, Ls, B, G4), dtype=torch.float32, device=dev)
+    gs = torch.empty((2, Ls, B, H, 4), dtype=torch.float32, device=dev)
     need = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(torch.bfloat16), B, Ls, H)
     groups = 1 if B <= 128 else (B + 127) // 128
     tbytes = groups * 2 * 8 * Ls * PH * 8
@@ -55,11 +55,14 @@ def main():
     dxg = torch.empty((B * Ls, 2 * G4), dtype=torch.bfloat16, device=dev)
     dwhh = torch.empty((2 * G4, H), dtype=torch.float32, device=dev)
     nb = L.lib().mmdx_lstm_workspace_size(bf, B, Ls, H)
-    wsb = torch.empty(nb, dtype=torch.uint8, device=dev)
+    nrb = (B + 15) // 16
+    tb2 = nrb * 2 * 4 * Ls * PH * 8
+    wsb = torch.zeros(nb + tb2, dtype=torch.uint8, device=dev)
 
-    def bwd():
+    def bwd(coop=True):
         L.call("mmdx_lstm_bwd", bf, L.ptr(whh), L.ptr(hout), L.ptr(cs), L.ptr(gs), L.ptr(dh), B,
-               Ls, H, L.ptr(dxg), L.ptr(dwhh), L.ptr(wsb), nb, L.stream())
+               Ls, H, L.ptr(dxg), L.ptr(dwhh), L.ptr(wsb), nb + tb2, L.ptr(status) if coop else None,
+               0, L.stream())
 
     def timed(fn, reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -84,6 +87,7 @@ def main():
                     torch.mm(A, Bm)
         f_ms = timed(fwd, a.reps)
         b_ms = timed(bwd, a.reps)
+        bp_ms = timed(lambda: bwd(False), a.reps)
         fwd(debug=2)
         torch.cuda.synchronize()
         assert int(status[0].item()) == 0, "recurrence timed out"
@@ -92,7 +96,8 @@ def main():
         d = np.diff(ts, axis=-1)                                # [.., step, 5 phases]
         step = ts[..., 1:, 0] - ts[..., :-1, 0]                 # start-to-start
         print(f"== {tag}: fwd {f_ms:.3f} ms/launch ({f_ms * 1e3 / Ls:.2f} us/step), "
-              f"bwd {b_ms:.3f} ms/launch ({b_ms * 1e3 / Ls:.2f} us/step)")
+              f"bwd {b_ms:.3f} ms/launch ({b_ms * 1e3 / Ls:.2f} us/step; batch-partitioned "
+              f"{bp_ms:.3f})")
         print(f"   step start-to-start: mean {step[..., 1:].mean() / 1e3:.2f} us, "
               f"p50 {np.median(step[..., 1:]) / 1e3:.2f}, p90 {np.percentile(step[..., 1:], 90) / 1e3:.2f}")
         for k, n in enumerate(NAMES):
@@ -117,6 +122,19 @@ def main():
                       f"{np.mean(rk == 7):4.2f}")
         skew = pub.max(axis=2) - pub.min(axis=2)
         print(f"   publish skew across the 8 workgroups: mean {skew.mean() / 1e3:.2f} us")
+        os.environ["MMDX_LSTM_BWD_PROBE"] = "1"
+        bwd()
+        torch.cuda.synchronize()
+        del os.environ["MMDX_LSTM_BWD_PROBE"]
+        tb = wsb[nb:].view(torch.int64).cpu().numpy().astype(np.float64)
+        tb = tb.reshape(nrb, 2, 4, Ls, PH)[..., :6] * 10.0
+        db = np.diff(tb, axis=-1)[..., :-1, :]               # the last step has no exchange
+        stepb = tb[..., 1:, 0] - tb[..., :-1, 0]
+        print(f"   backward step start-to-start: mean {stepb.mean() / 1e3:.2f} us")
+        for k, n in enumerate(["dG->LDS", "copy-out+publish", "wait", "peer loads", "MFMA"]):
+            v = db[..., k]
+            print(f"   bwd {n:17s} mean {v.mean() / 1e3:6.2f} us  p50 {np.median(v) / 1e3:6.2f}  "
+                  f"p90 {np.percentile(v, 90) / 1e3:6.2f}")
         torch.cuda.synchronize()
 
 
