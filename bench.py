@@ -75,10 +75,11 @@ def conv_flops_per_sample(trunk, hw=224):
 
 
 def load_traffic(cfg_name, batch):
-    """HBM bytes per conv launch from the committed PMC pass (tools/pmc_traffic.py), or None."""
+    """HBM bytes per launch of the dominant family (conv, or C5's dense GEMMs) from the newest
+    committed PMC pass of this config (tools/pmc_traffic.py), or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_conv_traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
         try:
             with open(f) as fh:
                 t = json.load(fh)
@@ -656,7 +657,8 @@ def main():
             "frac": round((conv_gbs / PEAK_HBM_GBS) if hbm_bound
                           else (conv_tf / PEAK_BF16_TFLOPS), 4),
             "traffic": traffic[0] if traffic else None,
-            "traffic_unit": "HBM bytes per conv launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)",
+            "traffic_unit": ("HBM bytes per %s launch (PMC, (2*FETCH_SIZE+WRITE_SIZE)*1KiB)"
+                             % ("GEMM" if vit else "conv")),
             "traffic_source": traffic[1] if traffic else None,
             "traffic_git_rev": traffic[2] if traffic else None,
             "algorithmic_bytes_per_launch": round(alg_bytes / alg_launches),

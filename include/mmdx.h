@@ -550,7 +550,8 @@ int mmdx_attention_bwd_lse(int dtype, const void* qkv, const void* out, const fl
                            void* workspace, size_t ws_bytes, void* stream);
 
 /* LSTM recurrence for one layer, both directions (build-defined C3/C4 tower).
- * xg: [B, L, 2, 4H] precomputed input gates (x W_ih^T + b_ih + b_hh, gate order i,f,g,o);
+ * xg: [B, L, 2, H, 4] precomputed input gates (x W_ih^T + b_ih + b_hh), the four gates
+ *     (i,f,g,o) of a unit adjacent;
  * w_hh: [2][4H][H] compute dtype; h_out: [B, L, 2H]; saved c: [2, L, B, H] fp32,
  * gates: [2, L, B, H, 4] fp32 post-activation, the four gates of a unit adjacent (for
  * backward). */

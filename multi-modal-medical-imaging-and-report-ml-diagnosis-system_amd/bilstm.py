@@ -102,9 +102,11 @@ def check_recurrence(block=True):
 # debug knobs of the cooperative forward (tests force the timeout path through these)
 DEBUG = {"spin_limit": 0, "flags": 0}
 
-# the cooperative recurrent backward (mmdx_lstm_bwd with a status word; MMDX_LSTM_BWD_COOP=0:
-# the batch-partitioned kernel, for A/B runs — bit-identical outputs)
-BWD_COOP = os.environ.get("MMDX_LSTM_BWD_COOP", "1") != "0"
+# the cooperative recurrent backward (mmdx_lstm_bwd with a status word) is opt-in
+# (MMDX_LSTM_BWD_COOP=1): 0.70 vs 1.0 ms per launch in the C4 step, but it holds 64 CUs
+# where the batch-partitioned kernel holds 16, and beside the throughput-bound image
+# backward CU-time is what counts: C4 8738 vs 8830 samples/s (r05, paired).  Bit-identical.
+BWD_COOP = os.environ.get("MMDX_LSTM_BWD_COOP", "0") == "1"
 
 
 def _cat_cast(ws, T, dev):
@@ -131,12 +133,17 @@ class _LSTMLayerFn(torch.autograd.Function):
         bias = torch.empty(2 * G4, dtype=torch.float32, device=dev)
         call("mmdx_axpby", G4, 1.0, ptr(bih_f), 1.0, ptr(bhh_f), ptr(bias[:G4]), stream())
         call("mmdx_axpby", G4, 1.0, ptr(bih_r), 1.0, ptr(bhh_r), ptr(bias[G4:]), stream())
+        # the recurrences read xg unit-interleaved ([M][2][H][4]: one 16-B load per (row,
+        # unit)), so the projection runs on W_ih / bias rows permuted (dir, g, u) -> (dir, u, g);
+        # the backward's GEMMs keep the gate-major W_ih (dG is gate-major)
+        wih_p = wih.view(2, 4, H, In).transpose(1, 2).reshape(2 * G4, In)
+        bias_p = bias.view(2, 4, H).transpose(1, 2).reshape(2 * G4)
         xg = torch.empty((M, 2 * G4), dtype=torch.float32, device=dev)
-        F.gemm(x.reshape(M, In), In, True, wih, In, True, M, 2 * G4, In, xg, 2 * G4, bias=bias,
-               compute_dtype=T)
+        F.gemm(x.reshape(M, In), In, True, wih_p, In, True, M, 2 * G4, In, xg, 2 * G4,
+               bias=bias_p, compute_dtype=T)
         hout = torch.empty((B, Ls, 2 * H), dtype=T, device=dev)
         cs = torch.empty((2, Ls, B, H), dtype=torch.float32, device=dev)
-        gs = torch.empty((2, Ls, B, G4), dtype=torch.float32, device=dev)
+        gs = torch.empty((2, Ls, B, H, 4), dtype=torch.float32, device=dev)
         fw = L.lib().mmdx_lstm_fwd_workspace_size(L.dtype_code(T), B, Ls, H)
         fws = L.workspace(fw, dev)
         status = coop_status(dev) if fw else None

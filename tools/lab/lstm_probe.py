@@ -22,7 +22,11 @@ import mmdx  # noqa: E402,F401
 from mmdx import _lib as L  # noqa: E402
 
 PH = 8
-NAMES = ["wait", "h->LDS", "issue", "gates+cell", "publish"]
+COOP4 = os.environ.get("MMDX_LSTM_FWD_COOP4", "1") != "0"
+# coop4 (default): 0 start 1 wait done 2 h in LDS 3 gates done 4 wave 0 published
+NAMES = (["wait", "h->LDS", "gates+cell", "publish"] if COOP4 else
+         ["wait", "h->LDS", "issue", "gates+cell", "publish"])
+NST = len(NAMES) + 1
 
 
 def main():
@@ -92,7 +96,7 @@ def main():
         torch.cuda.synchronize()
         assert int(status[0].item()) == 0, "recurrence timed out"
         ts = ws[need:].view(torch.int64).cpu().numpy().astype(np.float64)
-        ts = ts.reshape(groups, 2, 8, Ls, PH)[..., :6] * 10.0   # ns (100 MHz clock)
+        ts = ts.reshape(groups, 2, 8, Ls, PH)[..., :NST] * 10.0   # ns (100 MHz clock)
         d = np.diff(ts, axis=-1)                                # [.., step, 5 phases]
         step = ts[..., 1:, 0] - ts[..., :-1, 0]                 # start-to-start
         print(f"== {tag}: fwd {f_ms:.3f} ms/launch ({f_ms * 1e3 / Ls:.2f} us/step), "
@@ -106,7 +110,7 @@ def main():
                   f"p90 {np.percentile(v, 90) / 1e3:6.2f}  max {v.max() / 1e3:6.2f}")
         # the chain: how long after the LAST peer's publish (phase 5 stamp of step s-1) does
         # each workgroup leave its wait at step s
-        pub = ts[..., 5]            # [g, dir, blk, step]
+        pub = ts[..., NST - 1]      # [g, dir, blk, step]
         last = pub.max(axis=2)      # [g, dir, step]
         leave = ts[..., 1]
         lag = leave[..., 1:] - last[:, :, None, :-1]
@@ -114,7 +118,7 @@ def main():
               f"p90 {np.percentile(lag, 90) / 1e3:.2f}")
         for dr in range(2):
             for blk in range(8):
-                row = " ".join(f"{d[0, dr, blk, 1:, k].mean() / 1e3:5.2f}" for k in range(5))
+                row = " ".join(f"{d[0, dr, blk, 1:, k].mean() / 1e3:5.2f}" for k in range(len(NAMES)))
                 lg = lag[0, dr, blk]
                 rk = (pub[0, dr, :, :] < pub[0, dr, blk, :][None, :]).sum(axis=0)  # publish rank
                 print(f"   dir{dr} wg{blk}: {row}   (phase means, us)  lag mean "

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""HBM traffic of the conv kernels from two rocprofv3 PMC passes.
+"""HBM traffic of the conv kernels (C2-C4) or the dense GEMMs (C5, --family gemm) from two
+rocprofv3 PMC passes.
 
     rocprofv3 --pmc FETCH_SIZE  --output-format csv -d <dir_f> -- python3 bench.py ...
     rocprofv3 --pmc WRITE_SIZE  --output-format csv -d <dir_w> -- python3 bench.py ...
@@ -21,11 +22,16 @@ import os
 import re
 
 CONV = re.compile(r"igemm(_dma)?_kernel.*(Im2col|Dgrad|PhaseTap|PointFwdK|PointWgradR)")
+# C5's family: every implicit-GEMM instantiation (all dense there) + its split-K reduces
+GEMM = re.compile(r"igemm(_dma)?_kernel")
+GEMM_REDUCE = re.compile(r"splitk_reduce")
 STEP = re.compile(r"adamw_kernel")
 REDUCE = re.compile(r"wgrad_reduce_kernel")
 
 
-def load(d, counter):
+def load(d, counter, fam=None, red=None):
+    fam = fam or CONV
+    red = red or REDUCE
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -44,10 +50,10 @@ def load(d, counter):
     for name, v in per_dispatch.values():
         if STEP.search(name):
             n_step += 1
-        if CONV.search(name):
+        if fam.search(name):
             conv_kb += v
             n_conv += 1
-        elif REDUCE.search(name):
+        elif red.search(name):
             red_kb += v
     return conv_kb, red_kb, n_conv, n_step
 
@@ -60,12 +66,14 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--calls-per-step", type=int, default=158,
                     help="conv calls per train step (bench.py's conv_launches_per_step)")
+    ap.add_argument("--family", choices=("conv", "gemm"), default="conv")
     ap.add_argument("-o", "--out", required=True)
     ap.add_argument("--rev", default=os.environ.get("MMDX_GIT_REV", "unstamped"),
                     help="git revision the counters were measured on (the GPU box has no .git)")
     a = ap.parse_args()
-    f_conv, f_red, n_f, s_f = load(a.fetch_dir, "FETCH_SIZE")
-    w_conv, w_red, n_w, s_w = load(a.write_dir, "WRITE_SIZE")
+    fam, red = (GEMM, GEMM_REDUCE) if a.family == "gemm" else (CONV, REDUCE)
+    f_conv, f_red, n_f, s_f = load(a.fetch_dir, "FETCH_SIZE", fam, red)
+    w_conv, w_red, n_w, s_w = load(a.write_dir, "WRITE_SIZE", fam, red)
     if n_f == 0 or n_f != n_w or s_f == 0 or s_f != s_w:
         raise SystemExit(f"dispatch counts differ or zero: conv {n_f}/{n_w}, steps {s_f}/{s_w}")
     # per conv CALL (the unit bench.py's roofline times: one fwd, dgrad or wgrad call, which
@@ -77,7 +85,10 @@ def main():
         "config": a.config, "per_gpu_batch": a.batch, "git_rev": a.rev,
         "dispatches": n_f, "steps": s_f,
         "calls": calls,
-        "kernels": "igemm(_dma)_kernel (Im2colK/DgradK/DgradPhaseK/Im2colR/PointFwdK/PointDgradK/PointWgradR sources) + wgrad_reduce_kernel",
+        "family": a.family,
+        "kernels": ("igemm(_dma)_kernel (Im2colK/DgradK/DgradPhaseK/Im2colR/PointFwdK/PointDgradK/PointWgradR sources) + wgrad_reduce_kernel"
+                    if a.family == "conv" else
+                    "igemm(_dma)_kernel (dense GEMM instantiations) + splitk_reduce kernels"),
         "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
         "traffic_bytes_per_launch": round(fetch + write),
         "reduce_share": round((2 * f_red + w_red) * 1024 / calls / max(1.0, fetch + write), 4),
