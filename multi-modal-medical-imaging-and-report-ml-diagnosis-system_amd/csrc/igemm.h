@@ -202,6 +202,11 @@ struct DenseR {
 // x^T of a pointwise conv in its weight gradient (named apart from DenseR, see PointFwdK)
 template <typename T> struct PointWgradR : DenseR<T> {};
 
+// exactly the plain-matrix sources (the conv operands derived from them are not)
+template <class S> struct IsDenseSrc { static constexpr bool value = false; };
+template <typename T> struct IsDenseSrc<DenseK<T>> { static constexpr bool value = true; };
+template <typename T> struct IsDenseSrc<DenseR<T>> { static constexpr bool value = true; };
+
 struct ConvGeom {
   int N, H, W, C;      // input NHWC
   int K;               // output channels
@@ -1584,11 +1589,18 @@ __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
 // weight gradients (tools/conv_bench.py, isolated): splits of 2-32 tiles 4-30 % faster
 // (layer2 3x3 74 -> 55 us), 64-144 tiles neutral, the 36-tile layer3 3x3 14 % slower — so
 // larger splits keep the per-slice swizzle.
-__device__ __forceinline__ void block_tile(int nwg, int& tile, int& z) {
+// Dense split-K GEMMs (both operands plain matrices: the nn.Linear weight gradients) use the
+// split-major order up to MMDX_DENSE_SPLIT_XCD_MAX_TILES tiles per split (see the definition).
 #ifndef MMDX_SPLIT_XCD_MAX_TILES
 #define MMDX_SPLIT_XCD_MAX_TILES 32
 #endif
-  if (gridDim.z > 1 && nwg <= MMDX_SPLIT_XCD_MAX_TILES) {
+#ifndef MMDX_DENSE_SPLIT_XCD_MAX_TILES
+#define MMDX_DENSE_SPLIT_XCD_MAX_TILES 32
+#endif
+template <bool DENSE = false>
+__device__ __forceinline__ void block_tile(int nwg, int& tile, int& z) {
+  constexpr int MAXT = DENSE ? MMDX_DENSE_SPLIT_XCD_MAX_TILES : MMDX_SPLIT_XCD_MAX_TILES;
+  if (gridDim.z > 1 && nwg <= MAXT) {
     const int lg = xcd_swizzle((int)(blockIdx.z * gridDim.x + blockIdx.x), nwg * (int)gridDim.z);
     z = lg / nwg;
     tile = lg - z * nwg;
@@ -2032,7 +2044,8 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     tile = xcd_swizzle(blockIdx.x, nwg);
     zsplit = 0;
   } else {
-    block_tile(((M + BM - 1) / BM) * ((N + BN - 1) / BN), tile, zsplit);
+    block_tile<IsDenseSrc<typename OA::SrcT>::value && IsDenseSrc<typename OB::SrcT>::value>(
+        ((M + BM - 1) / BM) * ((N + BN - 1) / BN), tile, zsplit);
   }
   const int tiles_n = (N + BN - 1) / BN;
   if constexpr (Epi::SPLIT) epi.z = zsplit;
