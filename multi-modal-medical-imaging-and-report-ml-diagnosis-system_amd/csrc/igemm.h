@@ -1589,13 +1589,16 @@ __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
 // weight gradients (tools/conv_bench.py, isolated): splits of 2-32 tiles 4-30 % faster
 // (layer2 3x3 74 -> 55 us), 64-144 tiles neutral, the 36-tile layer3 3x3 14 % slower — so
 // larger splits keep the per-slice swizzle.
-// Dense split-K GEMMs (both operands plain matrices: the nn.Linear weight gradients) use the
-// split-major order up to MMDX_DENSE_SPLIT_XCD_MAX_TILES tiles per split (see the definition).
+// Dense split-K GEMMs (both operands plain matrices: the nn.Linear weight gradients) always
+// use the split-major order: a K split's tiles share its dY / X row range, and on one XCD they
+// read it from that XCD's L2.  Measured at C5 (r05, PMC): the 288-block weight-gradient GEMMs
+// 262.7 -> 163.1 MB of HBM traffic per call, 52.7 -> 43.7 GB per step for the GEMM family,
+// 2850 / 2851 vs 2833 / 2834 samples/s paired; C4 neutral.
 #ifndef MMDX_SPLIT_XCD_MAX_TILES
 #define MMDX_SPLIT_XCD_MAX_TILES 32
 #endif
 #ifndef MMDX_DENSE_SPLIT_XCD_MAX_TILES
-#define MMDX_DENSE_SPLIT_XCD_MAX_TILES 32
+#define MMDX_DENSE_SPLIT_XCD_MAX_TILES (1 << 30)
 #endif
 template <bool DENSE = false>
 __device__ __forceinline__ void block_tile(int nwg, int& tile, int& z) {
