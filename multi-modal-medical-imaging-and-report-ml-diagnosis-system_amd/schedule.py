@@ -11,11 +11,15 @@ is identical to `loss.backward()`.
 from __future__ import annotations
 
 import concurrent.futures
+import os
 import threading
 
 import torch
 
 from .trace import rng
+
+# MMDX_TEXT_BWD_FIRST=1: issue the text tower's backward before the image trunk's (A/B)
+TEXT_BWD_FIRST = os.environ.get("MMDX_TEXT_BWD_FIRST", "0") == "1"
 
 
 class TwoTowerForward:
@@ -88,11 +92,17 @@ def two_tower_backward(loss: torch.Tensor, z_img: torch.Tensor, z_txt: torch.Ten
         return
     main = torch.cuda.current_stream()
     text_stream.wait_stream(main)  # dL/dz_txt was produced on the current stream
+
+    def text():
+        with torch.cuda.stream(text_stream):
+            with rng("mmdx/text_bwd"):
+                _tower(z_txt)
+            if on_text_done is not None:
+                on_text_done()
+    if TEXT_BWD_FIRST:
+        text()
     with rng("mmdx/image_bwd"):
         _tower(z_img)
-    with torch.cuda.stream(text_stream):
-        with rng("mmdx/text_bwd"):
-            _tower(z_txt)
-        if on_text_done is not None:
-            on_text_done()
+    if not TEXT_BWD_FIRST:
+        text()
     main.wait_stream(text_stream)
