@@ -1582,20 +1582,24 @@ __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-// (tile, K split) of this block.  Split-K grids (the weight gradients) with at most 32 tiles
-// per split: the whole (split, tile) space is ordered split-major and XCD-swizzled as one, so
-// all the tiles of a K split run on one XCD — they read the same dY / im2col pixel range,
-// which then comes from that XCD's L2 once instead of once per XCD.  Measured on the C4
-// weight gradients (tools/conv_bench.py, isolated): splits of 2-32 tiles 4-30 % faster
-// (layer2 3x3 74 -> 55 us), 64-144 tiles neutral, the 36-tile layer3 3x3 14 % slower — so
-// larger splits keep the per-slice swizzle.
+// (tile, K split) of this block.  Split-K grids (the weight gradients): the whole
+// (split, tile) space is ordered split-major and XCD-swizzled as one, so all the tiles of a K
+// split run on one XCD — they read the same dY / im2col pixel range, which then comes from
+// that XCD's L2 once instead of once per XCD.  Measured on the C4 weight gradients
+// (tools/conv_bench.py, isolated): splits of 2-32 tiles 4-30 % faster (layer2 3x3 74 -> 55 us),
+// 64-144 tiles neutral, the 36-tile layer3 3x3 14 % slower, so rounds 3-4 kept the per-slice
+// swizzle above 32 tiles.  Round 5 measured the traffic (PMC): split-major everywhere cuts the
+// 540-block layer3 3x3 weight gradient from 214 to 89 MB of HBM traffic per call and the conv
+// family from 152.2 to 144.3 MB per launch, with the C4 step unchanged (8942 / 8955 vs
+// 8950 / 8935 samples/s, paired) and the isolated wgrad total 2.40 vs 2.33 ms — the lower HBM
+// load is what the concurrent dgrad / BN chain shares, so split-major is the default.
 // Dense split-K GEMMs (both operands plain matrices: the nn.Linear weight gradients) always
 // use the split-major order: a K split's tiles share its dY / X row range, and on one XCD they
 // read it from that XCD's L2.  Measured at C5 (r05, PMC): the 288-block weight-gradient GEMMs
 // 262.7 -> 163.1 MB of HBM traffic per call, 52.7 -> 43.7 GB per step for the GEMM family,
 // 2850 / 2851 vs 2833 / 2834 samples/s paired; C4 neutral.
 #ifndef MMDX_SPLIT_XCD_MAX_TILES
-#define MMDX_SPLIT_XCD_MAX_TILES 32
+#define MMDX_SPLIT_XCD_MAX_TILES (1 << 30)
 #endif
 #ifndef MMDX_DENSE_SPLIT_XCD_MAX_TILES
 #define MMDX_DENSE_SPLIT_XCD_MAX_TILES (1 << 30)
