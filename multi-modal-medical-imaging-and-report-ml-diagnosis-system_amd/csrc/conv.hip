@@ -330,6 +330,16 @@ static void launch_dma32(const SA& sa, const SB& sb, const Epi& epi, int M, int 
                        sa, sb, epi, M, N, K, K);
 }
 
+// 256 x 64 tiles, 4 waves of 64 x 64 (NS = 2 / 3 stages) for the narrow-N k-major conv GEMMs
+// (N <= 64: the layer1 3x3 / 1x1 C = K = 64 convs), where a 128 x 64 block runs a short K loop
+// (9 taps) of 16 MFMAs per wave per barrier: twice the rows per block halve the weight-tile
+// DMAs per output and double the MFMAs per barrier (MMDX_CONV_N64_WIDE = NS; 0 = off)
+static int conv_n64_wide() {
+  const char* e = getenv("MMDX_CONV_N64_WIDE");  // read per launch: A/B runs switch it
+  const int ns = e ? atoi(e) : 0;
+  return ns == 2 || ns == 3 ? ns : 0;
+}
+
 static bool fold_probe_on() {
   const char* e = getenv("MMDX_FOLD_PROBE");  // timing probe only (tools/conv_bench.py)
   return e && atoi(e) != 0;
@@ -374,6 +384,22 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
           launch_dma32<128, 128>(sa, sb, epi, M, N, K, ns32, st);
         MMDX_LAUNCH_CHECK();
         return 0;
+      }
+      if (N <= 64) {
+        if (const int nsw = conv_n64_wide()) {
+          if (fin_ok) *fin_ok = false;   // the fused finalize tail is built for 128-row tiles
+          typedef DmaK<256, SA, 64, 4> OA;
+          typedef DmaK<64, DenseK<T>, 64, 4> OB;
+          const int nwg = (M + 255) / 256;
+          if (nsw == 3)
+            hipLaunchKernelGGL((igemm_dma_kernel<256, 64, OA, OB, Epi, 3, bf16, 256, 4, 1>),
+                               dim3(nwg), dim3(256), 0, st, sa, sb, epi, M, N, K, K);
+          else
+            hipLaunchKernelGGL((igemm_dma_kernel<256, 64, OA, OB, Epi, 2, bf16, 256, 4, 1>),
+                               dim3(nwg), dim3(256), 0, st, sa, sb, epi, M, N, K, K);
+          MMDX_LAUNCH_CHECK();
+          return 0;
+        }
       }
       if (N <= 64 || tiles128 < kNarrowBelow)
         return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
