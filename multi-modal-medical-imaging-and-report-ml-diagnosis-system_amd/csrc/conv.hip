@@ -336,8 +336,9 @@ static void launch_dma32(const SA& sa, const SB& sb, const Epi& epi, int M, int 
 // DMAs per output and double the MFMAs per barrier (MMDX_CONV_N64_WIDE = NS; 0 = off)
 static int conv_n64_wide() {
   const char* e = getenv("MMDX_CONV_N64_WIDE");  // read per launch: A/B runs switch it
-  const int ns = e ? atoi(e) : 0;
-  return ns == 2 || ns == 3 ? ns : 0;
+  const int v = e ? atoi(e) : 0;
+  return v >= 2 && v <= 5 ? v : 0;   // 2 / 3: 256 x 64, 4 waves, NS 2 / 3; 4: 512 x 64, 8
+                                     // waves, NS 2; 5: 256 x 64, 8 waves (64 x 32), NS 2
 }
 
 static bool fold_probe_on() {
@@ -391,12 +392,23 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
           typedef DmaK<256, SA, 64, 4> OA;
           typedef DmaK<64, DenseK<T>, 64, 4> OB;
           const int nwg = (M + 255) / 256;
-          if (nsw == 3)
+          if (nsw == 4) {
+            hipLaunchKernelGGL((igemm_dma_kernel<512, 64, DmaK<512, SA, 64, 8>,
+                                                 DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512,
+                                                 8, 1>),
+                               dim3((M + 511) / 512), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+          } else if (nsw == 5) {
+            hipLaunchKernelGGL((igemm_dma_kernel<256, 64, DmaK<256, SA, 64, 8>,
+                                                 DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512,
+                                                 4, 2>),
+                               dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+          } else if (nsw == 3) {
             hipLaunchKernelGGL((igemm_dma_kernel<256, 64, OA, OB, Epi, 3, bf16, 256, 4, 1>),
                                dim3(nwg), dim3(256), 0, st, sa, sb, epi, M, N, K, K);
-          else
+          } else {
             hipLaunchKernelGGL((igemm_dma_kernel<256, 64, OA, OB, Epi, 2, bf16, 256, 4, 1>),
                                dim3(nwg), dim3(256), 0, st, sa, sb, epi, M, N, K, K);
+          }
           MMDX_LAUNCH_CHECK();
           return 0;
         }
