@@ -330,15 +330,19 @@ static void launch_dma32(const SA& sa, const SB& sb, const Epi& epi, int M, int 
                        sa, sb, epi, M, N, K, K);
 }
 
-// 256 x 64 tiles, 4 waves of 64 x 64 (NS = 2 / 3 stages) for the narrow-N k-major conv GEMMs
-// (N <= 64: the layer1 3x3 / 1x1 C = K = 64 convs), where a 128 x 64 block runs a short K loop
-// (9 taps) of 16 MFMAs per wave per barrier: twice the rows per block halve the weight-tile
-// DMAs per output and double the MFMAs per barrier (MMDX_CONV_N64_WIDE = NS; 0 = off)
-static int conv_n64_wide() {
-  const char* e = getenv("MMDX_CONV_N64_WIDE");  // read per launch: A/B runs switch it
-  const int v = e ? atoi(e) : 0;
-  return v >= 2 && v <= 5 ? v : 0;   // 2 / 3: 256 x 64, 4 waves, NS 2 / 3; 4: 512 x 64, 8
-                                     // waves, NS 2; 5: 256 x 64, 8 waves (64 x 32), NS 2
+// 256-row tiles for the narrow-N k-major conv GEMMs (N <= 64: the layer1 3x3 / 1x1 C = K = 64
+// convs), where a 128 x 64 block runs a short K loop (9 taps) of 16 MFMAs per wave per barrier:
+// twice the rows per block halve the weight-tile DMAs per output and double the MFMAs per
+// barrier.  Default (variant 5, 256 x 64 in 8 waves of 64 x 32, two stages) when the grid
+// still has >= 1024 such blocks: C4's layer1 (M 401408) fwd / dgrad 0.486 / 0.376 -> 0.45 /
+// 0.33 ms isolated, C4 8963 / 8991 vs 8911 / 8922 samples/s paired; C2's layer1 (M 200704,
+// 784 blocks) lost 18 % with it, so it keeps 128 x 64.  MMDX_CONV_N64_WIDE forces a variant
+// (0 off; 2 / 3: 4 waves of 64 x 64, NS 2 / 3; 4: 512 x 64, 8 waves; 5), read per launch.
+static int conv_n64_wide(long M) {
+  const char* e = getenv("MMDX_CONV_N64_WIDE");
+  if (!e) return (M + 255) / 256 >= 1024 ? 5 : 0;
+  const int v = atoi(e);
+  return v >= 2 && v <= 5 ? v : 0;
 }
 
 static bool fold_probe_on() {
@@ -387,7 +391,7 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
         return 0;
       }
       if (N <= 64) {
-        if (const int nsw = conv_n64_wide()) {
+        if (const int nsw = conv_n64_wide(M)) {
           if (fin_ok) *fin_ok = false;   // the fused finalize tail is built for 128-row tiles
           typedef DmaK<256, SA, 64, 4> OA;
           typedef DmaK<64, DenseK<T>, 64, 4> OB;
