@@ -790,6 +790,11 @@ static bool wgrad8_on() {
   return e && atoi(e) != 0;
 }
 
+static bool wgrad_tap_bn_on() {
+  const char* e = getenv("MMDX_WGRAD_TAP_BN");
+  return e && atoi(e) != 0;
+}
+
 static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   WgradPlan p;
   const int BK = dtype == BF16 ? KTile<bf16>::BK : KTile<float>::BK;
@@ -809,6 +814,11 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   }
   p.bm = M <= 64 ? 64 : 128;
   p.bn = N <= 64 ? 64 : 128;
+  // MMDX_WGRAD_TAP_BN=1 (A/B): 64-column tiles when 128 columns would straddle two filter taps
+  // (C % 128 != 0, C % 64 == 0: layer1's 3x3 at C = 64), so the row-quartered im2col^T image
+  // keeps one tap per K tile (DmaRq's one-bounds-test path)
+  if (dtype == BF16 && d->R * d->S > 1 && d->C % 128 != 0 && d->C % 64 == 0 && wgrad_tap_bn_on())
+    p.bn = 64;
   if (dtype == BF16 && stem_direct_geom(geom(d)) && d->R == 7) {
     // the pixel-pair stem: K splits of whole 2-row pixel tiles (~256 splits), the layout the
     // direct kernel needs; the implicit-GEMM kernel takes the same splits (same sums)
