@@ -345,6 +345,28 @@ static int conv_n64_wide(long M) {
   return v >= 2 && v <= 5 ? v : 0;
 }
 
+// 128 x 128 k-major conv tiles in 8 waves of 64 x 32 (two 512-thread blocks, 16 waves per CU)
+// instead of 4 waves of 64 x 64: twice the waves to cover the LDS-DMA and barrier waits at
+// half the accumulators per lane.  Default on: isolated C4 fwd / dgrad 2.48 / 2.25 -> 2.28 /
+// 2.15 ms, C4 8957 / 8969 -> 9250 / 9271 samples/s paired (r05 s22).  MMDX_CONV_8W128=0
+// restores the 4-wave tiles; read per launch.
+static bool conv_8w128_on() {
+  const char* e = getenv("MMDX_CONV_8W128");
+  return !(e && atoi(e) == 0);
+}
+
+// the same for the 128 x 64 tiles (8 waves of 32 x 32; A/B knob, default off)
+static bool conv_8w64_on() {
+  const char* e = getenv("MMDX_CONV_8W64");
+  return e && atoi(e) != 0;
+}
+
+// the weight gradients' 128 x 128 R-major tiles in 8 waves (A/B knob, default off)
+static bool wgrad_8w_on() {
+  const char* e = getenv("MMDX_WGRAD_8W");
+  return e && atoi(e) != 0;
+}
+
 static bool fold_probe_on() {
   const char* e = getenv("MMDX_FOLD_PROBE");  // timing probe only (tools/conv_bench.py)
   return e && atoi(e) != 0;
@@ -417,8 +439,28 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
           return 0;
         }
       }
-      if (N <= 64 || tiles128 < kNarrowBelow)
+      if (N <= 64 || tiles128 < kNarrowBelow) {
+        if (conv_8w64_on()) {
+          if (fin_ok) *fin_ok = false;
+          hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, SA, 64, 8>,
+                                               DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 4,
+                                               2>),
+                             dim3((unsigned)(((M + 127) / 128) * ((N + 63) / 64))), dim3(512), 0,
+                             st, sa, sb, epi, M, N, K, K);
+          MMDX_LAUNCH_CHECK();
+          return 0;
+        }
         return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
+      }
+      if (conv_8w128_on()) {
+        if (fin_ok) *fin_ok = false;
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA, 64, 8>,
+                                             DmaK<128, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 2,
+                                             4>),
+                           dim3((unsigned)tiles128), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+        MMDX_LAUNCH_CHECK();
+        return 0;
+      }
       return launch_dma<128, 128>(sa, sb, epi, M, N, K, 1, K, st);
     }
   }
@@ -718,6 +760,12 @@ static int conv_dgrad_phases_merged(const ConvGeom& g, const void* dy, const voi
     hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, DgradPhaseK<T>>,
                                          DmaK<64, PhaseTapK<T>>, EpiPhase<T>, 2>),
                        dim3(nwg, 1, np), dim3(NT), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
+  } else if (conv_8w128_on()) {
+    const int nwg = ((mmax + 127) / 128) * ((N + 127) / 128);
+    hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, DgradPhaseK<T>, 64, 8>,
+                                         DmaK<128, PhaseTapK<T>, 64, 8>, EpiPhase<T>, 2, bf16,
+                                         512, 2, 4>),
+                       dim3(nwg, 1, np), dim3(512), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
   } else {
     const int nwg = ((mmax + 127) / 128) * ((N + 127) / 128);
     hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, DgradPhaseK<T>>,
@@ -1009,9 +1057,23 @@ static int wgrad_dma(const WgradPlan& p, const DenseR<T>& sa, const SB& sb, cons
     MMDX_LAUNCH_CHECK();
     return 0;
   }
-  if (p.bm == 128 && p.bn == 128)
+  if (p.bm == 128 && p.bn == 128) {
+    if (wgrad_8w_on()) {
+      const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
+      if (use_three_stages((long)nwg * p.splits, (p.kper + 63) / 64))
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaR<128, DenseR<T>, 64, 8>,
+                                             DmaR<128, SB, 64, 8>, EpiPartial, 3, bf16, 512, 2, 4>),
+                           dim3(nwg, 1, p.splits), dim3(512), 0, st, sa, sb, epi, M, N, K, p.kper);
+      else
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaR<128, DenseR<T>, 64, 8>,
+                                             DmaR<128, SB, 64, 8>, EpiPartial, 2, bf16, 512, 2, 4>),
+                           dim3(nwg, 1, p.splits), dim3(512), 0, st, sa, sb, epi, M, N, K, p.kper);
+      MMDX_LAUNCH_CHECK();
+      return 0;
+    }
     return launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, SB>>(sa, sb, epi, M, N, K,
                                                                         p.splits, p.kper, st);
+  }
   if (p.bm == 128)
     return launch_dma_ops<128, 64, DmaR<128, DenseR<T>>, DmaR<64, SB>>(sa, sb, epi, M, N, K,
                                                                       p.splits, p.kper, st);

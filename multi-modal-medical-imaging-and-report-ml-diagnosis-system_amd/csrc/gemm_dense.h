@@ -138,6 +138,17 @@ static int gemm256_stages() {
   return ns == 3 || ns == 4 ? ns : 0;
 }
 
+// The 128 x 128 tiles as 8 waves of 64 x 32 (two 512-thread blocks per CU) instead of 4 waves
+// of 64 x 64, as conv.hip's k-major conv tiles.  Default on: C5 2870 / 2865 -> 2910 / 2896
+// samples/s paired; isolated C5 dgrad / wgrad shapes 1-8 % faster, the forward ones (mostly
+// 256 x 256 tiles) equal; the one loss in tools/gemm_bench.py is the 4096^3 weight gradient
+// (156 -> 216 us), which no config runs (r05 s24).  MMDX_GEMM_8W128=0 restores the 4-wave
+// tiles; read per launch.
+static bool gemm_8w128_on() {
+  const char* e = getenv("MMDX_GEMM_8W128");
+  return !(e && atoi(e) == 0);
+}
+
 template <typename T, int BM, int BN, bool AK, bool BKm, class Epi>
 static int launch_dense(const void* A, long lda, const void* B, long ldb, const Epi& epi,
                         int M, int N, int K, int splits, int kper, hipStream_t st) {
@@ -201,6 +212,22 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
           hipLaunchKernelGGL((igemm_dma_kernel<256, 128, OA8, OB8, Epi, 3, T, 512, 4, 2>),
                              dim3((unsigned)t8, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K,
                              kper);
+          MMDX_LAUNCH_CHECK();
+          return 0;
+        }
+      }
+      if constexpr (BM == 128 && BN == 128) {
+        if (gemm_8w128_on()) {  // 8 waves of 64 x 32
+          typedef typename std::conditional<AK, DmaK<128, SA, 64, 8>,
+                                            DmaR<128, SA, 64, 8>>::type OA8;
+          typedef typename std::conditional<BKm, DmaK<128, SB, 64, 8>,
+                                            DmaR<128, SB, 64, 8>>::type OB8;
+          if ((long)nwg * splits <= 256 && kper >= 256)
+            hipLaunchKernelGGL((igemm_dma_kernel<128, 128, OA8, OB8, Epi, 3, T, 512, 2, 4>),
+                               dim3(nwg, 1, splits), dim3(512), 0, st, sa, sb, epi, M, N, K, kper);
+          else
+            hipLaunchKernelGGL((igemm_dma_kernel<128, 128, OA8, OB8, Epi, 2, T, 512, 2, 4>),
+                               dim3(nwg, 1, splits), dim3(512), 0, st, sa, sb, epi, M, N, K, kper);
           MMDX_LAUNCH_CHECK();
           return 0;
         }

@@ -142,3 +142,32 @@ def test_bk32_stages_match_bk64(dev, cfg, ns, monkeypatch):
     for key in a:
         assert torch.isfinite(b[key].float()).all(), key
         assert torch.equal(a[key], b[key]), key
+
+
+@pytest.mark.parametrize("knob", ["MMDX_CONV_8W128", "MMDX_CONV_8W64", "MMDX_WGRAD_8W"])
+@pytest.mark.parametrize("cfg", SHAPES)
+def test_8wave_128row_tiles_match_4wave(dev, cfg, knob, monkeypatch):
+    """The 128-row tiles in 8 waves (MMDX_CONV_8W128: 128 x 128 as 2 x 4 waves of 64 x 32, the
+    default since round 5, also for the phase-decomposed strided dgrad; MMDX_CONV_8W64: 128 x 64
+    as 4 x 2 waves of 32 x 32; MMDX_WGRAD_8W: the R-major 128 x 128 weight-gradient tiles) run
+    the same K tiles in the same MFMA order per output, and the same K splits: every output
+    and partial is bit-identical to the 4-wave kernels, and so are the statistics slabs where
+    a wave still covers 64 rows (MMDX_CONV_8W64's 32-row wave slices merge a 128-row slab in
+    four Chan steps instead of two: last-bit differences, rtol 2e-6; its consumer-BN partial sums
+    add 32-row slices: per-channel totals to 1e-5)."""
+    for k in ("MMDX_CONV_8W128", "MMDX_CONV_8W64", "MMDX_WGRAD_8W"):
+        monkeypatch.setenv(k, "0")
+    a = _run_all(dev, cfg, "0", monkeypatch)
+    monkeypatch.setenv(knob, "1")
+    b = _run_all(dev, cfg, "0", monkeypatch)
+    for key in a:
+        assert torch.isfinite(b[key].float()).all(), key
+        if key == "stats" and knob == "MMDX_CONV_8W64":
+            torch.testing.assert_close(b[key], a[key], rtol=2e-6, atol=1e-6, msg=key)
+            continue
+        if key == "bnstat_part" and knob == "MMDX_CONV_8W64":  # 32-row partial sums: order
+            ta, tb = a[key].double().sum(1), b[key].double().sum(1)
+            err = ((ta - tb).abs().max() / ta.abs().max().clamp(min=1e-12)).item()
+            assert err <= 1e-5, (key, err)
+            continue
+        assert torch.equal(a[key], b[key]), (knob, key)

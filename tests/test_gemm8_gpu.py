@@ -1,5 +1,6 @@
-"""GPU: the 8-wave dense GEMM tiles — 256 x 128 (MMDX_GEMM8_MIN) and 256 x 256 with 128 x 64
-per wave (MMDX_GEMM256_MIN), gemm_dense.hip — against the 4-wave 128 x 128 kernel and a torch
+"""GPU: the 8-wave dense GEMM tiles — 256 x 128 (MMDX_GEMM8_MIN), 256 x 256 with 128 x 64
+per wave (MMDX_GEMM256_MIN) and 128 x 128 with 64 x 32 per wave (MMDX_GEMM_8W128, the default
+since round 5), gemm_dense.hip — against the 4-wave 128 x 128 kernel and a torch
 fp32 matmul, in the three operand layouts the Linear layers use: forward (A, B k-major),
 input gradient (B R-major), weight gradient (A and B R-major), fp16 and bf16, ragged M / N /
 K.
@@ -44,7 +45,7 @@ def _operands(layout, M, N, K, dt, dev, seed):
     return a.to(dev), b.to(dev), ref
 
 
-@pytest.mark.parametrize("knob", ["MMDX_GEMM8_MIN", "MMDX_GEMM256_MIN"])
+@pytest.mark.parametrize("knob", ["MMDX_GEMM8_MIN", "MMDX_GEMM256_MIN", "MMDX_GEMM_8W128"])
 @pytest.mark.parametrize("layout", ["fwd", "dgrad", "wgrad"])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("shape", SHAPES)
@@ -54,6 +55,7 @@ def test_gemm8_matches_4wave(dev, knob, layout, dt, shape, monkeypatch):
     monkeypatch.setenv("MMDX_GEMM8_MIN", "0")
     monkeypatch.setenv("MMDX_GEMM256_MIN", "0")
     monkeypatch.setenv("MMDX_GEMM256_FWD_MIN", "0")  # the 4-wave kernel is the baseline
+    monkeypatch.setenv("MMDX_GEMM_8W128", "0")
     for out_dtype in (dt, torch.float32):
         monkeypatch.setenv(knob, "0")
         c4 = _gemm(layout, a, b, M, N, K, out_dtype)
