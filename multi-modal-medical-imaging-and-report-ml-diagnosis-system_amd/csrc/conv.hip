@@ -348,11 +348,19 @@ static int conv_n64_wide(long M) {
 // 128 x 128 k-major conv tiles in 8 waves of 64 x 32 (two 512-thread blocks, 16 waves per CU)
 // instead of 4 waves of 64 x 64: twice the waves to cover the LDS-DMA and barrier waits at
 // half the accumulators per lane.  Default on: isolated C4 fwd / dgrad 2.48 / 2.25 -> 2.28 /
-// 2.15 ms, C4 8957 / 8969 -> 9250 / 9271 samples/s paired (r05 s22).  MMDX_CONV_8W128=0
+// 2.15 ms, C4 8957 / 8969 -> 9250 / 9271 samples/s paired (r05 s22; that run also had the
+// strided dgrad's phase tiles in 8 waves, now MMDX_DGRAD_PHASE_8W).  MMDX_CONV_8W128=0
 // restores the 4-wave tiles; read per launch.
 static bool conv_8w128_on() {
   const char* e = getenv("MMDX_CONV_8W128");
   return !(e && atoi(e) == 0);
+}
+
+// the phase-decomposed strided dgrad's 128 x 128 tiles in 8 waves (A/B knob, default off:
+// isolated times equal, but its HBM traffic rose 533 -> 780 MB per layer2 call, PMC r05)
+static bool dgrad_phase_8w_on() {
+  const char* e = getenv("MMDX_DGRAD_PHASE_8W");
+  return e && atoi(e) != 0;
 }
 
 // the same for the 128 x 64 tiles (8 waves of 32 x 32; A/B knob, default off)
@@ -760,7 +768,7 @@ static int conv_dgrad_phases_merged(const ConvGeom& g, const void* dy, const voi
     hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, DgradPhaseK<T>>,
                                          DmaK<64, PhaseTapK<T>>, EpiPhase<T>, 2>),
                        dim3(nwg, 1, np), dim3(NT), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
-  } else if (conv_8w128_on()) {
+  } else if (dgrad_phase_8w_on()) {
     const int nwg = ((mmax + 127) / 128) * ((N + 127) / 128);
     hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, DgradPhaseK<T>, 64, 8>,
                                          DmaK<128, PhaseTapK<T>, 64, 8>, EpiPhase<T>, 2, bf16,

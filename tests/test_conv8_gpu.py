@@ -144,18 +144,22 @@ def test_bk32_stages_match_bk64(dev, cfg, ns, monkeypatch):
         assert torch.equal(a[key], b[key]), key
 
 
-@pytest.mark.parametrize("knob", ["MMDX_CONV_8W128", "MMDX_CONV_8W64", "MMDX_WGRAD_8W"])
+KNOBS_8W = ["MMDX_CONV_8W128", "MMDX_DGRAD_PHASE_8W", "MMDX_CONV_8W64", "MMDX_WGRAD_8W"]
+
+
+@pytest.mark.parametrize("knob", KNOBS_8W)
 @pytest.mark.parametrize("cfg", SHAPES)
 def test_8wave_128row_tiles_match_4wave(dev, cfg, knob, monkeypatch):
     """The 128-row tiles in 8 waves (MMDX_CONV_8W128: 128 x 128 as 2 x 4 waves of 64 x 32, the
-    default since round 5, also for the phase-decomposed strided dgrad; MMDX_CONV_8W64: 128 x 64
+    default since round 5; MMDX_DGRAD_PHASE_8W: the same for the phase-decomposed strided
+    dgrad; MMDX_CONV_8W64: 128 x 64
     as 4 x 2 waves of 32 x 32; MMDX_WGRAD_8W: the R-major 128 x 128 weight-gradient tiles) run
     the same K tiles in the same MFMA order per output, and the same K splits: every output
     and partial is bit-identical to the 4-wave kernels, and so are the statistics slabs where
     a wave still covers 64 rows (MMDX_CONV_8W64's 32-row wave slices merge a 128-row slab in
     four Chan steps instead of two: last-bit differences, rtol 2e-6; its consumer-BN partial sums
     add 32-row slices: per-channel totals to 1e-5)."""
-    for k in ("MMDX_CONV_8W128", "MMDX_CONV_8W64", "MMDX_WGRAD_8W"):
+    for k in KNOBS_8W:
         monkeypatch.setenv(k, "0")
     a = _run_all(dev, cfg, "0", monkeypatch)
     monkeypatch.setenv(knob, "1")

@@ -1,4 +1,4 @@
-# r05 final measurements on the committed tree: bench lines (C4 with the CPU baseline, C5, C3,
+# r05 final measurements on the committed tree (8-wave 128x128 defaults): bench lines (C4 with the CPU baseline, C5, C3,
 # C2), C4 / C5 kernel traces, PMC traffic + MFMA passes for C4 and C5
 set -o pipefail
 R=$(pwd)
