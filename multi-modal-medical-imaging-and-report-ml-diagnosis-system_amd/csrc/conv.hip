@@ -375,6 +375,39 @@ static bool wgrad_8w_on() {
   return e && atoi(e) != 0;
 }
 
+// Halo-band A operand (DmaHalo) for the same-size stride-1 convs over 64 channels: the
+// 256-row tile's A operand over all taps is one band of 256 + (R-1)*W + S-1 pixels, staged
+// in LDS once per block (at W = 56, 3x3: 370 pixels, 47 KB).  MMDX_CONV_HALO=0 (default) keeps
+// the per-tap DmaK gather (bit-identical output); read per launch.
+constexpr int kHaloPx256 = 376;
+constexpr int kHaloPx128 = 248;  // the 128 x 64 4-wave tiles (C2's layer1: < 1024 wide blocks)
+template <class S> struct HaloSrc { static constexpr bool value = false; };
+template <> struct HaloSrc<Im2colK<bf16, true>> { static constexpr bool value = true; };
+template <> struct HaloSrc<DgradK<bf16, true>> { static constexpr bool value = true; };
+static bool halo_band_fits(const ConvGeom& g, int ch, int rows) {
+  return ch == 64 && g.sh == 1 && g.sw == 1 && g.P == g.H && g.Q == g.W && g.R * g.S <= 32 &&
+         g.R > 1 && rows + (g.R - 1) * g.W + g.S - 1 <= (rows == 256 ? kHaloPx256 : kHaloPx128);
+}
+static bool halo_fits(const Im2colK<bf16, true>& s, int rows) {
+  return halo_band_fits(s.g, s.g.C, rows);
+}
+static bool halo_fits(const DgradK<bf16, true>& s, int rows) {
+  return halo_band_fits(s.g, s.g.K, rows);
+}
+// Measured (r05, tools/lab/r05_halo_ab.sh): bit-identical but not faster — isolated layer1
+// 3x3 fwd / dgrad 60.9 / 59.3 us gathered vs 62.6 / 63.1 (2 weight stages), 63.3 / 61.7 (3),
+// 62.6 / 64.7 (4); C4 step 9271 / 9248 vs 9257 / 9237.  L2 -> LDS requests drop 2.9x (PMC
+// TCP_TCC_READ_REQ) but these launches are bound by the per-block prologue / epilogue
+// instructions (7.8 VALU + 5.8 SALU per MFMA), not by the gather.  Off by default (A/B knob):
+// weight-operand stages of the 256-row halo kernel (the band needs none): MMDX_CONV_HALO =
+// 2 / 3 / 4 (1 = 2; 0 = off)
+static int conv_halo_stages() {
+  const char* e = getenv("MMDX_CONV_HALO");
+  const int v = e ? atoi(e) : 0;
+  return v <= 0 ? 0 : v == 1 ? 2 : v > 4 ? 4 : v;
+}
+static bool conv_halo_on() { return conv_halo_stages() != 0; }  // (the 128 x 64 tiles too)
+
 static bool fold_probe_on() {
   const char* e = getenv("MMDX_FOLD_PROBE");  // timing probe only (tools/conv_bench.py)
   return e && atoi(e) != 0;
@@ -432,6 +465,23 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
                                                  8, 1>),
                                dim3((M + 511) / 512), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
           } else if (nsw == 5) {
+            if constexpr (HaloSrc<SA>::value) {
+              if (const int hns = conv_halo_stages(); hns && halo_fits(sa, 256)) {
+                typedef DmaHalo<256, SA, 8, kHaloPx256> HA;
+                typedef DmaK<64, DenseK<T>, 64, 8> HB;
+                if (hns == 4)
+                  hipLaunchKernelGGL((igemm_dma_kernel<256, 64, HA, HB, Epi, 4, bf16, 512, 4, 2>),
+                                     dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+                else if (hns == 3)
+                  hipLaunchKernelGGL((igemm_dma_kernel<256, 64, HA, HB, Epi, 3, bf16, 512, 4, 2>),
+                                     dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+                else
+                  hipLaunchKernelGGL((igemm_dma_kernel<256, 64, HA, HB, Epi, 2, bf16, 512, 4, 2>),
+                                     dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+                MMDX_LAUNCH_CHECK();
+                return 0;
+              }
+            }
             hipLaunchKernelGGL((igemm_dma_kernel<256, 64, DmaK<256, SA, 64, 8>,
                                                  DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512,
                                                  4, 2>),
@@ -458,6 +508,10 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
           MMDX_LAUNCH_CHECK();
           return 0;
         }
+        if constexpr (HaloSrc<SA>::value)
+          if (N <= 64 && conv_halo_on() && halo_fits(sa, 128))
+            return launch_dma_ops<128, 64, DmaHalo<128, SA, 4, kHaloPx128>, DmaK<64, DenseK<T>>>(
+                sa, sb, epi, M, N, K, 1, K, st);
         return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
       }
       if (conv_8w128_on()) {

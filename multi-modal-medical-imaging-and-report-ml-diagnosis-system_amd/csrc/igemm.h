@@ -316,6 +316,12 @@ struct Im2colK {
     toff = ((r * g.W + s) * g.C + c0) * (int)sizeof(T);
     tap = r * g.S + s;
   }
+  // halo band (DmaHalo; stride 1, P = H, Q = W): the input pixel of row m at tap (r, s) is
+  // m - ph*W - pw + r*W + s, so a tile's band starts at row0 + hstart() and tap (r, s) reads
+  // band pixel (m - row0) + hshift(r, s)
+  __device__ int hstart() const { return -g.ph * g.W - g.pw; }
+  __device__ int hshift(int r, int s) const { return r * g.W + s; }
+  __device__ int hS() const { return g.S; }
 };
 
 // conv dgrad A operand: rows = input pixels (n,h,w), k = (r, s, kout) with kout contiguous.
@@ -412,6 +418,11 @@ struct DgradK {
     toff = (kb - (r * g.Q + s) * g.K) * (int)sizeof(T);
     tap = r * g.S + s;
   }
+  // halo band (DmaHalo; stride 1, H = P, W = Q): the dY pixel of row m at tap (r, s) is
+  // m + ph*Q + pw - r*Q - s; the band starts at the lowest of them (tap (R-1, S-1))
+  __device__ int hstart() const { return g.ph * g.Q + g.pw - (g.R - 1) * g.Q - (g.S - 1); }
+  __device__ int hshift(int r, int s) const { return (g.R - 1 - r) * g.Q + (g.S - 1 - s); }
+  __device__ int hS() const { return g.S; }
 };
 
 // Strided-conv dgrad, one output phase (a, b) = (h mod sh, w mod sw) at a time: only the
@@ -1991,6 +2002,69 @@ struct DmaRq {
   }
 };
 
+// Halo A operand for the same-size stride-1 convs over 64 channels (forward: C = 64; dgrad:
+// K = 64 — ResNet layer1's 3x3 convs).  A row's pixel at tap (r, s) is affine in the row
+// (Im2colK / DgradK hstart, hshift), so the A operand of a ROWS-row tile over all R*S taps is
+// one contiguous band of ROWS + (R-1)*W + S-1 input pixels.  The band is DMA'd into LDS once
+// per block (128-B pixel rows; chunk c of band pixel p at slot c ^ (p & 7), the DmaK
+// swizzle) and every K tile (= one tap, C = BK) reads its fragments at a uniform per-tap
+// shift: at W = 56, ROWS = 256 the block moves 1.45x its rows' bytes through L2 -> LDS
+// instead of 9x.  Taps that leave the image read zeros by the row's tap mask (brow), so the
+// operand values, k order and MFMA sequence equal DmaK's (bit-identical output).  Only the
+// weight operand runs through the per-K-tile stages (INSTR = BYTES = 0 here).
+template <int ROWS, class Src, int NWV, int HPX>
+struct DmaHalo {
+  static constexpr int BK = 64;
+  static constexpr bool RMAJOR = false;
+  static constexpr bool HALO = true;
+  static constexpr int NW = NWV;
+  static constexpr int INSTR = 0;
+  static constexpr int BYTES = 0;
+  static constexpr int HALO_BYTES = HPX * 128;
+  static constexpr int HINSTR = HPX / 8;  // 1-KiB DMA instructions (8 pixels each)
+  static_assert(HPX % 8 == 0 && HPX >= ROWS, "band pixels");
+  typedef Src SrcT;
+  int row0;
+  __device__ void init(const Src&, int r0, int, int, int) { row0 = r0; }
+  __device__ void issue(const Src&, char*, int, int, int) {}
+  // the band: called once, before any K tile's DMA (vmcnt counts the K tiles' DMAs behind it)
+  __device__ void band(const Src& s, char* lds, int lane, int wid) const {
+    const __amdgpu_buffer_rsrc_t rsrc = dma_rsrc(s.bbase(), s.bbytes());
+    const int hb = row0 + s.hstart();  // global pixel of band pixel 0 (may be < 0)
+    const int slot = lane & 7;
+    for (int j = wid; j < HINSTR; j += NW) {
+      const int bp = j * 8 + (lane >> 3);
+      const int gp = hb + bp;
+      const unsigned voff =
+          gp >= 0 ? (unsigned)((gp * 64 + ((slot ^ (bp & 7)) << 3)) * 2) : DMA_OOB;
+      dma16(rsrc, lds + j * 1024, voff);
+    }
+  }
+  // tap masks of this lane's fragment rows (wm * WTM + i * 16 + (lane & 15))
+  template <int WTM, int RM>
+  __device__ void masks(const Src& s, int wm, int lane, unsigned (&mk)[RM]) const {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      unsigned m;
+      (void)s.brow(row0 + wm * WTM + i * 16 + (lane & 15), m);
+      mk[i] = m;
+    }
+  }
+  __device__ static bf16x8 hfrag(const char* band, int r16, int ks, int lane, int shift,
+                                 bool ok) {
+    const int p = ok ? r16 + (lane & 15) + shift : 0;
+    const int c = (ks >> 3) + (lane >> 4);
+    const bf16x8 v = *(const bf16x8*)(band + p * 128 + ((c ^ (p & 7)) << 4));
+    return ok ? v : bf16x8{};
+  }
+};
+template <class O, class = void> struct IsHalo { static constexpr bool value = false; };
+template <class O> struct IsHalo<O, decltype((void)O::HALO)> {
+  static constexpr bool value = O::HALO;
+};
+template <class O, bool = IsHalo<O>::value> struct HaloBytes { static constexpr int value = 0; };
+template <class O> struct HaloBytes<O, true> { static constexpr int value = O::HALO_BYTES; };
+
 // Stores a staged fp32 tile cst [BM][LDC] (CW columns) at output (m0, n0): 8 consecutive
 // columns per lane -> one 16-B store where the epilogue allows it, else 4-column pieces.
 template <int BM, int CW, int LDC, int NTH, class Epi>
@@ -2047,7 +2121,8 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
-  constexpr int OP_BYTES = NS * STAGE;
+  constexpr bool HALO = IsHalo<OA>::value;  // A operand from a per-block LDS band (DmaHalo)
+  constexpr int OP_BYTES = NS * STAGE + HaloBytes<OA>::value;
   constexpr int RED = WM * 3 > (NTH / 64) * 2 ? WM * 3 : (NTH / 64) * 2;  // floats per column
   // the fp32 tile is staged through LDS in NCH column passes: two for 256 x 256 tiles, whose
   // full staging (266 KB) exceeds the CU's 160 KB
@@ -2096,6 +2171,19 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   OB ob;
   oa.init(sa, tm * BM, lane, wid, kbeg);
   ob.init(sb, tn * BN, lane, wid, kbeg);
+  char* const band = lds_raw + NS * STAGE;
+  unsigned hmask[HALO ? RM : 1];
+  if constexpr (HALO) {
+    oa.band(sa, band, lane, wid);  // before tile 0's DMAs: its vmcnt wait covers the band
+    oa.template masks<WTM, RM>(sa, wm, lane, hmask);
+  }
+  // this K tile's tap (one tap per tile: C = BK) and band shift (DmaHalo)
+  // (generic: instantiated only by the DmaHalo kernels)
+  auto htap = [&](const auto& src, int t, int& shift) {
+    const int tap = kbeg / BK + t, S = src.hS(), r = tap / S;
+    shift = src.hshift(r, tap - r * S);
+    return tap;
+  };
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -2160,6 +2248,15 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     __builtin_amdgcn_s_barrier();
     const char* as = lds_raw + (t % NS) * STAGE;
     const char* bs = as + OA::BYTES;
+    int hsh = 0, htp = 0;
+    if constexpr (HALO) htp = htap(sa, t, hsh);
+    // A fragment i at k step ks: the K tile's stage, or the band at this tap's shift
+    auto afrag = [&](int i, int ks) {
+      if constexpr (HALO)
+        return OA::hfrag(band, wm * WTM + i * 16, ks, lane, hsh, (hmask[i] >> htp) & 1u);
+      else
+        return OA::frag(as, wm * WTM + i * 16, ks, lane);
+    };
     if constexpr (FRAG_FIRST) {
       // every fragment of the tile is requested before the next tile's DMAs are issued, so
       // the LDS read latency runs under the DMA issue instead of in front of the MFMAs
@@ -2168,7 +2265,7 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
 #pragma unroll
-        for (int i = 0; i < RM; ++i) af[s][i] = OA::frag(as, wm * WTM + i * 16, s * 32, lane);
+        for (int i = 0; i < RM; ++i) af[s][i] = afrag(i, s * 32);
 #pragma unroll
         for (int j = 0; j < RN; ++j) bfr[s][j] = OB::frag(bs, wn * WTN + j * 16, s * 32, lane);
       }
@@ -2218,7 +2315,7 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     for (int ks = 0; ks < BK; ks += 32) {
       bf16x8 af[RM], bfr[RN];
 #pragma unroll
-      for (int i = 0; i < RM; ++i) af[i] = OA::frag(as, wm * WTM + i * 16, ks, lane);
+      for (int i = 0; i < RM; ++i) af[i] = afrag(i, ks);
 #pragma unroll
       for (int j = 0; j < RN; ++j) bfr[j] = OB::frag(bs, wn * WTN + j * 16, ks, lane);
 #pragma unroll
