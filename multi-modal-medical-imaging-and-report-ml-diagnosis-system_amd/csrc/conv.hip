@@ -891,6 +891,17 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
 }
 
 struct WgradPlan { int bm, bn, splits, kper; };
+
+// split-K block target of the conv weight gradients (MMDX_WGRAD_TARGET; read per plan — the
+// workspace size query reads it too, so set it before the plan is built).  Re-swept on the
+// round-5 kernels (split-major order, 8-wave fwd / dgrad tiles; tools/lab/r05_wgrad_target*):
+// 256 vs 512 C4 9292 / 9305 / 9305 vs 9266 / 9293 / 9263 paired (+0.3 %), C2 +0.6 %, C3 -0.4 %,
+// 768 / 1024 -0.6 / -0.8 %; conv HBM traffic 145.2 -> 137.7 MB per launch (fewer fp32 slabs)
+static long wgrad_split_target() {
+  const char* e = getenv("MMDX_WGRAD_TARGET");
+  const long v = e ? atol(e) : 0L;
+  return v >= 64 && v <= 4096 ? v : 256L;
+}
 // 8-wave 256 x 128 weight-gradient tiles (one block per CU, three stages) for Kout >= 256
 // and C*R*S >= 128 (MMDX_WGRAD8=0: off); their splits target one block per CU
 // 8-wave 256 x 128 weight-gradient tiles (MMDX_WGRAD8=1; off by default: isolated C4 wgrads
@@ -940,11 +951,12 @@ static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   }
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
   const long ktiles = (K + BK - 1) / BK;
-  // ~2 blocks per CU, each split at least 16 K tiles deep (keeps the partial slabs small).
-  // Measured: 256 / 384 / 768 / 1024-block targets lose to 512 in the C4 step; ~4 per CU for
+  // ~1 block per CU, each split at least 16 K tiles deep (keeps the partial slabs small).
+  // Rounds 2-3 measured 512 best (256 / 384 / 768 / 1024 lost); round 5 re-swept: 256 (above);
+  // ~4 per CU for
   // the 3x3 convs of layer3/4 ran 4-12 % faster in isolation but 0.2 % slower in the train
   // step (more blocks contending with the dgrad chain); 8 / 16 / 32 least K tiles tie.
-  const long target = 512L;
+  const long target = wgrad_split_target();
   const long min_kt = 16L;
   long s = (target + tiles - 1) / tiles;
   s = std::max(1L, std::min(s, ktiles / min_kt));
