@@ -397,6 +397,39 @@ def cpu_baseline(cfg, bs=8, warmup=10, steps=50):
                       f"reference AdamW groups, clip 1.0), torch CPU fp32, {threads} threads"}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(n, argv, port):
+    """The command that starts `n` bench ranks (one process per GPU) on this node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` with no launcher around it: start the N ranks as child
+    processes of torch.distributed.run (this process has made no GPU call, and it waits for
+    the children instead of replacing itself) and return their exit status.  Rank 0 prints
+    the JSON line."""
+    import subprocess
+    backend = os.environ.get("MMDX_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        have = torch.cuda.device_count()   # counts devices without initialising HIP
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} GPUs for RCCL, {have} visible "
+                  f"(MMDX_DIST_BACKEND=gloo rehearses several ranks on one GPU)",
+                  file=sys.stderr, flush=True)
+            return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_cmd(n, argv, _free_port()), env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -407,11 +440,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=50)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["batch"] = args.batch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # MMDX_DIST_BACKEND=gloo rehearses the DP path with several ranks on one GPU (RCCL
@@ -426,6 +468,11 @@ def main():
         from mmdx.dist import init_distributed
         torch.cuda.set_device(local)
         init_distributed(backend, local)   # RCCL async errors / timeouts fail the job fast
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the process group has "
+                  f"{dist.get_world_size()} ranks", file=sys.stderr, flush=True)
+            sys.exit(2)
+        world = dist.get_world_size()
     dev = torch.device("cuda", local)
     # C5 is specified as "fp16 MFMA" (BASELINE.json); C2-C4 compute in bf16 (fp32 masters)
     dtype = torch.float16 if cfg["image"] == "vit_b_16" else torch.bfloat16
@@ -601,8 +648,14 @@ def main():
                   for tag, _, _ in timer.pairs)
     flop_ms = fam_flops / (PEAK_BF16_TFLOPS * 1e9)
     byte_ms = fam_bytes / (PEAK_HBM_GBS * 1e6)
-    conv_tf = fam_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-    conv_gbs = fam_bytes / (conv_ms * 1e-3) / 1e9 if conv_ms > 0 else 0.0
+    # The family's time is the union of its launch intervals (wall time with at least one of
+    # its kernels running; never more than the step).  The per-launch event SUM over-counts:
+    # each pair also spans the launch's dispatch gap behind the previous packet of its stream
+    # (≈ 7 µs per launch at C4, the sum exceeded the step), and launches on the weight-gradient
+    # stream overlap the dgrad chain.  The sum stays in the line as `family_event_sum_ms`.
+    fam_ms = busy_ms if busy_ms > 0 else conv_ms
+    conv_tf = fam_flops / (fam_ms * 1e-3) / 1e12 if fam_ms > 0 else 0.0
+    conv_gbs = fam_bytes / (fam_ms * 1e-3) / 1e9 if fam_ms > 0 else 0.0
     if vit:
         conv_flops = fam_flops / max(1, conv_steps) / B
     alg_bytes = fam_bytes / max(1, conv_steps)
@@ -626,6 +679,7 @@ def main():
         "launch": ("hipGraph (whole step)" if graph_step else
                    "eager" + (" (text tower: hipGraph replay)" if graph_text else "")),
         "stream_priority": "main+text",
+        "dist_backend": backend if dp else None,
         "config": {"workload": cfg["name"], "image_tower": cfg["image"],
                    "text_tower": cfg["text"], "global_batch": B * world,
                    "per_gpu_batch": B, "seq_len": cfg["seq"], "image_hw": 224,
@@ -667,12 +721,15 @@ def main():
             "hbm_achieved_gbs": round(conv_gbs, 1),
             "hbm_frac": round(conv_gbs / PEAK_HBM_GBS, 4),
             "combined_roof_ms_per_step": round(roof_ms / conv_steps, 3),
-            "combined_frac": round(roof_ms / conv_ms, 4) if conv_ms > 0 else None,
+            "combined_frac": round(roof_ms / fam_ms, 4) if fam_ms > 0 else None,
             "combined_frac_note": "sum over launches of max(FLOPs/2.5 PF, bytes/8 TB/s) "
-                                  "divided by the summed launch durations",
-            "family_ms_per_step": round(conv_ms / conv_steps, 3),
-            "busy_ms_per_step": round(busy_ms / conv_steps, 3),
-            "busy_combined_frac": (round(roof_ms / busy_ms, 4) if busy_ms > 0 else None),
+                                  "divided by the family's busy time",
+            "family_ms_per_step": round(fam_ms / conv_steps, 3),
+            "family_time": "union of the family's HIP-event launch intervals (busy time)",
+            "family_event_sum_ms_per_step": round(conv_ms / conv_steps, 3),
+            "event_sum_frac": (round((fam_bytes / (conv_ms * 1e6)) / PEAK_HBM_GBS if hbm_bound
+                                     else fam_flops / (conv_ms * 1e9) / PEAK_BF16_TFLOPS, 4)
+                               if conv_ms > 0 else None),
             "family_launches_per_step": n_conv // max(1, conv_steps),
             "family_gflop_per_sample": round(conv_flops / 1e9, 3),
             "family_alg_gb_per_step": round(alg_bytes / 1e9, 3),

@@ -40,6 +40,10 @@ enum { MMDX_ACT_NONE = 0, MMDX_ACT_RELU = 1, MMDX_ACT_GELU = 2, MMDX_ACT_GELU_BW
 
 int mmdx_version(void);
 const char* mmdx_last_error(void);
+/* Re-read the MMDX_* launch-heuristic environment knobs (tile / split choices; read once per
+ * process otherwise).  For tests and A/B runs that switch a knob between launches; not to be
+ * called while another thread issues launches. */
+int mmdx_reload_config(void);
 
 /* ---------------------------------------------------------------- GEMM (nn.Linear)
  * C[M,N] = act(alpha * sum_k A(m,k) B(n,k) + bias[n] + addend[m,n]) + beta * C
@@ -126,34 +130,6 @@ int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x, const void*
  * whatever MMDX_STEM_DIRECT says later; a size the kernels cannot write is an error). */
 int mmdx_conv_fwd_rows(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
                        void* y, float* stat_part, int stat_rows, void* stream);
-/* Train-mode conv whose epilogue also FINALIZES the BatchNorm statistics of its output
- * (mean / rstd / running-stat update / the apply pass's scale and shift, as mmdx_bn_fwd's
- * finalize): the blocks write their (mean, M2) slabs to stat_part as mmdx_conv_fwd does, and
- * the last block of each group of row tiles, then the last group of each column tile, merges
- * them inside the same launch (ticket counters in `scratch`), so no finalize launch sits
- * between the conv and its BN apply.  scratch: mmdx_conv_fwd_bnfin_scratch_size(d) bytes, zeroed
- * once before first use (the counters return to zero after every call).  Convs the fused
- * kernels do not cover (fp32, the pixel-pair stem, 256-row tiles) run mmdx_conv_fwd and then
- * mmdx_bn_finalize: the outputs are the same either way.  Follow with mmdx_bn_apply.
- * Replaces: the BatchNorm2d batch statistics + running-stat update after each backbone conv
- * (TP:183 / TP:223, train mode). */
-typedef struct {
-  const float* gamma;      /* [K] or NULL (1) */
-  const float* beta;       /* [K] or NULL (0) */
-  float* running_mean;     /* [K] or NULL (no running-stat update) */
-  float* running_var;
-  float momentum, eps;
-  float* save_mean;        /* [K] outputs */
-  float* save_rstd;
-  float* scale;            /* [K]: gamma * rstd */
-  float* shift;            /* [K]: beta - mean * gamma * rstd */
-  void* scratch;
-  size_t scratch_bytes;
-} mmdx_bn_fin;
-size_t mmdx_conv_fwd_bnfin_scratch_size(const mmdx_conv_desc* d);
-int mmdx_conv_fwd_bnfin(int dtype, const mmdx_conv_desc* d, const void* x, const void* w_krsc,
-                        void* y, float* stat_part, int stat_rows, const mmdx_bn_fin* fin,
-                        void* stream);
 /* Eval-mode conv + BatchNorm2d (running statistics) (+residual) (+ReLU) in one launch:
  * y = act(conv(x, w) * s + t + residual), s = gamma / sqrt(running_var + eps),
  * t = beta - running_mean * s, applied in the conv epilogue on the fp32 accumulators.
@@ -324,11 +300,9 @@ enum {
   MMDX_OP_GELU_BWD, MMDX_OP_BIAS_GRAD, MMDX_OP_ADD, MMDX_OP_DROPOUT_FWD, MMDX_OP_DROPOUT_BWD,
   MMDX_OP_AXPBY, MMDX_OP_ATTN_FWD_LSE, MMDX_OP_ATTN_BWD_LSE, MMDX_OP_LN_FWD_DROP,
   MMDX_OP_LN_BWD_DROP, MMDX_OP_GEMM_BIAS_GRAD,
-  /* conv + fused BN finalize (i: stat_rows; l: scratch (absolute), scratch_bytes; f: momentum,
-   * eps; p: x, w, y, stat_part, gamma, beta, running_mean, running_var, save_mean, save_rstd,
-   * scale, shift) and the BN apply pass (i: C, relu; l: rows; p: x, residual, scale, shift, y,
-   * relu_mask) */
-  MMDX_OP_CONV_FWD_BNFIN, MMDX_OP_BN_APPLY
+  /* (42: the retired conv + fused BN finalize op, tools/lab/RETIRED.md) and the BN apply pass
+   * (i: C, relu; l: rows; p: x, residual, scale, shift, y, relu_mask) */
+  MMDX_OP_RETIRED_42, MMDX_OP_BN_APPLY
 };
 typedef struct {
   int op, dtype, stream;

@@ -36,14 +36,6 @@ class AdamWTensor(C.Structure):
 CD = C.POINTER(ConvDesc)
 
 
-class BnFin(C.Structure):
-    """mmdx_bn_fin (include/mmdx.h): the BN finalize of mmdx_conv_fwd_bnfin."""
-    _fields_ = [("gamma", vp), ("beta", vp), ("running_mean", vp), ("running_var", vp),
-                ("momentum", C.c_float), ("eps", C.c_float), ("save_mean", vp),
-                ("save_rstd", vp), ("scale", vp), ("shift", vp), ("scratch", vp),
-                ("scratch_bytes", C.c_size_t)]
-
-
 class PackItem(C.Structure):
     """mmdx_pack_item (include/mmdx.h): one weight of a multi-tensor pack launch."""
     _fields_ = [("w", vp), ("krsc", vp), ("crsk", vp), ("K", C.c_int), ("C", C.c_int),
@@ -65,13 +57,14 @@ class PlanOp(C.Structure):
  OP_MAXPOOL_BN_FWD, OP_BN_BWD_POOL, OP_CONV_DGRAD_ACCMASK, OP_BN_BWD_MASKED_DY,
  OP_GEMM, OP_ATTN_FWD, OP_ATTN_BWD, OP_LN_FWD, OP_LN_BWD, OP_GELU_BWD, OP_BIAS_GRAD, OP_ADD,
  OP_DROPOUT_FWD, OP_DROPOUT_BWD, OP_AXPBY, OP_ATTN_FWD_LSE, OP_ATTN_BWD_LSE, OP_LN_FWD_DROP,
- OP_LN_BWD_DROP, OP_GEMM_BIAS_GRAD, OP_CONV_FWD_BNFIN, OP_BN_APPLY) = range(1, 44)
+ OP_LN_BWD_DROP, OP_GEMM_BIAS_GRAD, OP_RETIRED_42, OP_BN_APPLY) = range(1, 44)
 
 # name -> (restype, argtypes).  Kept in header order; tests check this table against
 # include/mmdx.h so the binding cannot drift from the ABI.
 SIGNATURES = {
     "mmdx_version": (i32, []),
     "mmdx_last_error": (C.c_char_p, []),
+    "mmdx_reload_config": (i32, []),
     "mmdx_gemm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_gemm": (i32, [i32, i32, i32, i32, vp, i64, i32, vp, i64, i32, vp, i64, i32, vp, vp,
                         i32, f32, f32, vp, vp, sz, vp]),
@@ -82,8 +75,6 @@ SIGNATURES = {
     "mmdx_conv_fwd_stat_rows": (i32, [CD]),
     "mmdx_conv_fwd": (i32, [i32, CD, vp, vp, vp, vp, vp]),
     "mmdx_conv_fwd_rows": (i32, [i32, CD, vp, vp, vp, vp, i32, vp]),
-    "mmdx_conv_fwd_bnfin_scratch_size": (sz, [CD]),
-    "mmdx_conv_fwd_bnfin": (i32, [i32, CD, vp, vp, vp, vp, i32, C.POINTER(BnFin), vp]),
     "mmdx_conv_fwd_bn_eval": (i32, [i32, CD, vp, vp, vp, vp, vp, vp, vp, f32, vp, i32, vp]),
     "mmdx_conv_dgrad": (i32, [i32, CD, vp, vp, vp, f32, vp]),
     "mmdx_conv_dgrad_stat_blocks": (i32, [i32, CD]),
@@ -238,6 +229,12 @@ def lib():
         h.mmdx_missing_symbols = missing
         _lib = h
     return _lib
+
+
+def reload_config():
+    """Re-read the MMDX_* launch-heuristic knobs (the library reads them once per process):
+    for tests / A-B runs that change one with os.environ between launches."""
+    call("mmdx_reload_config")
 
 
 def check(rc: int, name: str):

@@ -1088,31 +1088,17 @@ static size_t smem16(int L, int nw) {
 // queries per forward block: 128 (8 waves) halves the K/V staging per query and doubles the
 // resident waves per CU (the LDS, not the registers, bounds residency); MMDX_ATTN_FWD_NW=4
 // selects 64
-static int fwd16_nw() {
-  static const int nw = [] {
-    const char* e = getenv("MMDX_ATTN_FWD_NW");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  return nw;
-}
+static int fwd16_nw() { return knobs().attn_fwd_nw == 4 ? 4 : 8; }
 // the flash-style forward's block: 8 waves (128 queries); MMDX_ATTN_FWD_NW = 4 | 16 selects
 // 64 / 256 (16 waves = one block per ViT head, K and V staged once instead of twice: C5
 // 2631 / 2640 vs 2653 / 2664 samples/s with 8, paired, tools/lab_attnnw.sh)
 static int fwd16_lse_nw(int L) {
   (void)L;
-  static const int nw = [] {
-    const char* e = getenv("MMDX_ATTN_FWD_NW");
-    const int v = e ? atoi(e) : 0;
-    return v == 4 || v == 16 ? v : 8;
-  }();
-  return nw;
+  const int v = knobs().attn_fwd_nw;
+  return v == 4 || v == 16 ? v : 8;
 }
 static int bwd16_nw() {   // the same for the dQ kernel; MMDX_ATTN_BWD_NW=4 selects 64
-  static const int nw = [] {
-    const char* e = getenv("MMDX_ATTN_BWD_NW");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  return nw;
+  return knobs().attn_bwd_nw == 4 ? 4 : 8;
 }
 
 template <typename T>

@@ -24,6 +24,30 @@ enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3 };
 
 constexpr int WAVE = 64;
 
+// Launch-heuristic knobs (MMDX_* environment variables, documented where each is used), read
+// ONCE per process into this read-only struct instead of a getenv walk per launch (158 conv
+// launches per C4 step used to read up to 14 of them each).  mmdx_reload_config() re-reads the
+// environment: tests and A/B runs that switch a knob call it between launches, never while one
+// is being issued.
+struct Knobs {
+  int conv_n64_wide;      // MMDX_CONV_N64_WIDE: -1 auto (>= 1024 256-row blocks), 0 off, 1 on
+  bool conv_8w128;        // MMDX_CONV_8W128 (default on)
+  bool stem_direct;       // MMDX_STEM_DIRECT (default on)
+  long wgrad_target;      // MMDX_WGRAD_TARGET: conv weight-gradient split-K blocks (256)
+  bool wgrad_rq;          // MMDX_WGRAD_RQ (default on)
+  long gemm256_fwd_min;   // MMDX_GEMM256_FWD_MIN: 256 x 256 forward tiles from this many (90)
+  bool gemm_8w128;        // MMDX_GEMM_8W128 (default on)
+  long splitk_target;     // MMDX_SPLITK_TARGET: dense split-K blocks (256)
+  bool splitk_vec;        // MMDX_SPLITK_VEC (default on)
+  bool wgrad_bias_fused;  // MMDX_WGRAD_BIAS_FUSED (default on)
+  bool bias_grad_gemm;    // MMDX_BIAS_GRAD_GEMM (default off)
+  int ln_bwd_rpw;         // MMDX_LN_BWD_RPW: 4 | 8 (8)
+  int attn_fwd_nw;        // MMDX_ATTN_FWD_NW: raw value (0 = unset)
+  int attn_bwd_nw;        // MMDX_ATTN_BWD_NW: raw value (0 = unset)
+  bool lstm_bwd_probe;    // MMDX_LSTM_BWD_PROBE: lab phase stamps (tools/lab/lstm_probe.py)
+};
+const Knobs& knobs();
+
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
 __device__ __forceinline__ float to_f(f16 x) { return (float)x; }

@@ -280,242 +280,52 @@ static bool is_pointwise(const ConvGeom& g) {
 // C4 step: 256 and 384 tie, 640 is 1.5 % slower
 constexpr long kNarrowBelow = 384;
 
-// 8-wave 256 x 128 tiles (one 512-thread block per CU, three 48 KB operand stages): for the
-// k-major conv GEMMs with N >= 128 and at least this many tiles (MMDX_CONV8_MIN; 0 = off).
-// Off by default: at threshold 160 the isolated C4 forward convs took 2.51 vs 2.41 ms and the
-// dgrads 2.22 vs 2.11 ms, the train step 9001 / 8999 vs 9089 / 9059 samples/s (paired in one
-// call, profiles/r03_conv8_ab.txt) — one block per CU leaves no second block to cover a
-// block's barrier waits and epilogue
-static long conv8_min_tiles() {
-  const char* e = getenv("MMDX_CONV8_MIN");  // read per launch: tests / A-B runs switch it
-  return e ? atol(e) : 0L;
-}
-
-template <class SA, class SB, class Epi>
-static bool try_conv8(const SA& sa, const SB& sb, const Epi& epi, int M, int N, int K,
-                      hipStream_t st) {
-  const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
-  const long lim = conv8_min_tiles();
-  if (lim <= 0 || N < 128 || tiles < lim || K < 128) return false;
-  hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaK<256, SA, 64, 8>, DmaK<128, SB, 64, 8>, Epi,
-                                       3, bf16, 512, 4, 2>),
-                     dim3((unsigned)tiles, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-  return true;
-}
-
-// BK = 32 K tiles with NS = 3..5 stages (MMDX_CONV_BK32 = NS; 0 = off): at 128 x 128 a
-// 64-deep stage is 32 KB and two blocks per CU leave room for two stages only (one tile in
-// flight while one is consumed); 16 KB stages keep two blocks per CU with NS - 1 tiles in
-// flight.  A/B knob for tools/conv_bench.py.
-static int conv_bk32_stages() {
-  const char* e = getenv("MMDX_CONV_BK32");
-  const int ns = e ? atoi(e) : 0;
-  return ns >= 3 && ns <= 5 ? ns : 0;
-}
-
-template <int BM, int BN, class SA, class SB, class Epi>
-static void launch_dma32(const SA& sa, const SB& sb, const Epi& epi, int M, int N, int K,
-                         int ns, hipStream_t st) {
-  typedef DmaK<BM, SA, 32> OA;
-  typedef DmaK<BN, SB, 32> OB;
-  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (ns == 3)
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 3>), dim3(nwg), dim3(NT), 0, st,
-                       sa, sb, epi, M, N, K, K);
-  else if (ns == 4)
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 4>), dim3(nwg), dim3(NT), 0, st,
-                       sa, sb, epi, M, N, K, K);
-  else
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, OA, OB, Epi, 5>), dim3(nwg), dim3(NT), 0, st,
-                       sa, sb, epi, M, N, K, K);
-}
-
 // 256-row tiles for the narrow-N k-major conv GEMMs (N <= 64: the layer1 3x3 / 1x1 C = K = 64
 // convs), where a 128 x 64 block runs a short K loop (9 taps) of 16 MFMAs per wave per barrier:
 // twice the rows per block halve the weight-tile DMAs per output and double the MFMAs per
-// barrier.  Default (variant 5, 256 x 64 in 8 waves of 64 x 32, two stages) when the grid
-// still has >= 1024 such blocks: C4's layer1 (M 401408) fwd / dgrad 0.486 / 0.376 -> 0.45 /
-// 0.33 ms isolated, C4 8963 / 8991 vs 8911 / 8922 samples/s paired; C2's layer1 (M 200704,
-// 784 blocks) lost 18 % with it, so it keeps 128 x 64.  MMDX_CONV_N64_WIDE forces a variant
-// (0 off; 2 / 3: 4 waves of 64 x 64, NS 2 / 3; 4: 512 x 64, 8 waves; 5), read per launch.
-static int conv_n64_wide(long M) {
-  const char* e = getenv("MMDX_CONV_N64_WIDE");
-  if (!e) return (M + 255) / 256 >= 1024 ? 5 : 0;
-  const int v = atoi(e);
-  return v >= 2 && v <= 5 ? v : 0;
+// barrier.  256 x 64 in 8 waves of 64 x 32, two stages, when the grid still has >= 1024 such
+// blocks: C4's layer1 (M 401408) fwd / dgrad 0.486 / 0.376 -> 0.45 / 0.33 ms isolated, C4
+// 8963 / 8991 vs 8911 / 8922 samples/s paired; C2's layer1 (M 200704, 784 blocks) lost 18 %
+// with it, so it keeps 128 x 64.  MMDX_CONV_N64_WIDE = 0 off / 1 on forces it (knobs()).
+static bool conv_n64_wide(long M) {
+  const int v = knobs().conv_n64_wide;
+  return v < 0 ? (M + 255) / 256 >= 1024 : v != 0;
 }
 
 // 128 x 128 k-major conv tiles in 8 waves of 64 x 32 (two 512-thread blocks, 16 waves per CU)
 // instead of 4 waves of 64 x 64: twice the waves to cover the LDS-DMA and barrier waits at
 // half the accumulators per lane.  Default on: isolated C4 fwd / dgrad 2.48 / 2.25 -> 2.28 /
-// 2.15 ms, C4 8957 / 8969 -> 9250 / 9271 samples/s paired (r05 s22; that run also had the
-// strided dgrad's phase tiles in 8 waves, now MMDX_DGRAD_PHASE_8W).  MMDX_CONV_8W128=0
-// restores the 4-wave tiles; read per launch.
-static bool conv_8w128_on() {
-  const char* e = getenv("MMDX_CONV_8W128");
-  return !(e && atoi(e) == 0);
-}
+// 2.15 ms, C4 8957 / 8969 -> 9250 / 9271 samples/s paired (r05 s22).  MMDX_CONV_8W128=0
+// restores the 4-wave tiles.
+static bool conv_8w128_on() { return knobs().conv_8w128; }
 
-// the phase-decomposed strided dgrad's 128 x 128 tiles in 8 waves (A/B knob, default off:
-// isolated times equal, but its HBM traffic rose 533 -> 780 MB per layer2 call, PMC r05)
-static bool dgrad_phase_8w_on() {
-  const char* e = getenv("MMDX_DGRAD_PHASE_8W");
-  return e && atoi(e) != 0;
-}
+// Retired variants (measured slower, removed from the library in round 6; their code and
+// measurements: tools/lab/RETIRED.md): 8-wave 256 x 128 conv tiles (MMDX_CONV8_MIN), 32-deep K
+// tiles (MMDX_CONV_BK32), 8-wave phase-dgrad / 128 x 64 / weight-gradient tiles
+// (MMDX_DGRAD_PHASE_8W, MMDX_CONV_8W64, MMDX_WGRAD_8W), the halo-band A operand
+// (MMDX_CONV_HALO), the BN-fold timing probe (MMDX_FOLD_PROBE), the other 256-row variants of
+// MMDX_CONV_N64_WIDE, 256 x 128 weight-gradient tiles (MMDX_WGRAD8), tap-aligned 64-column
+// weight-gradient tiles (MMDX_WGRAD_TAP_BN) and the BN finalize fused into the conv
+// (MMDX_BN_FIN, mmdx_conv_fwd_bnfin).
 
-// the same for the 128 x 64 tiles (8 waves of 32 x 32; A/B knob, default off)
-static bool conv_8w64_on() {
-  const char* e = getenv("MMDX_CONV_8W64");
-  return e && atoi(e) != 0;
-}
-
-// the weight gradients' 128 x 128 R-major tiles in 8 waves (A/B knob, default off)
-static bool wgrad_8w_on() {
-  const char* e = getenv("MMDX_WGRAD_8W");
-  return e && atoi(e) != 0;
-}
-
-// Halo-band A operand (DmaHalo) for the same-size stride-1 convs over 64 channels: the
-// 256-row tile's A operand over all taps is one band of 256 + (R-1)*W + S-1 pixels, staged
-// in LDS once per block (at W = 56, 3x3: 370 pixels, 47 KB).  MMDX_CONV_HALO=0 (default) keeps
-// the per-tap DmaK gather (bit-identical output); read per launch.
-constexpr int kHaloPx256 = 376;
-constexpr int kHaloPx128 = 248;  // the 128 x 64 4-wave tiles (C2's layer1: < 1024 wide blocks)
-template <class S> struct HaloSrc { static constexpr bool value = false; };
-template <> struct HaloSrc<Im2colK<bf16, true>> { static constexpr bool value = true; };
-template <> struct HaloSrc<DgradK<bf16, true>> { static constexpr bool value = true; };
-static bool halo_band_fits(const ConvGeom& g, int ch, int rows) {
-  return ch == 64 && g.sh == 1 && g.sw == 1 && g.P == g.H && g.Q == g.W && g.R * g.S <= 32 &&
-         g.R > 1 && rows + (g.R - 1) * g.W + g.S - 1 <= (rows == 256 ? kHaloPx256 : kHaloPx128);
-}
-static bool halo_fits(const Im2colK<bf16, true>& s, int rows) {
-  return halo_band_fits(s.g, s.g.C, rows);
-}
-static bool halo_fits(const DgradK<bf16, true>& s, int rows) {
-  return halo_band_fits(s.g, s.g.K, rows);
-}
-// Measured (r05, tools/lab/r05_halo_ab.sh): bit-identical but not faster — isolated layer1
-// 3x3 fwd / dgrad 60.9 / 59.3 us gathered vs 62.6 / 63.1 (2 weight stages), 63.3 / 61.7 (3),
-// 62.6 / 64.7 (4); C4 step 9271 / 9248 vs 9257 / 9237.  L2 -> LDS requests drop 2.9x (PMC
-// TCP_TCC_READ_REQ) but these launches are bound by the per-block prologue / epilogue
-// instructions (7.8 VALU + 5.8 SALU per MFMA), not by the gather.  Off by default (A/B knob):
-// weight-operand stages of the 256-row halo kernel (the band needs none): MMDX_CONV_HALO =
-// 2 / 3 / 4 (1 = 2; 0 = off)
-static int conv_halo_stages() {
-  const char* e = getenv("MMDX_CONV_HALO");
-  const int v = e ? atoi(e) : 0;
-  return v <= 0 ? 0 : v == 1 ? 2 : v > 4 ? 4 : v;
-}
-static bool conv_halo_on() { return conv_halo_stages() != 0; }  // (the 128 x 64 tiles too)
-
-static bool fold_probe_on() {
-  const char* e = getenv("MMDX_FOLD_PROBE");  // timing probe only (tools/conv_bench.py)
-  return e && atoi(e) != 0;
-}
-
-// fin_ok (optional): set when the launched kernel is one whose epilogue runs the fused BN
-// finalize tail (the LDS-DMA kernel with 128-row tiles; EpiStore::fin)
 template <typename T, class SA, class Epi>
 static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int N, int K,
-                         hipStream_t st, bool dma_ok, bool* fin_ok = nullptr) {
+                         hipStream_t st, bool dma_ok) {
   DenseK<T> sb{(const T*)w, K, N, true};
-  if (fin_ok) *fin_ok = false;
   if constexpr (DmaOk<SA>::value) {
-    if (dma_ok && fold_probe_on()) {
-      if (fin_ok) *fin_ok = true;
-      const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-      const int bn = (N <= 64 || tiles128 < kNarrowBelow) ? 64 : 128;
-      const int nwg = ((M + 127) / 128) * ((N + bn - 1) / bn);
-      if (bn == 64)
-        hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, SA>, DmaK<64, DenseK<T>>, Epi, 2,
-                                             bf16, NT, 2, 2, 1>),
-                           dim3(nwg), dim3(NT), 0, st, sa, sb, epi, M, N, K, K);
-      else
-        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA>, DmaK<128, DenseK<T>>, Epi,
-                                             2, bf16, NT, 2, 2, 1>),
-                           dim3(nwg), dim3(NT), 0, st, sa, sb, epi, M, N, K, K);
-      MMDX_LAUNCH_CHECK();
-      return 0;
-    }
     if (dma_ok) {
-      if (try_conv8(sa, sb, epi, M, N, K, st)) {
-        MMDX_LAUNCH_CHECK();
-        return 0;
-      }
       // 128x64 tiles when N is narrow or 128x128 tiles would leave CUs idle (< 1.5 per CU)
       const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-      if (fin_ok) *fin_ok = true;
-      if (const int ns32 = conv_bk32_stages()) {
-        if (N <= 64 || tiles128 < kNarrowBelow)
-          launch_dma32<128, 64>(sa, sb, epi, M, N, K, ns32, st);
-        else
-          launch_dma32<128, 128>(sa, sb, epi, M, N, K, ns32, st);
+      if (N <= 64 && conv_n64_wide(M)) {
+        hipLaunchKernelGGL((igemm_dma_kernel<256, 64, DmaK<256, SA, 64, 8>,
+                                             DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 4, 2>),
+                           dim3((M + 255) / 256), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
         MMDX_LAUNCH_CHECK();
         return 0;
       }
-      if (N <= 64) {
-        if (const int nsw = conv_n64_wide(M)) {
-          if (fin_ok) *fin_ok = false;   // the fused finalize tail is built for 128-row tiles
-          typedef DmaK<256, SA, 64, 4> OA;
-          typedef DmaK<64, DenseK<T>, 64, 4> OB;
-          const int nwg = (M + 255) / 256;
-          if (nsw == 4) {
-            hipLaunchKernelGGL((igemm_dma_kernel<512, 64, DmaK<512, SA, 64, 8>,
-                                                 DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512,
-                                                 8, 1>),
-                               dim3((M + 511) / 512), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-          } else if (nsw == 5) {
-            if constexpr (HaloSrc<SA>::value) {
-              if (const int hns = conv_halo_stages(); hns && halo_fits(sa, 256)) {
-                typedef DmaHalo<256, SA, 8, kHaloPx256> HA;
-                typedef DmaK<64, DenseK<T>, 64, 8> HB;
-                if (hns == 4)
-                  hipLaunchKernelGGL((igemm_dma_kernel<256, 64, HA, HB, Epi, 4, bf16, 512, 4, 2>),
-                                     dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-                else if (hns == 3)
-                  hipLaunchKernelGGL((igemm_dma_kernel<256, 64, HA, HB, Epi, 3, bf16, 512, 4, 2>),
-                                     dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-                else
-                  hipLaunchKernelGGL((igemm_dma_kernel<256, 64, HA, HB, Epi, 2, bf16, 512, 4, 2>),
-                                     dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-                MMDX_LAUNCH_CHECK();
-                return 0;
-              }
-            }
-            hipLaunchKernelGGL((igemm_dma_kernel<256, 64, DmaK<256, SA, 64, 8>,
-                                                 DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512,
-                                                 4, 2>),
-                               dim3(nwg), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-          } else if (nsw == 3) {
-            hipLaunchKernelGGL((igemm_dma_kernel<256, 64, OA, OB, Epi, 3, bf16, 256, 4, 1>),
-                               dim3(nwg), dim3(256), 0, st, sa, sb, epi, M, N, K, K);
-          } else {
-            hipLaunchKernelGGL((igemm_dma_kernel<256, 64, OA, OB, Epi, 2, bf16, 256, 4, 1>),
-                               dim3(nwg), dim3(256), 0, st, sa, sb, epi, M, N, K, K);
-          }
-          MMDX_LAUNCH_CHECK();
-          return 0;
-        }
-      }
-      if (N <= 64 || tiles128 < kNarrowBelow) {
-        if (conv_8w64_on()) {
-          if (fin_ok) *fin_ok = false;
-          hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, SA, 64, 8>,
-                                               DmaK<64, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 4,
-                                               2>),
-                             dim3((unsigned)(((M + 127) / 128) * ((N + 63) / 64))), dim3(512), 0,
-                             st, sa, sb, epi, M, N, K, K);
-          MMDX_LAUNCH_CHECK();
-          return 0;
-        }
-        if constexpr (HaloSrc<SA>::value)
-          if (N <= 64 && conv_halo_on() && halo_fits(sa, 128))
-            return launch_dma_ops<128, 64, DmaHalo<128, SA, 4, kHaloPx128>, DmaK<64, DenseK<T>>>(
-                sa, sb, epi, M, N, K, 1, K, st);
+      if (N <= 64 || tiles128 < kNarrowBelow)
         return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
-      }
       if (conv_8w128_on()) {
-        if (fin_ok) *fin_ok = false;
         hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA, 64, 8>,
                                              DmaK<128, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 2,
                                              4>),
@@ -537,15 +347,13 @@ template <typename T, class SA>
 static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K, float beta,
                      hipStream_t st, float* stats = nullptr, bool dma_ok = false,
                      const BnStat& bs = BnStat{}, const void* acc_src = nullptr,
-                     const uint8_t* acc_mask = nullptr, const BnFinArgs* fin = nullptr,
-                     bool* fin_ok = nullptr) {
+                     const uint8_t* acc_mask = nullptr) {
   EpiStore<T> epi{(T*)out, N, M, N, nullptr, nullptr, ACT_NONE, 1.f, beta, nullptr,
                   (float2*)stats};
   epi.bs = bs;  // only the LDS-DMA kernel's epilogue honours it (see dgrad_bnstat_ok)
   epi.acc_src = (const T*)acc_src;
   epi.acc_mask = acc_mask;
-  if (fin) epi.fin = *fin;
-  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok, fin_ok);
+  return conv_gemm_epi<T>(sa, w, epi, M, N, K, st, dma_ok);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -565,10 +373,7 @@ static int conv_gemm(const SA& sa, const void* w, void* out, int M, int N, int K
 constexpr int STEM_PB = 2;   // output rows per block
 constexpr int STEM_LDY = 64 + 8;  // staged output row (bf16), padded
 
-static bool stem_direct_on() {
-  const char* e = getenv("MMDX_STEM_DIRECT");  // read per launch (A/B, tests)
-  return !e || atoi(e) != 0;
-}
+static bool stem_direct_on() { return knobs().stem_direct; }  // MMDX_STEM_DIRECT (A/B, tests)
 
 static bool stem_direct_geom(const ConvGeom& g) {
   return g.C == 8 && g.S == 4 && (g.R == 7 || g.R == 8) && g.sh == 2 && g.sw == 1 && g.ph == 0 &&
@@ -681,16 +486,12 @@ static int stem_direct_fwd(const ConvGeom& g, const void* x, const void* w, void
 }
 
 // stat_rows: the rows per statistics slab the caller sized `stats` for (128; 2*Q selects the
-// direct stem kernel, which writes one slab per block); without stats the env knob decides
-// fin / fin_ok: the fused BN finalize (mmdx_conv_fwd_bnfin); fin_ok reports whether the
-// launched kernel ran it
+// direct stem kernel, which writes one slab per block); without stats the knob decides
 template <typename T>
 static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, void* y,
-                      float* stats, int stat_rows, hipStream_t st,
-                      const BnFinArgs* fin = nullptr, bool* fin_ok = nullptr) {
+                      float* stats, int stat_rows, hipStream_t st) {
   const ConvGeom g = geom(d);
   const int M = g.N * g.P * g.Q, N = g.K, K = g.R * g.S * g.C;
-  if (fin_ok) *fin_ok = false;
   const bool direct = stem_direct_geom(g) && std::is_same<T, bf16>::value &&
                       (stats ? stat_rows == STEM_PB * g.Q : stem_direct_on());
   MMDX_CHECK_ARG(!stats || direct || stat_rows == 128,
@@ -700,37 +501,15 @@ static int conv_fwd_t(const mmdx_conv_desc* d, const void* x, const void* w, voi
     if (direct) return stem_direct_fwd(g, x, w, y, stats, st);
   if (g.C % KTile<T>::BK == 0 && is_pointwise(g))  // x itself is the [M][C] A operand
     return conv_gemm<T>(PointFwdK<T>{{(const T*)x, g.C, M, true}}, w, y, M, N, K, 0.f, st,
-                        stats, dma_geom_ok(g, false, 32, M), BnStat{}, nullptr, nullptr, fin,
-                        fin_ok);
+                        stats, dma_geom_ok(g, false, 32, M));
   if (g.C % KTile<T>::BK == 0)
     return conv_gemm<T>(Im2colK<T, true>{(const T*)x, g, M}, w, y, M, N, K, 0.f, st, stats,
-                        dma_geom_ok(g, false, 32, M), BnStat{}, nullptr, nullptr, fin, fin_ok);
+                        dma_geom_ok(g, false, 32, M));
   // channel count a power of two: the LDS-DMA kernel decodes each lane's tap itself
   const bool pow2 = g.C >= 8 && (g.C & (g.C - 1)) == 0 && g.R * g.S <= 64;
   Im2colK<T, false> sa{(const T*)x, g, M, pow2 ? __builtin_ctz(g.C) : 0, 1.f / (float)g.S};
   return conv_gemm<T>(sa, w, y, M, N, K, 0.f, st, stats, pow2 && dma_geom_ok(g, false, 64, M),
-                      BnStat{}, nullptr, nullptr, fin, fin_ok);
-}
-
-// Fused-finalize layout: row tiles (128 rows) in groups of ~sqrt(tiles) (each merge reads at
-// most 64 slabs per channel: bnfin_merge's 32 per thread x 2 threads per channel at BN = 128);
-// scratch = [tiles_n (BN 64) column counters + tiles_n x ngroups group counters] (u32, padded
-// to 256 B) + [N][ngroups] group slabs.  0 groups: too many row tiles for the fused merge.
-struct BnFinLayout { int group, ngroups; size_t ctr_bytes, bytes; };
-static BnFinLayout bnfin_layout(const ConvGeom& g) {
-  BnFinLayout L{0, 0, 0, 0};
-  const long M = (long)g.N * g.P * g.Q;
-  const long tiles_m = (M + 127) / 128;
-  long G = 1;
-  while (G * G < tiles_m) ++G;
-  const long ng = (tiles_m + G - 1) / G;
-  if (G > 64 || ng > 64) return L;
-  const long tiles_n = (g.K + 63) / 64;
-  L.group = (int)G;
-  L.ngroups = (int)ng;
-  L.ctr_bytes = (size_t)((tiles_n + tiles_n * ng) * 4 + 255) / 256 * 256;
-  L.bytes = L.ctr_bytes + (size_t)g.K * ng * sizeof(float2);
-  return L;
+                      BnStat{});
 }
 
 template <typename T>
@@ -808,26 +587,12 @@ static int conv_dgrad_phases_merged(const ConvGeom& g, const void* dy, const voi
     }
   }
   if (np == 0) return 0;
-  // 8-wave 256x128 tiles (opt-in) and the 128x64 / 128x128 choice on the whole grid's tiles
-  const long lim = conv8_min_tiles();
-  const long tiles256 = (long)np * ((mmax + 255) / 256) * ((N + 127) / 128);
-  if (lim > 0 && N >= 128 && tiles256 >= lim && kmax >= 128) {
-    hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaK<256, DgradPhaseK<T>, 64, 8>,
-                                         DmaK<128, PhaseTapK<T>, 64, 8>, EpiPhase<T>, 3, bf16,
-                                         512, 4, 2>),
-                       dim3((unsigned)(((mmax + 255) / 256) * ((N + 127) / 128)), 1, np),
-                       dim3(512), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
-  } else if (N <= 64 || tiles128 < kNarrowBelow) {
+  // the 128x64 / 128x128 choice on the whole grid's tiles
+  if (N <= 64 || tiles128 < kNarrowBelow) {
     const int nwg = ((mmax + 127) / 128) * ((N + 63) / 64);
     hipLaunchKernelGGL((igemm_dma_kernel<128, 64, DmaK<128, DgradPhaseK<T>>,
                                          DmaK<64, PhaseTapK<T>>, EpiPhase<T>, 2>),
                        dim3(nwg, 1, np), dim3(NT), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
-  } else if (dgrad_phase_8w_on()) {
-    const int nwg = ((mmax + 127) / 128) * ((N + 127) / 128);
-    hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, DgradPhaseK<T>, 64, 8>,
-                                         DmaK<128, PhaseTapK<T>, 64, 8>, EpiPhase<T>, 2, bf16,
-                                         512, 2, 4>),
-                       dim3(nwg, 1, np), dim3(512), 0, st, sa, sb, epi, mmax, N, kmax, kmax);
   } else {
     const int nwg = ((mmax + 127) / 128) * ((N + 127) / 128);
     hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, DgradPhaseK<T>>,
@@ -892,54 +657,19 @@ static int conv_dgrad_t(const mmdx_conv_desc* d, const void* dy, const void* w_c
 
 struct WgradPlan { int bm, bn, splits, kper; };
 
-// split-K block target of the conv weight gradients (MMDX_WGRAD_TARGET; read per plan — the
-// workspace size query reads it too, so set it before the plan is built).  Re-swept on the
-// round-5 kernels (split-major order, 8-wave fwd / dgrad tiles; tools/lab/r05_wgrad_target*):
+// split-K block target of the conv weight gradients (MMDX_WGRAD_TARGET, knobs()).  Re-swept on
+// the round-5 kernels (split-major order, 8-wave fwd / dgrad tiles; tools/lab/r05_wgrad_target*):
 // 256 vs 512 C4 9292 / 9305 / 9305 vs 9266 / 9293 / 9263 paired (+0.3 %), C2 +0.6 %, C3 -0.4 %,
 // 768 / 1024 -0.6 / -0.8 %; conv HBM traffic 145.2 -> 137.7 MB per launch (fewer fp32 slabs)
-static long wgrad_split_target() {
-  const char* e = getenv("MMDX_WGRAD_TARGET");
-  const long v = e ? atol(e) : 0L;
-  return v >= 64 && v <= 4096 ? v : 256L;
-}
-// 8-wave 256 x 128 weight-gradient tiles (one block per CU, three stages) for Kout >= 256
-// and C*R*S >= 128 (MMDX_WGRAD8=0: off); their splits target one block per CU
-// 8-wave 256 x 128 weight-gradient tiles (MMDX_WGRAD8=1; off by default: isolated C4 wgrads
-// 2.78 vs 2.51 ms, train step 8967 vs 9050 samples/s, profiles/r03_wgrad8_ab.txt)
-static bool wgrad8_on() {
-  const char* e = getenv("MMDX_WGRAD8");
-  return e && atoi(e) != 0;
-}
-
-static bool wgrad_tap_bn_on() {
-  const char* e = getenv("MMDX_WGRAD_TAP_BN");
-  return e && atoi(e) != 0;
-}
+static long wgrad_split_target() { return knobs().wgrad_target; }
 
 static WgradPlan plan_wgrad(int dtype, const mmdx_conv_desc* d) {
   WgradPlan p;
   const int BK = dtype == BF16 ? KTile<bf16>::BK : KTile<float>::BK;
   const int M = d->K, N = d->R * d->S * d->C;
   const long K = (long)d->N * d->P * d->Q;
-  if (dtype == BF16 && M >= 256 && N >= 128 && wgrad8_on()) {
-    p.bm = 256;
-    p.bn = 128;
-    const long tiles = (long)((M + 255) / 256) * ((N + 127) / 128);
-    const long ktiles = (K + BK - 1) / BK;
-    long s = (256L + tiles - 1) / tiles;
-    s = std::max(1L, std::min(s, ktiles / 16L));
-    const long kt_per = (ktiles + s - 1) / s;
-    p.kper = (int)(kt_per * BK);
-    p.splits = (int)((K + p.kper - 1) / p.kper);
-    return p;
-  }
   p.bm = M <= 64 ? 64 : 128;
   p.bn = N <= 64 ? 64 : 128;
-  // MMDX_WGRAD_TAP_BN=1 (A/B): 64-column tiles when 128 columns would straddle two filter taps
-  // (C % 128 != 0, C % 64 == 0: layer1's 3x3 at C = 64), so the row-quartered im2col^T image
-  // keeps one tap per K tile (DmaRq's one-bounds-test path)
-  if (dtype == BF16 && d->R * d->S > 1 && d->C % 128 != 0 && d->C % 64 == 0 && wgrad_tap_bn_on())
-    p.bn = 64;
   if (dtype == BF16 && stem_direct_geom(geom(d)) && d->R == 7) {
     // the pixel-pair stem: K splits of whole 2-row pixel tiles (~256 splits), the layout the
     // direct kernel needs; the implicit-GEMM kernel takes the same splits (same sums)
@@ -1100,16 +830,13 @@ __global__ __launch_bounds__(512, 1) void stem_direct_wgrad_kernel(
 
 // The im2col^T operand of the 3x3 / strided weight gradients in the row-quartered LDS image
 // (DmaRq: one pixel state per lane; MMDX_WGRAD_RQ=0 restores DmaR for A/B runs)
-static bool wgrad_rq_on() {
-  const char* e = getenv("MMDX_WGRAD_RQ");   // read per launch: tests / A-B runs switch it
-  return !(e && atoi(e) == 0);
-}
+static bool wgrad_rq_on() { return knobs().wgrad_rq; }
 
 template <typename T, class SB>
 static int wgrad_dma(const WgradPlan& p, const DenseR<T>& sa, const SB& sb, const EpiPartial& epi,
                      int M, int N, int K, hipStream_t st) {
   if constexpr (std::is_same<SB, Im2colR<T>>::value) {
-    if (p.bm != 256 && wgrad_rq_on()) {
+    if (wgrad_rq_on()) {
       if (p.bm == 128 && p.bn == 128)
         return launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaRq<128, SB>>(
             sa, sb, epi, M, N, K, p.splits, p.kper, st);
@@ -1123,31 +850,9 @@ static int wgrad_dma(const WgradPlan& p, const DenseR<T>& sa, const SB& sb, cons
                                                                        p.splits, p.kper, st);
     }
   }
-  if (p.bm == 256) {
-    const int nwg = ((M + 255) / 256) * ((N + 127) / 128);
-    hipLaunchKernelGGL((igemm_dma_kernel<256, 128, DmaR<256, DenseR<T>, 64, 8>, DmaR<128, SB, 64, 8>,
-                                         EpiPartial, 3, bf16, 512, 4, 2>),
-                       dim3(nwg, 1, p.splits), dim3(512), 0, st, sa, sb, epi, M, N, K, p.kper);
-    MMDX_LAUNCH_CHECK();
-    return 0;
-  }
-  if (p.bm == 128 && p.bn == 128) {
-    if (wgrad_8w_on()) {
-      const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
-      if (use_three_stages((long)nwg * p.splits, (p.kper + 63) / 64))
-        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaR<128, DenseR<T>, 64, 8>,
-                                             DmaR<128, SB, 64, 8>, EpiPartial, 3, bf16, 512, 2, 4>),
-                           dim3(nwg, 1, p.splits), dim3(512), 0, st, sa, sb, epi, M, N, K, p.kper);
-      else
-        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaR<128, DenseR<T>, 64, 8>,
-                                             DmaR<128, SB, 64, 8>, EpiPartial, 2, bf16, 512, 2, 4>),
-                           dim3(nwg, 1, p.splits), dim3(512), 0, st, sa, sb, epi, M, N, K, p.kper);
-      MMDX_LAUNCH_CHECK();
-      return 0;
-    }
+  if (p.bm == 128 && p.bn == 128)
     return launch_dma_ops<128, 128, DmaR<128, DenseR<T>>, DmaR<128, SB>>(sa, sb, epi, M, N, K,
                                                                         p.splits, p.kper, st);
-  }
   if (p.bm == 128)
     return launch_dma_ops<128, 64, DmaR<128, DenseR<T>>, DmaR<64, SB>>(sa, sb, epi, M, N, K,
                                                                       p.splits, p.kper, st);
@@ -1286,58 +991,6 @@ extern "C" int mmdx_conv_fwd_rows(int dtype, const mmdx_conv_desc* d, const void
   if (dtype == BF16)
     return conv_fwd_t<bf16>(d, x, w, y, stat_part, stat_rows, (hipStream_t)stream);
   return conv_fwd_t<float>(d, x, w, y, stat_part, stat_rows, (hipStream_t)stream);
-}
-
-extern "C" size_t mmdx_conv_fwd_bnfin_scratch_size(const mmdx_conv_desc* d) {
-  const BnFinLayout L = bnfin_layout(geom(d));
-  return std::max<size_t>(L.bytes, 256);
-}
-
-extern "C" int mmdx_conv_fwd_bnfin(int dtype, const mmdx_conv_desc* d, const void* x,
-                                   const void* w, void* y, float* stat_part, int stat_rows,
-                                   const mmdx_bn_fin* fin, void* stream) {
-  MMDX_CHECK_ARG(dtype != F16, "mmdx_conv_fwd_bnfin: fp16 is the C5 path only");
-  MMDX_CHECK_ARG(fin && stat_part && fin->save_mean && fin->save_rstd && fin->scale &&
-                     fin->shift,
-                 "conv fwd bnfin: statistics, outputs and the finalize arguments are required");
-  const ConvGeom g = geom(d);
-  const long M = (long)g.N * g.P * g.Q;
-  MMDX_CHECK_ARG(M < (1L << 31), "conv fwd bnfin: N*P*Q too large");
-  hipStream_t st = (hipStream_t)stream;
-  const BnFinLayout L = bnfin_layout(g);
-  const bool fusable = dtype == BF16 && L.group > 0 && fin->scratch &&
-                       fin->scratch_bytes >= L.bytes && stat_rows == 128;
-  BnFinArgs fa;
-  if (fusable) {
-    fa.ctr = (unsigned*)fin->scratch;
-    fa.gpart = (float2*)((char*)fin->scratch + L.ctr_bytes);
-    fa.group = L.group;
-    fa.ngroups = L.ngroups;
-    fa.gamma = fin->gamma;
-    fa.beta = fin->beta;
-    fa.rmean = fin->running_mean;
-    fa.rvar = fin->running_var;
-    fa.momentum = fin->momentum;
-    fa.eps = fin->eps;
-    fa.save_mean = fin->save_mean;
-    fa.save_rstd = fin->save_rstd;
-    fa.scale = fin->scale;
-    fa.shift = fin->shift;
-  }
-  bool done = false;
-  int rc;
-  if (dtype == BF16)
-    rc = conv_fwd_t<bf16>(d, x, w, y, stat_part, stat_rows, st, fusable ? &fa : nullptr, &done);
-  else
-    rc = conv_fwd_t<float>(d, x, w, y, stat_part, stat_rows, st);
-  if (rc) return rc;
-  if (fusable && done) return 0;
-  // not fused here (fp32, the direct stem, 256-row tiles, too many row tiles): the finalize
-  // launch over the same slabs
-  const long blocks = (M + stat_rows - 1) / stat_rows;
-  return mmdx_bn_finalize(stat_part, (int)blocks, stat_rows, M, g.K, fin->gamma, fin->beta,
-                          fin->running_mean, fin->running_var, fin->momentum, fin->eps,
-                          fin->save_mean, fin->save_rstd, fin->scale, fin->shift, stream);
 }
 
 extern "C" int mmdx_conv_fwd(int dtype, const mmdx_conv_desc* d, const void* x,

@@ -17,14 +17,7 @@ struct SplitPlan { int bm, bn, splits, kper; };
 // reads back, so the target trades slab traffic against idle CUs: C5 (paired, two boxes)
 // 128 / 192 / 256 / 512 / 1024 -> 2379 / 2539 / 2587-2656 / 2609 / 2529 samples/s, C4
 // neutral (tools/lab_splitk{,2}.sh, profiles/r04_splitk_sweep.txt).
-static long splitk_target() {
-  static const long v = [] {
-    const char* e = getenv("MMDX_SPLITK_TARGET");
-    const long t = e ? atol(e) : 0L;
-    return t >= 64 ? t : 256L;
-  }();
-  return v;
-}
+static long splitk_target() { return knobs().splitk_target; }
 
 // Tile + split-K choice; shared by the workspace query and the launch so both agree.
 static SplitPlan plan_dense(int dtype, int M, int N, int K) {
@@ -97,57 +90,30 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __rest
   }
 }
 
-// 8-wave 256 x 128 tiles (one block per CU, three 48 KB stages) for the unsplit 128 x 128
-// problems with at least this many 256-row tiles (read per launch for A/B runs).  Off by
-// default: on every C5 Linear shape and at 4096^3 they ran 2-20 % slower than two 4-wave
-// 128 x 128 blocks per CU (tools/gemm_bench.py, profiles/r03_gemm8_ab.txt)
-static long gemm8_min_tiles() {
-  const char* e = getenv("MMDX_GEMM8_MIN");
-  return e ? atol(e) : 0L;
-}
+// Retired (round 6, tools/lab/RETIRED.md): 8-wave 256 x 128 tiles (MMDX_GEMM8_MIN: 2-20 %
+// slower on every C5 Linear shape, profiles/r03_gemm8_ab.txt), 256 x 256 tiles for the backward
+// orientations (MMDX_GEMM256_MIN) and 32-deep K stages for them (MMDX_GEMM256_NS).
 
 // 8-wave 256 x 256 tiles (waves 2 x 4 of 128 x 64, two 64 KB stages, one block per CU: a
 // quarter of the LDS-DMA and half the fragment reads per MFMA of the 64 x 64-per-wave tiles)
-// for unsplit problems with at least this many 256 x 256 tiles; 0 disables
-static long gemm256_min_tiles() {
-  const char* e = getenv("MMDX_GEMM256_MIN");
-  return e ? atol(e) : 0L;
-}
-
-// The same threshold for the forward orientation only (both operands k-major: x W^T), where
-// the isolated C5 table has the 256 x 256 tiles 3-8 % ahead on the ViT-B shapes while the
+// for the forward orientation only (both operands k-major: x W^T), where the isolated C5 table has the 256 x 256 tiles 3-8 % ahead on the ViT-B shapes while the
 // backward orientations and the BERT-base shapes lose (profiles/r03n_gemm_bench_f16.txt).
 // Default 90 tiles: every C5 encoder forward GEMM (ViT-B QKV / FFN-up 450 / 600 tiles, ViT-B
 // N = 768 150, BERT-base QKV / FFN-up 288 / 384, BERT-base N = 768 96).  Round 3 set 400 (the
 // ViT-B QKV / FFN-up only; profiles/r03u_c5_ab_gemm256fwd.txt); on the round-4 kernels (vector
 // epilogue, residual input) 400 / 300 / 200 / 140 / 90 / 60 / 30 / 1 gave C5 2772 / 2781 / 2797
 // / 2831 / 2863-2876 / 2877 / 2877 / 2871 samples/s, C4 neutral
-// (profiles/r04_gemm256_fwd_sweep.txt); 0 disables.  Read per launch like the other tile
-// knobs, so a test can pin the 4-wave 128 x 128 kernel as its baseline.
-static long gemm256_fwd_min_tiles() {
-  const char* e = getenv("MMDX_GEMM256_FWD_MIN");
-  return e ? atol(e) : 90L;
-}
-
-// The 256 x 256 tiles with 32-deep K tiles in NS = 3 / 4 stages (MMDX_GEMM256_NS; 0 = the
-// 64-deep two-stage kernel): 32 KB stages, NS - 1 tiles in flight behind a counted vmcnt
-// instead of a vmcnt(0) drain per K tile (A/B knob)
-static int gemm256_stages() {
-  const char* e = getenv("MMDX_GEMM256_NS");
-  const int ns = e ? atoi(e) : 0;
-  return ns == 3 || ns == 4 ? ns : 0;
-}
+// (profiles/r04_gemm256_fwd_sweep.txt); 0 disables (knobs(): a test pins the 128 x 128 kernel
+// as its baseline).
+static long gemm256_fwd_min_tiles() { return knobs().gemm256_fwd_min; }
 
 // The 128 x 128 tiles as 8 waves of 64 x 32 (two 512-thread blocks per CU) instead of 4 waves
 // of 64 x 64, as conv.hip's k-major conv tiles.  Default on: C5 2870 / 2865 -> 2910 / 2896
 // samples/s paired; isolated C5 dgrad / wgrad shapes 1-8 % faster, the forward ones (mostly
 // 256 x 256 tiles) equal; the one loss in tools/gemm_bench.py is the 4096^3 weight gradient
 // (156 -> 216 us), which no config runs (r05 s24).  MMDX_GEMM_8W128=0 restores the 4-wave
-// tiles; read per launch.
-static bool gemm_8w128_on() {
-  const char* e = getenv("MMDX_GEMM_8W128");
-  return !(e && atoi(e) == 0);
-}
+// tiles.
+static bool gemm_8w128_on() { return knobs().gemm_8w128; }
 
 template <typename T, int BM, int BN, bool AK, bool BKm, class Epi>
 static int launch_dense(const void* A, long lda, const void* B, long ldb, const Epi& epi,
@@ -171,46 +137,14 @@ static int launch_dense(const void* A, long lda, const void* B, long ldb, const 
     const bool oka = va && (AK ? K % 8 == 0 : M % 8 == 0) && abytes < (1L << 31);
     const bool okb = vb && (BKm ? K % 8 == 0 : N % 8 == 0) && bbytes < (1L << 31);
     if (oka && okb) {
-      if constexpr (BM == 128 && BN == 128 && !HasBiasSum<Epi>::value) {
+      if constexpr (BM == 128 && BN == 128 && AK && BKm && !HasBiasSum<Epi>::value) {
         const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-        long lim256 = gemm256_min_tiles();
-        if (AK && BKm && lim256 == 0) lim256 = gemm256_fwd_min_tiles();
+        const long lim256 = gemm256_fwd_min_tiles();
         if (splits == 1 && lim256 > 0 && t256 >= lim256 && K >= 128) {
-          if (const int ns = gemm256_stages()) {
-            typedef typename std::conditional<AK, DmaK<256, SA, 32, 8>,
-                                              DmaR<256, SA, 32, 8>>::type OA32;
-            typedef typename std::conditional<BKm, DmaK<256, SB, 32, 8>,
-                                              DmaR<256, SB, 32, 8>>::type OB32;
-            if (ns == 3)
-              hipLaunchKernelGGL((igemm_dma_kernel<256, 256, OA32, OB32, Epi, 3, T, 512, 2, 4>),
-                                 dim3((unsigned)t256, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N,
-                                 K, kper);
-            else
-              hipLaunchKernelGGL((igemm_dma_kernel<256, 256, OA32, OB32, Epi, 4, T, 512, 2, 4>),
-                                 dim3((unsigned)t256, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N,
-                                 K, kper);
-            MMDX_LAUNCH_CHECK();
-            return 0;
-          }
-          typedef typename std::conditional<AK, DmaK<256, SA, 64, 8>, DmaR<256, SA, 64, 8>>::type
-              OA8;
-          typedef typename std::conditional<BKm, DmaK<256, SB, 64, 8>,
-                                            DmaR<256, SB, 64, 8>>::type OB8;
+          typedef DmaK<256, SA, 64, 8> OA8;
+          typedef DmaK<256, SB, 64, 8> OB8;
           hipLaunchKernelGGL((igemm_dma_kernel<256, 256, OA8, OB8, Epi, 2, T, 512, 2, 4>),
                              dim3((unsigned)t256, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K,
-                             kper);
-          MMDX_LAUNCH_CHECK();
-          return 0;
-        }
-        const long t8 = (long)((M + 255) / 256) * ((N + 127) / 128);
-        const long lim = gemm8_min_tiles();
-        if (splits == 1 && lim > 0 && t8 >= lim && K >= 128) {
-          typedef typename std::conditional<AK, DmaK<256, SA, 64, 8>, DmaR<256, SA, 64, 8>>::type
-              OA8;
-          typedef typename std::conditional<BKm, DmaK<128, SB, 64, 8>,
-                                            DmaR<128, SB, 64, 8>>::type OB8;
-          hipLaunchKernelGGL((igemm_dma_kernel<256, 128, OA8, OB8, Epi, 3, T, 512, 4, 2>),
-                             dim3((unsigned)t8, 1, 1), dim3(512), 0, st, sa, sb, epi, M, N, K,
                              kper);
           MMDX_LAUNCH_CHECK();
           return 0;
@@ -291,10 +225,7 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
   int rc = dispatch_major<T>(p, A, lda, ak, B, ldb, bk, part, M, N, K, st);
   if (rc) return rc;
   const long total = (long)M * N;
-  static const bool vec_reduce = [] {   // MMDX_SPLITK_VEC=0: the scalar reduce (A/B knob)
-    const char* e = getenv("MMDX_SPLITK_VEC");
-    return !(e && atoi(e) == 0);
-  }();
+  const bool vec_reduce = knobs().splitk_vec;   // MMDX_SPLITK_VEC=0: the scalar reduce (A/B)
   if (vec_reduce && N % 4 == 0 && total < (1L << 31) && ((uintptr_t)ws & 15) == 0) {
     const int blocks = (int)std::min<long>((total / 4 + 255) / 256, 8192);
     hipLaunchKernelGGL(splitk_reduce4_kernel<OutT>, dim3(blocks), dim3(256), 0, st,
@@ -313,13 +244,8 @@ static int gemm_typed(int M, int N, int K, const void* A, long lda, int ak, cons
 // reduced over the splits by the split-K reduce launch; bias partials follow the fp32 slabs
 // in the workspace.
 
-static bool wgrad_bias_fused_on() {   // MMDX_WGRAD_BIAS_FUSED=0: GEMM + column-sum kernels
-  static const bool on = [] {
-    const char* e = getenv("MMDX_WGRAD_BIAS_FUSED");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
+// MMDX_WGRAD_BIAS_FUSED=0: GEMM + column-sum kernels
+static bool wgrad_bias_fused_on() { return knobs().wgrad_bias_fused; }
 
 template <typename T, typename OutT>
 static int gemm_wgrad_bias_typed(const SplitPlan& p, int M, int N, int K, const void* A, long lda,

@@ -316,12 +316,6 @@ struct Im2colK {
     toff = ((r * g.W + s) * g.C + c0) * (int)sizeof(T);
     tap = r * g.S + s;
   }
-  // halo band (DmaHalo; stride 1, P = H, Q = W): the input pixel of row m at tap (r, s) is
-  // m - ph*W - pw + r*W + s, so a tile's band starts at row0 + hstart() and tap (r, s) reads
-  // band pixel (m - row0) + hshift(r, s)
-  __device__ int hstart() const { return -g.ph * g.W - g.pw; }
-  __device__ int hshift(int r, int s) const { return r * g.W + s; }
-  __device__ int hS() const { return g.S; }
 };
 
 // conv dgrad A operand: rows = input pixels (n,h,w), k = (r, s, kout) with kout contiguous.
@@ -418,11 +412,6 @@ struct DgradK {
     toff = (kb - (r * g.Q + s) * g.K) * (int)sizeof(T);
     tap = r * g.S + s;
   }
-  // halo band (DmaHalo; stride 1, H = P, W = Q): the dY pixel of row m at tap (r, s) is
-  // m + ph*Q + pw - r*Q - s; the band starts at the lowest of them (tap (R-1, S-1))
-  __device__ int hstart() const { return g.ph * g.Q + g.pw - (g.R - 1) * g.Q - (g.S - 1); }
-  __device__ int hshift(int r, int s) const { return (g.R - 1 - r) * g.Q + (g.S - 1 - s); }
-  __device__ int hS() const { return g.S; }
 };
 
 // Strided-conv dgrad, one output phase (a, b) = (h mod sh, w mod sw) at a time: only the
@@ -914,152 +903,6 @@ __device__ __forceinline__ void bn_stat_store(const BnStat& b, float* sg, float*
   }
 }
 
-// Train-mode BatchNorm finalize fused into the producing conv (TP:223 / TP:206: batch
-// statistics, running-stat update, the apply pass's per-channel scale / shift), replacing the
-// separate bn_finalize launch between the conv and its BN apply on the critical stream.
-// Every block writes its per-128-row (mean, M2) slab as before, write-through (sc1: 8-B
-// agent-scope atomic stores), drains, and takes a ticket on its column tile's group counter;
-// the block that draws the group's last ticket merges the group's `group` slabs into one group
-// slab (also sc1), then takes a ticket on the column tile's counter, and the last group merges
-// the `ngroups` group slabs and finalises the tile's BN columns.  Both merges are the exact
-// two-level decomposition mean = sum n_b mean_b / n, M2 = sum M2_b + n_b (mean_b - mean)^2 in a
-// fixed slab order, so the result does not depend on which block arrives last (deterministic).
-// The last arriver of each counter resets it (the scratch is zeroed once by its owner, and
-// mmdx_conv_fwd_bnfin re-zeroes it only on request).  Hand-off form: cdna_hip_programming.md
-// §6 G16 (sc1 payload + relaxed agent ticket; every load of a slab an sc1 load).
-struct BnFinArgs {
-  unsigned* ctr = nullptr;   // [tiles_n] column counters, then [tiles_n][ngroups] group counters
-  float2* gpart = nullptr;   // [N][ngroups] group (mean, M2)
-  int group = 1, ngroups = 1;
-  const float *gamma = nullptr, *beta = nullptr;
-  float *rmean = nullptr, *rvar = nullptr;
-  float momentum = 0.1f, eps = 1e-5f;
-  float *save_mean = nullptr, *save_rstd = nullptr, *scale = nullptr, *shift = nullptr;
-};
-
-typedef __attribute__((address_space(1))) unsigned long long bnfin_gu64;
-__device__ __forceinline__ void bnfin_store(float2* p, float2 v) {  // 8-B sc1 store
-  __hip_atomic_store((bnfin_gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float2 bnfin_load(const float2* p) {     // 8-B sc1 load
-  return __builtin_bit_cast(float2, __hip_atomic_load((bnfin_gu64*)p, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// the slab-merge of one level: channel c's `cnt` slabs src[c*ld + b0 + i] (i < cnt), slab i
-// holding nrows(b0 + i) rows; TPC threads per channel (256 / BN), slab i on sub-thread i % TPC,
-// at most 32 slabs per thread (the host keeps group and ngroups <= 32 * TPC); partial sums
-// combined through `red` (2 * 256 floats) in a fixed order.  Returns (n, mean, M2) on every
-// thread of the channel.
-constexpr int BNFIN_PER = 32;
-template <int BN, class NRows>
-__device__ __forceinline__ void bnfin_merge(const float2* src, long ld, int b0, int cnt,
-                                            bool cok, NRows nrows, float* red, float& n_out,
-                                            float& mean_out, float& m2_out) {
-  constexpr int TPC = NT / BN;
-  const int col = threadIdx.x % BN, sub = threadIdx.x / BN;
-  float2 v[BNFIN_PER];
-  float nb[BNFIN_PER];
-#pragma unroll
-  for (int i = 0; i < BNFIN_PER; ++i) {
-    const int b = sub + TPC * i;
-    const bool ok = cok && b < cnt;
-    v[i] = ok ? bnfin_load(src + (long)col * ld + b0 + b) : make_float2(0.f, 0.f);
-    nb[i] = ok ? nrows(b0 + b) : 0.f;
-  }
-  float sn = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int i = 0; i < BNFIN_PER; ++i) {
-    sn += nb[i];
-    s1 += nb[i] * v[i].x;
-  }
-  red[threadIdx.x] = sn;
-  red[NT + threadIdx.x] = s1;
-  __syncthreads();
-  float n = 0.f, t1 = 0.f;
-#pragma unroll
-  for (int q = 0; q < TPC; ++q) {
-    n += red[q * BN + col];
-    t1 += red[NT + q * BN + col];
-  }
-  const float mean = n > 0.f ? t1 / n : 0.f;
-  __syncthreads();
-  float s2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < BNFIN_PER; ++i) {
-    const float d = v[i].x - mean;
-    s2 += nb[i] > 0.f ? v[i].y + nb[i] * d * d : 0.f;
-  }
-  red[threadIdx.x] = s2;
-  __syncthreads();
-  float m2 = 0.f;
-#pragma unroll
-  for (int q = 0; q < TPC; ++q) m2 += red[q * BN + col];
-  __syncthreads();
-  n_out = n;
-  mean_out = mean;
-  m2_out = m2;
-}
-
-// The ticketed tail of a conv block whose epilogue wrote its (mean, M2) slab `tm` of column
-// tile `tn` (slabs of 128 rows: BM = 128).  `lds` is free scratch (>= 2 KiB + 16 B).
-template <int BN>
-__device__ void bnfin_tail(const BnFinArgs& f, const float2* part, int M, int N, int tm, int tn,
-                           char* lds) {
-  const int tiles_m = (M + 127) / 128, tiles_n = (N + BN - 1) / BN;
-  const int grp = tm / f.group;
-  const int g0 = grp * f.group, gcnt = min(f.group, tiles_m - g0);
-  unsigned* c1 = f.ctr + tiles_n + (long)tn * f.ngroups + grp;
-  unsigned* c2 = f.ctr + tn;
-  int* flag = (int*)lds;
-  float* red = (float*)(lds + 16);
-  // every wave's slab (and output) stores have landed before the ticket (R1: all storing waves
-  // drain, then the workgroup barrier, then ONE lane's relaxed agent-scope add)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    *flag = __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            (unsigned)(gcnt - 1);
-  __syncthreads();
-  if (!*flag) return;
-  if (threadIdx.x == 0) __hip_atomic_store(c1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the ticket
-  const int col = threadIdx.x % BN;
-  const int c = tn * BN + col;
-  const bool cok = c < N;
-  float n, mean, m2;
-  bnfin_merge<BN>(part + (long)tn * BN * tiles_m, tiles_m, g0, gcnt, cok,
-                  [&](int b) { return (float)min(128, M - b * 128); }, red, n, mean, m2);
-  if (cok && threadIdx.x < BN) bnfin_store(f.gpart + (long)c * f.ngroups + grp, make_float2(mean, m2));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    *flag = __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            (unsigned)(f.ngroups - 1);
-  __syncthreads();
-  if (!*flag) return;
-  if (threadIdx.x == 0) __hip_atomic_store(c2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int G = f.group;
-  bnfin_merge<BN>(f.gpart + (long)tn * BN * f.ngroups, f.ngroups, 0, f.ngroups, cok,
-                  [&](int g) { return (float)min(G * 128, M - g * G * 128); }, red, n, mean, m2);
-  if (!cok || threadIdx.x >= BN) return;
-  // bn_finalize_kernel's expressions (norm.hip): var, rstd, running stats, scale / shift
-  const float var = m2 / (float)M;
-  const float rstd = rsqrtf(var + f.eps);
-  f.save_mean[c] = mean;
-  f.save_rstd[c] = rstd;
-  if (f.rmean) {
-    const float unb = M > 1 ? m2 / (float)(M - 1) : var;
-    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
-    f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unb;
-  }
-  const float gm = f.gamma ? f.gamma[c] : 1.f;
-  f.scale[c] = gm * rstd;
-  f.shift[c] = (f.beta ? f.beta[c] : 0.f) - mean * gm * rstd;
-}
-
 // VEC_EPI: the 16-B-per-8-columns epilogue also for bias / addend / pre-activation / ReLU /
 // GELU (the dense GEMMs of gemm_dense.hip).  The conv instantiations keep the lean form
 // (their epilogues never carry those): the extra branch cost the C4 step 2.3 % when it was
@@ -1074,7 +917,6 @@ struct EpiStore {
   OutT* preact;         // optional copy of the pre-activation value, ld = ldc
   float2* stats;        // optional per-column (mean, M2) of each BM-row tile: [N][tiles_m]
   BnStat bs{};          // optional fused consumer-BN backward statistics (bs.part != null)
-  BnFinArgs fin{};      // optional fused BN finalize of `stats` (fin.ctr != null; BM = 128)
   // optional masked accumulation source (beta must be 0): C = acc + (bit ? acc_src : 0), bit
   // from a 1-bit ReLU mask ([M][N / VEC] bytes, bit e of byte n / VEC = column n) — the
   // gradient a residual unit's identity path adds, without materialising it
@@ -1348,8 +1190,8 @@ struct EpiStore {
         nn = tot;
       }
       if (nn > 0.f || SLABS == 1)
-        bnfin_store(stats + (long)(tn * BN + col) * ((M + SLAB - 1) / SLAB) + tm * SLABS + slab,
-                    make_float2(mu, mm));  // write-through: a fused finalize may read it
+        stats[(long)(tn * BN + col) * ((M + SLAB - 1) / SLAB) + tm * SLABS + slab] =
+            make_float2(mu, mm);
     }
   }
   __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
@@ -1575,11 +1417,6 @@ struct EpiPartialBias : EpiPartial {
 template <class E, class = void> struct HasBiasSum { static constexpr bool value = false; };
 template <class E> struct HasBiasSum<E, decltype((void)E::BIAS_SUM)> {
   static constexpr bool value = E::BIAS_SUM;
-};
-
-template <class E, class = void> struct HasBnFin { static constexpr bool value = false; };
-template <class E> struct HasBnFin<E, decltype((void)std::declval<E>().fin, void())> {
-  static constexpr bool value = true;
 };
 
 template <class E, class = void> struct IsPhased { static constexpr bool value = false; };
@@ -2002,69 +1839,6 @@ struct DmaRq {
   }
 };
 
-// Halo A operand for the same-size stride-1 convs over 64 channels (forward: C = 64; dgrad:
-// K = 64 — ResNet layer1's 3x3 convs).  A row's pixel at tap (r, s) is affine in the row
-// (Im2colK / DgradK hstart, hshift), so the A operand of a ROWS-row tile over all R*S taps is
-// one contiguous band of ROWS + (R-1)*W + S-1 input pixels.  The band is DMA'd into LDS once
-// per block (128-B pixel rows; chunk c of band pixel p at slot c ^ (p & 7), the DmaK
-// swizzle) and every K tile (= one tap, C = BK) reads its fragments at a uniform per-tap
-// shift: at W = 56, ROWS = 256 the block moves 1.45x its rows' bytes through L2 -> LDS
-// instead of 9x.  Taps that leave the image read zeros by the row's tap mask (brow), so the
-// operand values, k order and MFMA sequence equal DmaK's (bit-identical output).  Only the
-// weight operand runs through the per-K-tile stages (INSTR = BYTES = 0 here).
-template <int ROWS, class Src, int NWV, int HPX>
-struct DmaHalo {
-  static constexpr int BK = 64;
-  static constexpr bool RMAJOR = false;
-  static constexpr bool HALO = true;
-  static constexpr int NW = NWV;
-  static constexpr int INSTR = 0;
-  static constexpr int BYTES = 0;
-  static constexpr int HALO_BYTES = HPX * 128;
-  static constexpr int HINSTR = HPX / 8;  // 1-KiB DMA instructions (8 pixels each)
-  static_assert(HPX % 8 == 0 && HPX >= ROWS, "band pixels");
-  typedef Src SrcT;
-  int row0;
-  __device__ void init(const Src&, int r0, int, int, int) { row0 = r0; }
-  __device__ void issue(const Src&, char*, int, int, int) {}
-  // the band: called once, before any K tile's DMA (vmcnt counts the K tiles' DMAs behind it)
-  __device__ void band(const Src& s, char* lds, int lane, int wid) const {
-    const __amdgpu_buffer_rsrc_t rsrc = dma_rsrc(s.bbase(), s.bbytes());
-    const int hb = row0 + s.hstart();  // global pixel of band pixel 0 (may be < 0)
-    const int slot = lane & 7;
-    for (int j = wid; j < HINSTR; j += NW) {
-      const int bp = j * 8 + (lane >> 3);
-      const int gp = hb + bp;
-      const unsigned voff =
-          gp >= 0 ? (unsigned)((gp * 64 + ((slot ^ (bp & 7)) << 3)) * 2) : DMA_OOB;
-      dma16(rsrc, lds + j * 1024, voff);
-    }
-  }
-  // tap masks of this lane's fragment rows (wm * WTM + i * 16 + (lane & 15))
-  template <int WTM, int RM>
-  __device__ void masks(const Src& s, int wm, int lane, unsigned (&mk)[RM]) const {
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      unsigned m;
-      (void)s.brow(row0 + wm * WTM + i * 16 + (lane & 15), m);
-      mk[i] = m;
-    }
-  }
-  __device__ static bf16x8 hfrag(const char* band, int r16, int ks, int lane, int shift,
-                                 bool ok) {
-    const int p = ok ? r16 + (lane & 15) + shift : 0;
-    const int c = (ks >> 3) + (lane >> 4);
-    const bf16x8 v = *(const bf16x8*)(band + p * 128 + ((c ^ (p & 7)) << 4));
-    return ok ? v : bf16x8{};
-  }
-};
-template <class O, class = void> struct IsHalo { static constexpr bool value = false; };
-template <class O> struct IsHalo<O, decltype((void)O::HALO)> {
-  static constexpr bool value = O::HALO;
-};
-template <class O, bool = IsHalo<O>::value> struct HaloBytes { static constexpr int value = 0; };
-template <class O> struct HaloBytes<O, true> { static constexpr int value = O::HALO_BYTES; };
-
 // Stores a staged fp32 tile cst [BM][LDC] (CW columns) at output (m0, n0): 8 consecutive
 // columns per lane -> one 16-B store where the epilogue allows it, else 4-column pieces.
 template <int BM, int CW, int LDC, int NTH, class Epi>
@@ -2098,15 +1872,8 @@ __device__ __forceinline__ void epilogue_pass(const Epi& epi, const float* cst, 
 // NTH = 512 (8 waves, one block per CU, 256 x 128 tiles, WM x WN = 4 x 2 waves of 64 x 64):
 // half the operand bytes per MFMA of two 128 x 128 blocks and twice the K tiles in flight
 // (NS = 3 stages of 48 KB) for the same LDS.
-// FOLD (timing probe, tools/conv_bench.py --fold-probe): after its DMAs of a K tile land,
-// every lane re-reads the A chunks it issued, applies y*s[c]+t[c] and ReLU with per-channel
-// coefficients loaded for the tile's channels, and writes them back before the barrier —
-// the operand-side work a BatchNorm-apply folded into the consumer conv would add
-// (DESIGN.md §8).  The coefficients are probe constants: the results are not meaningful.
-__device__ float g_fold_probe_coef[2 * 2048];
-
 template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16,
-          int NTH = NT, int WM = 2, int WN = 2, int FOLD = 0>
+          int NTH = NT, int WM = 2, int WN = 2>
 __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                            typename OB::SrcT sb, Epi epi, int M,
                                                            int N, int K, int kper) {
@@ -2121,8 +1888,7 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
-  constexpr bool HALO = IsHalo<OA>::value;  // A operand from a per-block LDS band (DmaHalo)
-  constexpr int OP_BYTES = NS * STAGE + HaloBytes<OA>::value;
+  constexpr int OP_BYTES = NS * STAGE;
   constexpr int RED = WM * 3 > (NTH / 64) * 2 ? WM * 3 : (NTH / 64) * 2;  // floats per column
   // the fp32 tile is staged through LDS in NCH column passes: two for 256 x 256 tiles, whose
   // full staging (266 KB) exceeds the CU's 160 KB
@@ -2171,19 +1937,6 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   OB ob;
   oa.init(sa, tm * BM, lane, wid, kbeg);
   ob.init(sb, tn * BN, lane, wid, kbeg);
-  char* const band = lds_raw + NS * STAGE;
-  unsigned hmask[HALO ? RM : 1];
-  if constexpr (HALO) {
-    oa.band(sa, band, lane, wid);  // before tile 0's DMAs: its vmcnt wait covers the band
-    oa.template masks<WTM, RM>(sa, wm, lane, hmask);
-  }
-  // this K tile's tap (one tap per tile: C = BK) and band shift (DmaHalo)
-  // (generic: instantiated only by the DmaHalo kernels)
-  auto htap = [&](const auto& src, int t, int& shift) {
-    const int tap = kbeg / BK + t, S = src.hS(), r = tap / S;
-    shift = src.hshift(r, tap - r * S);
-    return tap;
-  };
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -2225,38 +1978,10 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (FOLD) {
-      static_assert(!OA::RMAJOR, "fold probe: k-major A operand");
-      char* st = lds_raw + (t % NS) * STAGE;
-      const int c0 = (kbeg + t * BK + oa.coff) & 2047;
-      float sc[8], sh[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sc[e] = g_fold_probe_coef[c0 + e];
-        sh[e] = g_fold_probe_coef[2048 + ((c0 + e) & 2047)];
-      }
-#pragma unroll
-      for (int j = 0; j < OA::INSTR; ++j) {
-        bf16x8* pch = (bf16x8*)(st + (j * OA::NW + wid) * 1024 + lane * 16);
-        bf16x8 v = *pch;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = from_f<bf16>(fmaxf(to_f(v[e]) * sc[e] + sh[e], 0.f));
-        *pch = v;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
     __builtin_amdgcn_s_barrier();
     const char* as = lds_raw + (t % NS) * STAGE;
     const char* bs = as + OA::BYTES;
-    int hsh = 0, htp = 0;
-    if constexpr (HALO) htp = htap(sa, t, hsh);
-    // A fragment i at k step ks: the K tile's stage, or the band at this tap's shift
-    auto afrag = [&](int i, int ks) {
-      if constexpr (HALO)
-        return OA::hfrag(band, wm * WTM + i * 16, ks, lane, hsh, (hmask[i] >> htp) & 1u);
-      else
-        return OA::frag(as, wm * WTM + i * 16, ks, lane);
-    };
+    auto afrag = [&](int i, int ks) { return OA::frag(as, wm * WTM + i * 16, ks, lane); };
     if constexpr (FRAG_FIRST) {
       // every fragment of the tile is requested before the next tile's DMAs are issued, so
       // the LDS read latency runs under the DMA issue instead of in front of the MFMAs
@@ -2426,12 +2151,6 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     return;
   }
   epilogue_pass<BM, CH, LDC, NTH>(epi, cst, tm * BM, tn * BN);
-  if constexpr (HasBnFin<Epi>::value && BM == 128 && NTH == NT) {
-    if (epi.fin.ctr != nullptr && epi.stats != nullptr) {
-      __syncthreads();  // the staging tile's readers are done with the LDS
-      bnfin_tail<BN>(epi.fin, epi.stats, M, N, tm, tn, lds_raw);
-    }
-  }
 }
 
 // Loader bundles (give the kernel template one type per operand).

@@ -534,211 +534,8 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_coop_kernel(
 #undef COOP_STAMP
 }
 
-// Cooperative forward, register variant (opt-in, MMDX_LSTM_FWD_COOP4=1): 4 waves per workgroup
-// (2 unit groups x 2 row groups, one wave per SIMD), each holding its 16 units' W_hh
-// fragments (4 gates x 8 k-steps = 128 VGPRs) in REGISTERS for all L steps.  The 8-wave LDS
-// variant read its 64 KB W_hh image once per row group per step (256 KB + 128 KB of h
-// fragments = 384 KB of LDS reads, ~1.3 us of a 7.4 us step); here only the h fragments go
-// through LDS (128 KB).  Roles after the gates: wave 0 publishes the h slice (16-B sc1
-// stores, drain, counter add) and polls the next step's counter with nothing else in its
-// memory queue; waves 1-3 write the step's gates, c and h for the backward from their LDS
-// staging as coalesced 16-B chunks and load their next-step operands meanwhile.  xg is
-// unit-interleaved ([.][2][H][4], bilstm.py permutes W_ih's rows): one 16-B load per
-// (row, unit).
-template <int RT>
-__global__ __launch_bounds__(256, 1) void lstm_fwd_coop4_kernel(
-    const float* __restrict__ xg, const bf16* __restrict__ whh, int B, int L,
-    bf16* __restrict__ hout, float* __restrict__ csave, float* __restrict__ gsave,
-    bf16* __restrict__ hx, unsigned* __restrict__ ctr, int* __restrict__ status, long spin_max,
-    int debug, unsigned long long* __restrict__ tst) {
-  constexpr int H = COOP_H, G4 = 4 * H, KS = H / 32;
-  constexpr int NROWS = 32 * RT;          // RT = 16-row tiles per wave: 2 (B <= 64) or 4
-  static_assert(RT == 2 || RT == 4, "row tiles per wave");
-  // h_{t-1} [NROWS][COOP_LDH] (MFMA A operand); the step's h slice [NROWS][32] (published,
-  // then saved); gates [NROWS][32] x f32x4 and c [NROWS][32] staged for the saves
-  __shared__ __attribute__((aligned(16))) bf16 sh[NROWS * COOP_LDH];
-  __shared__ __attribute__((aligned(16))) bf16 sout[NROWS * COOP_UB];
-  __shared__ f32x4 sgt[NROWS * COOP_UB];
-  __shared__ __attribute__((aligned(16))) float sct[NROWS * COOP_UB];
-  __shared__ int sgiveup;
-  __builtin_amdgcn_s_setprio(3);
-  const int dir = blockIdx.y, blk = blockIdx.x;
-  const int rb0 = blockIdx.z * NROWS;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int ug = wid & 1, rg = wid >> 1;
-  const int ul = ug * 16 + (lane & 15);        // this lane's unit within the workgroup's 32
-  const int ucol = blk * COOP_UB + ul;         // ... and within H
-  bf16x8 wf[4][KS];
-  {
-    const bf16* W = whh + (long)dir * G4 * H;
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        wf[g][ks] = *(const bf16x8*)(W + (long)(g * H + ucol) * H + ks * 32 + 8 * (lane >> 4));
-  }
-  float creg[RT][4];
-#pragma unroll
-  for (int i = 0; i < RT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) creg[i][r] = 0.f;
-  unsigned* myctr = ctr + dir * gridDim.z + blockIdx.z;
-  bf16* hxd = hx + (long)dir * 2 * B * H;
-  const __amdgpu_buffer_rsrc_t hrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)hxd, (short)0, 2 * B * H * 2, 0x00020000);
-  const int nrow = min(NROWS, B - rb0);
-  unsigned long long* tsw =
-      tst ? tst + ((long)(blockIdx.z * 2 + dir) * COOP_NB + blk) * L * COOP_TS_PHASES : nullptr;
-#define COOP_STAMP(k)                                                                       \
-  do {                                                                                      \
-    if (tsw && threadIdx.x == 0) tsw[s * COOP_TS_PHASES + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-  auto load_xv = [&](f32x4 (&x)[RT][4], int tt) {
-#pragma unroll
-    for (int i = 0; i < RT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = rb0 + (rg + 2 * i) * 16 + (lane >> 4) * 4 + r;
-        x[i][r] = *(const f32x4*)(xg + ((((long)min(b, B - 1) * L + tt) * 2 + dir) * H + ucol) * 4);
-      }
-  };
-  // step tt's staged outputs -> global (coalesced 16-B chunks), by waves 1-3
-  auto save = [&](int tt) {
-    const int tid = threadIdx.x - 64;
-    for (int e = tid; e < nrow * COOP_UB; e += 192) {
-      const int row = e / COOP_UB, u = e - row * COOP_UB;
-      const long sidx = ((long)dir * L + tt) * B + rb0 + row;
-      *(f32x4*)(gsave + (sidx * H + blk * COOP_UB + u) * 4) = sgt[e];
-    }
-    for (int e = tid; e < nrow * (COOP_UB / 4); e += 192) {
-      const int row = e / (COOP_UB / 4), q = e - row * (COOP_UB / 4);
-      const long sidx = ((long)dir * L + tt) * B + rb0 + row;
-      *(f32x4*)(csave + sidx * H + blk * COOP_UB + q * 4) = *(const f32x4*)(sct + row * COOP_UB + q * 4);
-    }
-    for (int e = tid; e < nrow * (COOP_UB / 8); e += 192) {
-      const int row = e / (COOP_UB / 8), q = e - row * (COOP_UB / 8);
-      *(coop_v4u*)(hout + ((long)(rb0 + row) * L + tt) * 2 * H + dir * H + blk * COOP_UB + q * 8) =
-          *(const coop_v4u*)(sout + row * COOP_UB + q * 8);
-    }
-  };
-  f32x4 xv[RT][4];
-  load_xv(xv, dir == 0 ? 0 : L - 1);
-  for (int s = 0; s < L; ++s) {
-    const int t = dir == 0 ? s : L - 1 - s;
-    COOP_STAMP(0);
-    if (s > 0) {
-      if (threadIdx.x == 0) {
-        const unsigned target = (unsigned)(COOP_NB * s);
-        long spins = 0;
-        int giveup = 0;
-        while (__hip_atomic_load(myctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-          __builtin_amdgcn_s_sleep(1);
-          ++spins;
-          if (spins > spin_max) {
-            __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            giveup = 1;
-            break;
-          }
-          if ((spins & 255) == 0 &&
-              __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-            giveup = 1;
-            break;
-          }
-        }
-        sgiveup = giveup;
-      }
-      __syncthreads();
-      if (sgiveup) return;
-    }
-    COOP_STAMP(1);
-    // h_{t-1} -> LDS (sc1 loads, all chunks requested before any LDS write)
-    constexpr int HCH = NROWS * (H / 8) / 256;     // 16-B chunks per thread
-    constexpr int HB = HCH < 8 ? HCH : 8;
-    const int hrow = threadIdx.x >> 5;
-    bf16* hdst = sh + hrow * COOP_LDH + (threadIdx.x & 31) * 8;
-    if (s > 0) {
-      const unsigned hsrc = (unsigned)(((s + 1) & 1) * B * H * 2 +
-                                       ((rb0 + hrow) * H + (threadIdx.x & 31) * 8) * 2);
-#pragma unroll
-      for (int i0 = 0; i0 < HCH; i0 += HB) {
-        coop_v4u v[HB];
-#pragma unroll
-        for (int i = 0; i < HB; ++i)
-          v[i] = __builtin_amdgcn_raw_buffer_load_b128(
-              hrs, rb0 + hrow + 8 * (i0 + i) < B ? hsrc + (i0 + i) * 8 * H * 2 : DMA_OOB, 0,
-              COOP_SC1);
-#pragma unroll
-        for (int i = 0; i < HB; ++i) *(coop_v4u*)(hdst + (i0 + i) * 8 * COOP_LDH) = v[i];
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < HCH; ++i) *(coop_v4u*)(hdst + i * 8 * COOP_LDH) = coop_v4u{0u, 0u, 0u, 0u};
-    }
-    // wave 0's next-step operands (waves 1-3 loaded theirs after the previous step's gates)
-    f32x4 xn[RT][4];
-    if (wid == 0 && s + 1 < L) load_xv(xn, dir == 0 ? s + 1 : L - 2 - s);
-    __syncthreads();
-    COOP_STAMP(2);
-    f32x4 accs[RT][4];
-#pragma unroll
-    for (int i = 0; i < RT; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) accs[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-      for (int i = 0; i < RT; ++i) {
-        const bf16x8 af = *(const bf16x8*)(sh + ((rg + 2 * i) * 16 + (lane & 15)) * COOP_LDH +
-                                           8 * (lane >> 4) + ks * 32);
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          accs[i][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[g][ks], accs[i][g], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      const int rt16 = (rg + 2 * i) * 16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gi = sigm_fast(accs[i][0][r] + xv[i][r][0]);
-        const float gf = sigm_fast(accs[i][1][r] + xv[i][r][1]);
-        const float gg = tanh_fast(accs[i][2][r] + xv[i][r][2]);
-        const float go = sigm_fast(accs[i][3][r] + xv[i][r][3]);
-        const float c = gf * creg[i][r] + gi * gg;
-        creg[i][r] = c;
-        const int row = rt16 + (lane >> 4) * 4 + r;
-        sout[row * COOP_UB + ul] = from_f<bf16>(go * tanh_fast(c));
-        sgt[row * COOP_UB + ul] = f32x4{gi, gf, gg, go};
-        sct[row * COOP_UB + ul] = c;
-      }
-    }
-    __syncthreads();
-    COOP_STAMP(3);
-    if (wid == 0) {
-      if (s + 1 < L) {   // publish h_t: 16-B sc1 stores, drain, one agent counter add
-        const int par_out = (s & 1) * B * H * 2;
-        for (int e = lane; e < nrow * (COOP_UB / 8); e += 64) {
-          const int row = e / (COOP_UB / 8), c8 = e - row * (COOP_UB / 8);
-          const coop_v4u v = *(const coop_v4u*)(sout + row * COOP_UB + c8 * 8);
-          __builtin_amdgcn_raw_buffer_store_b128(
-              v, hrs, par_out + ((rb0 + row) * H + blk * COOP_UB + c8 * 8) * 2, 0, COOP_SC1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0 && !((debug & COOP_DEBUG_DROP_PEER) && blk == 0 && dir == 0))
-          __hip_atomic_fetch_add(myctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      save(t);
-      if (s + 1 < L) load_xv(xn, dir == 0 ? s + 1 : L - 2 - s);
-    }
-    COOP_STAMP(4);
-#pragma unroll
-    for (int i = 0; i < RT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xv[i][r] = xn[i][r];
-  }
-#undef COOP_STAMP
-}
+// (The 4-wave register-W_hh variant of this forward, MMDX_LSTM_FWD_COOP4, was retired in
+// round 6: 1.10 vs 0.81 ms per launch isolated, tools/lab/RETIRED.md.)
 
 // W_hh [2][4H][H] -> the backward's B-operand fragments, [2][H/16][4H/KS][64 lanes][FRAG]:
 // lane l of k-step ks of column tile c holds W_hh[ks*KS + (l>>4)*FRAG + e][16c + (l&15)],
@@ -1037,13 +834,6 @@ static bool coop_resident(K kernel, int threads, int groups) {
   return v > 0 && v >= 2 * COOP_NB * groups;
 }
 
-// MMDX_LSTM_FWD_COOP4=1: the 4-wave register-W_hh forward (opt-in, read per launch).  Measured
-// against the 8-wave LDS variant at C4's shape: 1.10 vs 0.81 ms per launch isolated — its one
-// wave per SIMD leaves the LDS reads and the cell update unhidden (r05_lstm_probe.txt).
-static bool fwd_coop4_on() {
-  const char* e = getenv("MMDX_LSTM_FWD_COOP4");
-  return e && atoi(e) != 0;
-}
 
 extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B, int L, int H,
                              void* h_out, float* c_save, float* gates_save, void* ws,
@@ -1077,17 +867,10 @@ extern "C" int mmdx_lstm_fwd(int dtype, const void* xg, const void* w_hh, int B,
                        (const bf16*)w_hh, B, L, (bf16*)h_out, c_save, gates_save, hx, ctr,   \
                        status, spin_max, debug_flags, tst);                                  \
   } while (0)
-    if (fwd_coop4_on()) {
-      if (B <= 64)
-        COOP_LAUNCH(lstm_fwd_coop4_kernel, 2, 256);
-      else
-        COOP_LAUNCH(lstm_fwd_coop4_kernel, 4, 256);
-    } else {
-      if (B <= 64)
-        COOP_LAUNCH(lstm_fwd_coop_kernel, 1, 512);
-      else
-        COOP_LAUNCH(lstm_fwd_coop_kernel, 2, 512);
-    }
+    if (B <= 64)
+      COOP_LAUNCH(lstm_fwd_coop_kernel, 1, 512);
+    else
+      COOP_LAUNCH(lstm_fwd_coop_kernel, 2, 512);
 #undef COOP_LAUNCH
     MMDX_LAUNCH_CHECK();
     return 0;
@@ -1172,8 +955,7 @@ extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, con
     // lab probe (tools/lab/lstm_probe.py): MMDX_LSTM_BWD_PROBE=1 stamps the phases into the
     // [groups][2][CB_NU][L][8] u64 that follow the workspace (the caller passes them)
     unsigned long long* tst = nullptr;
-    const char* pe = getenv("MMDX_LSTM_BWD_PROBE");
-    if (pe && atoi(pe) != 0) {
+    if (knobs().lstm_bwd_probe) {
       const size_t tb2 = (size_t)groups * 2 * CB_NU * L * COOP_TS_PHASES * 8;
       MMDX_CHECK_ARG(ws_bytes >= mmdx_lstm_workspace_size(dtype, B, L, H) + tb2,
                      "lstm bwd: the timing probe needs %zu more workspace bytes", tb2);

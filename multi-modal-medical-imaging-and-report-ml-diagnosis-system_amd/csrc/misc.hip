@@ -549,10 +549,7 @@ extern "C" int mmdx_gelu_bwd(int dtype, const void* pre, const void* dy, long n,
 // column-sum passes below (2624 / 2624 vs 2647 / 2655 samples/s, paired) — its ~200 blocks
 // of mostly idle 64 x 128 MFMA tiles hold CUs the other tower's kernels want.
 static bool bias_grad_gemm_ok(int dtype, long M, int N) {
-  static const bool on = [] {
-    const char* e = getenv("MMDX_BIAS_GRAD_GEMM");
-    return e && atoi(e) == 1;
-  }();
+  const bool on = knobs().bias_grad_gemm;
   return on && dtype != F32 && M % 8 == 0 && N % 8 == 0 && M < (1L << 30);
 }
 static size_t bias_grad_ones_bytes(long M) { return ((size_t)M * 2 + 255) & ~(size_t)255; }

@@ -653,13 +653,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
 // and no prefetch).  The workspace is sized for the smallest rpw (the most partials).
 constexpr int LN_RPW_MIN = 4;
 constexpr int LN_BWD_ROWS = 4 * LN_RPW_MIN;   // rows per block at LN_RPW_MIN
-static int ln_bwd_rpw() {   // MMDX_LN_BWD_RPW = 4 | 8 (default 8)
-  static const int r = [] {
-    const char* e = getenv("MMDX_LN_BWD_RPW");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  return r;
-}
+static int ln_bwd_rpw() { return knobs().ln_bwd_rpw; }   // MMDX_LN_BWD_RPW = 4 | 8 (8)
 
 // dx per row; per-block partial dgamma/dbeta -> part[blk][2][D]
 // MV: 16-B vectors per lane (ceil(D / VEC / 64)), a template argument so the register arrays

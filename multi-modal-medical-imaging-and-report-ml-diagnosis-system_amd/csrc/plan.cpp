@@ -246,23 +246,6 @@ int run_one(const mmdx_plan_op& o, void* const* ext, void* const* events, void* 
     case MMDX_OP_AXPBY:  // l: n; f: a, b; p: x, y, out
       return mmdx_axpby(o.l[0], o.f[0], (const float*)P(o, 0, ext), o.f[1],
                         (const float*)P(o, 1, ext), (float*)P(o, 2, ext), s);
-    case MMDX_OP_CONV_FWD_BNFIN: {
-      mmdx_bn_fin fin;
-      fin.gamma = (const float*)P(o, 4, ext);
-      fin.beta = (const float*)P(o, 5, ext);
-      fin.running_mean = (float*)P(o, 6, ext);
-      fin.running_var = (float*)P(o, 7, ext);
-      fin.momentum = o.f[0];
-      fin.eps = o.f[1];
-      fin.save_mean = (float*)P(o, 8, ext);
-      fin.save_rstd = (float*)P(o, 9, ext);
-      fin.scale = (float*)P(o, 10, ext);
-      fin.shift = (float*)P(o, 11, ext);
-      fin.scratch = (void*)o.l[0];
-      fin.scratch_bytes = (size_t)o.l[1];
-      return mmdx_conv_fwd_bnfin(o.dtype, &o.d, P(o, 0, ext), P(o, 1, ext), P(o, 2, ext),
-                                 (float*)P(o, 3, ext), o.i[0], &fin, s);
-    }
     case MMDX_OP_BN_APPLY:
       return mmdx_bn_apply(o.dtype, P(o, 0, ext), P(o, 1, ext), o.l[0], o.i[0],
                            (const float*)P(o, 2, ext), (const float*)P(o, 3, ext), o.i[1],

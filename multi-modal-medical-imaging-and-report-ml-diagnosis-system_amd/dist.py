@@ -16,6 +16,7 @@ from __future__ import annotations
 import os
 import sys
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -82,6 +83,11 @@ class GradAllReducer:
         # flat buffer (keyed by its storage) -> [(lo, hi)] already launched by launch_region
         self._regions = {}
         self._comm = None
+        # id(param) -> (weakref to the bucket view finish() rebound as its .grad, bucket kind):
+        # a gradient that is still that view next step (accumulated, zero_grad(set_to_none=
+        # False)) stays on the packed-bucket path of its kind, although the views together
+        # tile one whole storage like an arena would
+        self._rebound = {}
 
     def trunk_hook(self, grads, regions):
         """resnet.TRUNK_GRAD_HOOK: start the all-reduce of each layer's slice of the trunk's
@@ -158,10 +164,15 @@ class GradAllReducer:
     def _launch(self, params):
         ps = self.params if params is None else [p for p in params if p.requires_grad]
         pairs = []
+        loose = {"t": [], "a": []}   # per-tensor gradients / small whole arenas
         for p in ps:
             if id(p) in self._launched or p.grad is None:
                 continue
             self._launched.add(id(p))
+            r = self._rebound.get(id(p))
+            if r is not None and r[0]() is p.grad:
+                loose[r[1]].append((p, p.grad))
+                continue
             pairs.append((p, p.grad))
         # Gradients that together tile one whole flat buffer (the ResNet trunk's gradient
         # arena, the encoder stacks') are reduced in place on that buffer, minus what
@@ -170,10 +181,11 @@ class GradAllReducer:
         # does not survive.  Small flat buffers (the BiLSTM's per-layer weight and bias
         # pairs, a few MB each) join the packed bucket instead: one collective per ~64 MB,
         # not one per buffer (each costs ~20 us of host issue at the end of the backward).
+        # Small arenas keep fp32 in their bucket whatever bucket_dtype says: they were whole
+        # fp32 buffers reduced in place before they joined the packed path.
         by_store = {}
         for p, g in pairs:
             by_store.setdefault(_store_key(g), []).append((p, g))
-        loose = []
         for key, pgs in by_store.items():
             gs = [g for _, g in pgs]
             # a buffer that launch_region already started is the trunk's arena even when
@@ -181,20 +193,27 @@ class GradAllReducer:
             # rest must not also travel through the packed buckets
             started = key in self._regions
             flat = _whole_buffer(gs, allow_gaps=started)
-            if flat is None or (not started and
-                                flat.numel() * flat.element_size() < self.small_arena_bytes):
-                loose += pgs
+            if flat is None:
+                loose["t"] += pgs
+                continue
+            if not started and flat.numel() * flat.element_size() < self.small_arena_bytes:
+                loose["a"] += pgs
                 continue
             for a, z in _complement(self._regions.get(key, []), flat.numel()):
                 part = flat[a:z]   # what launch_region left
                 work = self._all_reduce(part, "arena")
                 self._pending.append((None, part, work, None))
-        for bucket in self._buckets(loose):
-            flat = torch._utils._flatten_dense_tensors([g for _, g in bucket])
-            if self.bucket_dtype is not None and flat.dtype != self.bucket_dtype:
-                flat = flat.to(self.bucket_dtype)
-            work = self._all_reduce(flat, f"bucket[{len(bucket)}]")
-            self._pending.append((bucket, flat, work, None))
+        if self.bucket_dtype is None:   # one dtype: one packed path
+            loose["t"] += loose.pop("a")
+        for kind in loose:
+            for bucket in self._buckets(loose[kind]):
+                flat = torch._utils._flatten_dense_tensors([g for _, g in bucket])
+                if (kind == "t" and self.bucket_dtype is not None
+                        and flat.dtype != self.bucket_dtype):
+                    flat = flat.to(self.bucket_dtype)
+                work = self._all_reduce(flat, f"bucket{'' if kind == 't' else '-arena'}"
+                                              f"[{len(bucket)}]")
+                self._pending.append((bucket, flat, work, None, kind))
 
     def _all_reduce(self, t, kind):
         if _TRACE is not None:
@@ -218,7 +237,7 @@ class GradAllReducer:
     def _finish(self):
         inv = 1.0 / self.world
         cur = None
-        for bucket, flat, work, dest in self._pending:
+        for bucket, flat, work, dest, *kind in self._pending:
             work.wait()
             if flat.is_cuda:
                 # the buffer may have been allocated on another stream (launch() issued from
@@ -240,6 +259,7 @@ class GradAllReducer:
                 views = torch._utils._unflatten_dense_tensors(flat, [g for _, g in bucket])
                 for (p, _), v in zip(bucket, views):
                     p.grad = v
+                    self._rebound[id(p)] = (weakref.ref(v), kind[0])
         self._pending = []
         self._launched = set()
         self._regions = {}

@@ -420,34 +420,16 @@ class _Plan:
             # (one byte per 16-B channel vector) instead of re-reading its output
             rmask = (A.new((rows, K // vec), torch.uint8, dev)
                      if keep and relu and res is not None and out is not None else None)
-            if train and BN_FIN_FUSED:
-                # the conv finalizes its own batch statistics (mmdx_conv_fwd_bnfin: mean, rstd,
-                # running stats, scale / shift from the slabs inside the conv launch); the BN
-                # is then the apply pass alone — no finalize launch between them
-                scale = A.new((K,), torch.float32, dev)
-                shift = A.new((K,), torch.float32, dev)
-                nsc = int(L.lib().mmdx_conv_fwd_bnfin_scratch_size(d))
-                scratch = A.new((nsc,), torch.uint8, dev).zero_()  # ticket counters: zero once
-                fw.timed(cost("fwd"), L.OP_CONV_FWD_BNFIN, stream=st, dtype=dt, i=(rpb,),
-                         l=(scratch.data_ptr(), nsc), f=(bn.momentum, bn.eps),
-                         p=(x, wk, y, part, bn.weight, bn.bias, bn.running_mean,
-                            bn.running_var, mean, rstd, scale, shift), d=d)
-                if join is not None:
-                    fw.add(L.OP_WAIT, p=(join,), stream=st)
-                if out is not None:
-                    fw.add(L.OP_BN_APPLY, dt, i=(K, int(relu)), l=(rows,), stream=st,
-                           p=(y, res, scale, shift, out, rmask))
-            else:
-                fw.timed(cost("fwd"), L.OP_CONV_FWD, stream=st, dtype=dt,
-                         i=(rpb if train else 0,), p=(x, wk, y, part), d=d)
-                wsn = L.lib().mmdx_bn_workspace_size(rows, K)
-                ws_for(wsn, st)
-                if join is not None:
-                    fw.add(L.OP_WAIT, p=(join,), stream=st)
-                fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, rpb, wsn),
-                       f=(bn.momentum, bn.eps), stream=st,
-                       p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean,
-                          rstd, res, out, _WS2 if st else _WS, rmask))
+            fw.timed(cost("fwd"), L.OP_CONV_FWD, stream=st, dtype=dt,
+                     i=(rpb if train else 0,), p=(x, wk, y, part), d=d)
+            wsn = L.lib().mmdx_bn_workspace_size(rows, K)
+            ws_for(wsn, st)
+            if join is not None:
+                fw.add(L.OP_WAIT, p=(join,), stream=st)
+            fw.add(L.OP_BN_FWD, dt, i=(int(train), K, nstat, int(relu)), l=(rows, rpb, wsn),
+                   f=(bn.momentum, bn.eps), stream=st,
+                   p=(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, mean,
+                      rstd, res, out, _WS2 if st else _WS, rmask))
             u = dict(conv=conv, bn=bn, relu=relu, d=d, cm=cm, x=x, y=y, out=out, mean=mean,
                      rstd=rstd, wc=wc, pair=pair is not None, rmask=rmask, res=res, cost=cost)
             units.append(u)
@@ -798,13 +780,6 @@ TRUNK_GRAD_HOOK = None
 # current one) starts when the slice is final, with no stream or event of its own
 # (dist.GradAllReducer.trunk_segment).  Takes precedence over TRUNK_GRAD_HOOK.  None = off.
 TRUNK_SEGMENT_HOOK = None
-
-# Train-mode BN statistics finalized inside the producing conv launch (mmdx_conv_fwd_bnfin) and
-# the BN forward reduced to its apply pass (MMDX_BN_FIN=1; read when a plan is built).  Off by
-# default: the ticket drain at the end of every conv block and the last blocks' serial slab
-# merges added 0.78 ms/step of conv time against the 0.47 ms of finalize launches they remove
-# (C4 8733 / 8725 vs 8818 / 8817 samples/s paired).
-BN_FIN_FUSED = os.environ.get("MMDX_BN_FIN", "0") == "1"
 
 # Downsample branch of the forward on the side stream (False: in order on the main stream;
 # read when a plan is built — for A/B runs, tools/step_probe.py --ds-main).

@@ -316,3 +316,65 @@ def test_stack_segment_allreduce_gloo(monkeypatch):
     for r in range(world):
         for got, a, b in zip(out[r], exp[0], exp[1]):
             assert torch.allclose(got, (a + b) / 2, atol=1e-6)
+
+
+SHAPES3 = ((16,), (5, 5), (60,))
+
+
+def _worker_accum(rank, world, port, out, bf16):
+    """Two reduces with ACCUMULATED gradients (zero_grad(set_to_none=False)): after the first,
+    the packed gradients are views that tile the averaged bucket — a whole storage above
+    small_arena_bytes — yet the second reduce must send them through the same packed bucket
+    in the same dtype, not reduce that storage in place as an arena."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmdx.dist import GradAllReducer
+    arena_p = [torch.nn.Parameter(torch.zeros(s)) for s in ((40, 3), (7,))]
+    tens_p = [torch.nn.Parameter(torch.zeros(s)) for s in SHAPES3]
+    params = arena_p + tens_p
+    g = torch.Generator().manual_seed(600 + rank)
+    flat = torch.randn(127, generator=g)
+    arena_p[0].grad = flat[:120].view(40, 3).detach()
+    arena_p[1].grad = flat[120:].detach()
+    for p in tens_p:
+        p.grad = torch.randn(p.shape, generator=g)
+    red = GradAllReducer(params, world, small_arena_bytes=200,
+                         bucket_dtype=torch.bfloat16 if bf16 else None)
+    calls = []
+    real = red._all_reduce
+    red._all_reduce = lambda t, kind: (calls.append((kind, t.numel(), t.dtype)), real(t, kind))[1]
+    red.reduce()
+    first, calls[:] = list(calls), []
+    for p in params:   # the second micro-step's gradients accumulate into the reduced ones
+        p.grad.add_(torch.randn(p.shape, generator=g))
+    red.reduce()
+    out[rank] = {"calls": (first, list(calls)), "grads": [p.grad.clone() for p in params]}
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_accumulated_grads_keep_bucket_path_gloo(bf16):
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_accum, args=(world, port, out, bf16), nprocs=world, join=True)
+    bdt = torch.bfloat16 if bf16 else torch.float32
+    want_calls = [("arena", 127, torch.float32), ("bucket[3]", 101, bdt)]
+    first, second = out[0]["calls"]
+    assert first == want_calls and second == want_calls, (first, second)
+    draws = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(600 + r)
+        flat = torch.randn(127, generator=g)
+        s1 = [flat[:120].view(40, 3), flat[120:]] + [torch.randn(s, generator=g) for s in SHAPES3]
+        s2 = [torch.randn(t.shape, generator=g) for t in s1]
+        draws.append((s1, s2))
+    mean1 = [(a + b) / 2 for a, b in zip(draws[0][0], draws[1][0])]
+    mean2 = [(m + (a + b) / 2) for m, a, b in zip(mean1, draws[0][1], draws[1][1])]
+    tol = 2e-2 if bf16 else 1e-6
+    for r in range(world):
+        for got, want in zip(out[r]["grads"], mean2):
+            assert got.dtype == torch.float32
+            assert (got - want).abs().max() <= tol * max(1.0, want.abs().max())

@@ -888,7 +888,7 @@ def test_stem_pixel_pair_conv(dev, cfg, beta):
 
 @pytest.mark.parametrize("cfg", [(2, 3, 32, 32, 64, 7, 2, 3), (3, 3, 64, 96, 64, 7, 2, 3),
                                  (4, 3, 224, 224, 64, 7, 2, 3)])
-def test_stem_direct_matches_implicit_gemm(dev, cfg, monkeypatch):
+def test_stem_direct_matches_implicit_gemm(dev, cfg, knobs):
     """The direct stem forward and weight gradient (input rows staged in LDS once, operand
     fragments read from them; MMDX_STEM_DIRECT) against the implicit-GEMM kernels on the same
     pixel-pair operands: the
@@ -909,7 +909,7 @@ def test_stem_direct_matches_implicit_gemm(dev, cfg, monkeypatch):
     M = N * d.P * d.Q
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("MMDX_STEM_DIRECT", mode)
+        knobs("MMDX_STEM_DIRECT", mode)
         rpb = L.lib().mmdx_conv_fwd_stat_rows(d)
         nst = L.lib().mmdx_conv_fwd_stat_blocks(d)
         assert rpb == (128 if mode == "0" else 2 * d.Q)
@@ -936,7 +936,7 @@ def test_stem_direct_matches_implicit_gemm(dev, cfg, monkeypatch):
     ws = torch.empty(max(1, ws_n), dtype=torch.uint8, device=dev)
     dws = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("MMDX_STEM_DIRECT", mode)
+        knobs("MMDX_STEM_DIRECT", mode)
         dwp = torch.full((K, 8, d.R, d.S), float("nan"), device=dev)
         L.call("mmdx_conv_wgrad", 1, d, 8, xp.data_ptr(), dy.data_ptr(), dwp.data_ptr(), 0.0,
                ws.data_ptr(), ws_n, L.stream())

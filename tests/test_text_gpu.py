@@ -176,16 +176,13 @@ def test_text_encoder_transformer_bert(dev, dt):
     assert rel_err(out["logits"], out_ref["logits"]) <= tol
 
 
-@pytest.mark.parametrize("variant", ["coop4", "coop8"])
 @pytest.mark.parametrize("B", [128, 200, 40])
-def test_lstm_coop_forward_matches_partitioned(dev, B, variant, monkeypatch):
-    """The cooperative bf16 recurrences (coop4: 4 waves, W_hh in registers; coop8: 8 waves,
-    W_hh in LDS; h exchanged through a counter barrier; B = 200 runs as two independent
-    128-row groups, the second ragged; B = 40 the 64-row variant) reproduce the
-    batch-partitioned kernel (same MFMA k order; fp32 contraction
-    order of the cell update may differ, so h may differ by one bf16 ulp): max abs
-    difference <= 1e-2 on h (bf16, |h| < 1), c and gates."""
-    monkeypatch.setenv("MMDX_LSTM_FWD_COOP4", "1" if variant == "coop4" else "0")
+def test_lstm_coop_forward_matches_partitioned(dev, B):
+    """The cooperative bf16 recurrence (8 waves, W_hh in LDS; h exchanged through a counter
+    barrier; B = 200 runs as two independent 128-row groups, the second ragged; B = 40 the
+    64-row variant) reproduces the batch-partitioned kernel (same MFMA k order; fp32
+    contraction order of the cell update may differ, so h may differ by one bf16 ulp): max
+    abs difference <= 1e-2 on h (bf16, |h| < 1), c and gates."""
     H, Ls = 256, 24
     g = torch.Generator().manual_seed(B)
     xg = (torch.randn(B * Ls, 2 * 4 * H, generator=g) * 0.5).to(dev)

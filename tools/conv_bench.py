@@ -62,12 +62,7 @@ def main():
     ap.add_argument("--ref-gemm", action="store_true",
                     help="also time torch.matmul (hipBLASLt) on the same M x N x K in bf16: "
                          "what a tuned explicit GEMM of that size reaches (no im2col)")
-    ap.add_argument("--fold-probe", action="store_true",
-                    help="forward convs with the BN-apply fold's operand work added "
-                         "(MMDX_FOLD_PROBE: timing only, results not meaningful)")
     a = ap.parse_args()
-    if a.fold_probe:
-        os.environ["MMDX_FOLD_PROBE"] = "1"
     import mmdx
     from mmdx import _lib as L
     if a.lib:

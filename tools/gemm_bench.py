@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dense GEMM throughput of the mmdx MFMA core (mmdx_gemm) with the 4-wave 128 x 128, the
-8-wave 256 x 128 (MMDX_GEMM8_MIN) and the 8-wave 256 x 256 (MMDX_GEMM256_MIN, 128 x 64 per
-wave) tiles, next to torch.matmul (hipBLASLt) on the same
+8-wave 128 x 128 (MMDX_GEMM_8W128) and, forward orientation, the 8-wave 256 x 256
+(MMDX_GEMM256_FWD_MIN, 128 x 64 per wave) tiles, next to torch.matmul (hipBLASLt) on the same
 shapes: the C5 Linear layers (ViT-B/16 12608 tokens, BERT-base 8192 tokens; forward, input
 gradient, weight gradient) plus square calibration points.
     python tools/gemm_bench.py [--reps 20] [--dtype f16|bf16]
@@ -43,14 +43,12 @@ def main():
     from mmdx import functional as F
     dt = torch.float16 if a.dtype == "f16" else torch.bfloat16
     dev = torch.device("cuda", 0)
-    tot = {"4w": 0.0, "8w": 0.0, "256": 0.0, "256s3": 0.0, "256s4": 0.0, "blas": 0.0}
-    off = {"MMDX_GEMM8_MIN": "0", "MMDX_GEMM256_MIN": "0", "MMDX_GEMM256_NS": "0"}
+    from mmdx import _lib as L
+    tot = {"4w": 0.0, "8w": 0.0, "256": 0.0, "blas": 0.0}
+    off = {"MMDX_GEMM_8W128": "0", "MMDX_GEMM256_FWD_MIN": "0"}
     arms = (("4w", dict(off)),
-            ("8w", dict(off, MMDX_GEMM8_MIN="1")),
-            ("256", dict(off, MMDX_GEMM256_MIN="1")),
-            # 256 x 256 with 32-deep K tiles, 3 / 4 stages behind a counted vmcnt
-            ("256s3", dict(off, MMDX_GEMM256_MIN="1", MMDX_GEMM256_NS="3")),
-            ("256s4", dict(off, MMDX_GEMM256_MIN="1", MMDX_GEMM256_NS="4")))
+            ("8w", dict(off, MMDX_GEMM_8W128="1")),
+            ("256", dict(off, MMDX_GEMM256_FWD_MIN="1")))
     for T, O, I in LINEARS:
         X = (torch.rand(T, I, device=dev) * 2 - 1).to(dt)
         W = (torch.rand(O, I, device=dev) * 2 - 1).to(dt)
@@ -69,6 +67,7 @@ def main():
             ref = None
             for mode, env in arms:
                 os.environ.update(env)
+                L.reload_config()
                 res[mode] = timeit(lambda: fn(C), a.reps)
                 fn(C)
                 torch.cuda.synchronize()
@@ -88,6 +87,7 @@ def main():
     print("total ms: " + "  ".join(f"{k} {v:.3f}" for k, v in tot.items()), flush=True)
     for k in off:
         os.environ.pop(k, None)
+    L.reload_config()
 
 
 if __name__ == "__main__":
