@@ -551,7 +551,10 @@ size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H);
  * and B <= 512 run the cooperative recurrence (4 workgroups per 16-row block and direction
  * exchanging dG slices, W_hh^T held in registers), whose bounded wait sets *status = 2 when
  * a peer never arrives within spin_limit polls (<= 0: the default).  NULL: the
- * batch-partitioned kernel.  Both give bit-identical outputs. */
+ * batch-partitioned kernel.  Both use the same bf16 dG operand, packed fragments and k order;
+ * their fp32 cell math may contract a multiply-add differently, and the recurrence carries
+ * such a difference on, so the outputs agree to one bf16 ulp of the tensor's scale (most
+ * elements exactly; tests/test_text_gpu.py). */
 int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                   const float* gates_save, const void* dh_out, int B, int L, int H,
                   void* dxg, float* dw_hh, void* workspace, size_t ws_bytes, int* status,

@@ -16,6 +16,8 @@ in AdamW's `grad_scale`, an overflowed step is skipped inside the AdamW launch
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 
 from . import _lib as L
@@ -78,7 +80,8 @@ class GradScaler:
         self._opt_inf = {}           # id(optimizer) -> its own found_inf device scalar
         self._step_infs = {}         # the optimizers checked since the last update()
         self._unscaled = {}
-        self._noop = False           # a step / clip_and_step since the last update() found no grads
+        self._noop = False           # a clip_and_step since the last update() found no grads
+        self._warned_noop = False
 
     def is_enabled(self):
         return self._enabled
@@ -139,8 +142,9 @@ class GradScaler:
             return optimizer.step(*args, **kwargs)
         ps = self._params(optimizer)
         if not ps:
-            self._noop = True
-            return None
+            # torch.amp.GradScaler.step's behaviour: gradients that never reached the
+            # optimizer (a detached graph, a wrong param list) are an error, not a skipped step
+            raise AssertionError("No inf checks were recorded for this optimizer.")
         if id(optimizer) in self._unscaled:
             return optimizer.step(*args, found_inf=self._opt_inf[id(optimizer)], **kwargs)
         fi = self._inf_for(optimizer, ps[0].device)
@@ -153,6 +157,10 @@ class GradScaler:
         ps = params if params is not None else self._params(optimizer)
         ps = [p for p in ps if p.grad is not None]
         if not ps:   # no gradients: nothing to clip or step (clip_grad_norm_ returns 0)
+            if not self._warned_noop:
+                warnings.warn("GradScaler.clip_and_step: no parameter has a gradient; the "
+                              "step is skipped and the loss scale kept", RuntimeWarning)
+                self._warned_noop = True
             self._noop = True
             return torch.zeros(())
         if not self._enabled:

@@ -105,7 +105,9 @@ DEBUG = {"spin_limit": 0, "flags": 0}
 # the cooperative recurrent backward (mmdx_lstm_bwd with a status word) is opt-in
 # (MMDX_LSTM_BWD_COOP=1): 0.70 vs 1.0 ms per launch in the C4 step, but it holds 64 CUs
 # where the batch-partitioned kernel holds 16, and beside the throughput-bound image
-# backward CU-time is what counts: C4 8738 vs 8830 samples/s (r05, paired).  Bit-identical.
+# backward CU-time is what counts: C4 8738 vs 8830 samples/s (r05, paired).  Same outputs as
+# the partitioned kernel to one bf16 ulp of scale (fp32 contraction differences in the cell
+# math propagate through the recurrence; tests/test_text_gpu.py).
 BWD_COOP = os.environ.get("MMDX_LSTM_BWD_COOP", "0") == "1"
 
 

@@ -192,13 +192,19 @@ def test_clip_and_step_without_gradients(dev):
     ps = [torch.nn.Parameter(torch.zeros(8, device=dev))]
     opt = mmdx.AdamW(ps, lr=1e-3)
     sc = mmdx.GradScaler()
-    norm = sc.clip_and_step(opt, 1.0)
+    with pytest.warns(RuntimeWarning, match="no parameter has a gradient"):
+        norm = sc.clip_and_step(opt, 1.0)
     assert float(norm) == 0.0
     sc.scale(torch.ones((), device=dev))
-    sc.clip_and_step(opt, 1.0)
+    sc.clip_and_step(opt, 1.0)   # (warned once per scaler)
     sc.update()                # a no-gradient step records no inf check: update() keeps state
     torch.cuda.synchronize()
     assert sc.get_scale() == 2.0 ** 16
+    # GradScaler.step without gradients is an error, as torch.amp.GradScaler's is (gradients
+    # that never reached the optimizer must not turn into silently skipped steps)
+    sc.scale(torch.ones((), device=dev))
+    with pytest.raises(AssertionError, match="No inf checks were recorded"):
+        sc.step(opt)
 
 
 @pytest.mark.parametrize("bad", [float("inf"), float("nan")])

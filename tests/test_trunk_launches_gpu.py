@@ -175,7 +175,10 @@ def _bn_bwd_checks(rep, tag, u, plan, grads):
     rep.check(f"bn-dbeta {tag}", gb, sg, ACC * s1 + band + TINY)
 
 
-@pytest.mark.parametrize("arch,B", [("resnet50", 128), ("resnet18", 64)])
+# C4's per-GPU batch, C2's, and C3's 256 on one GPU: at 256 the dispatcher picks other tiles,
+# stage counts and split-K depths for some launches (tools/dispatch_diff.py lists them;
+# profiles/r06_dispatch_b128_vs_b256.txt), so C3's geometry is checked launch by launch too
+@pytest.mark.parametrize("arch,B", [("resnet50", 128), ("resnet18", 64), ("resnet50", 256)])
 def test_every_trunk_launch_bf16(dev, arch, B):
     torch.manual_seed(0)
     img = mmdx.ImageEncoderCNN(arch, 1024, 13, compute_dtype=torch.bfloat16).to(dev)
