@@ -2060,17 +2060,6 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-#if defined(MMDX_LAB_EPI) && MMDX_LAB_EPI == 3   // lab timing probe: no epilogue at all
-  {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) s += acc[i][j][0] + acc[i][j][3];
-    if (s == 1.2345e-30f) epi.apply4(tm * BM, tn * BN, acc[0][0]);
-    return;
-  }
-#endif
   if constexpr (BSUM) {
     // every column of a bsum tile holds the row sums: lanes 0, 16, 32, 48 store rows
     // (lane >> 4) * 4 + r of each row tile
@@ -2105,21 +2094,8 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                   : bn_y8{};
       }
     }
-#if !(defined(MMDX_LAB_EPI) && MMDX_LAB_EPI == 1)   // lab 1: no statistics
     if constexpr (Epi::REG_STATS)
       epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
-#endif
-#if defined(MMDX_LAB_EPI) && MMDX_LAB_EPI == 2      // lab 2: statistics only, no staging / store
-    {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) s += acc[i][j][0] + acc[i][j][3];
-      if (s == 1.2345e-30f) epi.apply4(tm * BM, tn * BN, acc[0][0]);
-      return;
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
