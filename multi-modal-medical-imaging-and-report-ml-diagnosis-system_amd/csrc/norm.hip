@@ -144,20 +144,34 @@ __device__ __forceinline__ float slab_sum_regs(const float2* vals, int nblk, int
 // slabs per thread held in registers by the finalize kernels (more: two passes over memory)
 constexpr int FIN_PER = 16;
 
+struct BnFinArgs {
+  const float2* part;
+  int nblk;
+  long rows, rpb;
+  int C;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;
+  float* save_rstd;
+  float* scale;
+  float* shift;
+};
+
 // TPC = threads per channel: 64 (one wave; few slabs) or 256 (whole block; thousands of
-// slabs, e.g. the 3136 per-128-row slabs of a layer1 conv at batch 128)
+// slabs, e.g. the 3136 per-128-row slabs of a layer1 conv at batch 128).  `bid` is the
+// finalize block index.
 template <int TPC>
-__global__ __launch_bounds__(256) void bn_finalize_kernel(
-    const float2* __restrict__ part, int nblk, long rows, long rpb, int C,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
-    float* running_var, float momentum, float eps, float* save_mean, float* save_rstd,
-    float* scale, float* shift) {
-  __shared__ float red[4];
+__device__ __forceinline__ void bn_finalize_body(const BnFinArgs& a, int bid, float* red) {
   const int sub = threadIdx.x % TPC;
-  const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
-  if (c >= C) return;  // uniform per wave (TPC = 64) or per block (TPC = 256)
+  const int c = bid * (256 / TPC) + threadIdx.x / TPC;
+  if (c >= a.C) return;  // uniform per wave (TPC = 64) or per block (TPC = 256)
+  const int nblk = a.nblk;
+  const long rows = a.rows, rpb = a.rpb;
   const long last = rows - (long)(nblk - 1) * rpb;  // rows of the final (short) slab
-  const float2* pc = part + (long)c * nblk;          // this channel's slabs, contiguous
+  const float2* pc = a.part + (long)c * nblk;        // this channel's slabs, contiguous
   float mean, m2;
   if (nblk <= TPC * FIN_PER) {  // one read of the slabs (all loads in flight together)
     float2 v[FIN_PER];
@@ -183,20 +197,25 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
       return p.y + (b == nblk - 1 ? (float)last : (float)rpb) * d * d;
     });
   }
-  const int lane = sub;
-  if (lane != 0) return;
+  if (sub != 0) return;
   const float var = m2 / (float)rows;
-  const float rstd = rsqrtf(var + eps);
-  save_mean[c] = mean;
-  save_rstd[c] = rstd;
-  if (running_mean) {
+  const float rstd = rsqrtf(var + a.eps);
+  a.save_mean[c] = mean;
+  a.save_rstd[c] = rstd;
+  if (a.running_mean) {
     const float unb = rows > 1 ? m2 / (float)(rows - 1) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mean;
+    a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
   }
-  const float g = gamma ? gamma[c] : 1.f;
-  scale[c] = g * rstd;
-  shift[c] = (beta ? beta[c] : 0.f) - mean * g * rstd;
+  const float g = a.gamma ? a.gamma[c] : 1.f;
+  a.scale[c] = g * rstd;
+  a.shift[c] = (a.beta ? a.beta[c] : 0.f) - mean * g * rstd;
+}
+
+template <int TPC>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinArgs a) {
+  __shared__ float red[4];
+  bn_finalize_body<TPC>(a, blockIdx.x, red);
 }
 
 __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma,
@@ -248,6 +267,30 @@ __device__ __forceinline__ void bn_coef(const float* gamma, const float* beta, f
 // row, bit e = (stored y[e] > 0) — the ReLU mask the backward of a residual unit reads
 // instead of y itself (1 bit per element instead of 16)
 template <typename T>
+__device__ __forceinline__ void bn_apply_vec(const typename Vec16<T>::type& v,
+                                             const typename Vec16<T>::type& rr, bool has_res,
+                                             const float* sc, const float* sh, int relu, long i,
+                                             T* __restrict__ y, uint8_t* __restrict__ mask) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  V o;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    float f = to_f(v[e]) * sc[e] + sh[e];
+    if (has_res) f += to_f(rr[e]);
+    if (relu) f = fmaxf(f, 0.f);
+    o[e] = from_f<T>(f);
+  }
+  ((V*)y)[i] = o;
+  if (mask) {
+    unsigned b = 0;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) b |= (to_f(o[e]) > 0.f ? 1u : 0u) << e;
+    mask[i] = (uint8_t)b;
+  }
+}
+
+template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res, long rows,
                                                        int C, const float* __restrict__ scale,
@@ -267,21 +310,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
       const V v = ((const V*)x)[i];
       V rr{};
       if (res) rr = ((const V*)res)[i];
-      V o;
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        float f = to_f(v[e]) * sc[e] + sh[e];
-        if (res) f += to_f(rr[e]);
-        if (relu) f = fmaxf(f, 0.f);
-        o[e] = from_f<T>(f);
-      }
-      ((V*)y)[i] = o;
-      if (mask) {
-        unsigned b = 0;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) b |= (to_f(o[e]) > 0.f ? 1u : 0u) << e;
-        mask[i] = (uint8_t)b;
-      }
+      bn_apply_vec<T>(v, rr, res != nullptr, sc, sh, relu, i, y, mask);
     }
   }
 }
@@ -364,17 +393,29 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
 // coef: a[c] = gamma*rstd, b[c] = -gamma*rstd*sum_g/n, k[c] = -gamma*rstd*sum_gx/n
 // Per channel: sum the (sum g, sum g*xhat) slab partials (slab_sum), then the apply-pass
 // coefficients.
+struct BnBwdFinArgs {
+  const float2* part;
+  int nblk;
+  long rows;
+  int C, train;
+  const float* gamma;
+  const float* bbeta;
+  const float* mean;
+  const float* rstd;
+  float* dgamma;
+  float* dbeta;
+  float beta_acc;
+  float* coef;
+};
+
 template <int TPC>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
-    const float2* __restrict__ part, int nblk, long rows, int C, int train,
-    const float* __restrict__ gamma, const float* __restrict__ bbeta,
-    const float* __restrict__ mean, const float* __restrict__ rstd, float* dgamma,
-    float* dbeta, float beta_acc, float* coef) {
-  __shared__ float red[4];
+__device__ __forceinline__ void bn_bwd_finalize_body(const BnBwdFinArgs& a, int bid,
+                                                     float* red) {
   const int sub = threadIdx.x % TPC;
-  const int c = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
+  const int c = bid * (256 / TPC) + threadIdx.x / TPC;
+  const int C = a.C, nblk = a.nblk;
   if (c >= C) return;
-  const float2* pc = part + (long)c * nblk;  // this channel's slabs, contiguous
+  const float2* pc = a.part + (long)c * nblk;  // this channel's slabs, contiguous
   float sg, sgx;
   if (nblk <= TPC * FIN_PER) {  // one read of the slabs for both sums
     float2 v[FIN_PER];
@@ -390,31 +431,83 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     sgx = slab_sum<TPC>(nblk, sub, red, [&](int b) { return pc[b].y; });
   }
   if (sub != 0) return;
-  if (dgamma) dgamma[c] = beta_acc != 0.f ? beta_acc * dgamma[c] + sgx : sgx;
-  if (dbeta) dbeta[c] = beta_acc != 0.f ? beta_acc * dbeta[c] + sg : sg;
+  const float beta_acc = a.beta_acc;
+  if (a.dgamma) a.dgamma[c] = beta_acc != 0.f ? beta_acc * a.dgamma[c] + sgx : sgx;
+  if (a.dbeta) a.dbeta[c] = beta_acc != 0.f ? beta_acc * a.dbeta[c] + sg : sg;
   // dx = a*g + cb + ck*x  (== a*g + b + k*xhat);  scale/shift: the forward's pre-activation
-  const float a = (gamma ? gamma[c] : 1.f) * rstd[c];
-  const float b = train ? -a * sg / (float)rows : 0.f;
-  const float k = (train ? -a * sgx / (float)rows : 0.f) * rstd[c];
-  coef[c] = a;
-  coef[C + c] = b - k * mean[c];
-  coef[2 * C + c] = k;
+  const float rs = a.rstd[c], mu = a.mean[c];
+  const float ga = (a.gamma ? a.gamma[c] : 1.f) * rs;
+  const float b = a.train ? -ga * sg / (float)a.rows : 0.f;
+  const float k = (a.train ? -ga * sgx / (float)a.rows : 0.f) * rs;
+  a.coef[c] = ga;
+  a.coef[C + c] = b - k * mu;
+  a.coef[2 * C + c] = k;
   float sc, sh;
-  bn_coef(gamma, bbeta, mean[c], rstd[c], c, sc, sh);
-  coef[3 * C + c] = sc;
-  coef[4 * C + c] = sh;
+  bn_coef(a.gamma, a.bbeta, mu, rs, c, sc, sh);
+  a.coef[3 * C + c] = sc;
+  a.coef[4 * C + c] = sh;
+}
+
+template <int TPC>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(BnBwdFinArgs a) {
+  __shared__ float red[4];
+  bn_bwd_finalize_body<TPC>(a, blockIdx.x, red);
 }
 
 // dx = a*g + b + k*xhat  ==  a*g + (b - k*mean*rstd) + (k*rstd)*x,  g = dy*relu'(y)
+// One channel vector of one row: its loads (BnBwdIn) and its arithmetic (bn_bwd_vec), split so
+// the fused finalize + apply kernel can issue the loads before its coefficients exist.
+template <typename T>
+struct BnBwdIn {
+  typename Vec16<T>::type vx, vd, vy;
+  unsigned mb;
+};
+
+template <typename T, class G>
+__device__ __forceinline__ BnBwdIn<T> bn_bwd_load(const T* __restrict__ x,
+                                                  const T* __restrict__ y, const G& dy, long r,
+                                                  int j, long i, int relu, bool mask_x,
+                                                  const uint8_t* __restrict__ mask) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  BnBwdIn<T> in;
+  in.vx = ((const V*)x)[i];
+  in.vd = dy.row(r, j * VEC);
+  in.vy = V{};
+  in.mb = 0;
+  if (relu && mask) in.mb = mask[i];
+  else if (relu && !mask_x) in.vy = ((const V*)y)[i];
+  return in;
+}
+
+template <typename T>
+__device__ __forceinline__ void bn_bwd_vec(const BnBwdIn<T>& in, const float* ca,
+                                           const float* cb, const float* ck, const float* sc,
+                                           const float* sh, int relu, bool mask_x, bool has_mask,
+                                           long i, T* __restrict__ dx, T* __restrict__ dres) {
+  typedef typename Vec16<T>::type V;
+  constexpr int VEC = Vec16<T>::N;
+  V o, og;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    float g = to_f(in.vd[e]);
+    const float a = mask_x ? to_f(in.vx[e]) * sc[e] + sh[e] : to_f(in.vy[e]);
+    const bool pos = has_mask ? ((in.mb >> e) & 1u) != 0 : a > 0.f;
+    if (relu && !pos) g = 0.f;
+    // explicit: the compiler may contract a*g + b + k*x either way round, per call site
+    o[e] = from_f<T>(fmaf(ck[e], to_f(in.vx[e]), fmaf(ca[e], g, cb[e])));
+    og[e] = from_f<T>(g);
+  }
+  ((V*)dx)[i] = o;
+  if (dres) ((V*)dres)[i] = og;
+}
+
 template <typename T, class G>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
-    const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ coef, int relu, const float* __restrict__ gamma,
-    const float* __restrict__ bbeta, T* __restrict__ dx, T* __restrict__ dres,
+    const float* __restrict__ coef, int relu, T* __restrict__ dx, T* __restrict__ dres,
     const uint8_t* __restrict__ mask) {
   const bool mask_x = relu && !y && !mask;
-  typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   const RowTile rt = row_tile(C, VEC);
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
@@ -427,24 +520,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     load_coef<VEC>(coef + 4 * C + j * VEC, sh);
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
-      const V vx = ((const V*)x)[i];
-      const V vd = dy.row(r, j * VEC);
-      V vy{};
-      unsigned mb = 0;
-      if (relu && mask) mb = mask[i];
-      else if (relu && !mask_x) vy = ((const V*)y)[i];
-      V o, og;
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        float g = to_f(vd[e]);
-        const float a = mask_x ? to_f(vx[e]) * sc[e] + sh[e] : to_f(vy[e]);
-        const bool pos = mask ? ((mb >> e) & 1u) != 0 : a > 0.f;
-        if (relu && !pos) g = 0.f;
-        o[e] = from_f<T>(ca[e] * g + cb[e] + ck[e] * to_f(vx[e]));
-        og[e] = from_f<T>(g);
-      }
-      ((V*)dx)[i] = o;
-      if (dres) ((V*)dres)[i] = og;
+      const BnBwdIn<T> in = bn_bwd_load<T, G>(x, y, dy, r, j, i, relu, mask_x, mask);
+      bn_bwd_vec<T>(in, ca, cb, ck, sc, sh, relu, mask_x, mask != nullptr, i, dx, dres);
     }
   }
 }
@@ -491,14 +568,14 @@ static int bn_fwd_t(int train, const void* x, long rows, int C, const float* sta
       hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0, st,
                          (const T*)x, rows, C, L.ct, L.rows_per_block, part);
     }
-    if (nblk > fin_wide())
-      hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
-                         (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv, momentum,
-                         eps, smean, srstd, scale, shift);
+    const BnFinArgs fa{(const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv,
+                       momentum, eps, smean, srstd, scale, shift};
+    const bool wide = nblk > fin_wide();
+    const int nfin = wide ? C : (C + FIN_W - 1) / FIN_W;
+    if (wide)
+      hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(nfin), dim3(256), 0, st, fa);
     else
-      hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0,
-                         st, (const float2*)part, nblk, rows, rpb, C, gamma, beta, rm, rv,
-                         momentum, eps, smean, srstd, scale, shift);
+      hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3(nfin), dim3(256), 0, st, fa);
   } else {
     MMDX_CHECK_ARG(rm && rv, "bn eval: running stats required");
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma,
@@ -536,17 +613,17 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
                        st, (const T*)x, (const T*)y, dy, rows, C, L.ct, L.rows_per_block,
                        smean, srstd, relu, gamma, bbeta, part, mask);
   }
-  if (nblk > fin_wide())
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
-                       (const float2*)part, nblk, rows, C, train, gamma, bbeta, smean,
-                       srstd, dgamma, dbeta, beta_acc, coef);
+  const BnBwdFinArgs fa{(const float2*)part, nblk, rows, C, train, gamma, bbeta, smean, srstd,
+                        dgamma, dbeta, beta_acc, coef};
+  const bool wide = nblk > fin_wide();
+  const int nfin = wide ? C : (C + FIN_W - 1) / FIN_W;
+  if (wide)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(nfin), dim3(256), 0, st, fa);
   else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0,
-                       st, (const float2*)part, nblk, rows, C, train, gamma, bbeta, smean,
-                       srstd, dgamma, dbeta, beta_acc, coef);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3(nfin), dim3(256), 0, st, fa);
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G>), dim3(grid_rows(rows, C, VEC)), dim3(256), 0,
-                     st, (const T*)x, (const T*)y, dy, rows, C, smean, srstd,
-                     (const float*)coef, relu, gamma, bbeta, (T*)dx, (T*)dres, mask);
+                     st, (const T*)x, (const T*)y, dy, rows, C, (const float*)coef, relu,
+                     (T*)dx, (T*)dres, mask);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
@@ -852,9 +929,8 @@ extern "C" int mmdx_bn_fwd_ex(int dtype, int train, const void* x, long rows, in
 }
 
 // The finalize alone (slabs from a conv epilogue -> mean / rstd / running stats / scale /
-// shift) and the apply alone: the two halves of mmdx_bn_fwd_ex's train forward, for callers
-// whose conv did not finalize its own statistics (mmdx_conv_fwd_bnfin's fallback) and for the
-// apply pass behind one that did.
+// shift) and the apply alone: the two halves of mmdx_bn_fwd_ex's train forward, as separate
+// entry points (plan op MMDX_OP_BN_APPLY).
 extern "C" int mmdx_bn_finalize(const float* stat_part, int stat_blocks, long stat_rows,
                                 long rows, int C, const float* gamma, const float* beta,
                                 float* running_mean, float* running_var, float momentum,
@@ -865,16 +941,14 @@ extern "C" int mmdx_bn_finalize(const float* stat_part, int stat_blocks, long st
                      shift,
                  "bn finalize: bad args");
   hipStream_t st = (hipStream_t)stream;
+  const BnFinArgs fa{(const float2*)stat_part, stat_blocks, rows, stat_rows, C, gamma, beta,
+                     running_mean, running_var, momentum, eps, save_mean, save_rstd, scale,
+                     shift};
   if (stat_blocks > fin_wide())
-    hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st,
-                       (const float2*)stat_part, stat_blocks, rows, stat_rows, C, gamma, beta,
-                       running_mean, running_var, momentum, eps, save_mean, save_rstd, scale,
-                       shift);
+    hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st, fa);
   else
     hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + FIN_W - 1) / FIN_W), dim3(256), 0, st,
-                       (const float2*)stat_part, stat_blocks, rows, stat_rows, C, gamma, beta,
-                       running_mean, running_var, momentum, eps, save_mean, save_rstd, scale,
-                       shift);
+                       fa);
   MMDX_LAUNCH_CHECK();
   return 0;
 }
