@@ -271,8 +271,11 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
     text_early = os.environ.get("MMDX_DP_TEXT_EARLY", "1") != "0"
 
     def step():
+        mk = step.marks
         opt.zero_grad(set_to_none=True)
         main = torch.cuda.current_stream()
+        if mk:
+            mk("start", main)
         side.wait_stream(main)
         # both towers issued at once: the image trunk (one native plan call) from this
         # thread onto the main stream, the text tower (Python-issued) from a worker thread
@@ -280,10 +283,15 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
         z_img, z_txt = towers(lambda: img(x)["embeddings"],
                               text_fn or (lambda: txt(input_ids=ids, attention_mask=mask)
                                                      ["embeddings"]))
+        if mk:
+            mk("image_fwd", main)
+            mk("text_fwd", side)
         main.wait_stream(side)
         with rng("mmdx/fusion_fwd"):
             logits = fus(z_img, z_txt)["disease_logits"]
             loss = mmdx.BCEWithLogitsLoss()(logits, y)
+        if mk:
+            mk("head_fwd", main)
         # = loss.backward(), with the text tower's backward queued before the image trunk's;
         # N > 1: the text tower's and fusion head's gradients start their RCCL all-reduce
         # (from the text stream) while the image trunk is still in its backward
@@ -292,7 +300,7 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
             early = lambda: reducer.launch(list(txt.parameters()) + list(fus.parameters()))
         two_tower_backward(scaler.scale(loss) if scaler is not None else loss, z_img, z_txt,
                            fus.parameters(), text_stream=side if side_bwd is None else side_bwd,
-                           on_text_done=early)
+                           on_text_done=early, mark=mk)
         if reducer is not None:
             reducer.reduce()
         with rng("mmdx/optimizer"):
@@ -303,8 +311,11 @@ def make_step(img, txt, fus, opt, params, reducer, x, ids, mask, y, side, side_b
             else:
                 step.norm, scale = MO.grad_norm(params, 1.0)
                 opt.step(grad_scale=scale)
+        if mk:
+            mk("optimizer", torch.cuda.current_stream())
         return loss
     step.norm = None
+    step.marks = None   # diagnostics: mark(name, stream) once each part is issued
     step.towers = towers   # (tools/host_profile.py profiles the text thread through it)
     return step
 
@@ -593,6 +604,38 @@ def main():
     host_one = time.perf_counter() - t1
     torch.cuda.synchronize()
     timer.enabled = was
+    # MMDX_BENCH_TIMELINE=N (diagnostics): N more steps after the timed region with a HIP event
+    # recorded when each part of the step has been issued, on the stream it runs on — when
+    # each part ENDS on the device, in ms after the step's start (mean over the N steps): which
+    # stream the step's tail waits for
+    timeline = None
+    tl_steps = int(os.environ.get("MMDX_BENCH_TIMELINE", "0") or 0)
+    if tl_steps > 0 and not graph_step:
+        recs = []
+        only = os.environ.get("MMDX_BENCH_TIMELINE_MARKS")  # e.g. "start,optimizer"
+        only = set(only.split(",")) | {"start"} if only else None
+
+        def mark(name, stream):
+            if only is None or name in only:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(stream)
+                recs[-1].append((name, e))
+        step.marks = mark
+        for _ in range(tl_steps):
+            recs.append([])
+            step()
+        step.marks = None
+        torch.cuda.synchronize()
+        # device time per marked step over the second half (steady state): the start mark of
+        # its first step to the last step's final mark
+        half = len(recs) // 2
+        tl_wall = recs[half][0][1].elapsed_time(recs[-1][-1][1]) / (len(recs) - half)
+        acc = {}
+        for rec in recs[len(recs) // 2:]:   # the second half: steady state
+            for name, e in rec[1:]:
+                acc.setdefault(name, []).append(rec[0][1].elapsed_time(e))
+        timeline = {k: round(sum(v) / len(v), 3) for k, v in acc.items()}
+        timeline["ms_per_step"] = round(tl_wall, 3)
     conv_steps = ev_steps
     timer.enabled = False
     if dp:
@@ -690,6 +733,7 @@ def main():
         "dp_bucket_dtype": ("bf16" if bdt is not None else "fp32") if dp else None,
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "host_ms_one_step_idle_device": round(host_one * 1e3, 3),
+        **({"timeline_ms": timeline} if timeline else {}),
         "model_tflops": round(total_flops * samples / el / 1e12, 2),
         "mfma_util_pct_end_to_end": round(100 * total_flops * samples / el / 1e12 /
                                           (PEAK_BF16_TFLOPS * world), 2),

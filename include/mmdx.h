@@ -44,6 +44,11 @@ const char* mmdx_last_error(void);
  * process otherwise).  For tests and A/B runs that switch a knob between launches; not to be
  * called while another thread issues launches. */
 int mmdx_reload_config(void);
+/* A non-blocking HIP stream on `cus` of the device's compute units (evenly spread; 0 = all)
+ * with the given priority (cus < all: hipExtStreamCreateWithCUMask, default priority).  Used
+ * for the trunk's weight-gradient stream (MMDX_WGRAD_CUS).  *out: the hipStream_t. */
+int mmdx_stream_create(int priority, int cus, void** out);
+int mmdx_stream_destroy(void* stream);
 
 /* ---------------------------------------------------------------- GEMM (nn.Linear)
  * C[M,N] = act(alpha * sum_k A(m,k) B(n,k) + bias[n] + addend[m,n]) + beta * C
@@ -554,11 +559,12 @@ size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H);
  * batch-partitioned kernel.  Both use the same bf16 dG operand, packed fragments and k order;
  * their fp32 cell math may contract a multiply-add differently, and the recurrence carries
  * such a difference on, so the outputs agree to one bf16 ulp of the tensor's scale (most
- * elements exactly; tests/test_text_gpu.py). */
+ * elements exactly; tests/test_text_gpu.py).  debug_flags bit 0 (tests only): workgroup 0 of
+ * direction 0 of the cooperative kernel never signals, so the peers' waits time out. */
 int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                   const float* gates_save, const void* dh_out, int B, int L, int H,
                   void* dxg, float* dw_hh, void* workspace, size_t ws_bytes, int* status,
-                  long spin_limit, void* stream);
+                  long spin_limit, int debug_flags, void* stream);
 
 /* ---------------------------------------------------------------- T5 report head
  * (TP:545-618 cond_proj + T5ForConditionalGeneration, TP:983-991 /

@@ -65,6 +65,8 @@ SIGNATURES = {
     "mmdx_version": (i32, []),
     "mmdx_last_error": (C.c_char_p, []),
     "mmdx_reload_config": (i32, []),
+    "mmdx_stream_create": (i32, [i32, i32, C.POINTER(vp)]),
+    "mmdx_stream_destroy": (i32, [vp]),
     "mmdx_gemm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_gemm": (i32, [i32, i32, i32, i32, vp, i64, i32, vp, i64, i32, vp, i64, i32, vp, vp,
                         i32, f32, f32, vp, vp, sz, vp]),
@@ -162,7 +164,8 @@ SIGNATURES = {
     "mmdx_lstm_fwd": (i32, [i32, vp, vp, i32, i32, i32, vp, vp, vp, vp, sz, vp, i64, i32, vp]),
     "mmdx_lstm_workspace_size": (sz, [i32, i32, i32, i32]),
     "mmdx_lstm_fwd_workspace_size": (sz, [i32, i32, i32, i32]),
-    "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp, i64, vp]),
+    "mmdx_lstm_bwd": (i32, [i32, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, sz, vp, i64, i32,
+                            vp]),
     "mmdx_patchify": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
     "mmdx_vit_tokens_fwd": (i32, [i32, vp, vp, vp, i32, i32, i32, vp, vp]),
     "mmdx_vit_tokens_bwd": (i32, [i32, vp, i32, i32, i32, vp, vp]),

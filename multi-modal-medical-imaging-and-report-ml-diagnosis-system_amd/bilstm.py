@@ -177,7 +177,7 @@ class _LSTMLayerFn(torch.autograd.Function):
         status = coop_status(dev) if fw and BWD_COOP else None
         call("mmdx_lstm_bwd", L.dtype_code(T), ptr(whh), ptr(hout), ptr(cs), ptr(gs), ptr(dh), B,
              Ls, H, ptr(dxg), ptr(dwhh), ptr(ws), n, ptr(status.word) if status else None,
-             int(DEBUG["spin_limit"]), stream())
+             int(DEBUG["spin_limit"]), int(DEBUG["flags"]), stream())
         if status is not None:
             status.after_launch()
         dwih = torch.empty((2 * G4, In), dtype=torch.float32, device=dev)

@@ -4,6 +4,9 @@
 #include <stdlib.h>
 
 #include <mutex>
+#include <vector>
+
+#include <hip/hip_ext.h>
 
 #include "../../include/mmdx.h"
 #include "common.h"
@@ -64,5 +67,39 @@ const Knobs& knobs() {
 extern "C" int mmdx_reload_config(void) {
   mmdx::knobs();  // the first read, if it has not happened yet
   mmdx::g_knobs = mmdx::read_knobs();
+  return 0;
+}
+
+// A HIP stream restricted to `cus` of the device's compute units (0 or >= the device's
+// count: all of them), spread evenly over the mask so every XCD keeps its share; priority as
+// hipStreamCreateWithPriority.  The caller owns it (mmdx_stream_destroy).
+extern "C" int mmdx_stream_create(int priority, int cus, void** out) {
+  MMDX_CHECK_ARG(out, "mmdx_stream_create: out is NULL");
+  *out = nullptr;
+  int dev = 0, n = 0;
+  MMDX_CHECK_ARG(hipGetDevice(&dev) == hipSuccess &&
+                     hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                         hipSuccess && n > 0,
+                 "mmdx_stream_create: no device");
+  hipStream_t s = nullptr;
+  if (cus <= 0 || cus >= n) {
+    MMDX_CHECK_ARG(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority) == hipSuccess,
+                   "mmdx_stream_create: hipStreamCreateWithPriority failed");
+  } else {
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (int i = 0; i < cus; ++i) {
+      const int cu = (int)((long)i * n / cus);  // evenly spaced
+      mask[cu / 32] |= 1u << (cu % 32);
+    }
+    MMDX_CHECK_ARG(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) ==
+                       hipSuccess,
+                   "mmdx_stream_create: hipExtStreamCreateWithCUMask failed");
+  }
+  *out = (void*)s;
+  return 0;
+}
+
+extern "C" int mmdx_stream_destroy(void* s) {
+  MMDX_CHECK_ARG(s && hipStreamDestroy((hipStream_t)s) == hipSuccess, "mmdx_stream_destroy");
   return 0;
 }

@@ -596,7 +596,7 @@ __global__ __launch_bounds__(CB_NT, 1) void lstm_bwd_coop_kernel(
     const float* __restrict__ gsave, const bf16* __restrict__ dhout, int B, int L,
     bf16* __restrict__ dxg, bf16* __restrict__ hprev, bf16* __restrict__ xbuf,
     unsigned* __restrict__ ctr, int* __restrict__ status, long spin_max,
-    unsigned long long* __restrict__ tst) {
+    unsigned long long* __restrict__ tst, int debug) {
   constexpr int H = COOP_H;
   __shared__ __attribute__((aligned(16))) bf16 sA[CB_RB * CB_G4];
   __shared__ int sgiveup;
@@ -697,7 +697,9 @@ __global__ __launch_bounds__(CB_NT, 1) void lstm_bwd_coop_kernel(
     if (!more) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
+    // (debug flag COOP_DEBUG_DROP_PEER: workgroup 0 of direction 0 never signals, so its
+    // peers' bounded waits must give up — tests/test_text_gpu.py)
+    if (threadIdx.x == 0 && !((debug & COOP_DEBUG_DROP_PEER) && j == 0 && dir == 0))
       __hip_atomic_fetch_add(myctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     CB_STAMP(2);
     // 3. wait for the peers' slices of this step (monotonic: CB_NU per step published)
@@ -924,7 +926,7 @@ extern "C" size_t mmdx_lstm_workspace_size(int dtype, int B, int L, int H) {
 extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, const float* c_save,
                              const float* gates_save, const void* dh_out, int B, int L, int H,
                              void* dxg, float* dw_hh, void* ws, size_t ws_bytes, int* status,
-                             long spin_limit, void* stream) {
+                             long spin_limit, int debug_flags, void* stream) {
   MMDX_CHECK_ARG(dtype != F16, "mmdx_lstm_bwd: fp16 is the C5 path only");
   MMDX_CHECK_ARG(H == 128 || H == 256, "lstm bwd: hidden size %d unsupported", H);
   MMDX_CHECK_ARG(B > 0 && L > 0, "lstm bwd: bad args");
@@ -964,7 +966,7 @@ extern "C" int mmdx_lstm_bwd(int dtype, const void* w_hh, const void* h_out, con
     hipLaunchKernelGGL(lstm_bwd_coop_kernel, dim3(CB_NU, 2, groups), dim3(CB_NT), 0, st,
                        (const bf16*)whp, (const bf16*)h_out, c_save, gates_save,
                        (const bf16*)dh_out, B, L, (bf16*)dxg, (bf16*)hprev, xbuf, ctr, status,
-                       spin_max, tst);
+                       spin_max, tst, debug_flags & COOP_DEBUG_DROP_PEER);
   } else {
     dim3 grid((B + LSTM_RB - 1) / LSTM_RB, 2);
 #define LSTM_BWD(T, HH)                                                                         \

@@ -790,11 +790,41 @@ _WS_TOKEN, _WS2_TOKEN = 0x1, 0x2
 _WS, _WS2 = _WS_TOKEN, _WS2_TOKEN
 
 
+# MMDX_WGRAD_CUS=n: the weight-gradient stream confined to n evenly spread compute units
+# (mmdx_stream_create, a CU-masked HIP stream), leaving the rest to the dgrad / BN chain on
+# the main stream; unset or 0 = all CUs (an ordinary stream).
+WGRAD_CUS = int(os.environ.get("MMDX_WGRAD_CUS", "0") or 0)
+
+
+class _NativeStream:
+    """Owns a stream made by mmdx_stream_create; `.stream` is its torch.cuda.ExternalStream."""
+
+    def __init__(self, dev, cus):
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            L.call("mmdx_stream_create", 0, cus, ctypes.byref(h))
+        self.handle = h.value
+        self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
+
+    def __del__(self):
+        if self.handle:
+            try:
+                L.lib().mmdx_stream_destroy(self.handle)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None
+
+
 def _side_stream(trunk, dev):
     key = "_mmdx_wgrad_stream_%d" % dev.index
     st = trunk.__dict__.get(key)
     if st is None:
-        st = trunk.__dict__[key] = torch.cuda.Stream(device=dev)
+        if WGRAD_CUS > 0:
+            ns = trunk.__dict__[key + "_owner"] = _NativeStream(dev, WGRAD_CUS)
+            st = ns.stream
+        else:
+            st = torch.cuda.Stream(device=dev)
+        trunk.__dict__[key] = st
     return st
 
 

@@ -70,18 +70,21 @@ def _tower(z: torch.Tensor) -> None:
 
 
 def two_tower_backward(loss: torch.Tensor, z_img: torch.Tensor, z_txt: torch.Tensor,
-                       head_params, text_stream=None, on_text_done=None) -> None:
+                       head_params, text_stream=None, on_text_done=None, mark=None) -> None:
     """`text_stream`: the stream the text tower's forward ran on.  Its backward is issued
     with that stream current, so the engine's end-of-backward stream sync does not make the
     image-trunk backward (current stream) wait for it; the current stream waits for the
     text stream only at the end, before the optimizer reads the gradients.
     `on_text_done()` is called with the text stream current once the text tower's and the
     fusion head's gradients are final (e.g. to start their data-parallel all-reduce while
-    the image trunk is still in its backward)."""
+    the image trunk is still in its backward).  `mark(name, stream)` (optional, diagnostics):
+    called once each part is issued, with the stream that part runs on."""
     head = [p for p in head_params if p.requires_grad]
     inputs = [t for t in (z_img, z_txt) if t.requires_grad] + head
     with rng("mmdx/head_bwd"):
         loss.backward(inputs=inputs, retain_graph=True)
+    if mark is not None:
+        mark("head_bwd", torch.cuda.current_stream())
     if text_stream is None or not torch.cuda.is_available():
         with rng("mmdx/image_bwd"):
             _tower(z_img)
@@ -97,12 +100,16 @@ def two_tower_backward(loss: torch.Tensor, z_img: torch.Tensor, z_txt: torch.Ten
         with torch.cuda.stream(text_stream):
             with rng("mmdx/text_bwd"):
                 _tower(z_txt)
+            if mark is not None:
+                mark("text_bwd", text_stream)
             if on_text_done is not None:
                 on_text_done()
     if TEXT_BWD_FIRST:
         text()
     with rng("mmdx/image_bwd"):
         _tower(z_img)
+    if mark is not None:
+        mark("image_bwd", main)
     if not TEXT_BWD_FIRST:
         text()
     main.wait_stream(text_stream)

@@ -236,7 +236,7 @@ def test_lstm_coop_backward_matches_partitioned(dev, B):
         wsb = torch.empty(nb, dtype=torch.uint8, device=dev)
         L.call("mmdx_lstm_bwd", bf, whh.data_ptr(), hout.data_ptr(), cs.data_ptr(),
                gs.data_ptr(), dh.data_ptr(), B, Ls, H, dxg.data_ptr(), dwhh.data_ptr(),
-               wsb.data_ptr(), nb, status.data_ptr() if coop else None, 0, L.stream())
+               wsb.data_ptr(), nb, status.data_ptr() if coop else None, 0, 0, L.stream())
         torch.cuda.synchronize()
         assert int(status[0]) == 0
         outs.append((dxg.float(), dwhh))
@@ -250,6 +250,52 @@ def test_lstm_coop_backward_matches_partitioned(dev, B):
     same = (a_dg == b_dg).float().mean().item()
     assert same >= 0.9, same
     assert (a_dw - b_dw).abs().max().item() <= 1e-2 * b_dw.abs().max().item()
+
+
+def test_lstm_coop_backward_lost_peer_raises(dev):
+    """The cooperative backward's bounded wait: with workgroup 0 of direction 0 never
+    signalling (debug flag 1), every peer gives up, the launch completes (the grid drains),
+    the sticky status word reads 2 and the host's poll raises RecurrenceError naming
+    mmdx_lstm_bwd; a healthy launch afterwards (status reset) leaves it at 0."""
+    from mmdx import bilstm as BL
+    B, H, Ls = 128, 256, 16
+    bf = L.dtype_code(torch.bfloat16)
+    g = torch.Generator().manual_seed(3)
+    xg = (torch.randn(B * Ls, 2 * 4 * H, generator=g) * 0.5).to(dev)
+    whh = (torch.randn(2 * 4 * H, H, generator=g) * 0.05).to(dev, torch.bfloat16)
+    dh = (torch.randn(B, Ls, 2 * H, generator=g) * 0.1).to(dev, torch.bfloat16)
+    hout = torch.empty(B, Ls, 2 * H, dtype=torch.bfloat16, device=dev)
+    cs = torch.empty(2, Ls, B, H, device=dev)
+    gs = torch.empty(2, Ls, B, H, 4, device=dev)
+    n = L.lib().mmdx_lstm_fwd_workspace_size(bf, B, Ls, H)
+    ws = torch.empty(n, dtype=torch.uint8, device=dev)
+    st = BL.coop_status(dev)
+    st.reset()
+    L.call("mmdx_lstm_fwd", bf, xg.data_ptr(), whh.data_ptr(), B, Ls, H, hout.data_ptr(),
+           cs.data_ptr(), gs.data_ptr(), ws.data_ptr(), n, st.word.data_ptr(), 0, 0, L.stream())
+    nb = L.lib().mmdx_lstm_workspace_size(bf, B, Ls, H)
+    wsb = torch.empty(nb, dtype=torch.uint8, device=dev)
+    dxg = torch.empty(B * Ls, 2 * 4 * H, dtype=torch.bfloat16, device=dev)
+    dwhh = torch.empty(2 * 4 * H, H, device=dev)
+
+    def bwd(flags, spin):
+        L.call("mmdx_lstm_bwd", bf, whh.data_ptr(), hout.data_ptr(), cs.data_ptr(),
+               gs.data_ptr(), dh.data_ptr(), B, Ls, H, dxg.data_ptr(), dwhh.data_ptr(),
+               wsb.data_ptr(), nb, st.word.data_ptr(), spin, flags, L.stream())
+        st.after_launch()
+        torch.cuda.synchronize()
+    try:
+        bwd(1, 20000)
+        assert int(st.word[0]) == 2
+        with pytest.raises(BL.RecurrenceError, match="mmdx_lstm_bwd"):
+            BL.check_recurrence()
+    finally:
+        torch.cuda.synchronize()
+        st.reset()
+    bwd(0, 0)
+    BL.check_recurrence()
+    assert int(st.word[0]) == 0
+    assert torch.isfinite(dxg.float()).all()
 
 
 def test_lstm_coop_lost_peer_raises(dev):

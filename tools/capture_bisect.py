@@ -115,7 +115,7 @@ def run_case(name):
         def f():
             L.call("mmdx_lstm_bwd", L.BF16, whh.data_ptr(), hout.data_ptr(), cs.data_ptr(),
                    gs.data_ptr(), dh.data_ptr(), B, Ls, H, dxg.data_ptr(), dwhh.data_ptr(),
-                   ws.data_ptr(), n, None, 0, L.stream())
+                   ws.data_ptr(), n, None, 0, 0, L.stream())
             return [dxg, dwhh]
         return check(f, [dxg, dwhh])
     if name == "linear_bwd_engine":   # an mmdx autograd node's backward on the engine thread

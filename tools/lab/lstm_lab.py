@@ -22,7 +22,7 @@ wsn = L.lib().mmdx_lstm_workspace_size(1, B, Ls, H)
 ws = torch.empty(wsn, dtype=torch.uint8, device=dev)
 def run():
     L.call("mmdx_lstm_bwd", 1, L.ptr(whh), L.ptr(hout), L.ptr(cs), L.ptr(gs), L.ptr(dh), B, Ls, H,
-           L.ptr(dxg), L.ptr(dw), L.ptr(ws), wsn, None, 0, L.stream())
+           L.ptr(dxg), L.ptr(dw), L.ptr(ws), wsn, None, 0, 0, L.stream())
 for _ in range(3):
     run()
 torch.cuda.synchronize()

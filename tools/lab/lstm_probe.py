@@ -66,7 +66,7 @@ def main():
     def bwd(coop=True):
         L.call("mmdx_lstm_bwd", bf, L.ptr(whh), L.ptr(hout), L.ptr(cs), L.ptr(gs), L.ptr(dh), B,
                Ls, H, L.ptr(dxg), L.ptr(dwhh), L.ptr(wsb), nb + tb2, L.ptr(status) if coop else None,
-               0, L.stream())
+               0, 0, L.stream())
 
     def timed(fn, reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
