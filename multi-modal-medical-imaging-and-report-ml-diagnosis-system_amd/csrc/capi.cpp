@@ -36,7 +36,6 @@ static Knobs read_knobs() {
   const long w = env_long("MMDX_CONV_N64_WIDE", -1);
   k.conv_n64_wide = w < 0 ? -1 : w == 0 ? 0 : 1;
   k.conv_8w128 = env_long("MMDX_CONV_8W128", 1) != 0;
-  k.conv_mf32 = env_long("MMDX_CONV_MF32", 0) != 0;
   k.stem_direct = env_long("MMDX_STEM_DIRECT", 1) != 0;
   const long t = env_long("MMDX_WGRAD_TARGET", 256);
   k.wgrad_target = t >= 64 && t <= 4096 ? t : 256;

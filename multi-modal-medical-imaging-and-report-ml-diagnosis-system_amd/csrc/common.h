@@ -32,7 +32,6 @@ constexpr int WAVE = 64;
 struct Knobs {
   int conv_n64_wide;      // MMDX_CONV_N64_WIDE: -1 auto (>= 1024 256-row blocks), 0 off, 1 on
   bool conv_8w128;        // MMDX_CONV_8W128 (default on)
-  bool conv_mf32;         // MMDX_CONV_MF32: 32x32x16 MFMA tiles for the 8-wave 128 x 128 convs
   bool stem_direct;       // MMDX_STEM_DIRECT (default on)
   long wgrad_target;      // MMDX_WGRAD_TARGET: conv weight-gradient split-K blocks (256)
   bool wgrad_rq;          // MMDX_WGRAD_RQ (default on)

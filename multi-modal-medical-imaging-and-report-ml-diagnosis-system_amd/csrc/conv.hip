@@ -326,16 +326,10 @@ static int conv_gemm_epi(const SA& sa, const void* w, const Epi& epi, int M, int
       if (N <= 64 || tiles128 < kNarrowBelow)
         return launch_dma<128, 64>(sa, sb, epi, M, N, K, 1, K, st);
       if (conv_8w128_on()) {
-        if (knobs().conv_mf32)  // the same tiles on v_mfma_f32_32x32x16 (waves of 2 x 1 tiles)
-          hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA, 64, 8>,
-                                               DmaK<128, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 2,
-                                               4, 32>),
-                             dim3((unsigned)tiles128), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
-        else
-          hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA, 64, 8>,
-                                               DmaK<128, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 2,
-                                               4>),
-                             dim3((unsigned)tiles128), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 128, DmaK<128, SA, 64, 8>,
+                                             DmaK<128, DenseK<T>, 64, 8>, Epi, 2, bf16, 512, 2,
+                                             4>),
+                           dim3((unsigned)tiles128), dim3(512), 0, st, sa, sb, epi, M, N, K, K);
         MMDX_LAUNCH_CHECK();
         return 0;
       }

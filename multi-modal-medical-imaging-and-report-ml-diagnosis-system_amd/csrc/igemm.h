@@ -1194,82 +1194,6 @@ struct EpiStore {
             make_float2(mu, mm);
     }
   }
-  // the same statistics from v_mfma_f32_32x32x16 accumulators (RM x RN tiles of 32 x 32:
-  // lane l holds column l & 31, rows (v & 3) + 8 (v >> 2) + 4 (l >> 5) in register v): each
-  // lane reduces its 16 * RM rows of a column, the two half-waves merge by one xor-32 shuffle,
-  // the WM waves of a column in LDS as above
-  template <int BM, int BN, int WM, int WN, int RM, int RN>
-  __device__ __forceinline__ void reg_stats32(const f32x16 (&acc)[RM][RN], float* red, int tm,
-                                              int tn, int wm, int wn, int lane) const {
-    if (!stats) return;
-    if (M - tm * BM >= BM)
-      reg_stats32_t<BM, BN, WM, WN, RM, RN, true>(acc, red, tm, tn, wm, wn, lane);
-    else
-      reg_stats32_t<BM, BN, WM, WN, RM, RN, false>(acc, red, tm, tn, wm, wn, lane);
-  }
-  template <int BM, int BN, int WM, int WN, int RM, int RN, bool FULL>
-  __device__ __forceinline__ void reg_stats32_t(const f32x16 (&acc)[RM][RN], float* red, int tm,
-                                                int tn, int wm, int wn, int lane) const {
-    constexpr int WTM = BM / WM, WTN = BN / WN;
-    static_assert(BM <= 128, "one statistics slab per tile");
-    const int rows_valid = min(BM, M - tm * BM);
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      float cnt = 0.f, s = 0.f;
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const bool ok =
-              FULL || wm * WTM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5) < rows_valid;
-          cnt += ok ? 1.f : 0.f;
-          s += ok ? acc[i][j][v] : 0.f;
-        }
-      if constexpr (FULL) cnt = (float)(RM * 16);
-      const float mean = cnt > 0.f ? s / cnt : 0.f;
-      float m2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const bool ok =
-              FULL || wm * WTM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5) < rows_valid;
-          const float d = acc[i][j][v] - mean;
-          m2 += ok ? d * d : 0.f;
-        }
-      float n_a = cnt, mu = mean, mm = m2;
-      {
-        const float n_b = FULL ? n_a : __shfl_xor(n_a, 32, 64);
-        const float mu_b = __shfl_xor(mu, 32, 64), mm_b = __shfl_xor(mm, 32, 64);
-        const float tot = n_a + n_b;
-        const float d = mu_b - mu, f = FULL ? 0.5f : (tot > 0.f ? n_b / tot : 0.f);
-        mu += d * f;
-        mm += mm_b + d * d * n_a * f;
-        n_a = tot;
-      }
-      if (lane < 32) {
-        float* o = red + (wm * BN + wn * WTN + j * 32 + lane) * 3;
-        o[0] = n_a; o[1] = mu; o[2] = mm;
-      }
-    }
-    __syncthreads();
-    const int col = threadIdx.x % BN;
-    if (threadIdx.x < BN && tn * BN + col < N) {
-      float nn = 0.f, mu = 0.f, mm = 0.f;
-#pragma unroll
-      for (int qq = 0; qq < WM; ++qq) {
-        const float* o = red + (qq * BN + col) * 3;
-        const float nb = FULL ? (float)WTM : o[0], mb = o[1], m2b = o[2];
-        if (nb == 0.f) continue;
-        if (nn == 0.f) { nn = nb; mu = mb; mm = m2b; continue; }
-        const float tot = nn + nb, d = mb - mu, f = FULL ? 1.f / (float)(qq + 1) : nb / tot;
-        mu += d * f;
-        mm += m2b + d * d * nn * f;
-        nn = tot;
-      }
-      stats[(long)(tn * BN + col) * ((M + BM - 1) / BM) + tm] = make_float2(mu, mm);
-    }
-  }
   __device__ __forceinline__ void apply4(int m, int n, f32x4 v) const {
     if (m >= M) return;
     const long off = (long)m * ldc + n;
@@ -1758,12 +1682,6 @@ struct DmaK {
     const int c = (ks >> 3) + (lane >> 4);
     return *(const bf16x8*)(stage + row * (BK * 2) + ((c ^ swz(row)) << 4));
   }
-  // the v_mfma_f32_32x32x16 operand: lane l holds row r32 + (l & 31), k = ks + 8 (l >> 5) .. +7
-  __device__ static bf16x8 frag32(const char* stage, int r32, int ks, int lane) {
-    const int row = r32 + (lane & 31);
-    const int c = (ks >> 3) + (lane >> 5);
-    return *(const bf16x8*)(stage + row * (BK * 2) + ((c ^ swz(row)) << 4));
-  }
 };
 
 // R-major operand (rows contiguous in global: dY^T / im2col^T of the wgrad GEMM): LDS image
@@ -1954,19 +1872,12 @@ __device__ __forceinline__ void epilogue_pass(const Epi& epi, const float* cst, 
 // NTH = 512 (8 waves, one block per CU, 256 x 128 tiles, WM x WN = 4 x 2 waves of 64 x 64):
 // half the operand bytes per MFMA of two 128 x 128 blocks and twice the K tiles in flight
 // (NS = 3 stages of 48 KB) for the same LDS.
-// MF = 32: v_mfma_f32_32x32x16_bf16 tiles instead of 16x16x32 (half the MFMA instructions
-// per FLOP; k-major operands, EpiStore statistics, one staging pass: the conv fwd / dgrad
-// tiles, MMDX_CONV_MF32).
 template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16,
-          int NTH = NT, int WM = 2, int WN = 2, int MF = 16>
+          int NTH = NT, int WM = 2, int WN = 2>
 __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                                            typename OB::SrcT sb, Epi epi, int M,
                                                            int N, int K, int kper) {
   constexpr int BK = OA::BK;
-  static_assert(MF == 16 || MF == 32, "MFMA tile");
-  static_assert(MF == 16 || (!OA::RMAJOR && !OB::RMAJOR && std::is_same<ET, bf16>::value &&
-                             BM <= 128 && !IsPhased<Epi>::value),
-                "32x32x16 tiles: k-major bf16 operands, one statistics slab per tile");
   static_assert(WM * WN * 64 == NTH && OA::NW * 64 == NTH && OB::NW * 64 == NTH, "waves");
   // fragments-first K loop (below): measured on the C4 conv shapes, 5-13 % faster for the
   // R-major (weight-gradient) operands and most 128-wide tiles, mixed on the 128x64 k-major
@@ -1975,9 +1886,7 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   constexpr bool FRAG_FIRST = BN == 128 || (OA::RMAJOR && BN < 256);
   static_assert(OB::BK == BK, "operand K tile depths differ");
   constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int RM = WTM / MF, RN = WTN / MF;
-  typedef typename std::conditional<MF == 32, f32x16, f32x4>::type AccV;
-  constexpr int NACC = MF == 32 ? 16 : 4;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int OP_BYTES = NS * STAGE;
   constexpr int RED = WM * 3 > (NTH / 64) * 2 ? WM * 3 : (NTH / 64) * 2;  // floats per column
@@ -2029,16 +1938,13 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   oa.init(sa, tm * BM, lane, wid, kbeg);
   ob.init(sb, tn * BN, lane, wid, kbeg);
 
-  AccV acc[RM][RN];
+  f32x4 acc[RM][RN];
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int v = 0; v < NACC; ++v) acc[i][j][v] = 0.f;
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused bias gradient (EpiPartialBias): row sums of A in the column-tile-0 blocks
   constexpr bool BSUM = HasBiasSum<Epi>::value;
-  static_assert(MF == 16 || !BSUM, "bias sums ride the 16x16x32 loop");
   static_assert(!BSUM || FRAG_FIRST, "bias sums ride the fragments-first K loop");
   const bool bias_blk = BSUM && tn == 0 && wn == 0;   // wave-uniform
   f32x4 bsum[BSUM ? RM : 1];
@@ -2076,16 +1982,17 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
     const char* as = lds_raw + (t % NS) * STAGE;
     const char* bs = as + OA::BYTES;
     auto afrag = [&](int i, int ks) { return OA::frag(as, wm * WTM + i * 16, ks, lane); };
-    if constexpr (MF == 32) {
-      // 32x32x16: every fragment of the tile first (as FRAG_FIRST), then 4 K steps of RM x RN
-      constexpr int KS = BK / 16;
+    if constexpr (FRAG_FIRST) {
+      // every fragment of the tile is requested before the next tile's DMAs are issued, so
+      // the LDS read latency runs under the DMA issue instead of in front of the MFMAs
+      constexpr int KS = BK / 32;
       bf16x8 af[KS][RM], bfr[KS][RN];
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
 #pragma unroll
-        for (int i = 0; i < RM; ++i) af[s][i] = OA::frag32(as, wm * WTM + i * 32, s * 16, lane);
+        for (int i = 0; i < RM; ++i) af[s][i] = afrag(i, s * 32);
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bfr[s][j] = OB::frag32(bs, wn * WTN + j * 32, s * 16, lane);
+        for (int j = 0; j < RN; ++j) bfr[s][j] = OB::frag(bs, wn * WTN + j * 16, s * 32, lane);
       }
       if (t + NS - 1 < nt) {
         char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
@@ -2097,87 +2004,58 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
-          for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s][i], bfr[s][j], acc[i][j],
-                                                                0, 0, 0);
-      continue;
-    }
-    if constexpr (MF == 16) {
-      if constexpr (FRAG_FIRST) {
-        // every fragment of the tile is requested before the next tile's DMAs are issued, so
-        // the LDS read latency runs under the DMA issue instead of in front of the MFMAs
-        constexpr int KS = BK / 32;
-        bf16x8 af[KS][RM], bfr[KS][RN];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-#pragma unroll
-          for (int i = 0; i < RM; ++i) af[s][i] = afrag(i, s * 32);
-#pragma unroll
-          for (int j = 0; j < RN; ++j) bfr[s][j] = OB::frag(bs, wn * WTN + j * 16, s * 32, lane);
-        }
-        if (t + NS - 1 < nt) {
-          char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
-          oa.issue(sa, st, kbeg + (t + NS - 1) * BK, kend, wid);
-          ob.issue(sb, st + OA::BYTES, kbeg + (t + NS - 1) * BK, kend, wid);
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-          for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int j = 0; j < RN; ++j) {
-              if constexpr (std::is_same<ET, f16>::value)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                    __builtin_bit_cast(f16x8, af[s][i]), __builtin_bit_cast(f16x8, bfr[s][j]),
-                    acc[i][j], 0, 0, 0);
-              else
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j],
-                                                                     acc[i][j], 0, 0, 0);
-            }
-        if constexpr (BSUM) {
-          if (bias_blk) {
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-#pragma unroll
-              for (int i = 0; i < RM; ++i) {
-                if constexpr (std::is_same<ET, f16>::value)
-                  bsum[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                      __builtin_bit_cast(f16x8, af[s][i]), __builtin_bit_cast(f16x8, ones8),
-                      bsum[i], 0, 0, 0);
-                else
-                  bsum[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], ones8, bsum[i], 0,
-                                                                     0, 0);
-              }
-          }
-        }
-        continue;
-      }
-      if (t + NS - 1 < nt) {  // its stage was consumed in iteration t-1 by every wave
-        char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
-        oa.issue(sa, st, kbeg + (t + NS - 1) * BK, kend, wid);
-        ob.issue(sb, st + OA::BYTES, kbeg + (t + NS - 1) * BK, kend, wid);
-      }
-#pragma unroll
-      for (int ks = 0; ks < BK; ks += 32) {
-        bf16x8 af[RM], bfr[RN];
-#pragma unroll
-        for (int i = 0; i < RM; ++i) af[i] = afrag(i, ks);
-#pragma unroll
-        for (int j = 0; j < RN; ++j) bfr[j] = OB::frag(bs, wn * WTN + j * 16, ks, lane);
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
           for (int j = 0; j < RN; ++j) {
-            // the LDS-DMA path moves 16-bit elements; the MFMA reads them as ET
             if constexpr (std::is_same<ET, f16>::value)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                  __builtin_bit_cast(f16x8, af[i]), __builtin_bit_cast(f16x8, bfr[j]), acc[i][j],
-                  0, 0, 0);
+                  __builtin_bit_cast(f16x8, af[s][i]), __builtin_bit_cast(f16x8, bfr[s][j]),
+                  acc[i][j], 0, 0, 0);
             else
-              acc[i][j] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j],
+                                                                   acc[i][j], 0, 0, 0);
           }
+      if constexpr (BSUM) {
+        if (bias_blk) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int i = 0; i < RM; ++i) {
+              if constexpr (std::is_same<ET, f16>::value)
+                bsum[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                    __builtin_bit_cast(f16x8, af[s][i]), __builtin_bit_cast(f16x8, ones8),
+                    bsum[i], 0, 0, 0);
+              else
+                bsum[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], ones8, bsum[i], 0,
+                                                                   0, 0);
+            }
+        }
       }
+      continue;
+    }
+    if (t + NS - 1 < nt) {  // its stage was consumed in iteration t-1 by every wave
+      char* st = lds_raw + ((t + NS - 1) % NS) * STAGE;
+      oa.issue(sa, st, kbeg + (t + NS - 1) * BK, kend, wid);
+      ob.issue(sb, st + OA::BYTES, kbeg + (t + NS - 1) * BK, kend, wid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = afrag(i, ks);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfr[j] = OB::frag(bs, wn * WTN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          // the LDS-DMA path moves 16-bit elements; the MFMA reads them as ET
+          if constexpr (std::is_same<ET, f16>::value)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                __builtin_bit_cast(f16x8, af[i]), __builtin_bit_cast(f16x8, bfr[j]), acc[i][j],
+                0, 0, 0);
+          else
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2216,29 +2094,16 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
                                   : bn_y8{};
       }
     }
-    if constexpr (MF == 32) {
-      if constexpr (Epi::REG_STATS)
-        epi.template reg_stats32<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
+    if constexpr (Epi::REG_STATS)
+      epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+    for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
+      for (int j = 0; j < RN; ++j)
 #pragma unroll
-          for (int v = 0; v < 16; ++v)
-            cst[(wm * WTM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)) * LDC + wn * WTN +
-                j * 32 + (lane & 31)] = acc[i][j][v];
-    } else {
-      if constexpr (Epi::REG_STATS)
-        epi.template reg_stats<BM, BN, WM, WN, RM, RN>(acc, red, tm, tn, wm, wn, lane);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 +
-                (lane & 15)] = acc[i][j][r];
-    }
+        for (int r = 0; r < 4; ++r)
+          cst[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WTN + j * 16 +
+              (lane & 15)] = acc[i][j][r];
     __syncthreads();
     if constexpr (!Epi::REG_STATS) epi.template tile_stats<BM, BN, LDC>(cst, red, tm, tn);
     if (bst) {  // vec8 stores + the statistics of every stored chunk (rows >= M excluded)
@@ -2261,7 +2126,7 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
       bn_stat_store<BN, NTH / 64, (BM > 128 ? BM / 128 : 1)>(epi.bs, sg, sgx, red, tm, tn, N, M);
       return;
     }
-  } else if constexpr (MF == 16) {
+  } else {
     // column passes (256 x 256 tiles): the waves whose columns fall in pass h stage them; the
     // epilogues used here take their statistics from the registers (REG_STATS) or keep none
     // (EpiPartial, EpiPhase), and the fused consumer-BN path is not instantiated

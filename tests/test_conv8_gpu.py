@@ -152,38 +152,3 @@ def test_256row_n64_tiles_match_128row(dev, cfg, knobs):
     b = _run_all(dev, cfg)
     _compare(a, b, "n64wide")
 
-
-def _close_mf32(a, b, key):
-    """Two fp32 accumulation orders, one bf16 rounding each: at most one bf16 step apart
-    (2^-7 relative, plus the fp32 sums' own error), and most elements identical."""
-    x, y = a.float(), b.float()
-    err = (x - y).abs()
-    bound = 2.0 ** -7 * torch.maximum(x.abs(), y.abs()) + 1e-6 * x.abs().max()
-    assert (err <= bound).all(), (key, (err - bound).max().item())
-    assert (x == y).float().mean().item() >= 0.8, key
-
-
-@pytest.mark.parametrize("cfg", SHAPES128)
-def test_mf32_tiles_match_16x16(dev, cfg, knobs):
-    """MMDX_CONV_MF32: the 8-wave 128 x 128 conv tiles on v_mfma_f32_32x32x16_bf16 (2 x 1
-    tiles of 32 x 32 per wave) against the same tiles on 16x16x32.  The MFMA accumulates K in
-    steps of 16 instead of 32, so the outputs are one rounding apart at most (not bit-equal);
-    the per-128-row BN slabs within 1e-4; the fused consumer-BN partial totals within 1e-4;
-    the weight gradients (R-major, never 32x32) identical."""
-    knobs("MMDX_CONV_N64_WIDE", 0)
-    knobs("MMDX_CONV_8W128", 1)
-    a = _run_all(dev, cfg)
-    knobs("MMDX_CONV_MF32", 1)
-    b = _run_all(dev, cfg)
-    for key in a:
-        assert torch.isfinite(b[key].float()).all(), key
-        if key == "stats":
-            torch.testing.assert_close(b[key], a[key], rtol=1e-4, atol=1e-4, msg=key)
-        elif key == "bnstat_part":
-            ta, tb = a[key].double().sum(1), b[key].double().sum(1)
-            err = ((ta - tb).abs().max() / ta.abs().max().clamp(min=1e-12)).item()
-            assert err <= 1e-4, (key, err)
-        elif key == "wgrad":
-            assert torch.equal(a[key], b[key]), key
-        else:
-            _close_mf32(a[key], b[key], key)
