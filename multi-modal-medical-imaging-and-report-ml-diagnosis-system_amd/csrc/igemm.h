@@ -859,7 +859,7 @@ __device__ __forceinline__ void bst_store8(const Epi& e, int m, int n, f32x4 lo,
       o[j] = from_f<OutT>(lo[j]);
       o[j + 4] = from_f<OutT>(hi[j]);
     }
-    *(O8*)(e.C + off) = o;
+    __builtin_nontemporal_store(o, (O8*)(e.C + off));  // (streaming: see apply8_fast)
   }
 }
 
@@ -1099,7 +1099,11 @@ struct EpiStore {
         o[j + 4] = from_f<OutT>(alpha * hi[j]);
       }
     }
-    *(O8*)(C + off) = o;
+    // nontemporal (streaming) 16-B stores: an output tile is written once and next read by
+    // another launch, long after it would have left the L2; isolated C4 conv fwd / dgrad
+    // families 2.31 / 2.17 -> 2.20 / 2.11 ms, C4 9318 / 9335 -> 9516 / 9515 samples/s paired
+    // (profiles/r06_nt_store_ab.txt)
+    __builtin_nontemporal_store(o, (O8*)(C + off));
   }
   // Per-column (mean, M2) of this BM-row tile straight from the MFMA accumulators: each lane
   // reduces its 4*RM rows of a column exactly (two passes in registers), the four lane groups
