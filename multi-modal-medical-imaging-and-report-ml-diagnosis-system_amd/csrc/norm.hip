@@ -307,9 +307,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
     load_coef<VEC>(shift + j * VEC, sh);
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
-      const V v = ((const V*)x)[i];
+      // nontemporal loads: the conv output and the residual are read once here (their next
+      // readers come in the backward, long after): C4 +0.9 % (profiles/r06_nt_store_ab.txt)
+      const V v = __builtin_nontemporal_load((const V*)x + i);
       V rr{};
-      if (res) rr = ((const V*)res)[i];
+      if (res) rr = __builtin_nontemporal_load((const V*)res + i);
       bn_apply_vec<T>(v, rr, res != nullptr, sc, sh, relu, i, y, mask);
     }
   }
@@ -471,7 +473,7 @@ __device__ __forceinline__ BnBwdIn<T> bn_bwd_load(const T* __restrict__ x,
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   BnBwdIn<T> in;
-  in.vx = ((const V*)x)[i];
+  in.vx = __builtin_nontemporal_load((const V*)x + i);  // (read once: see bn_apply_kernel)
   in.vd = dy.row(r, j * VEC);
   in.vy = V{};
   in.mb = 0;

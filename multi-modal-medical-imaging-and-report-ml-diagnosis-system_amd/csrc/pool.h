@@ -77,7 +77,9 @@ struct DenseGrad {
   typedef typename Vec16<T>::type V;
   const T* dy;
   int C;
-  __device__ __forceinline__ V row(long r, int c) const { return *(const V*)(dy + r * C + c); }
+  __device__ __forceinline__ V row(long r, int c) const {  // streaming (nontemporal) load
+    return __builtin_nontemporal_load((const V*)(dy + r * C + c));
+  }
 };
 
 // dy with a 1-bit ReLU mask applied on the fly ([rows][C / VEC] bytes, mmdx_bn_fwd_ex): the
