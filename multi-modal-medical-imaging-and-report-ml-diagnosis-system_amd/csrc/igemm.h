@@ -436,13 +436,11 @@ template <typename T>
 struct DgradPhaseK {
   const T* dy; ConvGeom g; PhaseGeom ph; int M;
   PhaseGeom phs[MAX_PHASES]; int Ms[MAX_PHASES];
-  // constant indices only (a dynamically indexed by-value kernel argument would be copied to
-  // scratch); p is wave-uniform (blockIdx.z), so this is a scalar branch
-  __device__ void select(int p) {
-    if (p == 0) { ph = phs[0]; M = Ms[0]; }
-    else if (p == 1) { ph = phs[1]; M = Ms[1]; }
-    else if (p == 2) { ph = phs[2]; M = Ms[2]; }
-    else { ph = phs[3]; M = Ms[3]; }
+  // phase p's geometry from the (unwritten) kernel argument `k` (igemm_dma_kernel): p is
+  // block-uniform (blockIdx.z), so these are scalar loads from the kernarg segment
+  __device__ void select_from(const DgradPhaseK& k, int p) {
+    ph = k.phs[p];
+    M = k.Ms[p];
   }
   struct RowState { const T* img; int i, j; };
   struct KT { int dr, ds, kb, k0, klim; };
@@ -513,12 +511,7 @@ template <typename T>
 struct PhaseTapK {
   const T* w; long ld; int C, K, S, sh, sw; PhaseGeom ph;  // w[c][r][s][k], ld = R*S*K
   PhaseGeom phs[MAX_PHASES];
-  __device__ void select(int p) {  // constant indices (see DgradPhaseK::select)
-    if (p == 0) ph = phs[0];
-    else if (p == 1) ph = phs[1];
-    else if (p == 2) ph = phs[2];
-    else ph = phs[3];
-  }
+  __device__ void select_from(const PhaseTapK& k, int p) { ph = k.phs[p]; }  // (DgradPhaseK)
   typedef const T* RowState;
   struct KT { long kg; int k0, klim; };
   typedef typename Vec16<T>::type V;
@@ -1331,15 +1324,9 @@ struct EpiPhase {
   int Ms[MAX_PHASES], Ks[MAX_PHASES], Hps[MAX_PHASES], Wps[MAX_PHASES], as[MAX_PHASES],
       bs_[MAX_PHASES], tile0s[MAX_PHASES];
   int Kp = 0;  // the selected phase's K depth
-  template <int P> __device__ void select_c() {
-    M = Ms[P]; Kp = Ks[P]; Hp = Hps[P]; Wp = Wps[P]; a = as[P]; b = bs_[P];
-    bs.tile0 = tile0s[P];
-  }
-  __device__ void select(int p) {  // constant indices (see DgradPhaseK::select)
-    if (p == 0) select_c<0>();
-    else if (p == 1) select_c<1>();
-    else if (p == 2) select_c<2>();
-    else select_c<3>();
+  __device__ void select_from(const EpiPhase& k, int p) {  // (see DgradPhaseK::select_from)
+    M = k.Ms[p]; Kp = k.Ks[p]; Hp = k.Hps[p]; Wp = k.Wps[p]; a = k.as[p]; b = k.bs_[p];
+    bs.tile0 = k.tile0s[p];
   }
   __device__ __forceinline__ long bn_off(int m, int n) const { return pix(m) * ldc + n; }
   __device__ __forceinline__ long pix(int m) const {
@@ -1878,10 +1865,17 @@ __device__ __forceinline__ void epilogue_pass(const Epi& epi, const float* cst, 
 // (NS = 3 stages of 48 KB) for the same LDS.
 template <int BM, int BN, class OA, class OB, class Epi, int NS = 2, typename ET = bf16,
           int NTH = NT, int WM = 2, int WN = 2>
-__global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
-                                                           typename OB::SrcT sb, Epi epi, int M,
-                                                           int N, int K, int kper) {
+__global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa_k,
+                                                           typename OB::SrcT sb_k, Epi epi_k,
+                                                           int M, int N, int K, int kper) {
   constexpr int BK = OA::BK;
+  // working copies: the kernel arguments themselves are never written, so the merged-phase
+  // selection below reads their per-phase arrays straight from the kernarg segment (a
+  // by-value argument that is written is copied to scratch, and its phase arrays indexed
+  // there: 208 B of scratch per lane in the phase dgrads before round 6)
+  typename OA::SrcT sa = sa_k;
+  typename OB::SrcT sb = sb_k;
+  Epi epi = epi_k;
   static_assert(WM * WN * 64 == NTH && OA::NW * 64 == NTH && OB::NW * 64 == NTH, "waves");
   // fragments-first K loop (below): measured on the C4 conv shapes, 5-13 % faster for the
   // R-major (weight-gradient) operands and most 128-wide tiles, mixed on the 128x64 k-major
@@ -1912,9 +1906,9 @@ __global__ __launch_bounds__(NTH, 2) void igemm_dma_kernel(typename OA::SrcT sa,
   if constexpr (IsPhased<Epi>::value) {
     // merged strided-dgrad phases: blockIdx.z is this block's phase (not a K split)
     const int ph = blockIdx.z;
-    sa.select(ph);
-    sb.select(ph);
-    epi.select(ph);
+    sa.select_from(sa_k, ph);
+    sb.select_from(sb_k, ph);
+    epi.select_from(epi_k, ph);
     M = epi.M;
     K = kper = epi.Kp;
     const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
