@@ -1,9 +1,9 @@
-# round 6 final measurement set (76162ac): full GPU suite (verbose), smoke, C4 line (CPU
+# round 6 final measurement set (6b01b6c): full GPU suite (verbose), smoke, C4 line (CPU
 # baseline), C4 launch table, C5 / C3 / C2 lines, C4 kernel trace + stats, PMC passes
 set -o pipefail
 R=$(pwd)
 mkdir -p gpurun_out
-export MMDX_GIT_REV=76162ac
+export MMDX_GIT_REV=6b01b6c
 run() { local label=$1 to=$2; shift 2; timeout -k 10 $to "$@" > $R/gpurun_out/$label.log 2>&1; local rc=$?; echo "[$label] rc=$rc"; tail -2 $R/gpurun_out/$label.log | cut -c1-300; [ $rc -le 1 ] || exit $rc; }
 run m3_suite 800 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread -p no:cacheprovider
 run m3_smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
@@ -13,7 +13,7 @@ run m3_c5 300 python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baselin
 run m3_c3 300 python bench.py --config c3 --steps 20 --warmup 5 --no-cpu-baseline
 run m3_c2 300 python bench.py --config c2 --steps 50 --warmup 10 --no-cpu-baseline
 cd /tmp && export TMPDIR=/tmp
-run m3_prof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_r06f -o run -- python3 $R/bench.py --steps 14 --warmup 3 --no-cpu-baseline
-run m3_pf 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcf_r06f -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
-run m3_pw 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcw_r06f -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
-run m3_pm 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/pmcm_r06f -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
+run m3_prof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_r06g -o run -- python3 $R/bench.py --steps 14 --warmup 3 --no-cpu-baseline
+run m3_pf 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcf_r06g -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
+run m3_pw 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcw_r06g -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
+run m3_pm 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/pmcm_r06g -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
