@@ -319,13 +319,15 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
 
 // backward reduce: partial[c][b] = (sum g, sum g*xhat), g = dy * relu'(y); dy row r comes
 // from the gradient source G (DenseGrad: the [rows][C] tensor; Pool3s2Grad: gathered from the
-// stem pool's output gradient and argmax, pool.h)
-template <typename T, class G>
+// stem pool's output gradient and argmax, pool.h); MODE as bn_bwd_apply_kernel's
+template <typename T, class G, int MODE>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
-    int ct, long rpb, const float* __restrict__ mean, const float* __restrict__ rstd, int relu,
+    int ct, long rpb, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ gamma, const float* __restrict__ bbeta, float2* __restrict__ part,
-    const uint8_t* __restrict__ mask) {
+    const uint8_t* __restrict__ mask_k) {
+  constexpr int relu = MODE != 0;
+  const uint8_t* mask = MODE == 1 ? mask_k : nullptr;
   typedef typename Vec16<T>::type V;
   constexpr int VEC = Vec16<T>::N;
   __shared__ float s_a[BN_NT * VEC], s_b[BN_NT * VEC];
@@ -335,13 +337,13 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
   float sg[VEC], sgx[VEC], mu[VEC], rs[VEC], sc[VEC], sh[VEC];
   // ReLU mask source: the forward's bit mask, else y (the unit's output), else recomputed
   // from x (no residual)
-  const bool mask_x = relu && !y && !mask;
+  constexpr bool mask_x = MODE == 3;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) sg[j] = sgx[j] = mu[j] = rs[j] = sc[j] = sh[j] = 0.f;
   if (c0 < C) {
     load_coef<VEC>(mean + c0, mu);
     load_coef<VEC>(rstd + c0, rs);
-    if (mask_x) {
+    if constexpr (mask_x) {
       float ga[VEC], be[VEC];
       if (gamma) load_coef<VEC>(gamma + c0, ga);
       if (bbeta) load_coef<VEC>(bbeta + c0, be);
@@ -359,13 +361,13 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(
       const V vd = dy.row(r, c0);
       V vy{};
       unsigned mb = 0;
-      if (relu && mask) mb = mask[r * (C / VEC) + c0 / VEC];
-      else if (relu && !mask_x) vy = *(const V*)(y + r * C + c0);
+      if (MODE == 1) mb = mask[r * (C / VEC) + c0 / VEC];
+      else if (MODE == 2) vy = *(const V*)(y + r * C + c0);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         float g = to_f(vd[j]);
         const float a = mask_x ? to_f(vx[j]) * sc[j] + sh[j] : to_f(vy[j]);
-        const bool pos = mask ? ((mb >> j) & 1u) != 0 : a > 0.f;
+        const bool pos = MODE == 1 ? ((mb >> j) & 1u) != 0 : a > 0.f;
         if (relu && !pos) g = 0.f;
         sg[j] += g;
         sgx[j] += g * (to_f(vx[j]) - mu[j]) * rs[j];
@@ -504,26 +506,33 @@ __device__ __forceinline__ void bn_bwd_vec(const BnBwdIn<T>& in, const float* ca
   if (dres) ((V*)dres)[i] = og;
 }
 
-template <typename T, class G>
+// MODE (host-chosen): 0 no ReLU, 1 ReLU mask saved by the forward, 2 ReLU from y, 3 ReLU
+// recomputed from x (the only mode that needs scale/shift: keeping them out of the others'
+// registers lifts the bf16 kernel from 5 to 6+ waves per SIMD)
+template <typename T, class G, int MODE>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
-    const float* __restrict__ coef, int relu, T* __restrict__ dx, T* __restrict__ dres,
+    const float* __restrict__ coef, T* __restrict__ dx, T* __restrict__ dres,
     const uint8_t* __restrict__ mask) {
-  const bool mask_x = relu && !y && !mask;
+  constexpr int relu = MODE != 0;
+  constexpr bool mask_x = MODE == 3;
   constexpr int VEC = Vec16<T>::N;
+  const uint8_t* mk = MODE == 1 ? mask : nullptr;
   const RowTile rt = row_tile(C, VEC);
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
-    float ca[VEC], cb[VEC], ck[VEC], sc[VEC], sh[VEC];
+    float ca[VEC], cb[VEC], ck[VEC], sc[VEC] = {}, sh[VEC] = {};
     load_coef<VEC>(coef + j * VEC, ca);
     load_coef<VEC>(coef + C + j * VEC, cb);
     load_coef<VEC>(coef + 2 * C + j * VEC, ck);
-    load_coef<VEC>(coef + 3 * C + j * VEC, sc);
-    load_coef<VEC>(coef + 4 * C + j * VEC, sh);
+    if constexpr (mask_x) {
+      load_coef<VEC>(coef + 3 * C + j * VEC, sc);
+      load_coef<VEC>(coef + 4 * C + j * VEC, sh);
+    }
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
-      const BnBwdIn<T> in = bn_bwd_load<T, G>(x, y, dy, r, j, i, relu, mask_x, mask);
-      bn_bwd_vec<T>(in, ca, cb, ck, sc, sh, relu, mask_x, mask != nullptr, i, dx, dres);
+      const BnBwdIn<T> in = bn_bwd_load<T, G>(x, y, dy, r, j, i, relu, mask_x, mk);
+      bn_bwd_vec<T>(in, ca, cb, ck, sc, sh, relu, mask_x, MODE == 1, i, dx, dres);
     }
   }
 }
@@ -606,14 +615,26 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
   float2* part = (float2*)ws;
   float* coef = (float*)((char*)ws + (size_t)L.rblocks * C * sizeof(float2));
   int nblk = L.rblocks;
+  // ReLU mask source (the MODE of the reduce and apply kernels): none, the forward's bit mask,
+  // y (the unit's output), or recomputed from x (no residual)
+  const int mode = !relu ? 0 : mask ? 1 : y ? 2 : 3;
   if (stat_part) {  // (sum g, sum g*xhat) partials already made by the dgrad epilogue
     MMDX_CHECK_ARG(stat_blocks > 0 && relu, "bn bwd: precomputed partials need a ReLU unit");
     part = (float2*)stat_part;
     nblk = stat_blocks;
   } else {
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, G>), dim3(L.rblocks, L.cgroups), dim3(BN_NT), 0,
-                       st, (const T*)x, (const T*)y, dy, rows, C, L.ct, L.rows_per_block,
-                       smean, srstd, relu, gamma, bbeta, part, mask);
+    const dim3 g(L.rblocks, L.cgroups);
+#define MMDX_BN_BWD_REDUCE(M)                                                                \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, G, M>), g, dim3(BN_NT), 0, st, (const T*)x,   \
+                     (const T*)y, dy, rows, C, L.ct, L.rows_per_block, smean, srstd, gamma,  \
+                     bbeta, part, mask)
+    switch (mode) {
+      case 0: MMDX_BN_BWD_REDUCE(0); break;
+      case 1: MMDX_BN_BWD_REDUCE(1); break;
+      case 2: MMDX_BN_BWD_REDUCE(2); break;
+      default: MMDX_BN_BWD_REDUCE(3); break;
+    }
+#undef MMDX_BN_BWD_REDUCE
   }
   const BnBwdFinArgs fa{(const float2*)part, nblk, rows, C, train, gamma, bbeta, smean, srstd,
                         dgamma, dbeta, beta_acc, coef};
@@ -623,9 +644,17 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(nfin), dim3(256), 0, st, fa);
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3(nfin), dim3(256), 0, st, fa);
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G>), dim3(grid_rows(rows, C, VEC)), dim3(256), 0,
-                     st, (const T*)x, (const T*)y, dy, rows, C, (const float*)coef, relu,
-                     (T*)dx, (T*)dres, mask);
+  const dim3 g(grid_rows(rows, C, VEC));
+#define MMDX_BN_BWD_APPLY(M)                                                                 \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G, M>), g, dim3(256), 0, st, (const T*)x,      \
+                     (const T*)y, dy, rows, C, (const float*)coef, (T*)dx, (T*)dres, mask)
+  switch (mode) {
+    case 0: MMDX_BN_BWD_APPLY(0); break;
+    case 1: MMDX_BN_BWD_APPLY(1); break;
+    case 2: MMDX_BN_BWD_APPLY(2); break;
+    default: MMDX_BN_BWD_APPLY(3); break;
+  }
+#undef MMDX_BN_BWD_APPLY
   MMDX_LAUNCH_CHECK();
   return 0;
 }
