@@ -6,6 +6,7 @@
 // reproducible, no E[x^2]-E[x]^2 cancellation across the 10^5..10^6 rows of a layer).
 // All elementwise passes move 16 B per lane (8 bf16 / 4 fp32).
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
@@ -510,8 +511,8 @@ __device__ __forceinline__ void bn_bwd_vec(const BnBwdIn<T>& in, const float* ca
 // recomputed from x (the only mode that needs scale/shift: keeping them out of the others'
 // registers lifts the bf16 kernel from 5 to 6+ waves per SIMD)
 template <typename T, class G, int MODE>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
+__device__ __forceinline__ void bn_bwd_apply_body(
+    const T* __restrict__ x, const T* __restrict__ y, const G& dy, long rows, int C,
     const float* __restrict__ coef, T* __restrict__ dx, T* __restrict__ dres,
     const uint8_t* __restrict__ mask) {
   constexpr int relu = MODE != 0;
@@ -521,20 +522,37 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const RowTile rt = row_tile(C, VEC);
   const int j0 = threadIdx.x % rt.tpr, ro = threadIdx.x / rt.tpr;
   for (int j = j0; j < rt.cv; j += rt.tpr) {
-    float ca[VEC], cb[VEC], ck[VEC], sc[VEC] = {}, sh[VEC] = {};
+    // the forward's scale (coef[3C..]) is bit-equal to a = gamma * rstd (coef[0..C)), both
+    // formed as (gamma ? gamma[c] : 1) * rstd: MODE 3 reads only the shift besides a
+    float ca[VEC], cb[VEC], ck[VEC], sh[VEC] = {};
     load_coef<VEC>(coef + j * VEC, ca);
     load_coef<VEC>(coef + C + j * VEC, cb);
     load_coef<VEC>(coef + 2 * C + j * VEC, ck);
-    if constexpr (mask_x) {
-      load_coef<VEC>(coef + 3 * C + j * VEC, sc);
-      load_coef<VEC>(coef + 4 * C + j * VEC, sh);
-    }
+    if constexpr (mask_x) load_coef<VEC>(coef + 4 * C + j * VEC, sh);
     for (long r = (long)blockIdx.x * rt.rpi + ro; r < rows; r += (long)gridDim.x * rt.rpi) {
       const long i = r * rt.cv + j;
       const BnBwdIn<T> in = bn_bwd_load<T, G>(x, y, dy, r, j, i, relu, mask_x, mk);
-      bn_bwd_vec<T>(in, ca, cb, ck, sc, sh, relu, mask_x, MODE == 1, i, dx, dres);
+      bn_bwd_vec<T>(in, ca, cb, ck, ca, sh, relu, mask_x, MODE == 1, i, dx, dres);
     }
   }
+}
+
+template <typename T, class G, int MODE>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const T* __restrict__ x, const T* __restrict__ y, const G dy, long rows, int C,
+    const float* __restrict__ coef, T* __restrict__ dx, T* __restrict__ dres,
+    const uint8_t* __restrict__ mask) {
+  bn_bwd_apply_body<T, G, MODE>(x, y, dy, rows, C, coef, dx, dres, mask);
+}
+
+// the dense-gradient instances with a 7-waves-per-SIMD register target (MODE 3: 76 -> 72
+// VGPRs, no scratch; the gathered-gradient instances would spill under it)
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void
+bn_bwd_apply_dense_kernel(const T* __restrict__ x, const T* __restrict__ y, const DenseGrad<T> dy,
+                          long rows, int C, const float* __restrict__ coef, T* __restrict__ dx,
+                          T* __restrict__ dres, const uint8_t* __restrict__ mask) {
+  bn_bwd_apply_body<T, DenseGrad<T>, MODE>(x, y, dy, rows, C, coef, dx, dres, mask);
 }
 
 // slab count above which a whole block (not one wave) reduces a channel's partials
@@ -646,8 +664,12 @@ static int bn_bwd_t(int train, const void* x, const void* y, const G& dy, long r
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3(nfin), dim3(256), 0, st, fa);
   const dim3 g(grid_rows(rows, C, VEC));
 #define MMDX_BN_BWD_APPLY(M)                                                                 \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G, M>), g, dim3(256), 0, st, (const T*)x,      \
-                     (const T*)y, dy, rows, C, (const float*)coef, (T*)dx, (T*)dres, mask)
+  if constexpr (std::is_same<G, DenseGrad<T>>::value)                                        \
+    hipLaunchKernelGGL((bn_bwd_apply_dense_kernel<T, M>), g, dim3(256), 0, st, (const T*)x,  \
+                       (const T*)y, dy, rows, C, (const float*)coef, (T*)dx, (T*)dres, mask); \
+  else                                                                                       \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, G, M>), g, dim3(256), 0, st, (const T*)x,    \
+                       (const T*)y, dy, rows, C, (const float*)coef, (T*)dx, (T*)dres, mask)
   switch (mode) {
     case 0: MMDX_BN_BWD_APPLY(0); break;
     case 1: MMDX_BN_BWD_APPLY(1); break;
